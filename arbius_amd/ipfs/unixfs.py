@@ -1,0 +1,191 @@
+"""Offline IPFS CIDv0 computation: dag-pb / UnixFS importer semantics.
+
+What the reference obtains from a kubo daemon / Pinata (``miner/src/ipfs.ts:11-16``:
+``cidVersion 0, sha2-256, chunker size-262144, rawLeaves false``;
+``wrapWithDirectory: true`` for solutions, ``:37-47``) computed locally, so a
+solution CID is known the moment the PNG bytes exist (commitment can be
+signalled before the pin completes).
+
+* single chunk (<= 262144 B): leaf PBNode{Data=UnixFS{File, Data, filesize}}
+  - identical to the on-chain ``IPFS.getIPFSCID`` (contract/contracts/libraries/IPFS.sol:38-65)
+* multi chunk: balanced DAG, <= 174 links per node, leaves as above,
+  internal nodes UnixFS{File, filesize, blocksizes[]}, links {Hash, Name "", Tsize}
+* directory wrap: PBNode{Links sorted by name {Hash, Name, Tsize}, Data=UnixFS{Directory}}
+
+PBNode serialisation order is Links (field 2) then Data (field 1), as dag-pb
+requires.  ``Tsize`` = total bytes of the child's DAG.
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass
+from typing import Dict, List, Sequence, Tuple
+
+CHUNK = 262144
+MAX_LINKS = 174
+B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
+
+
+def varint(n: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def b58encode(b: bytes) -> str:
+    n = int.from_bytes(b, "big")
+    s = ""
+    while n:
+        n, r = divmod(n, 58)
+        s = B58[r] + s
+    pad = len(b) - len(b.lstrip(b"\0"))
+    return "1" * pad + s
+
+
+def b58decode(s: str) -> bytes:
+    n = 0
+    for ch in s:
+        n = n * 58 + B58.index(ch)
+    body = n.to_bytes((n.bit_length() + 7) // 8, "big") if n else b""
+    pad = len(s) - len(s.lstrip("1"))
+    return b"\0" * pad + body
+
+
+def multihash_sha256(data: bytes) -> bytes:
+    return b"\x12\x20" + hashlib.sha256(data).digest()
+
+
+def _field_bytes(num: int, data: bytes) -> bytes:
+    return varint((num << 3) | 2) + varint(len(data)) + data
+
+
+def _field_varint(num: int, v: int) -> bytes:
+    return varint(num << 3) + varint(v)
+
+
+def unixfs_data(type_: int, data: bytes = None, filesize: int = None, blocksizes: Sequence[int] = ()) -> bytes:
+    out = _field_varint(1, type_)
+    if data is not None:
+        out += _field_bytes(2, data)
+    if filesize is not None:
+        out += _field_varint(3, filesize)
+    for bs in blocksizes:
+        out += _field_varint(4, bs)
+    return out
+
+
+@dataclass
+class Link:
+    hash: bytes  # multihash bytes (34)
+    name: str
+    tsize: int
+
+
+def pb_node(links: Sequence[Link], data: bytes) -> bytes:
+    out = b""
+    for l in links:
+        lb = _field_bytes(1, l.hash) + _field_bytes(2, l.name.encode()) + _field_varint(3, l.tsize)
+        out += _field_bytes(2, lb)
+    out += _field_bytes(1, data)
+    return out
+
+
+@dataclass
+class DagResult:
+    root: bytes        # root block bytes
+    cid: bytes         # multihash of root (CIDv0 bytes)
+    tsize: int         # cumulative DAG size
+    blocks: Dict[bytes, bytes]  # multihash -> block (for MockIPFS / pinning)
+    filesize: int
+
+    @property
+    def cid_str(self) -> str:
+        return b58encode(self.cid)
+
+    @property
+    def cid_hex(self) -> str:
+        return "0x" + self.cid.hex()
+
+
+def _leaf(chunk: bytes) -> Tuple[bytes, int, int]:
+    blk = pb_node([], unixfs_data(2, chunk, len(chunk)))
+    return blk, len(chunk), len(blk)
+
+
+def add_file(content: bytes, chunk_size: int = CHUNK) -> DagResult:
+    """kubo ``add`` (balanced layout, dag-pb leaves) -> root CID."""
+    blocks: Dict[bytes, bytes] = {}
+    if len(content) <= chunk_size:
+        blk, fsz, _ = _leaf(content)
+        mh = multihash_sha256(blk)
+        blocks[mh] = blk
+        return DagResult(blk, mh, len(blk), blocks, fsz)
+
+    # nodes as (mh, filesize, tsize)
+    leaves = []
+    for off in range(0, len(content), chunk_size):
+        blk, fsz, _ = _leaf(content[off:off + chunk_size])
+        mh = multihash_sha256(blk)
+        blocks[mh] = blk
+        leaves.append((mh, fsz, len(blk)))
+
+    def make_parent(children):
+        links = [Link(mh, "", ts) for mh, _, ts in children]
+        data = unixfs_data(2, None, sum(f for _, f, _ in children), [f for _, f, _ in children])
+        blk = pb_node(links, data)
+        mh = multihash_sha256(blk)
+        blocks[mh] = blk
+        return (mh, sum(f for _, f, _ in children), len(blk) + sum(ts for _, _, ts in children)), blk
+
+    # balanced builder: depth-d subtrees hold MAX_LINKS**d leaves, filled left to right
+    level = leaves
+    root_blk = None
+    while True:
+        parents = []
+        for i in range(0, len(level), MAX_LINKS):
+            node, blk = make_parent(level[i:i + MAX_LINKS])
+            parents.append(node)
+            root_blk = blk
+        if len(parents) == 1:
+            mh, fsz, ts = parents[0]
+            return DagResult(root_blk, mh, ts, blocks, fsz)
+        level = parents
+
+
+def wrap_directory(files: Sequence[Tuple[str, bytes]], chunk_size: int = CHUNK) -> DagResult:
+    """kubo ``addAll(..., wrapWithDirectory: true)`` -> directory CID (the solution CID)."""
+    blocks: Dict[bytes, bytes] = {}
+    links = []
+    total = 0
+    for name, content in files:
+        r = add_file(content, chunk_size)
+        blocks.update(r.blocks)
+        links.append(Link(r.cid, name, r.tsize))
+        total += r.filesize
+    links.sort(key=lambda l: l.name.encode())
+    blk = pb_node(links, unixfs_data(1))
+    mh = multihash_sha256(blk)
+    blocks[mh] = blk
+    return DagResult(blk, mh, len(blk) + sum(l.tsize for l in links), blocks, total)
+
+
+def onchain_cid(content: bytes) -> bytes:
+    """``IPFS.getIPFSCID`` (contract/contracts/libraries/IPFS.sol:38-65): single-chunk CIDv0."""
+    if len(content) > 65536:
+        raise ValueError("Max content size is 65536 bytes")
+    return multihash_sha256(pb_node([], unixfs_data(2, content, len(content))))
+
+
+def cid_str_to_hex(cid: str) -> str:
+    """base58 CIDv0 -> '0x1220..' (``miner/src/models.ts:52``)."""
+    return "0x" + b58decode(cid).hex()
+
+
+def cid_hex_to_str(h: str) -> str:
+    return b58encode(bytes.fromhex(h[2:] if h.startswith("0x") else h))

@@ -1,0 +1,149 @@
+"""anythingv3 / SD1.5 text-to-image pipeline (the in-process replacement of the
+Cog container's ``POST /predictions``, ``miner/src/index.ts:852-875``).
+
+  prompt, negative_prompt -> CLIP text encoder (once)
+  seed -> deterministic Gaussian latent (CPU generator -> identical on every GPU)
+  N x { CFG batch-2 UNet (replayed hipGraph) -> guidance combine -> sampler step }
+  VAE decode -> uint8 RGB -> deterministic PNG bytes
+
+On a GPU the UNet forward for a fixed (batch, latent shape) is captured once
+into a hipGraph (torch.cuda.CUDAGraph on ROCm) and replayed for every
+denoising step: the ~600 kernel launches of one UNet evaluation cost one
+graph launch, so the step is bound by the kernels, not by Python.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from .clip_text import CLIPTextConfig, CLIPTextEncoder
+from .layers import init_weights
+from .schedulers import make_scheduler
+from .tokenizer import CLIPTokenizer
+from .unet2d import UNet2DCondition, UNetConfig
+from .vae import VAEConfig, VAEDecoder
+
+
+@dataclass
+class SD15Config:
+    unet: UNetConfig = field(default_factory=UNetConfig.sd15)
+    vae: VAEConfig = field(default_factory=VAEConfig)
+    text: CLIPTextConfig = field(default_factory=CLIPTextConfig.vit_l14)
+
+    @staticmethod
+    def tiny():
+        return SD15Config(unet=UNetConfig.tiny(), vae=VAEConfig.tiny(), text=CLIPTextConfig.tiny(32))
+
+
+class _GraphedUNet:
+    """Static-shape hipGraph wrapper around one UNet forward."""
+
+    def __init__(self, unet, x_shape, ctx, dtype):
+        dev = ctx.device
+        self.unet = unet
+        self.x = torch.zeros(x_shape, dtype=dtype, device=dev)
+        self.t = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.ctx = ctx.clone()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm-up: allocator + kernel-library load outside capture
+                self.out = unet(self.x, self.t, self.ctx)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = unet(self.x, self.t, self.ctx)
+
+    def __call__(self, x, t, ctx):
+        self.x.copy_(x)
+        self.t.fill_(float(t))
+        if ctx.data_ptr() != self.ctx.data_ptr():
+            self.ctx.copy_(ctx)
+        self.graph.replay()
+        return self.out
+
+
+class SD15Pipeline:
+    def __init__(self, cfg: SD15Config = None, device="cpu", dtype=None, weight_seed: int = 0,
+                 use_graphs: Optional[bool] = None, tokenizer_dir: Optional[str] = None, init=True):
+        self.cfg = cfg or SD15Config()
+        self.device = torch.device(device)
+        if dtype is None:
+            dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        self.dtype = dtype
+        self.unet = UNet2DCondition(self.cfg.unet)
+        self.vae = VAEDecoder(self.cfg.vae)
+        self.text = CLIPTextEncoder(self.cfg.text)
+        if init:
+            init_weights(self.unet, weight_seed)
+            init_weights(self.vae, weight_seed + 1)
+            init_weights(self.text, weight_seed + 2)
+        for m in (self.unet, self.vae, self.text):
+            m.to(device=self.device, dtype=dtype).eval()
+        self.tokenizer = CLIPTokenizer(tokenizer_dir, self.cfg.text.max_len, self.cfg.text.vocab)
+        self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
+        self._graphs: Dict[tuple, _GraphedUNet] = {}
+        self.timings: Dict[str, float] = {}
+
+    def modules(self):
+        return {"unet": self.unet, "vae": self.vae, "text": self.text}
+
+    # ------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def encode_prompt(self, prompt: str, negative_prompt: str = ""):
+        ids = torch.tensor([self.tokenizer(negative_prompt), self.tokenizer(prompt)], dtype=torch.long,
+                           device=self.device)
+        hidden, _ = self.text(ids)
+        return hidden  # [2, 77, C]: (uncond, cond)
+
+    @staticmethod
+    def initial_noise(seed: int, h: int, w: int, channels: int = 4):
+        g = torch.Generator(device="cpu").manual_seed(int(seed))
+        n = torch.randn((1, channels, h, w), generator=g, dtype=torch.float32)
+        return n.permute(0, 2, 3, 1).contiguous(), g  # NHWC
+
+    def _unet_eval(self, x2, t, ctx):
+        if not self.use_graphs:
+            return self.unet(x2, torch.tensor([float(t)], device=self.device), ctx)
+        key = tuple(x2.shape)
+        if key not in self._graphs:
+            self._graphs[key] = _GraphedUNet(self.unet, x2.shape, ctx, self.dtype)
+        return self._graphs[key](x2, t, ctx)
+
+    @torch.no_grad()
+    def __call__(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
+                 num_inference_steps: int = 50, guidance_scale: float = 7.5, scheduler: str = "DDIM",
+                 seed: int = 0, output: str = "uint8"):
+        sync = torch.cuda.synchronize if self.device.type == "cuda" else (lambda: None)
+        t0 = time.perf_counter()
+        ctx = self.encode_prompt(prompt, negative_prompt)
+        h, w = height // 8, width // 8
+        x, gen = self.initial_noise(seed, h, w, self.cfg.unet.in_channels)
+        sched = make_scheduler(scheduler, num_inference_steps)
+        x = (x * sched.init_noise_sigma).to(self.device)
+        sync()
+        t1 = time.perf_counter()
+        for i, t in enumerate(sched.timesteps):
+            xin = sched.scale_model_input(x, i).to(self.dtype)
+            eps2 = self._unet_eval(torch.cat([xin, xin]), t, ctx)
+            eps = ops.ref.cfg_combine(eps2, guidance_scale)
+            x = sched.step(eps, i, x, gen)
+        sync()
+        t2 = time.perf_counter()
+        img = self.decode(x)
+        sync()
+        t3 = time.perf_counter()
+        self.timings = {"text_s": t1 - t0, "denoise_s": t2 - t1, "vae_s": t3 - t2}
+        return img
+
+    @torch.no_grad()
+    def decode(self, latent):
+        z = (latent / self.cfg.vae.scaling_factor).to(self.dtype)
+        img = self.vae(z)[0].float()
+        img = ((img / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
+        return img.cpu().numpy()  # [H, W, 3]

@@ -1,0 +1,278 @@
+"""SD1.5-architecture conditional UNet (anythingv3), channels-last, inference only.
+
+Implied compute of the anythingv3 Cog container (template
+``templates/anythingv3.json:1``): 4 resolution levels (320/640/1280/1280),
+2 ResBlocks per down level, 3 per up level, Transformer2D blocks with
+self-attention (8 heads), cross-attention to 77x768 CLIP tokens, GEGLU FF.
+
+MI355X-first choices (not a translation of any reference code - the reference
+has none, inference lives in an external container):
+  * NHWC everywhere; 1x1 proj_in/proj_out are plain GEMMs over [B*HW, C].
+  * Q/K/V of self-attention are ONE fused GEMM; K/V of cross-attention one
+    GEMM; the attention kernel reads q/k/v through strides (no reshapes).
+  * out-projections and FF down-projections fuse the residual add into the
+    GEMM (addmm, beta=1).
+  * all 22 ResBlock time-embedding projections are ONE batched GEMM per step.
+  * GroupNorm+SiLU is one HIP kernel; the nearest-x2 upsample is fused into
+    the following conv's input indexing.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .layers import Conv2d, GroupNorm, LayerNorm, Linear, timestep_embedding
+
+
+@dataclass
+class UNetConfig:
+    in_channels: int = 4
+    out_channels: int = 4
+    block_channels: Tuple[int, ...] = (320, 640, 1280, 1280)
+    attn_levels: Tuple[bool, ...] = (True, True, True, False)
+    layers_per_block: int = 2
+    heads: int = 8
+    head_dim: Optional[int] = None  # if set, heads = C // head_dim (SD2-style)
+    cross_dim: int = 768
+    groups: int = 32
+    eps: float = 1e-5
+    time_dim: int = 320  # == block_channels[0]
+
+    @staticmethod
+    def sd15():
+        return UNetConfig()
+
+    @staticmethod
+    def tiny():
+        return UNetConfig(block_channels=(32, 64, 64, 64), heads=2, cross_dim=32, groups=8, time_dim=32)
+
+
+class SelfAttention(nn.Module):
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.heads = heads
+        self.to_qkv = Linear(dim, 3 * dim, bias=False)
+        self.to_out = Linear(dim, dim)
+
+    def forward(self, x, residual):
+        B, N, C = x.shape
+        H = self.heads
+        qkv = self.to_qkv(x).view(B, N, 3, H, C // H)
+        o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])
+        return self.to_out(o.reshape(B, N, C), residual=residual)
+
+
+class CrossAttention(nn.Module):
+    def __init__(self, dim, ctx_dim, heads):
+        super().__init__()
+        self.heads = heads
+        self.to_q = Linear(dim, dim, bias=False)
+        self.to_kv = Linear(ctx_dim, 2 * dim, bias=False)
+        self.to_out = Linear(dim, dim)
+
+    def forward(self, x, ctx, residual):
+        B, N, C = x.shape
+        H = self.heads
+        q = self.to_q(x).view(B, N, H, C // H)
+        kv = self.to_kv(ctx).view(B, ctx.shape[1], 2, H, C // H)
+        o = ops.attention(q, kv[:, :, 0], kv[:, :, 1])
+        return self.to_out(o.reshape(B, N, C), residual=residual)
+
+
+class FeedForward(nn.Module):
+    """GEGLU FF: C -> 8C (value|gate) -> gelu-gated 4C -> C."""
+
+    def __init__(self, dim, mult=4):
+        super().__init__()
+        self.proj = Linear(dim, 2 * mult * dim)
+        self.out = Linear(mult * dim, dim)
+
+    def forward(self, x, residual):
+        return self.out(ops.geglu(self.proj(x)), residual=residual)
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim, ctx_dim, heads):
+        super().__init__()
+        self.norm1 = LayerNorm(dim)
+        self.attn1 = SelfAttention(dim, heads)
+        self.norm2 = LayerNorm(dim)
+        self.attn2 = CrossAttention(dim, ctx_dim, heads)
+        self.norm3 = LayerNorm(dim)
+        self.ff = FeedForward(dim)
+
+    def forward(self, h, ctx):
+        h = self.attn1(self.norm1(h), residual=h)
+        h = self.attn2(self.norm2(h), ctx, residual=h)
+        h = self.ff(self.norm3(h), residual=h)
+        return h
+
+
+class Transformer2D(nn.Module):
+    def __init__(self, dim, ctx_dim, heads, groups):
+        super().__init__()
+        self.norm = GroupNorm(groups, dim, eps=1e-6)
+        self.proj_in = Linear(dim, dim)
+        self.block = BasicTransformerBlock(dim, ctx_dim, heads)
+        self.proj_out = Linear(dim, dim)
+
+    def forward(self, x, ctx):
+        B, H, W, C = x.shape
+        h = self.norm(x).view(B, H * W, C)
+        h = self.proj_in(h)
+        h = self.block(h, ctx)
+        return self.proj_out(h, residual=x.view(B, H * W, C)).view(B, H, W, C)
+
+
+class ResBlock(nn.Module):
+    def __init__(self, cin, cout, temb_dim, groups, eps):
+        super().__init__()
+        self.norm1 = GroupNorm(groups, cin, eps, silu=True)
+        self.conv1 = Conv2d(cin, cout, 3)
+        self.temb_proj = Linear(temb_dim, cout) if temb_dim else None
+        self.norm2 = GroupNorm(groups, cout, eps, silu=True)
+        self.conv2 = Conv2d(cout, cout, 3)
+        self.shortcut = Conv2d(cin, cout, 1) if cin != cout else None
+        self.cout = cout
+
+    def forward(self, x, temb_out=None):
+        """temb_out: this block's projected time embedding [B, cout] (batched GEMM)."""
+        h = self.conv1(self.norm1(x))
+        if temb_out is not None:
+            h = h + temb_out[:, None, None, :]
+        h = self.norm2(h)
+        skip = self.shortcut(x) if self.shortcut is not None else x
+        return self.conv2(h, residual=skip)
+
+
+class Downsample(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = Conv2d(c, c, 3, stride=2, padding=1)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class Upsample(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = Conv2d(c, c, 3)
+
+    def forward(self, x):
+        return self.conv(x, upsample=True)
+
+
+class UNet2DCondition(nn.Module):
+    def __init__(self, cfg: UNetConfig = None):
+        super().__init__()
+        cfg = cfg or UNetConfig()
+        self.cfg = cfg
+        ch = cfg.block_channels
+        tdim = cfg.time_dim * 4
+        self.conv_in = Conv2d(cfg.in_channels, ch[0], 3)
+        self.time_lin1 = Linear(cfg.time_dim, tdim)
+        self.time_lin2 = Linear(tdim, tdim)
+
+        def heads_for(c):
+            return c // cfg.head_dim if cfg.head_dim else cfg.heads
+
+        self.down = nn.ModuleList()
+        skip_ch = [ch[0]]
+        cur = ch[0]
+        for lvl, c in enumerate(ch):
+            blk = nn.Module()
+            blk.resnets = nn.ModuleList()
+            blk.attns = nn.ModuleList()
+            for _ in range(cfg.layers_per_block):
+                blk.resnets.append(ResBlock(cur, c, tdim, cfg.groups, cfg.eps))
+                cur = c
+                if cfg.attn_levels[lvl]:
+                    blk.attns.append(Transformer2D(c, cfg.cross_dim, heads_for(c), cfg.groups))
+                skip_ch.append(c)
+            blk.downsample = Downsample(c) if lvl < len(ch) - 1 else None
+            if blk.downsample is not None:
+                skip_ch.append(c)
+            self.down.append(blk)
+
+        self.mid_res1 = ResBlock(cur, cur, tdim, cfg.groups, cfg.eps)
+        self.mid_attn = Transformer2D(cur, cfg.cross_dim, heads_for(cur), cfg.groups)
+        self.mid_res2 = ResBlock(cur, cur, tdim, cfg.groups, cfg.eps)
+
+        self.up = nn.ModuleList()
+        rch = list(reversed(ch))
+        rattn = list(reversed(cfg.attn_levels))
+        for lvl, c in enumerate(rch):
+            blk = nn.Module()
+            blk.resnets = nn.ModuleList()
+            blk.attns = nn.ModuleList()
+            for _ in range(cfg.layers_per_block + 1):
+                s = skip_ch.pop()
+                blk.resnets.append(ResBlock(cur + s, c, tdim, cfg.groups, cfg.eps))
+                cur = c
+                if rattn[lvl]:
+                    blk.attns.append(Transformer2D(c, cfg.cross_dim, heads_for(c), cfg.groups))
+            blk.upsample = Upsample(c) if lvl < len(rch) - 1 else None
+            self.up.append(blk)
+
+        self.norm_out = GroupNorm(cfg.groups, ch[0], cfg.eps, silu=True)
+        self.conv_out = Conv2d(ch[0], cfg.out_channels, 3)
+        self._temb_cache = None
+
+    # ---- batched time-embedding projection for all ResBlocks -------------------------------
+    def _resblocks(self) -> List[ResBlock]:
+        return [m for m in self.modules() if isinstance(m, ResBlock)]
+
+    def _temb_weights(self):
+        rbs = self._resblocks()
+        key = tuple(r.temb_proj.weight.data_ptr() for r in rbs)
+        if self._temb_cache is None or self._temb_cache[0] != key:
+            w = torch.cat([r.temb_proj.weight for r in rbs], dim=0)
+            b = torch.cat([r.temb_proj.bias for r in rbs], dim=0)
+            self._temb_cache = (key, w, b, [r.cout for r in rbs])
+        return self._temb_cache[1:]
+
+    def time_embed(self, t, batch, dtype):
+        """t: scalar / [B] timestep -> per-ResBlock projected embeddings (dict)."""
+        if not torch.is_tensor(t):
+            t = torch.tensor([t], dtype=torch.float32)
+        t = t.reshape(-1).to(self.conv_in.weight.device)
+        if t.numel() == 1:
+            t = t.expand(batch)
+        emb = timestep_embedding(t, self.cfg.time_dim).to(dtype)
+        emb = self.time_lin2(ops.silu(self.time_lin1(emb)))
+        w, b, couts = self._temb_weights()
+        allp = ops.linear(ops.silu(emb), w, b)  # one GEMM for every ResBlock
+        return dict(zip(self._resblocks(), torch.split(allp, couts, dim=1)))
+
+    def forward(self, x, t, ctx, temb=None):
+        """x [B, H, W, 4] latent (channels-last), t timestep, ctx [B, 77, cross_dim]."""
+        if temb is None:
+            temb = self.time_embed(t, x.shape[0], x.dtype)
+        h = self.conv_in(x)
+        skips = [h]
+        for blk in self.down:
+            for i, rb in enumerate(blk.resnets):
+                h = rb(h, temb[rb])
+                if len(blk.attns):
+                    h = blk.attns[i](h, ctx)
+                skips.append(h)
+            if blk.downsample is not None:
+                h = blk.downsample(h)
+                skips.append(h)
+        h = self.mid_res1(h, temb[self.mid_res1])
+        h = self.mid_attn(h, ctx)
+        h = self.mid_res2(h, temb[self.mid_res2])
+        for blk in self.up:
+            for i, rb in enumerate(blk.resnets):
+                h = torch.cat([h, skips.pop()], dim=-1)
+                h = rb(h, temb[rb])
+                if len(blk.attns):
+                    h = blk.attns[i](h, ctx)
+            if blk.upsample is not None:
+                h = blk.upsample(h)
+        return self.conv_out(self.norm_out(h))

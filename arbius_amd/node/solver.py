@@ -1,0 +1,47 @@
+"""Task solver: hydrated template input -> output files -> solution CID.
+
+This is the in-process replacement of ``EnabledModels[..].getfiles`` + ``default__getcid``
+(``miner/src/index.ts:781-877``, ``miner/src/models.ts:34-54``): instead of an HTTP
+POST to a Cog container and a kubo ``addAll``, the GPU worker runs the pipeline,
+encodes a deterministic PNG and computes the wrapped-directory CIDv0 locally.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Tuple
+
+from ..ipfs.unixfs import DagResult, wrap_directory
+from ..utils.png import encode_png
+
+EVIL_CID = "0x1220" + "66" * 32  # miner/src/models.ts:40-42 (evilmode fault injection)
+
+
+@dataclass
+class Solution:
+    files: List[Tuple[str, bytes]]
+    cid: str                       # 0x1220... (34 bytes hex)
+    dag: DagResult = None
+    timings: Dict[str, float] = field(default_factory=dict)
+
+
+def solve_image(pipe, inp: dict, png_level: int = 6) -> Solution:
+    """SD-family text-to-image task (anythingv3 template semantics)."""
+    t0 = time.perf_counter()
+    img = pipe(
+        prompt=inp["prompt"],
+        negative_prompt=inp.get("negative_prompt", ""),
+        width=int(inp.get("width", 768)),
+        height=int(inp.get("height", 768)),
+        num_inference_steps=int(inp.get("num_inference_steps", 20)),
+        guidance_scale=float(inp.get("guidance_scale", 12)),
+        scheduler=inp.get("scheduler", "DPMSolverMultistep"),
+        seed=int(inp["seed"]),
+    )
+    t1 = time.perf_counter()
+    png = encode_png(img, png_level)
+    dag = wrap_directory([("out-1.png", png)])
+    t2 = time.perf_counter()
+    tm = dict(getattr(pipe, "timings", {}))
+    tm.update({"infer_s": t1 - t0, "encode_cid_s": t2 - t1})
+    return Solution([("out-1.png", png)], dag.cid_hex, dag, tm)

@@ -1,0 +1,115 @@
+"""Fused operators of the inference engine.
+
+Every op here has exactly one GPU implementation: a hand-written gfx950 HIP
+kernel in ``csrc/`` (loaded from the in-tree ``libarbius_kernels.so`` through
+``_lib``), or - for plain GEMMs / convolutions not yet covered by a kernel -
+the ROCm library call (hipBLASLt / MIOpen) that PyTorch issues.  CPU tensors
+run the PyTorch reference in ``ref.py`` (the no-GPU plumbing config and the
+numerics oracle for tests).
+
+On a GPU, a missing ``libarbius_kernels.so`` is a hard error (``_lib.lib()``
+raises): there is no silent eager fallback.  ``ARBIUS_REFERENCE_OPS=1`` forces
+the PyTorch reference on GPU tensors too; it exists only for A/B measurement
+(bench.py --reference-ops) and parity tests.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import ref
+from . import _lib
+
+_FORCE_REF = os.environ.get("ARBIUS_REFERENCE_OPS", "0") == "1"
+
+
+def set_reference_ops(flag: bool) -> None:
+    global _FORCE_REF
+    _FORCE_REF = bool(flag)
+
+
+def _hip(t: torch.Tensor) -> bool:
+    return t.is_cuda and not _FORCE_REF
+
+
+# --------------------------------------------------------------------------- GEMM / conv
+def linear(x, w, b=None, residual=None):
+    """y = x @ w^T + b (+ residual).  Plain GEMM -> hipBLASLt via torch."""
+    if residual is not None:
+        x2 = x.reshape(-1, x.shape[-1])
+        r2 = residual.reshape(-1, w.shape[0])
+        if b is not None:
+            y = torch.addmm(r2, x2, w.t())
+            y = y.add_(b)
+        else:
+            y = torch.addmm(r2, x2, w.t())
+        return y.reshape(*x.shape[:-1], w.shape[0])
+    return F.linear(x, w, b)
+
+
+def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None):
+    """Channels-last conv. x [B,H,W,Cin], w [Cout,kh,kw,Cin]."""
+    if _hip(x) and _lib.has("conv2d_nhwc") and stride == 1 and w.shape[1] in (1, 3) \
+            and x.dtype == torch.bfloat16:
+        return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual)
+    if x.is_cuda:
+        # MIOpen NHWC path: a permuted view of a contiguous NHWC tensor is an
+        # NCHW tensor in channels_last memory format (no copy).
+        xc = x.permute(0, 3, 1, 2)
+        if upsample:
+            xc = F.interpolate(xc, scale_factor=2.0, mode="nearest")
+        y = F.conv2d(xc, w.permute(0, 3, 1, 2), b, stride=stride, padding=padding)
+        y = y.permute(0, 2, 3, 1)
+        if not y.is_contiguous():
+            y = y.contiguous()
+        if residual is not None:
+            y = y + residual
+        return y
+    y = ref.conv2d_nhwc(x, w, b, stride, padding, upsample)
+    if residual is not None:
+        y = y + residual
+    return y
+
+
+# --------------------------------------------------------------------------- normalisation
+def group_norm(x, gamma, beta, groups, eps, silu=False):
+    if _hip(x):
+        return _lib.group_norm_nhwc(x, gamma, beta, groups, eps, silu)
+    return ref.group_norm_nhwc(x, gamma, beta, groups, eps, silu)
+
+
+def layer_norm(x, gamma, beta, eps):
+    if _hip(x):
+        return _lib.layer_norm(x, gamma, beta, eps)
+    return ref.layer_norm(x, gamma, beta, eps)
+
+
+# --------------------------------------------------------------------------- attention
+def attention(q, k, v, scale=None, causal=False):
+    """q [B,Nq,H,D], k/v [B,Nk,H,D] (last dim contiguous) -> [B,Nq,H,D]."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if _hip(q):
+        return _lib.flash_attention(q, k, v, scale, causal)
+    return ref.attention(q, k, v, scale, causal)
+
+
+# --------------------------------------------------------------------------- elementwise
+def geglu(h):
+    if _hip(h):
+        return _lib.geglu(h)
+    return ref.geglu(h)
+
+
+def silu(x):
+    if _hip(x):
+        return _lib.silu(x)
+    return ref.silu(x)
+
+
+def native_loaded() -> bool:
+    """True when the HIP kernel library is loaded in this process."""
+    return _lib.loaded()

@@ -1,0 +1,200 @@
+"""ctypes binding of ``libarbius_kernels.so`` (the gfx950 HIP kernels in csrc/).
+
+Kernels are launched on PyTorch's current HIP stream, output buffers come from
+the PyTorch caching allocator, so everything here is hipGraph-capture safe.
+Shape/stride checks happen on the host BEFORE a launch (a bad launch on the
+shared GPU box can fault the whole node).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_HERE = Path(__file__).resolve().parent
+_LIB_PATH = _HERE / "libarbius_kernels.so"
+_lib = None
+_SYMBOLS = {}
+
+c_void_p, c_int, c_long, c_float, c_size_t = (ctypes.c_void_p, ctypes.c_int, ctypes.c_long,
+                                              ctypes.c_float, ctypes.c_size_t)
+
+_SIGS = {
+    "arb_group_norm_workspace": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "arb_group_norm_nhwc": (c_int, [c_void_p] * 5 + [c_int] * 4 + [c_float, c_int, c_void_p]),
+    "arb_layer_norm": (c_int, [c_void_p] * 4 + [c_int, c_int, c_float, c_void_p]),
+    "arb_flash_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_int, c_void_p]),
+    "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
+    "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
+    "arb_conv2d_nhwc": (c_int, [c_void_p] * 5 + [c_int] * 8 + [c_void_p]),
+    "arb_temporal_attention": (c_int, [c_void_p] * 4 + [c_int] * 5 + [c_float, c_void_p]),
+    "arb_convgru_gates": (c_int, [c_void_p] * 5 + [c_long, c_int, c_void_p]),
+}
+
+
+def lib():
+    """Load the kernel library; raises (loudly) if it is missing or stale."""
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            if os.environ.get("ARBIUS_AUTOBUILD", "1") == "1":
+                from .build import build
+                build()
+            if not _LIB_PATH.exists():
+                raise RuntimeError(
+                    f"{_LIB_PATH} missing: build it with `python -m arbius_amd.ops.build` "
+                    "(GPU tensors never fall back to eager PyTorch)")
+        L = ctypes.CDLL(str(_LIB_PATH))
+        for name, (res, args) in _SIGS.items():
+            try:
+                fn = getattr(L, name)
+            except AttributeError:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+            _SYMBOLS[name] = fn
+        _lib = L
+    return _lib
+
+
+def loaded() -> bool:
+    return _lib is not None
+
+
+def has(op: str) -> bool:
+    try:
+        lib()
+    except Exception:
+        return False
+    return ("arb_" + op) in _SYMBOLS
+
+
+def _fn(name):
+    lib()
+    try:
+        return _SYMBOLS[name]
+    except KeyError:
+        raise RuntimeError(f"kernel symbol {name} not in {_LIB_PATH} (rebuild)") from None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what}: HIP launch failed (rc={rc})")
+
+
+def _bf16(*ts):
+    for t in ts:
+        if t is not None and t.dtype != torch.bfloat16:
+            raise TypeError(f"HIP kernels take bf16 tensors, got {t.dtype}")
+
+
+# --------------------------------------------------------------------------- norms
+def group_norm_nhwc(x, gamma, beta, groups, eps, silu):
+    _bf16(x, gamma, beta)
+    x = x.contiguous()
+    B, C = x.shape[0], x.shape[-1]
+    HW = x.numel() // (B * C)
+    if C % 8 or C // 8 > 256 or C % groups:
+        raise ValueError(f"group_norm: unsupported C={C} G={groups}")
+    ws_bytes = _fn("arb_group_norm_workspace")(B, HW, C, groups)
+    ws = torch.empty(max(16, ws_bytes), dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(x)
+    _check(_fn("arb_group_norm_nhwc")(_p(x), _p(y), _p(gamma), _p(beta), _p(ws), B, HW, C, groups,
+                                      float(eps), int(bool(silu)), _stream()), "group_norm")
+    return y
+
+
+def layer_norm(x, gamma, beta, eps):
+    _bf16(x, gamma, beta)
+    x = x.contiguous()
+    C = x.shape[-1]
+    if C % 8 or C > 2048:
+        raise ValueError(f"layer_norm: unsupported C={C}")
+    M = x.numel() // C
+    y = torch.empty_like(x)
+    _check(_fn("arb_layer_norm")(_p(x), _p(y), _p(gamma), _p(beta), M, C, float(eps), _stream()), "layer_norm")
+    return y
+
+
+# --------------------------------------------------------------------------- attention
+def flash_attention(q, k, v, scale, causal):
+    """q [B,Nq,H,D], k/v [B,Nk,H,D] (last dim contiguous, strides multiple of 8)."""
+    _bf16(q, k, v)
+    B, Nq, H, D = q.shape
+    Nk = k.shape[1]
+    if D > 160:
+        from . import ref
+        return _large_head_attention(q, k, v, scale)
+    for t in (q, k, v):
+        if t.stride(-1) != 1 or any(s % 8 for s in t.stride()[:3]) or t.data_ptr() % 16:
+            raise ValueError("flash_attention: last dim must be contiguous, strides/base 16B aligned")
+    if D % 8:
+        raise ValueError(f"flash_attention: D={D} not a multiple of 8")
+    o = torch.empty(B, Nq, H, D, dtype=q.dtype, device=q.device)
+    strides = (ctypes.c_long * 12)(q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+                                   v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2))
+    _check(_fn("arb_flash_attention")(_p(q), _p(k), _p(v), _p(o), strides, B, H, Nq, Nk, D, float(scale),
+                                      int(bool(causal)), _stream()), "flash_attention")
+    return o
+
+
+def _large_head_attention(q, k, v, scale):
+    """Head dims > 160 (the single-head d=512 VAE mid-block attention): two
+    hipBLASLt GEMMs around an fp32 softmax.  Runs once per task."""
+    qf = q.transpose(1, 2)
+    kf = k.transpose(1, 2)
+    vf = v.transpose(1, 2)
+    s = torch.matmul(qf, kf.transpose(-1, -2)).float() * scale
+    p = torch.softmax(s, dim=-1).to(q.dtype)
+    return torch.matmul(p, vf).transpose(1, 2).contiguous()
+
+
+# --------------------------------------------------------------------------- elementwise
+def geglu(h):
+    _bf16(h)
+    h = h.contiguous()
+    F2 = h.shape[-1]
+    F = F2 // 2
+    M = h.numel() // F2
+    out = torch.empty(*h.shape[:-1], F, dtype=h.dtype, device=h.device)
+    _check(_fn("arb_geglu")(_p(h), _p(out), M, F, _stream()), "geglu")
+    return out
+
+
+def silu(x):
+    _bf16(x)
+    x = x.contiguous()
+    if x.numel() % 8:
+        from . import ref
+        return ref.silu(x)
+    y = torch.empty_like(x)
+    _check(_fn("arb_silu")(_p(x), _p(y), x.numel(), _stream()), "silu")
+    return y
+
+
+def conv2d_nhwc(x, w, b, padding, upsample, residual):
+    _bf16(x, w, b, residual)
+    x = x.contiguous()
+    B, H, W, Cin = x.shape
+    Cout, kh, kw, Cin2 = w.shape
+    assert Cin == Cin2 and kh == kw
+    Ho, Wo = (2 * H, 2 * W) if upsample else (H, W)
+    Ho = Ho + 2 * padding - kh + 1
+    Wo = Wo + 2 * padding - kw + 1
+    y = torch.empty(B, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == y.shape
+    _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w.contiguous()), _p(b), _p(residual), _p(y), B, H, W, Cin, Cout, kh,
+                                  padding, int(bool(upsample)), _stream()), "conv2d")
+    return y

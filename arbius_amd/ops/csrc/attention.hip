@@ -1,0 +1,260 @@
+// Flash attention forward for gfx950 (bf16 in/out, fp32 softmax + accumulate).
+//
+// Serves every attention of the engine: UNet self-attention (seq 4096/1024/256/64,
+// head dims 40/80/160), cross-attention against 77 text tokens, CLIP causal
+// self-attention (d 64), Kandinsky joint attention and the UNet3D temporal
+// attention (seq = frames).  SURVEY.md §2.6 (a)-(c), §5.7.
+//
+// Structure (one workgroup = 4 waves, QT x 16 query rows per wave):
+//   * swapped product S^T = K Q^T on mfma_f32_16x16x32_bf16, so each lane
+//     owns ONE query column (q = lane&15) and 4 keys per 16-key tile:
+//     the softmax row statistics need only two cross-lane steps (xor 16/32)
+//     and the O^T accumulator rows are already lane-aligned with them.
+//   * P^T goes straight from the S^T accumulators into the B operand of
+//     O^T = V^T P^T with a permuted k order (no LDS round-trip for P).
+//   * V^T fragments come from the row-major V tile in LDS through the CDNA4
+//     transposing read ds_read_b64_tr_b16 (two per 32-key step / 16-col tile),
+//     row stride 16*(odd) elements -> conflict-free (cdna_hip_programming T10).
+//   * K tile rows padded by 16 B; Q fragments live in registers.
+//   * head dim is padded to 32 (QK^T k-dim) / 16 (PV n-dim) with zero fill;
+//     key padding is masked with -inf, V padding rows are zeroed.
+//   * 1-D XCD-aware block remap: the q-blocks of one (batch, head) share an L2.
+//   * no atomics, fixed reduction order -> bitwise deterministic.
+#include "common.h"
+
+#define KV_BLK 64
+
+struct AttnArgs {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  bf16_t* o;
+  long q_sb, q_sn, q_sh;
+  long k_sb, k_sn, k_sh;
+  long v_sb, v_sn, v_sh;
+  long o_sb, o_sn, o_sh;
+  int B, H, Nq, Nk, D;
+  float scale_log2;
+  int causal;
+};
+
+template <int KSTEPS, int DT, int QT>
+__global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
+  constexpr int KROW = KSTEPS * 32 + 8;    // K tile row (elements): 16 B pad
+  constexpr int VROW = 16 * (DT | 1);      // V tile row: 16*(odd) -> tr-read conflict free
+  constexpr int QBLK = 4 * QT * 16;        // queries per workgroup
+  __shared__ __attribute__((aligned(16))) bf16_t sK[KV_BLK * KROW];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[KV_BLK * VROW];
+
+  const int nqb = (a.Nq + QBLK - 1) / QBLK;
+  const int total = nqb * a.H * a.B;
+  const int lin = xcd_remap(blockIdx.x, total);
+  const int qb = lin % nqb;
+  const int h = (lin / nqb) % a.H;
+  const int b = lin / (nqb * a.H);
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lq = lane & 15, g = lane >> 4;
+  const int D = a.D;
+
+  const bf16_t* qbase = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16_t* kbase = a.k + b * a.k_sb + h * a.k_sh;
+  const bf16_t* vbase = a.v + b * a.v_sb + h * a.v_sh;
+
+  // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[q][32s + 8g .. +7]
+  bf16x8 qf[QT][KSTEPS];
+  int qidx[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    qidx[qt] = qb * QBLK + (wave * QT + qt) * 16 + lq;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      const int d = 32 * s + 8 * g;
+      uint4 raw = make_uint4(0, 0, 0, 0);
+      if (qidx[qt] < a.Nq && d < D) raw = ld16(qbase + (long)qidx[qt] * a.q_sn + d);
+      qf[qt][s] = __builtin_bit_cast(bf16x8, raw);
+    }
+  }
+
+  f32x4 o[QT][DT];
+  float m_run[QT], l_run[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    m_run[qt] = -INFINITY;
+    l_run[qt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[qt][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+
+  int kv_end = a.Nk;
+  if (a.causal) {
+    const int qmax = min(a.Nq, (qb + 1) * QBLK) - 1;
+    kv_end = min(a.Nk, qmax + 1);
+  }
+
+  for (int kv0 = 0; kv0 < kv_end; kv0 += KV_BLK) {
+    __syncthreads();
+    // ---- cooperative K / V tile load (16-byte chunks), zero fill outside (Nk, D)
+    constexpr int KCH = KV_BLK * KSTEPS * 4;
+    for (int c = tid; c < KCH; c += 256) {
+      const int r = c / (KSTEPS * 4), col = (c % (KSTEPS * 4)) * 8;
+      uint4 raw = make_uint4(0, 0, 0, 0);
+      if (kv0 + r < a.Nk && col < D) raw = ld16(kbase + (long)(kv0 + r) * a.k_sn + col);
+      st16(&sK[r * KROW + col], raw);
+    }
+    constexpr int VCH = KV_BLK * DT * 2;
+    for (int c = tid; c < VCH; c += 256) {
+      const int r = c / (DT * 2), col = (c % (DT * 2)) * 8;
+      uint4 raw = make_uint4(0, 0, 0, 0);
+      if (kv0 + r < a.Nk && col < D) raw = ld16(vbase + (long)(kv0 + r) * a.v_sn + col);
+      st16(&sV[r * VROW + col], raw);
+    }
+    __syncthreads();
+
+    // ---- S^T tiles: 4 key tiles x QT query tiles
+    f32x4 st[QT][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) st[qt][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        const bf16x8 kf = __builtin_bit_cast(bf16x8, ld16(&sK[(16 * t + lq) * KROW + 32 * s + 8 * g]));
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          st[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][s], st[qt][t], 0, 0, 0);
+      }
+    }
+
+    // ---- online softmax (per query column = lane&15)
+    bf16x8 pf[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      float mloc = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kv0 + 16 * t + 4 * g + r;
+          float sv = st[qt][t][r] * a.scale_log2;
+          const bool masked = key >= a.Nk || (a.causal && key > qidx[qt]);
+          sv = masked ? -INFINITY : sv;
+          st[qt][t][r] = sv;
+          mloc = fmaxf(mloc, sv);
+        }
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float m_new = fmaxf(m_run[qt], mloc);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run[qt] - m_use);
+      m_run[qt] = m_new;
+      float lsum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(st[qt][t][r] - m_use);
+          st[qt][t][r] = p;
+          lsum += p;
+        }
+      }
+      l_run[qt] = l_run[qt] * alpha + lsum;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[qt][dt] *= alpha;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 p;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          p[j] = (__bf16)st[qt][2 * ks][j];
+          p[j + 4] = (__bf16)st[qt][2 * ks + 1][j];
+        }
+        pf[qt][ks] = p;
+      }
+    }
+
+    // ---- O^T += V^T P^T  (A = V^T via transposing LDS reads)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int qq = (lane & 15) >> 2, pp = lane & 3;
+        const bf16_t* a0 = &sV[(32 * ks + 4 * g + qq) * VROW + 16 * dt + 4 * pp];
+        const bf16_t* a1 = a0 + 16 * VROW;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, vv);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][ks], o[qt][dt], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: combine l across the 4 lane groups, normalise, store O[q][d]
+  bf16_t* obase = a.o + b * a.o_sb + h * a.o_sh;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    float l = l_run[qt];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    if (qidx[qt] < a.Nq) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int d = 16 * dt + 4 * g;
+        if (d < D) {
+          uint2 w;
+          w.x = (uint32_t)f2bf(o[qt][dt][0] * inv) | ((uint32_t)f2bf(o[qt][dt][1] * inv) << 16);
+          w.y = (uint32_t)f2bf(o[qt][dt][2] * inv) | ((uint32_t)f2bf(o[qt][dt][3] * inv) << 16);
+          *reinterpret_cast<uint2*>(obase + (long)qidx[qt] * a.o_sn + d) = w;
+        }
+      }
+    }
+  }
+}
+
+template <int KSTEPS, int DT, int QT>
+static void launch_fa(const AttnArgs& a, hipStream_t s) {
+  constexpr int QBLK = 4 * QT * 16;
+  const int nqb = (a.Nq + QBLK - 1) / QBLK;
+  dim3 grid(nqb * a.H * a.B);
+  flash_attn_fwd_kernel<KSTEPS, DT, QT><<<grid, 256, 0, s>>>(a);
+}
+
+ARB_API int arb_flash_attention(const void* q, const void* k, const void* v, void* o, const long* strides, int B,
+                                int H, int Nq, int Nk, int D, float scale, int causal, hipStream_t stream) {
+  if (D % 8 != 0 || D > 160) return -1;
+  AttnArgs a;
+  a.q = (const bf16_t*)q;
+  a.k = (const bf16_t*)k;
+  a.v = (const bf16_t*)v;
+  a.o = (bf16_t*)o;
+  a.q_sb = strides[0]; a.q_sn = strides[1]; a.q_sh = strides[2];
+  a.k_sb = strides[3]; a.k_sn = strides[4]; a.k_sh = strides[5];
+  a.v_sb = strides[6]; a.v_sn = strides[7]; a.v_sh = strides[8];
+  a.o_sb = strides[9]; a.o_sn = strides[10]; a.o_sh = strides[11];
+  a.B = B; a.H = H; a.Nq = Nq; a.Nk = Nk; a.D = D;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.causal = causal;
+  const int ks = (D + 31) / 32, dt = (D + 15) / 16;
+  // Small query counts: 1 q-tile per wave keeps more workgroups in flight.
+  const bool small = (long)B * H * Nq < 256L * 128;
+#define FA_CASE(KS, DTT)                                  \
+  if (ks == KS && dt == DTT) {                            \
+    if (small) launch_fa<KS, DTT, 1>(a, stream);          \
+    else launch_fa<KS, DTT, 2>(a, stream);                \
+    return (int)hipGetLastError();                        \
+  }
+  FA_CASE(1, 1) FA_CASE(1, 2)
+  FA_CASE(2, 3) FA_CASE(2, 4)
+  FA_CASE(3, 5) FA_CASE(3, 6)
+  FA_CASE(4, 7) FA_CASE(4, 8)
+  FA_CASE(5, 9) FA_CASE(5, 10)
+#undef FA_CASE
+  return -2;
+}

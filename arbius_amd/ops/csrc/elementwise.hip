@@ -1,0 +1,50 @@
+// Vectorised (16-byte per lane) elementwise kernels: GEGLU gate, SiLU, add.
+// Memory-bound; grid capped at ~2048 blocks with a grid-stride loop
+// (cdna_hip_programming.md Guideline 11/13).
+#include "common.h"
+
+// h: [M, 2F] (value | gate) -> out [M, F] = value * gelu(gate)
+__global__ void __launch_bounds__(256) geglu_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ out,
+                                                    long M, int F) {
+  const int FV = F >> 3;
+  const long total = M * FV;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long row = i / FV;
+    const int col = (int)(i - row * FV) * 8;
+    float a[8], g[8];
+    unpack8(ld16(h + row * 2 * F + col), a);
+    unpack8(ld16(h + row * 2 * F + F + col), g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = a[e] * gelu_f(g[e]);
+    st16(out + row * F + col, pack8(a));
+  }
+}
+
+__global__ void __launch_bounds__(256) silu_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long n8) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float f[8];
+    unpack8(ld16(x + i * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = silu_f(f[e]);
+    st16(y + i * 8, pack8(f));
+  }
+}
+
+static int grid_for(long work) {
+  long g = (work + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+ARB_API int arb_geglu(const void* h, void* out, long M, int F, hipStream_t stream) {
+  if (F % 8 != 0) return -1;
+  geglu_kernel<<<grid_for(M * (F / 8)), 256, 0, stream>>>((const bf16_t*)h, (bf16_t*)out, M, F);
+  return (int)hipGetLastError();
+}
+
+ARB_API int arb_silu(const void* x, void* y, long n, hipStream_t stream) {
+  if (n % 8 != 0) return -1;
+  silu_kernel<<<grid_for(n / 8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, n / 8);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,246 @@
+// GroupNorm (+SiLU) over channels-last activations and LayerNorm over token rows.
+//
+// GroupNorm is the normalisation of every ResBlock / Transformer2D input of the
+// SD1.5 UNet and VAE.  Activations are [B, HW, C] bf16.
+// Deterministic two-phase reduction (no atomics, fixed combine order, so the
+// same task gives the same bytes on every GPU - SURVEY.md §7.3.1):
+//   1. gn_partial : grid (chunks, B).  Each block reduces `rows` rows of one
+//      batch into per-group (n, mean, M2) with a per-channel shift (first row)
+//      and Chan's parallel combine -> robust to |mean| >> std.
+//   2. gn_apply   : grid (chunks, B).  Every block re-combines the partials of
+//      its batch in a fixed order (256 threads, G groups x 256/G slices), then
+//      normalises its rows with gamma/beta (+SiLU) and 16-byte stores.
+#include "common.h"
+
+struct Stat {
+  float n, mean, m2, pad;
+};
+
+__device__ __forceinline__ Stat chan_combine(Stat a, Stat b) {
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float n = a.n + b.n;
+  const float d = b.mean - a.mean;
+  Stat r;
+  r.n = n;
+  r.mean = a.mean + d * (b.n / n);
+  r.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / n);
+  r.pad = 0.f;
+  return r;
+}
+
+// x: [B, HW, C]; part: [B, chunks, G] Stat
+__global__ void __launch_bounds__(256) gn_partial_kernel(const bf16_t* __restrict__ x, Stat* __restrict__ part,
+                                                         int HW, int C, int G, int rows_per_chunk) {
+  const int chunk = blockIdx.x, b = blockIdx.y, chunks = gridDim.x;
+  const int NV = C >> 3;
+  const int k = 256 / NV;  // row lanes per block (NV <= 256)
+  const int t = threadIdx.x;
+  const int v = t % NV, rl = t / NV;
+  const int r_begin = chunk * rows_per_chunk;
+  const int r_end = min(HW, r_begin + rows_per_chunk);
+  __shared__ float sh_n[256];
+  __shared__ float sh_mean[256 * 8];
+  __shared__ float sh_m2[256 * 8];
+
+  float shift[8], s[8], ss[8];
+  float n = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s[i] = 0.f; ss[i] = 0.f; shift[i] = 0.f; }
+  if (rl < k) {
+    const bf16_t* base = x + ((size_t)b * HW) * C + v * 8;
+    int r = r_begin + rl;
+    if (r < r_end) unpack8(ld16(base + (size_t)r * C), shift);
+    for (; r < r_end; r += k) {
+      float f[8];
+      unpack8(ld16(base + (size_t)r * C), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = f[i] - shift[i];
+        s[i] += d;
+        ss[i] += d * d;
+      }
+      n += 1.f;
+    }
+  }
+  sh_n[t] = n;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float mean = n > 0.f ? shift[i] + s[i] / n : 0.f;
+    const float m2 = n > 0.f ? fmaxf(ss[i] - s[i] * s[i] / n, 0.f) : 0.f;
+    sh_mean[t * 8 + i] = mean;
+    sh_m2[t * 8 + i] = m2;
+  }
+  __syncthreads();
+  const int Cg = C / G;
+  if (t < G) {
+    Stat acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c = t * Cg; c < (t + 1) * Cg; ++c) {
+      const int vv = c >> 3, e = c & 7;
+      for (int j = 0; j < k; ++j) {
+        const int tt = j * NV + vv;
+        Stat it = {sh_n[tt], sh_mean[tt * 8 + e], sh_m2[tt * 8 + e], 0.f};
+        acc = chan_combine(acc, it);
+      }
+    }
+    part[((size_t)b * chunks + chunk) * G + t] = acc;
+  }
+}
+
+__global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                       const Stat* __restrict__ part, const bf16_t* __restrict__ gamma,
+                                                       const bf16_t* __restrict__ beta, int HW, int C, int G,
+                                                       int rows_per_chunk, float eps, int silu) {
+  const int chunk = blockIdx.x, b = blockIdx.y, chunks = gridDim.x;
+  const int t = threadIdx.x;
+  __shared__ Stat sh[256];
+  __shared__ float sh_mean[256], sh_rstd[256];
+  const int slices = (G <= 256 && 256 % G == 0) ? 256 / G : 1;
+  {
+    Stat acc = {0.f, 0.f, 0.f, 0.f};
+    const int g = t % G, sl = t / G;
+    if (sl < slices && t < G * slices) {
+      for (int c = sl; c < chunks; c += slices) acc = chan_combine(acc, part[((size_t)b * chunks + c) * G + g]);
+    }
+    sh[t] = acc;
+  }
+  __syncthreads();
+  if (t < G) {
+    Stat acc = sh[t];
+    for (int sl = 1; sl < slices; ++sl) acc = chan_combine(acc, sh[sl * G + t]);
+    sh_mean[t] = acc.mean;
+    sh_rstd[t] = rsqrtf(acc.m2 / fmaxf(acc.n, 1.f) + eps);
+  }
+  __syncthreads();
+
+  const int NV = C >> 3;
+  const int k = 256 / NV;
+  const int v = t % NV, rl = t / NV;
+  if (rl >= k) return;
+  const int Cg = C / G;
+  float sc[8], sf[8];
+  {
+    float gm[8], bt[8];
+    unpack8(ld16(gamma + v * 8), gm);
+    unpack8(ld16(beta + v * 8), bt);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int g = (v * 8 + i) / Cg;
+      sc[i] = sh_rstd[g] * gm[i];
+      sf[i] = bt[i] - sh_mean[g] * sc[i];
+    }
+  }
+  const int r_begin = chunk * rows_per_chunk;
+  const int r_end = min(HW, r_begin + rows_per_chunk);
+  const size_t off = ((size_t)b * HW) * C + v * 8;
+  for (int r = r_begin + rl; r < r_end; r += k) {
+    float f[8];
+    unpack8(ld16(x + off + (size_t)r * C), f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float o = f[i] * sc[i] + sf[i];
+      f[i] = silu ? silu_f(o) : o;
+    }
+    st16(y + off + (size_t)r * C, pack8(f));
+  }
+}
+
+static int gn_rows_per_chunk(int B, int HW, int C) {
+  const int NV = C / 8;
+  const int k = 256 / NV;
+  int target_chunks = 640 / (B > 0 ? B : 1);
+  if (target_chunks < 1) target_chunks = 1;
+  int rows = (HW + target_chunks - 1) / target_chunks;
+  if (rows < 4 * k) rows = 4 * k;
+  return rows;
+}
+
+ARB_API size_t arb_group_norm_workspace(int B, int HW, int C, int G) {
+  const int rows = gn_rows_per_chunk(B, HW, C);
+  const int chunks = (HW + rows - 1) / rows;
+  return (size_t)B * chunks * G * sizeof(Stat);
+}
+
+ARB_API int arb_group_norm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* workspace, int B,
+                                int HW, int C, int G, float eps, int silu, hipStream_t stream) {
+  if (C % 8 != 0 || C / 8 > 256 || C % G != 0) return -1;
+  const int rows = gn_rows_per_chunk(B, HW, C);
+  const int chunks = (HW + rows - 1) / rows;
+  dim3 grid(chunks, B);
+  gn_partial_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)x, (Stat*)workspace, HW, C, G, rows);
+  gn_apply_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const Stat*)workspace,
+                                            (const bf16_t*)gamma, (const bf16_t*)beta, HW, C, G, rows, eps, silu);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// LayerNorm: one wave per row, row held in registers (exact two-pass mean/var), 4 rows/block.
+template <int NVMAX>
+__global__ void __launch_bounds__(256) layer_norm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                         const bf16_t* __restrict__ gamma,
+                                                         const bf16_t* __restrict__ beta, int M, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int NV = C >> 3;
+  const bf16_t* xr = x + (size_t)row * C;
+  float v[NVMAX][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NVMAX; ++i) {
+    const int vi = lane + 64 * i;
+    if (vi < NV) {
+      unpack8(ld16(xr + vi * 8), v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[i][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NVMAX; ++i) {
+    const int vi = lane + 64 * i;
+    if (vi < NV) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[i][e] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / (float)C + eps);
+#pragma unroll
+  for (int i = 0; i < NVMAX; ++i) {
+    const int vi = lane + 64 * i;
+    if (vi < NV) {
+      float g[8], bb[8], o[8];
+      unpack8(ld16(gamma + vi * 8), g);
+      unpack8(ld16(beta + vi * 8), bb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + bb[e];
+      st16(y + (size_t)row * C + vi * 8, pack8(o));
+    }
+  }
+}
+
+ARB_API int arb_layer_norm(const void* x, void* y, const void* gamma, const void* beta, int M, int C, float eps,
+                           hipStream_t stream) {
+  if (C % 8 != 0) return -1;
+  const int NV = C / 8;
+  dim3 grid((M + 3) / 4);
+  if (NV <= 64)
+    layer_norm_kernel<1><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const bf16_t*)gamma,
+                                                   (const bf16_t*)beta, M, C, eps);
+  else if (NV <= 128)
+    layer_norm_kernel<2><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const bf16_t*)gamma,
+                                                   (const bf16_t*)beta, M, C, eps);
+  else if (NV <= 256)
+    layer_norm_kernel<4><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const bf16_t*)gamma,
+                                                   (const bf16_t*)beta, M, C, eps);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}

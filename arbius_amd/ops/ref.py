@@ -1,0 +1,98 @@
+"""Plain-PyTorch reference implementations of every fused op.
+
+These are the numerics oracle for the HIP kernels in ``csrc/`` (tests compare
+the kernels against these in fp32) and the execution path for CPU tensors
+(the CPU plumbing config: anythingv3 64x64 2-step DDIM).
+
+Tensor conventions (shared with the HIP kernels):
+  * activations are channels-last: images ``[B, H, W, C]``, tokens ``[B, N, C]``
+  * conv weights are ``[Cout, kh, kw, Cin]`` (OHWI) so a 3x3 conv is an
+    implicit GEMM over K = kh*kw*Cin with contiguous Cin.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+
+def conv2d_nhwc(x, w, b=None, stride=1, padding=1, upsample=False):
+    """x [B,H,W,Cin], w [Cout,kh,kw,Cin] -> [B,Ho,Wo,Cout].
+
+    ``upsample=True`` applies a nearest x2 upsample to ``x`` first (the fused
+    Upsample2D + conv of the UNet / VAE decoders)."""
+    xc = x.permute(0, 3, 1, 2)
+    if upsample:
+        xc = F.interpolate(xc, scale_factor=2.0, mode="nearest")
+    y = F.conv2d(xc, w.permute(0, 3, 1, 2), b, stride=stride, padding=padding)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def group_norm_nhwc(x, gamma, beta, groups, eps, silu=False, residual=None):
+    """GroupNorm over a channels-last tensor [B, *spatial, C] (+ optional SiLU)."""
+    B, C = x.shape[0], x.shape[-1]
+    xf = x.float().reshape(B, -1, groups, C // groups)
+    mean = xf.mean(dim=(1, 3), keepdim=True)
+    var = xf.var(dim=(1, 3), unbiased=False, keepdim=True)
+    y = (xf - mean) * torch.rsqrt(var + eps)
+    y = y.reshape(x.shape) * gamma.float() + beta.float()
+    if silu:
+        y = F.silu(y)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
+def layer_norm(x, gamma, beta, eps):
+    return F.layer_norm(x.float(), (x.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)
+
+
+def attention(q, k, v, scale=None, causal=False):
+    """Token-major multi-head attention.
+
+    q [B, Nq, H, D], k/v [B, Nk, H, D] (any strides) -> out [B, Nq, H, D]."""
+    D = q.shape[-1]
+    if scale is None:
+        scale = 1.0 / math.sqrt(D)
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        n_q, n_k = s.shape[-2], s.shape[-1]
+        mask = torch.ones(n_q, n_k, dtype=torch.bool, device=s.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    o = torch.matmul(p, vf)
+    return o.transpose(1, 2).to(q.dtype)
+
+
+def geglu(h):
+    """h [..., 2F] -> a * gelu(gate) with (a, gate) = split(h)."""
+    a, gate = h.float().chunk(2, dim=-1)
+    return (a * F.gelu(gate)).to(h.dtype)
+
+
+def silu(x):
+    return F.silu(x.float()).to(x.dtype)
+
+
+def cfg_combine(eps, scale):
+    """eps [2B, ...] = cat(uncond, cond) -> uncond + scale*(cond-uncond), fp32."""
+    u, c = eps.float().chunk(2)
+    return u + scale * (c - u)
+
+
+def temporal_attention(x, wq, wk, wv, wo, bo, heads, scale=None):
+    """Attention along the frame axis. x [B, F, N, C] -> [B, F, N, C] (fp32 ref)."""
+    B, Fr, N, C = x.shape
+    D = C // heads
+    xf = x.float()
+    q = (xf @ wq.float().t()).reshape(B, Fr, N, heads, D)
+    k = (xf @ wk.float().t()).reshape(B, Fr, N, heads, D)
+    v = (xf @ wv.float().t()).reshape(B, Fr, N, heads, D)
+    # [B, N, F, H, D] so frames become the sequence axis
+    q, k, v = (t.permute(0, 2, 1, 3, 4).reshape(B * N, Fr, heads, D) for t in (q, k, v))
+    o = attention(q, k, v, scale)
+    o = o.reshape(B, N, Fr, C).permute(0, 2, 1, 3)
+    o = o @ wo.float().t() + bo.float()
+    return o.to(x.dtype)

@@ -1,0 +1,55 @@
+"""Deterministic PNG encoder (no timestamps, no metadata, fixed zlib level).
+
+Consensus requires byte-identical outputs for identical pixels (SURVEY.md
+§7.3.1): every miner must produce the same ``out-1.png`` bytes and therefore
+the same directory CID.  Rows use PNG filter 0 (None); the zlib level is fixed.
+"""
+from __future__ import annotations
+
+import struct
+import zlib
+
+import numpy as np
+
+PNG_SIG = b"\x89PNG\r\n\x1a\n"
+
+
+def _chunk(tag: bytes, data: bytes) -> bytes:
+    return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+
+def encode_png(img: np.ndarray, level: int = 6) -> bytes:
+    """img: uint8 [H, W, 3] (RGB) or [H, W, 4] (RGBA) or [H, W] (gray)."""
+    img = np.ascontiguousarray(img)
+    if img.dtype != np.uint8:
+        raise TypeError("encode_png expects uint8")
+    if img.ndim == 2:
+        img = img[:, :, None]
+    h, w, c = img.shape
+    color = {1: 0, 3: 2, 4: 6}[c]
+    raw = np.zeros((h, 1 + w * c), dtype=np.uint8)
+    raw[:, 1:] = img.reshape(h, w * c)
+    ihdr = struct.pack(">IIBBBBB", w, h, 8, color, 0, 0, 0)
+    idat = zlib.compress(raw.tobytes(), level)
+    return PNG_SIG + _chunk(b"IHDR", ihdr) + _chunk(b"IDAT", idat) + _chunk(b"IEND", b"")
+
+
+def decode_png(data: bytes) -> np.ndarray:
+    """Decoder for the files this module writes (filter 0, 8-bit)."""
+    assert data[:8] == PNG_SIG
+    pos, idat = 8, b""
+    w = h = c = None
+    while pos < len(data):
+        (ln,) = struct.unpack(">I", data[pos:pos + 4])
+        tag = data[pos + 4:pos + 8]
+        body = data[pos + 8:pos + 8 + ln]
+        pos += 12 + ln
+        if tag == b"IHDR":
+            w, h, _, color = struct.unpack(">IIBB", body[:10])
+            c = {0: 1, 2: 3, 6: 4}[color]
+        elif tag == b"IDAT":
+            idat += body
+    raw = np.frombuffer(zlib.decompress(idat), dtype=np.uint8).reshape(h, 1 + w * c)
+    if (raw[:, 0] != 0).any():
+        raise ValueError("only filter-0 PNGs supported")
+    return raw[:, 1:].reshape(h, w, c)

@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Headline benchmark: tasks solved / hour (whole node) + p50 task latency,
+anythingv3 (SD1.5 architecture) 512x512, 50 denoising steps (BASELINE.json).
+
+One "step" = every rank solves ONE complete task end to end: CLIP text encode,
+50 CFG (batch 2) UNet evaluations + sampler, VAE decode, deterministic PNG
+encode, wrapped-directory CIDv0 and the solution commitment.  Synthetic
+prompts, random-init weights of the real architecture (no checkpoints offline).
+
+N GPUs = N independent task workers (task-level data parallel, weak scaling);
+rank 0 initialises the weights and RCCL-broadcasts them over xGMI (outside the
+timed region, reported separately).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--denoise-steps", type=int, default=50)
+    ap.add_argument("--scheduler", default="DPMSolverMultistep")
+    ap.add_argument("--guidance", type=float, default=12.0)
+    ap.add_argument("--reference-ops", action="store_true", help="A/B: PyTorch ops instead of HIP kernels")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--tiny", action="store_true", help="tiny config (CPU plumbing check only)")
+    ap.add_argument("--device", default=None)
+    args = ap.parse_args()
+
+    from arbius_amd import ops
+    from arbius_amd.models.sd15 import SD15Config, SD15Pipeline
+    from arbius_amd.node.solver import solve_image
+    from arbius_amd.parallel import dist as D
+    from arbius_amd.utils.protocol import generate_commitment, taskid2seed
+    from arbius_amd.utils.keccak import keccak256
+
+    if args.reference_ops:
+        ops.set_reference_ops(True)
+    dev_type = "cuda" if (args.device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda") else "cpu"
+    rank, local, world, dev = D.init(device_type=dev_type)
+    n = world
+
+    cfg = SD15Config.tiny() if args.tiny else SD15Config()
+    t_init = time.perf_counter()
+    pipe = SD15Pipeline(cfg, device=dev, init=(rank == 0), use_graphs=(dev.type == "cuda" and not args.no_graphs))
+    bstats = D.broadcast_modules(pipe.modules().values())
+    t_init = time.perf_counter() - t_init
+
+    wallet = "0x" + "11" * 20
+    lat = []
+
+    def one_task(i):
+        taskid = "0x" + keccak256(f"bench-task-{rank}-{i}".encode()).hex()
+        inp = {
+            "prompt": f"a detailed anime illustration of a castle on a hill, task {i}",
+            "negative_prompt": "lowres, bad anatomy, bad hands, text, error",
+            "width": args.res, "height": args.res,
+            "num_inference_steps": args.denoise_steps,
+            "guidance_scale": args.guidance,
+            "scheduler": args.scheduler,
+            "seed": taskid2seed(taskid),
+        }
+        t0 = time.perf_counter()
+        sol = solve_image(pipe, inp)
+        generate_commitment(wallet, taskid, sol.cid)
+        lat.append(time.perf_counter() - t0)
+        return sol
+
+    for i in range(args.warmup):
+        one_task(-1 - i)
+    lat.clear()
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    D.barrier(dev)
+    sync()
+    t0 = time.perf_counter()
+    last = None
+    for i in range(args.steps):
+        last = one_task(i)
+    sync()
+    D.barrier(dev)
+    elapsed = time.perf_counter() - t0
+    ms_per_step = D.max_over_ranks(elapsed * 1000.0 / args.steps, dev)
+    all_lat = D.all_gather_floats(lat, dev)
+    flat = sorted(x for r in all_lat for x in r)
+    p50 = statistics.median(flat) * 1000.0 if flat else float("nan")
+
+    if rank == 0:
+        tasks_per_hour = n * 3600.0 * 1000.0 / ms_per_step
+        out = {
+            "metric": "tasks_solved_per_hour",
+            "value": round(tasks_per_hour, 2),
+            "unit": "tasks/hour",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
+            "data": "synthetic prompts, random-init weights (SD1.5 architecture)",
+            "config": {
+                "model": "anythingv3 (SD1.5 UNet + KL-VAE + CLIP ViT-L/14 text)" + (" TINY" if args.tiny else ""),
+                "global_batch": n,
+                "seq_len": (args.res // 8) ** 2,
+                "resolution": args.res,
+                "denoise_steps": args.denoise_steps,
+                "scheduler": args.scheduler,
+                "cfg_batch": 2,
+                "parallelism": f"task-dp{n}",
+            },
+            "p50_task_latency_ms": round(p50, 2),
+            "stage_s": {k: round(v, 4) for k, v in (last.timings.items() if last else [])},
+            "weight_broadcast": {"bytes": bstats["bytes"], "seconds": round(bstats["seconds"], 4)},
+            "init_s": round(t_init, 2),
+            "native_kernels_loaded": ops.native_loaded(),
+            "reference_ops": bool(args.reference_ops),
+        }
+        print(json.dumps(out), flush=True)
+    if D.is_dist():
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
