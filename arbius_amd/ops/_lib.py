@@ -104,7 +104,7 @@ def group_norm_nhwc(x, gamma, beta, groups, eps, silu):
     x = x.contiguous()
     B, C = x.shape[0], x.shape[-1]
     HW = x.numel() // (B * C)
-    if C % 8 or C // 8 > 256 or C % groups:
+    if C % 8 or C // 8 > 512 or C % groups or groups > 256:
         raise ValueError(f"group_norm: unsupported C={C} G={groups}")
     ws_bytes = _fn("arb_group_norm_workspace")(B, HW, C, groups)
     ws = torch.empty(max(16, ws_bytes), dtype=torch.uint8, device=x.device)

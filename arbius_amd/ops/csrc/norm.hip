@@ -29,48 +29,63 @@ __device__ __forceinline__ Stat chan_combine(Stat a, Stat b) {
   return r;
 }
 
-// x: [B, HW, C]; part: [B, chunks, G] Stat
+// x: [B, HW, C]; part: [B, chunks, G] Stat.  Thread t owns channel vectors
+// {v, v+256, ..} (VPT of them, C up to 4096) and row lane rl (k row lanes when NV < 256).
+template <int VPT>
 __global__ void __launch_bounds__(256) gn_partial_kernel(const bf16_t* __restrict__ x, Stat* __restrict__ part,
                                                          int HW, int C, int G, int rows_per_chunk) {
   const int chunk = blockIdx.x, b = blockIdx.y, chunks = gridDim.x;
   const int NV = C >> 3;
-  const int k = 256 / NV;  // row lanes per block (NV <= 256)
+  const int k = NV >= 256 ? 1 : 256 / NV;  // row lanes per block
   const int t = threadIdx.x;
-  const int v = t % NV, rl = t / NV;
+  const int v = NV >= 256 ? t : t % NV, rl = NV >= 256 ? 0 : t / NV;
   const int r_begin = chunk * rows_per_chunk;
   const int r_end = min(HW, r_begin + rows_per_chunk);
   __shared__ float sh_n[256];
-  __shared__ float sh_mean[256 * 8];
-  __shared__ float sh_m2[256 * 8];
+  __shared__ float sh_mean[256 * 8 * VPT];
+  __shared__ float sh_m2[256 * 8 * VPT];
 
-  float shift[8], s[8], ss[8];
+  float shift[VPT][8], s[VPT][8], ss[VPT][8];
   float n = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { s[i] = 0.f; ss[i] = 0.f; shift[i] = 0.f; }
-  if (rl < k) {
-    const bf16_t* base = x + ((size_t)b * HW) * C + v * 8;
-    int r = r_begin + rl;
-    if (r < r_end) unpack8(ld16(base + (size_t)r * C), shift);
-    for (; r < r_end; r += k) {
-      float f[8];
-      unpack8(ld16(base + (size_t)r * C), f);
+  for (int j = 0; j < VPT; ++j)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float d = f[i] - shift[i];
-        s[i] += d;
-        ss[i] += d * d;
+    for (int i = 0; i < 8; ++i) { s[j][i] = 0.f; ss[j][i] = 0.f; shift[j][i] = 0.f; }
+  if (rl < k) {
+    const bf16_t* base = x + ((size_t)b * HW) * C;
+    int r = r_begin + rl;
+    if (r < r_end) {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j)
+        if (v + 256 * j < NV) unpack8(ld16(base + (size_t)r * C + (v + 256 * j) * 8), shift[j]);
+    }
+    for (; r < r_end; r += k) {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        if (v + 256 * j < NV) {
+          float f[8];
+          unpack8(ld16(base + (size_t)r * C + (v + 256 * j) * 8), f);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float d = f[i] - shift[j][i];
+            s[j][i] += d;
+            ss[j][i] += d * d;
+          }
+        }
       }
       n += 1.f;
     }
   }
   sh_n[t] = n;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const float mean = n > 0.f ? shift[i] + s[i] / n : 0.f;
-    const float m2 = n > 0.f ? fmaxf(ss[i] - s[i] * s[i] / n, 0.f) : 0.f;
-    sh_mean[t * 8 + i] = mean;
-    sh_m2[t * 8 + i] = m2;
-  }
+  for (int j = 0; j < VPT; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float mean = n > 0.f ? shift[j][i] + s[j][i] / n : 0.f;
+      const float m2 = n > 0.f ? fmaxf(ss[j][i] - s[j][i] * s[j][i] / n, 0.f) : 0.f;
+      sh_mean[(t * VPT + j) * 8 + i] = mean;
+      sh_m2[(t * VPT + j) * 8 + i] = m2;
+    }
   __syncthreads();
   const int Cg = C / G;
   if (t < G) {
@@ -78,8 +93,9 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const bf16_t* __restric
     for (int c = t * Cg; c < (t + 1) * Cg; ++c) {
       const int vv = c >> 3, e = c & 7;
       for (int j = 0; j < k; ++j) {
-        const int tt = j * NV + vv;
-        Stat it = {sh_n[tt], sh_mean[tt * 8 + e], sh_m2[tt * 8 + e], 0.f};
+        const int tt = NV >= 256 ? (vv & 255) : j * NV + vv;
+        const int slot = NV >= 256 ? (vv >> 8) : 0;
+        Stat it = {sh_n[tt], sh_mean[(tt * VPT + slot) * 8 + e], sh_m2[(tt * VPT + slot) * 8 + e], 0.f};
         acc = chan_combine(acc, it);
       }
     }
@@ -114,40 +130,43 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict_
   __syncthreads();
 
   const int NV = C >> 3;
-  const int k = 256 / NV;
-  const int v = t % NV, rl = t / NV;
+  const int k = NV >= 256 ? 1 : 256 / NV;
+  const int v = NV >= 256 ? t : t % NV, rl = NV >= 256 ? 0 : t / NV;
   if (rl >= k) return;
   const int Cg = C / G;
-  float sc[8], sf[8];
-  {
-    float gm[8], bt[8];
-    unpack8(ld16(gamma + v * 8), gm);
-    unpack8(ld16(beta + v * 8), bt);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int g = (v * 8 + i) / Cg;
-      sc[i] = sh_rstd[g] * gm[i];
-      sf[i] = bt[i] - sh_mean[g] * sc[i];
-    }
-  }
   const int r_begin = chunk * rows_per_chunk;
   const int r_end = min(HW, r_begin + rows_per_chunk);
-  const size_t off = ((size_t)b * HW) * C + v * 8;
-  for (int r = r_begin + rl; r < r_end; r += k) {
-    float f[8];
-    unpack8(ld16(x + off + (size_t)r * C), f);
+  for (int vv = v; vv < NV; vv += 256) {
+    float sc[8], sf[8];
+    {
+      float gm[8], bt[8];
+      unpack8(ld16(gamma + vv * 8), gm);
+      unpack8(ld16(beta + vv * 8), bt);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float o = f[i] * sc[i] + sf[i];
-      f[i] = silu ? silu_f(o) : o;
+      for (int i = 0; i < 8; ++i) {
+        const int g = (vv * 8 + i) / Cg;
+        sc[i] = sh_rstd[g] * gm[i];
+        sf[i] = bt[i] - sh_mean[g] * sc[i];
+      }
     }
-    st16(y + off + (size_t)r * C, pack8(f));
+    const size_t off = ((size_t)b * HW) * C + vv * 8;
+    for (int r = r_begin + rl; r < r_end; r += k) {
+      float f[8];
+      unpack8(ld16(x + off + (size_t)r * C), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float o = f[i] * sc[i] + sf[i];
+        f[i] = silu ? silu_f(o) : o;
+      }
+      st16(y + off + (size_t)r * C, pack8(f));
+    }
+    if (NV < 256) break;
   }
 }
 
 static int gn_rows_per_chunk(int B, int HW, int C) {
   const int NV = C / 8;
-  const int k = 256 / NV;
+  const int k = NV >= 256 ? 1 : 256 / NV;
   int target_chunks = 640 / (B > 0 ? B : 1);
   if (target_chunks < 1) target_chunks = 1;
   int rows = (HW + target_chunks - 1) / target_chunks;
@@ -163,11 +182,14 @@ ARB_API size_t arb_group_norm_workspace(int B, int HW, int C, int G) {
 
 ARB_API int arb_group_norm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* workspace, int B,
                                 int HW, int C, int G, float eps, int silu, hipStream_t stream) {
-  if (C % 8 != 0 || C / 8 > 256 || C % G != 0) return -1;
+  if (C % 8 != 0 || C / 8 > 512 || C % G != 0 || G > 256) return -1;
   const int rows = gn_rows_per_chunk(B, HW, C);
   const int chunks = (HW + rows - 1) / rows;
   dim3 grid(chunks, B);
-  gn_partial_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)x, (Stat*)workspace, HW, C, G, rows);
+  if (C / 8 > 256)
+    gn_partial_kernel<2><<<grid, 256, 0, stream>>>((const bf16_t*)x, (Stat*)workspace, HW, C, G, rows);
+  else
+    gn_partial_kernel<1><<<grid, 256, 0, stream>>>((const bf16_t*)x, (Stat*)workspace, HW, C, G, rows);
   gn_apply_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const Stat*)workspace,
                                             (const bf16_t*)gamma, (const bf16_t*)beta, HW, C, G, rows, eps, silu);
   return (int)hipGetLastError();

@@ -16,7 +16,9 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("B,H,W,C,G,silu", [(2, 64, 64, 320, 32, True), (2, 32, 32, 640, 32, False),
                                             (2, 8, 8, 1280, 32, True), (1, 128, 128, 256, 32, True),
-                                            (2, 16, 16, 1280, 32, False), (1, 7, 9, 64, 8, True)])
+                                            (2, 16, 16, 1280, 32, False), (1, 7, 9, 64, 8, True),
+                                            (2, 16, 16, 2560, 32, True), (2, 32, 32, 1920, 32, True),
+                                            (2, 64, 64, 960, 32, False), (2, 8, 8, 2048, 32, True)])
 def test_group_norm(cuda, B, H, W, C, G, silu):
     torch.manual_seed(0)
     x = (torch.randn(B, H, W, C, device=cuda) * 3 + 5).bfloat16()
