@@ -1,0 +1,119 @@
+"""``MiningConfig.json`` - byte-compatible with the reference schema
+(``miner/src/types.ts:3-54``, example ``miner/MiningConfig.example.json``).
+
+Unknown keys (including the ``"//"`` comment keys) are ignored, exactly as the
+reference does.  One optional extension block, ``"mi355x"``, configures this
+node; the reference ignores it as an unknown key.
+"""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+from typing import Dict, List, Literal, Optional
+
+from pydantic import BaseModel, ConfigDict, Field, model_validator
+
+
+class _Base(BaseModel):
+    model_config = ConfigDict(extra="ignore", populate_by_name=True)
+
+
+class BlockchainConfig(_Base):
+    private_key: str = ""
+    rpc_url: str = ""
+    use_delegated_validator: bool = False
+    delegated_validator_address: str = ""
+
+
+class RPCConfig(_Base):
+    host: str = "localhost"
+    port: int = 8335
+
+
+class AutomineConfig(_Base):
+    enabled: bool = False
+    delay: int = 60
+    version: int = 0
+    model: str = ""
+    fee: str = "0"
+    input: dict = Field(default_factory=dict)
+
+
+class CogEntry(_Base):
+    url: str = ""
+
+
+class ReplicateConfig(_Base):
+    api_token: Optional[str] = None
+
+
+class MLConfig(_Base):
+    strategy: Literal["cog", "replicate", "local"] = "local"
+    cog: Dict[str, CogEntry] = Field(default_factory=dict)
+    replicate: ReplicateConfig = Field(default_factory=ReplicateConfig)
+
+    @model_validator(mode="before")
+    @classmethod
+    def _drop_comments(cls, v):
+        if isinstance(v, dict) and isinstance(v.get("cog"), dict):
+            v = dict(v)
+            v["cog"] = {k: e for k, e in v["cog"].items() if k != "//" and isinstance(e, dict)}
+        return v
+
+
+class HttpClientConfig(_Base):
+    url: str = "http://127.0.0.1:5001"
+
+
+class PinataConfig(_Base):
+    jwt: str = ""
+
+
+class IPFSConfig(_Base):
+    strategy: Literal["http_client", "pinata", "local"] = "local"
+    http_client: HttpClientConfig = Field(default_factory=HttpClientConfig)
+    pinata: PinataConfig = Field(default_factory=PinataConfig)
+
+
+class MI355XConfig(_Base):
+    """Extension block (ignored by the reference miner)."""
+    gpus: Optional[int] = None            # default: all visible
+    dtype: Literal["bf16", "fp16"] = "bf16"
+    models: List[str] = Field(default_factory=lambda: ["kandinsky2"])  # enabled model names
+    weights_dir: Optional[str] = None     # safetensors; None = random-init (benchmark only)
+    reference_hydration_quirks: bool = False  # mirror models.ts:185-194 quirks Q2/Q3
+    job_lease_seconds: float = 900.0
+    poll_interval_ms: int = 100           # index.ts:1081
+    min_model_filter_fee: str = "0"
+    chain_id: Optional[int] = None
+    mock_chain: bool = False              # in-process MockEngine (testing / plumbing config)
+
+
+class MiningConfig(_Base):
+    log_path: Optional[str] = None
+    db_path: str = "db.sqlite"
+    stake_buffer_percent: float = 20
+    stake_buffer_topup_percent: float = 1
+    evilmode: bool = False
+    blockchain: BlockchainConfig = Field(default_factory=BlockchainConfig)
+    rpc: RPCConfig = Field(default_factory=RPCConfig)
+    automine: AutomineConfig = Field(default_factory=AutomineConfig)
+    ml: MLConfig = Field(default_factory=MLConfig)
+    ipfs: IPFSConfig = Field(default_factory=IPFSConfig)
+    mi355x: MI355XConfig = Field(default_factory=MI355XConfig)
+
+    @model_validator(mode="after")
+    def _check(self):
+        # reference defect Q14 (blockchain.ts:31-35): delegated validator leaves `solver`
+        # undefined -> reject at load instead of failing later.
+        if self.blockchain.use_delegated_validator:
+            raise ValueError("use_delegated_validator is not supported (reference leaves solver undefined)")
+        return self
+
+    @staticmethod
+    def load(path: str) -> "MiningConfig":
+        return MiningConfig.model_validate(json.loads(Path(path).read_text()))
+
+    @staticmethod
+    def from_dict(d: dict) -> "MiningConfig":
+        return MiningConfig.model_validate(d)

@@ -52,9 +52,9 @@ class Conv2d(nn.Module):
         if self.bias is not None:
             self.bias.data.uniform_(-bound, bound, generator=gen)
 
-    def forward(self, x, upsample=False, residual=None):
+    def forward(self, x, upsample=False, residual=None, temb=None):
         return ops.conv2d(x, self.weight, self.bias, stride=self.stride, padding=self.padding,
-                          upsample=upsample, residual=residual)
+                          upsample=upsample, residual=residual, temb=temb)
 
 
 class GroupNorm(nn.Module):

@@ -141,9 +141,7 @@ class ResBlock(nn.Module):
 
     def forward(self, x, temb_out=None):
         """temb_out: this block's projected time embedding [B, cout] (batched GEMM)."""
-        h = self.conv1(self.norm1(x))
-        if temb_out is not None:
-            h = h + temb_out[:, None, None, :]
+        h = self.conv1(self.norm1(x), temb=temb_out)  # time-embedding add fused in the epilogue
         h = self.norm2(h)
         skip = self.shortcut(x) if self.shortcut is not None else x
         return self.conv2(h, residual=skip)

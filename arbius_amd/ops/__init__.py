@@ -37,26 +37,35 @@ def _hip(t: torch.Tensor) -> bool:
 
 # --------------------------------------------------------------------------- GEMM / conv
 def linear(x, w, b=None, residual=None):
-    """y = x @ w^T + b (+ residual).  Plain GEMM -> hipBLASLt via torch."""
+    """y = x @ w^T + b (+ residual).
+
+    GPU: with a residual (attention out-proj, FF down-proj, proj_out) the
+    implicit-GEMM kernel fuses bias + residual into its epilogue; plain
+    projections go to hipBLASLt (bias fused by the library)."""
+    if residual is not None and _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]):
+        return _lib.gemm(x, w, b, residual)
     if residual is not None:
         x2 = x.reshape(-1, x.shape[-1])
         r2 = residual.reshape(-1, w.shape[0])
+        y = torch.addmm(r2, x2, w.t())
         if b is not None:
-            y = torch.addmm(r2, x2, w.t())
             y = y.add_(b)
-        else:
-            y = torch.addmm(r2, x2, w.t())
         return y.reshape(*x.shape[:-1], w.shape[0])
     return F.linear(x, w, b)
 
 
-def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None):
-    """Channels-last conv. x [B,H,W,Cin], w [Cout,kh,kw,Cin]."""
-    if _hip(x) and _lib.has("conv2d_nhwc") and stride == 1 and w.shape[1] in (1, 3) \
-            and x.dtype == torch.bfloat16:
-        return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual)
+def _gemm_ok(K, N):
+    return K % 64 == 0 and N % 8 == 0
+
+
+def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, temb=None):
+    """Channels-last conv. x [B,H,W,Cin], w [Cout,kh,kw,Cin]; fused epilogue
+    (+bias, +temb[b, n] per-batch bias, +residual)."""
+    if _hip(x) and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0 and w.shape[1] in (1, 3):
+        return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride)
     if x.is_cuda:
-        # MIOpen NHWC path: a permuted view of a contiguous NHWC tensor is an
+        # MIOpen NHWC path (channel counts the kernel does not tile: 3/4-channel
+        # conv_in / conv_out).  A permuted view of a contiguous NHWC tensor is an
         # NCHW tensor in channels_last memory format (no copy).
         xc = x.permute(0, 3, 1, 2)
         if upsample:
@@ -65,10 +74,10 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None):
         y = y.permute(0, 2, 3, 1)
         if not y.is_contiguous():
             y = y.contiguous()
-        if residual is not None:
-            y = y + residual
-        return y
-    y = ref.conv2d_nhwc(x, w, b, stride, padding, upsample)
+    else:
+        y = ref.conv2d_nhwc(x, w, b, stride, padding, upsample)
+    if temb is not None:
+        y = y + temb[:, None, None, :].to(y.dtype)
     if residual is not None:
         y = y + residual
     return y

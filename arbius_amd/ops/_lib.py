@@ -28,7 +28,9 @@ _SIGS = {
     "arb_flash_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_int, c_void_p]),
     "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
-    "arb_conv2d_nhwc": (c_int, [c_void_p] * 5 + [c_int] * 8 + [c_void_p]),
+    "arb_conv2d_nhwc": (c_int, [c_void_p] * 7 + [c_int] * 9 + [c_void_p]),
+    "arb_conv2d_workspace": (c_size_t, [c_int] * 9),
+    "arb_gemm_bias_res": (c_int, [c_void_p] * 6 + [c_int] * 3 + [c_void_p]),
     "arb_temporal_attention": (c_int, [c_void_p] * 4 + [c_int] * 5 + [c_float, c_void_p]),
     "arb_convgru_gates": (c_int, [c_void_p] * 5 + [c_long, c_int, c_void_p]),
 }
@@ -182,19 +184,51 @@ def silu(x):
     return y
 
 
-def conv2d_nhwc(x, w, b, padding, upsample, residual):
-    _bf16(x, w, b, residual)
+def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1):
+    """Implicit-GEMM conv (csrc/conv.hip).  x [B,H,W,Cin], w [Cout,k,k,Cin] -> [B,Ho,Wo,Cout].
+    Fused epilogue: + bias[n] + temb[b, n] + residual[m, n]."""
+    _bf16(x, w, b, residual, temb)
     x = x.contiguous()
+    w = w.contiguous()
     B, H, W, Cin = x.shape
     Cout, kh, kw, Cin2 = w.shape
-    assert Cin == Cin2 and kh == kw
-    Ho, Wo = (2 * H, 2 * W) if upsample else (H, W)
-    Ho = Ho + 2 * padding - kh + 1
-    Wo = Wo + 2 * padding - kw + 1
+    if Cin != Cin2 or kh != kw or kh not in (1, 3) or Cin % 64 or Cout % 8 or stride not in (1, 2):
+        raise ValueError(f"conv2d: unsupported shape x={tuple(x.shape)} w={tuple(w.shape)} stride={stride}")
+    Hl, Wl = (2 * H, 2 * W) if upsample else (H, W)
+    Ho = (Hl + 2 * padding - kh) // stride + 1
+    Wo = (Wl + 2 * padding - kw) // stride + 1
     y = torch.empty(B, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     if residual is not None:
         residual = residual.contiguous()
-        assert residual.shape == y.shape
-    _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w.contiguous()), _p(b), _p(residual), _p(y), B, H, W, Cin, Cout, kh,
-                                  padding, int(bool(upsample)), _stream()), "conv2d")
+        if tuple(residual.shape) != tuple(y.shape):
+            raise ValueError(f"conv2d residual {tuple(residual.shape)} != out {tuple(y.shape)}")
+    if temb is not None:
+        temb = temb.contiguous()
+        if tuple(temb.shape) != (B, Cout):
+            raise ValueError("conv2d temb must be [B, Cout]")
+    if b is not None and b.numel() != Cout:
+        raise ValueError("conv2d bias size")
+    args = (B, H, W, Cin, Cout, kh, padding, int(bool(upsample)), stride)
+    ws_bytes = _fn("arb_conv2d_workspace")(*args)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
+    _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), *args, _stream()),
+           "conv2d")
     return y
+
+
+def gemm(x, w, b=None, residual=None):
+    """out = x @ w^T (+ b + residual) on the implicit-GEMM kernel. x [...,K], w [N,K]."""
+    _bf16(x, w, b, residual)
+    K = x.shape[-1]
+    N = w.shape[0]
+    x2 = x.reshape(-1, K).contiguous()
+    M = x2.shape[0]
+    if K % 64 or N % 8 or w.shape[1] != K:
+        raise ValueError(f"gemm: unsupported K={K} N={N}")
+    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    r2 = residual.reshape(M, N).contiguous() if residual is not None else None
+    ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
+    _check(_fn("arb_gemm_bias_res")(_p(x2), _p(w.contiguous()), _p(b), _p(r2), _p(y), _p(ws), M, N, K, _stream()),
+           "gemm")
+    return y.reshape(*x.shape[:-1], N)

@@ -1,0 +1,305 @@
+// Implicit-GEMM convolution / GEMM for gfx950 (bf16 in, fp32 accumulate, bf16 out).
+//
+// Channels-last:  out[m, n] = sum_k A[m, k] * W[n, k]   (+ bias[n] + temb[b(m), n] + residual[m, n])
+//   m = (b, ho, wo) output pixel, n = output channel, k = (r, s, cin)
+//   A[m, k] = x[b, hi, wi, cin]  gathered on the fly (zero padding, stride 1/2,
+//   optional nearest-x2 upsample folded into the index: src = (hi>>1, wi>>1)).
+// A 1x1 conv over H=1 is a plain linear layer, so this one kernel family serves
+// every UNet / VAE conv AND can serve the transformer linears with fused epilogues.
+//
+// Mapping (SURVEY.md §2.6a "conv2d 3x3 implicit-GEMM on MFMA"):
+//   * swapped product C^T = W X^T on mfma_f32_16x16x32_bf16: each lane ends with 4
+//     CONSECUTIVE output channels of one pixel -> 8-byte epilogue stores / residual loads.
+//   * 256 threads = 2x2 waves; block tile BN (channels) x BM (pixels) x BK=64.
+//   * K tile of 64 always lies inside one (r, s) tap (Cin % 64 == 0), so every A chunk
+//     is one 16-byte load of 8 contiguous channels of one input pixel.
+//   * LDS rows of 128 B with XOR chunk swizzle (chunk ^ (row & 7)): the ds_read_b128
+//     fragment reads are bank-conflict free (checked against the 16-lane groups of
+//     MI355X_MICROARCH §LDS).
+//   * register-staged double buffer (issue the next tile's global loads before the
+//     MFMAs, write LDS after them), ONE barrier per K tile.
+//   * XCD-aware bijective block remap: the N-tiles of one pixel tile share an L2.
+//   * deterministic split-K for under-filled grids: fp32 slabs + an ordered reduce
+//     kernel that applies the epilogue (no atomics -> bitwise reproducible).
+#include "common.h"
+
+struct ConvArgs {
+  const bf16_t* x;      // [B, H, W, Cin]
+  const bf16_t* w;      // [N, K]
+  const bf16_t* bias;   // [N] or null
+  const bf16_t* temb;   // [B, N] or null (per-batch bias, e.g. ResBlock time embedding)
+  const bf16_t* res;    // [M, N] or null
+  bf16_t* out;          // [M, N]
+  float* ws;            // split-K slabs [S, M, N]
+  int B, H, W, Cin;     // input (pre-upsample)
+  int Hl, Wl;           // logical input dims (after upsample)
+  int Ho, Wo;
+  int N, K, M;
+  int kw, pad, stride, upsample;
+  int ktiles, kt_per_split;
+  int tiles_n, tiles_total;
+};
+
+template <int BN, int BM, bool SPLIT>
+__global__ void __launch_bounds__(256, 2) conv_igemm_kernel(ConvArgs p) {
+  constexpr int BK = 64;
+  constexpr int TN = BN / 32, TM = BM / 32;   // 16x16 tiles per wave (2x2 waves)
+  constexpr int WCH = BN * 8 / 256;           // 16-byte chunks per thread (W tile)
+  constexpr int XCH = BM * 8 / 256;           // 16-byte chunks per thread (X tile)
+  __shared__ __attribute__((aligned(16))) bf16_t sW[2][BN * BK];
+  __shared__ __attribute__((aligned(16))) bf16_t sX[2][BM * BK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wm = wave & 1;
+  const int g = lane >> 4, l16 = lane & 15;
+
+  const int lin = xcd_remap(blockIdx.x, p.tiles_total);
+  const int n0 = (lin % p.tiles_n) * BN;
+  const int m0 = (lin / p.tiles_n) * BM;
+  const int kt0 = SPLIT ? blockIdx.y * p.kt_per_split : 0;
+  const int kt1 = SPLIT ? min(p.ktiles, kt0 + p.kt_per_split) : p.ktiles;
+
+  // ---- per-thread staging geometry (rows fixed across the K loop)
+  const int cc = tid & 7;  // 16-byte chunk within the 128-byte K row
+  int xb[XCH], xho[XCH], xwo[XCH];
+  bool xok[XCH];
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    xok[i] = m < p.M;
+    const int mm = xok[i] ? m : 0;
+    const int hw = p.Ho * p.Wo;
+    xb[i] = mm / hw;
+    const int rem = mm - xb[i] * hw;
+    xho[i] = (rem / p.Wo) * p.stride - p.pad;
+    xwo[i] = (rem % p.Wo) * p.stride - p.pad;
+  }
+
+  uint4 rw[WCH], rx[XCH];
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+    const int rs = k0 / p.Cin;
+    const int c0 = k0 - rs * p.Cin + cc * 8;
+    const int r = rs / p.kw, s = rs - (rs / p.kw) * p.kw;
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      rw[i] = n < p.N ? ld16(p.w + (size_t)n * p.K + k0 + cc * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      int hi = xho[i] + r, wi = xwo[i] + s;
+      const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
+      if (p.upsample) { hi >>= 1; wi >>= 1; }
+      rx[i] = ok ? ld16(p.x + (((size_t)xb[i] * p.H + hi) * p.W + wi) * p.Cin + c0) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      st16(&sW[buf][row * BK + ((cc ^ (row & 7)) << 3)], rw[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      st16(&sX[buf][row * BK + ((cc ^ (row & 7)) << 3)], rx[i]);
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) load_tile(kt + 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TN], bfr[TM];
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int row = wn * (BN / 2) + a * 16 + l16;
+        af[a] = __builtin_bit_cast(bf16x8, ld16(&sW[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+      }
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        const int row = wm * (BM / 2) + b * 16 + l16;
+        bfr[b] = __builtin_bit_cast(bf16x8, ld16(&sX[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+      }
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds out[m][n .. n+3]
+  const int hw = p.Ho * p.Wo;
+#pragma unroll
+  for (int b = 0; b < TM; ++b) {
+    const int m = m0 + wm * (BM / 2) + b * 16 + l16;
+    if (m >= p.M) continue;
+    const int bb = m / hw;
+#pragma unroll
+    for (int a = 0; a < TN; ++a) {
+      const int n = n0 + wn * (BN / 2) + a * 16 + 4 * g;
+      if (n >= p.N) continue;
+      float v0 = acc[a][b][0], v1 = acc[a][b][1], v2 = acc[a][b][2], v3 = acc[a][b][3];
+      if (SPLIT) {
+        *reinterpret_cast<float4*>(p.ws + ((size_t)blockIdx.y * p.M + m) * p.N + n) = make_float4(v0, v1, v2, v3);
+        continue;
+      }
+      if (p.bias) {
+        const uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
+        v0 += __uint_as_float(bv.x << 16); v1 += __uint_as_float(bv.x & 0xffff0000u);
+        v2 += __uint_as_float(bv.y << 16); v3 += __uint_as_float(bv.y & 0xffff0000u);
+      }
+      if (p.temb) {
+        const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)bb * p.N + n);
+        v0 += __uint_as_float(tv.x << 16); v1 += __uint_as_float(tv.x & 0xffff0000u);
+        v2 += __uint_as_float(tv.y << 16); v3 += __uint_as_float(tv.y & 0xffff0000u);
+      }
+      if (p.res) {
+        const uint2 rv = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.N + n);
+        v0 += __uint_as_float(rv.x << 16); v1 += __uint_as_float(rv.x & 0xffff0000u);
+        v2 += __uint_as_float(rv.y << 16); v3 += __uint_as_float(rv.y & 0xffff0000u);
+      }
+      uint2 o;
+      o.x = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+      o.y = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
+      *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
+    }
+  }
+}
+
+// Ordered split-K reduction + epilogue: out[m, n..n+7] from S fp32 slabs.
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
+  const long total = (long)p.M * (p.N / 8);
+  const int hw = p.Ho * p.Wo;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int m = (int)(i / (p.N / 8));
+    const int n = (int)(i - (long)m * (p.N / 8)) * 8;
+    float v[8];
+    {
+      const float4* src = reinterpret_cast<const float4*>(p.ws + (size_t)m * p.N + n);
+      const float4 a = src[0], b = src[1];
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    for (int s = 1; s < S; ++s) {
+      const float4* src = reinterpret_cast<const float4*>(p.ws + ((size_t)s * p.M + m) * p.N + n);
+      const float4 a = src[0], b = src[1];
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    float t[8];
+    if (p.bias) {
+      unpack8(ld16(p.bias + n), t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    if (p.temb) {
+      unpack8(ld16(p.temb + (size_t)(m / hw) * p.N + n), t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    if (p.res) {
+      unpack8(ld16(p.res + (size_t)m * p.N + n), t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    st16(p.out + (size_t)m * p.N + n, pack8(v));
+  }
+}
+
+struct ConvPlan {
+  int bn, bm, split, kt_per_split;
+};
+
+static ConvPlan conv_plan(int M, int N, int ktiles) {
+  // Prefer the largest tile that still fills the 256 CUs; otherwise split K.
+  const int cfg[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
+  ConvPlan best = {64, 64, 1, ktiles};
+  for (int i = 0; i < 4; ++i) {
+    const int bn = cfg[i][0], bm = cfg[i][1];
+    const long tiles = (long)((N + bn - 1) / bn) * ((M + bm - 1) / bm);
+    if (bn == 128 && N <= 64) continue;
+    if (tiles >= 240) return {bn, bm, 1, ktiles};
+  }
+  const long tiles = (long)((N + 63) / 64) * ((M + 63) / 64);
+  int split = (int)((384 + tiles - 1) / tiles);
+  if (split > 8) split = 8;
+  if (split > ktiles / 2) split = ktiles / 2 > 0 ? ktiles / 2 : 1;
+  if (split < 1) split = 1;
+  const int per = (ktiles + split - 1) / split;
+  split = (ktiles + per - 1) / per;
+  best.split = split;
+  best.kt_per_split = per;
+  return best;
+}
+
+ARB_API size_t arb_conv2d_workspace(int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample, int stride) {
+  const int Hl = upsample ? 2 * H : H, Wl = upsample ? 2 * W : W;
+  const int Ho = (Hl + 2 * pad - k) / stride + 1, Wo = (Wl + 2 * pad - k) / stride + 1;
+  const int M = B * Ho * Wo;
+  const int ktiles = k * k * Cin / 64;
+  const ConvPlan pl = conv_plan(M, Cout, ktiles);
+  return pl.split > 1 ? (size_t)pl.split * M * Cout * sizeof(float) : 0;
+}
+
+template <int BN, int BM>
+static void launch_conv(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
+  ConvArgs p = a;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
+  if (pl.split > 1) {
+    p.kt_per_split = pl.kt_per_split;
+    dim3 grid(p.tiles_total, pl.split);
+    conv_igemm_kernel<BN, BM, true><<<grid, 256, 0, s>>>(p);
+    long work = (long)p.M * (p.N / 8);
+    long blocks = (work + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
+  } else {
+    dim3 grid(p.tiles_total, 1);
+    conv_igemm_kernel<BN, BM, false><<<grid, 256, 0, s>>>(p);
+  }
+}
+
+// x [B,H,W,Cin] bf16, w [Cout, k, k, Cin], out [B,Ho,Wo,Cout]; Cin % 64 == 0, Cout % 8 == 0.
+ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* temb, const void* res,
+                            void* out, void* ws, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
+                            int stride, hipStream_t stream) {
+  if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3) || (stride != 1 && stride != 2)) return -1;
+  ConvArgs a;
+  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = (const bf16_t*)bias; a.temb = (const bf16_t*)temb;
+  a.res = (const bf16_t*)res; a.out = (bf16_t*)out; a.ws = (float*)ws;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin;
+  a.Hl = upsample ? 2 * H : H; a.Wl = upsample ? 2 * W : W;
+  a.Ho = (a.Hl + 2 * pad - k) / stride + 1; a.Wo = (a.Wl + 2 * pad - k) / stride + 1;
+  a.N = Cout; a.K = k * k * Cin; a.M = B * a.Ho * a.Wo;
+  a.kw = k; a.pad = pad; a.stride = stride; a.upsample = upsample;
+  a.ktiles = a.K / 64; a.kt_per_split = a.ktiles;
+  const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles);
+  if (pl.split > 1 && ws == nullptr) return -3;
+  if (pl.bn == 128 && pl.bm == 128) launch_conv<128, 128>(a, pl, stream);
+  else if (pl.bn == 64 && pl.bm == 128) launch_conv<64, 128>(a, pl, stream);
+  else if (pl.bn == 128 && pl.bm == 64) launch_conv<128, 64>(a, pl, stream);
+  else launch_conv<64, 64>(a, pl, stream);
+  return (int)hipGetLastError();
+}
+
+// Plain GEMM with fused epilogue: out[M,N] = x[M,K] W[N,K]^T (+bias +residual); K % 64 == 0.
+ARB_API int arb_gemm_bias_res(const void* x, const void* w, const void* bias, const void* res, void* out, void* ws,
+                              int M, int N, int K, hipStream_t stream) {
+  return arb_conv2d_nhwc(x, w, bias, nullptr, res, out, ws, 1, 1, M, K, N, 1, 0, 0, 1, stream);
+}

@@ -81,3 +81,41 @@ def test_geglu_silu(cuda):
     assert _rel(_lib.geglu(h), ref.geglu(h.float())) < 1e-2
     x = torch.randn(4096, 320, device=cuda).bfloat16()
     assert _rel(_lib.silu(x), ref.silu(x.float())) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,up,stride,temb,res", [
+    (2, 64, 64, 320, 320, 3, False, 1, True, False), (2, 32, 32, 640, 640, 3, False, 1, False, True),
+    (2, 8, 8, 1280, 1280, 3, False, 1, True, True), (2, 16, 16, 2560, 1280, 1, False, 1, False, False),
+    (2, 32, 32, 320, 320, 3, True, 1, False, False), (2, 64, 64, 320, 320, 3, False, 2, False, False),
+    (1, 64, 64, 512, 512, 3, False, 1, False, True), (1, 9, 13, 128, 24, 3, False, 1, True, True),
+    (3, 5, 7, 64, 72, 3, True, 2, False, False), (2, 16, 16, 960, 640, 1, False, 1, False, True)])
+def test_conv2d(cuda, B, H, W, Cin, Cout, k, up, stride, temb, res):
+    torch.manual_seed(2)
+    x = torch.randn(B, H, W, Cin, device=cuda).bfloat16()
+    w = (torch.randn(Cout, k, k, Cin, device=cuda) / math.sqrt(k * k * Cin)).bfloat16()
+    b = torch.randn(Cout, device=cuda).bfloat16()
+    pad = k // 2
+    Hl, Wl = (2 * H, 2 * W) if up else (H, W)
+    Ho, Wo = (Hl + 2 * pad - k) // stride + 1, (Wl + 2 * pad - k) // stride + 1
+    t = torch.randn(B, Cout, device=cuda).bfloat16() if temb else None
+    r = torch.randn(B, Ho, Wo, Cout, device=cuda).bfloat16() if res else None
+    y = _lib.conv2d_nhwc(x, w, b, pad, up, r, t, stride)
+    ref_y = ref.conv2d_nhwc(x.float(), w.float(), b.float(), stride, pad, up)
+    if temb:
+        ref_y = ref_y + t.float()[:, None, None, :]
+    if res:
+        ref_y = ref_y + r.float()
+    assert y.shape == ref_y.shape
+    assert _rel(y, ref_y) < 1e-2, _rel(y, ref_y)
+    assert torch.equal(y, _lib.conv2d_nhwc(x, w, b, pad, up, r, t, stride))
+
+
+@pytest.mark.parametrize("M,K,N", [(8192, 320, 320), (8192, 1280, 320), (2048, 2560, 640), (128, 5120, 1280),
+                                   (77, 768, 640), (100, 64, 24)])
+def test_gemm(cuda, M, K, N):
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    r = torch.randn(M, N, device=cuda).bfloat16()
+    y = _lib.gemm(x, w, b, r)
+    assert _rel(y, x.float() @ w.float().t() + b.float() + r.float()) < 1e-2
