@@ -28,9 +28,10 @@ _SIGS = {
     "arb_flash_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_int, c_void_p]),
     "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
-    "arb_conv2d_nhwc": (c_int, [c_void_p] * 7 + [c_int] * 9 + [c_void_p]),
-    "arb_conv2d_workspace": (c_size_t, [c_int] * 9),
-    "arb_gemm_bias_res": (c_int, [c_void_p] * 6 + [c_int] * 3 + [c_void_p]),
+    "arb_conv2d_nhwc": (c_int, [c_void_p] * 7 + [c_int] * 11 + [c_void_p]),
+    "arb_conv2d_workspace": (c_size_t, [c_int] * 11),
+    "arb_conv2d_plan": (c_int, [c_int] * 9 + [c_void_p]),
+    "arb_gemm_bias_res": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p]),
     "arb_temporal_attention": (c_int, [c_void_p] * 4 + [c_int] * 5 + [c_float, c_void_p]),
     "arb_convgru_gates": (c_int, [c_void_p] * 5 + [c_long, c_int, c_void_p]),
 }
@@ -184,7 +185,13 @@ def silu(x):
     return y
 
 
-def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1):
+def conv_plan(B, H, W, Cin, Cout, k, pad, upsample, stride):
+    out = (ctypes.c_int * 2)()
+    _fn("arb_conv2d_plan")(B, H, W, Cin, Cout, k, pad, int(bool(upsample)), stride, out)
+    return out[0], out[1]
+
+
+def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-1, split=-1):
     """Implicit-GEMM conv (csrc/conv.hip).  x [B,H,W,Cin], w [Cout,k,k,Cin] -> [B,Ho,Wo,Cout].
     Fused epilogue: + bias[n] + temb[b, n] + residual[m, n]."""
     _bf16(x, w, b, residual, temb)
@@ -208,7 +215,7 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1):
             raise ValueError("conv2d temb must be [B, Cout]")
     if b is not None and b.numel() != Cout:
         raise ValueError("conv2d bias size")
-    args = (B, H, W, Cin, Cout, kh, padding, int(bool(upsample)), stride)
+    args = (B, H, W, Cin, Cout, kh, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
     _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), *args, _stream()),
@@ -216,7 +223,7 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1):
     return y
 
 
-def gemm(x, w, b=None, residual=None):
+def gemm(x, w, b=None, residual=None, cfg=-1, split=-1):
     """out = x @ w^T (+ b + residual) on the implicit-GEMM kernel. x [...,K], w [N,K]."""
     _bf16(x, w, b, residual)
     K = x.shape[-1]
@@ -227,8 +234,8 @@ def gemm(x, w, b=None, residual=None):
         raise ValueError(f"gemm: unsupported K={K} N={N}")
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
-    ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1)
+    ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
-    _check(_fn("arb_gemm_bias_res")(_p(x2), _p(w.contiguous()), _p(b), _p(r2), _p(y), _p(ws), M, N, K, _stream()),
-           "gemm")
+    _check(_fn("arb_gemm_bias_res")(_p(x2), _p(w.contiguous()), _p(b), _p(r2), _p(y), _p(ws), M, N, K, int(cfg),
+                                    int(split), _stream()), "gemm")
     return y.reshape(*x.shape[:-1], N)

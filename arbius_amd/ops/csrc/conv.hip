@@ -40,17 +40,18 @@ struct ConvArgs {
   int tiles_n, tiles_total;
 };
 
-template <int BN, int BM, bool SPLIT>
-__global__ void __launch_bounds__(256, 2) conv_igemm_kernel(ConvArgs p) {
+template <int BN, int BM, int WN, int WM, int MINW, bool SPLIT>
+__global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   constexpr int BK = 64;
-  constexpr int TN = BN / 32, TM = BM / 32;   // 16x16 tiles per wave (2x2 waves)
+  static_assert(WN * WM == 4, "4 waves");
+  constexpr int TN = BN / WN / 16, TM = BM / WM / 16;  // 16x16 tiles per wave
   constexpr int WCH = BN * 8 / 256;           // 16-byte chunks per thread (W tile)
   constexpr int XCH = BM * 8 / 256;           // 16-byte chunks per thread (X tile)
   __shared__ __attribute__((aligned(16))) bf16_t sW[2][BN * BK];
   __shared__ __attribute__((aligned(16))) bf16_t sX[2][BM * BK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave >> 1, wm = wave & 1;
+  const int wn = wave / WM, wm = wave % WM;
   const int g = lane >> 4, l16 = lane & 15;
 
   const int lin = xcd_remap(blockIdx.x, p.tiles_total);
@@ -127,12 +128,12 @@ __global__ void __launch_bounds__(256, 2) conv_igemm_kernel(ConvArgs p) {
       bf16x8 af[TN], bfr[TM];
 #pragma unroll
       for (int a = 0; a < TN; ++a) {
-        const int row = wn * (BN / 2) + a * 16 + l16;
+        const int row = wn * (BN / WN) + a * 16 + l16;
         af[a] = __builtin_bit_cast(bf16x8, ld16(&sW[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
       }
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
-        const int row = wm * (BM / 2) + b * 16 + l16;
+        const int row = wm * (BM / WM) + b * 16 + l16;
         bfr[b] = __builtin_bit_cast(bf16x8, ld16(&sX[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
       }
 #pragma unroll
@@ -148,12 +149,12 @@ __global__ void __launch_bounds__(256, 2) conv_igemm_kernel(ConvArgs p) {
   const int hw = p.Ho * p.Wo;
 #pragma unroll
   for (int b = 0; b < TM; ++b) {
-    const int m = m0 + wm * (BM / 2) + b * 16 + l16;
+    const int m = m0 + wm * (BM / WM) + b * 16 + l16;
     if (m >= p.M) continue;
     const int bb = m / hw;
 #pragma unroll
     for (int a = 0; a < TN; ++a) {
-      const int n = n0 + wn * (BN / 2) + a * 16 + 4 * g;
+      const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
       if (n >= p.N) continue;
       float v0 = acc[a][b][0], v1 = acc[a][b][1], v2 = acc[a][b][2], v3 = acc[a][b][3];
       if (SPLIT) {
@@ -221,42 +222,94 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tile configurations (BN channels x BM pixels, WN x WM waves) and the plan.  The plan is a
+// pure function of the shape (pinned table for the model shapes, cost model otherwise), so
+// every GPU runs the same reduction order for the same task (determinism).
+struct TileCfg {
+  int bn, bm, wn, wm, minw;
+};
+static const TileCfg kCfgs[] = {
+    {128, 128, 2, 2, 2}, {64, 128, 2, 2, 2}, {128, 64, 2, 2, 2}, {64, 64, 2, 2, 2}, {160, 64, 2, 2, 2},
+    {160, 128, 2, 2, 1}, {320, 32, 4, 1, 1}, {256, 64, 4, 1, 1}, {128, 256, 2, 2, 1}, {64, 256, 1, 4, 1},
+};
+static const int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
 struct ConvPlan {
-  int bn, bm, split, kt_per_split;
+  int cfg, split, kt_per_split;
 };
 
-static ConvPlan conv_plan(int M, int N, int ktiles) {
-  // Prefer the largest tile that still fills the 256 CUs; otherwise split K.
-  const int cfg[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
-  ConvPlan best = {64, 64, 1, ktiles};
-  for (int i = 0; i < 4; ++i) {
-    const int bn = cfg[i][0], bm = cfg[i][1];
-    const long tiles = (long)((N + bn - 1) / bn) * ((M + bm - 1) / bm);
-    if (bn == 128 && N <= 64) continue;
-    if (tiles >= 240) return {bn, bm, 1, ktiles};
+// Pinned choices for shapes measured on MI355X (M, N, K) -> (cfg, split).  Filled by
+// scripts/autotune_conv.py; entries not listed fall back to the cost model.
+struct PinnedPlan {
+  int M, N, K, cfg, split;
+};
+#include "conv_plans.inc"
+
+static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
+  const int K = ktiles * 64;
+  if (want_cfg >= 0 && want_cfg < kNumCfgs) {
+    int split = want_split < 1 ? 1 : want_split;
+    if (split > ktiles) split = ktiles;
+    const int per = (ktiles + split - 1) / split;
+    return {want_cfg, (ktiles + per - 1) / per, per};
   }
-  const long tiles = (long)((N + 63) / 64) * ((M + 63) / 64);
-  int split = (int)((384 + tiles - 1) / tiles);
-  if (split > 8) split = 8;
-  if (split > ktiles / 2) split = ktiles / 2 > 0 ? ktiles / 2 : 1;
-  if (split < 1) split = 1;
-  const int per = (ktiles + split - 1) / split;
-  split = (ktiles + per - 1) / per;
-  best.split = split;
-  best.kt_per_split = per;
-  return best;
+  for (const PinnedPlan& pp : kPinnedPlans) {
+    if (pp.M == M && pp.N == N && pp.K == K) {
+      const int per = (ktiles + pp.split - 1) / pp.split;
+      return {pp.cfg, (ktiles + per - 1) / per, per};
+    }
+  }
+  // cost model: waves of resident workgroups x per-workgroup work / tile efficiency
+  double best = 1e30;
+  ConvPlan bp = {3, 1, ktiles};
+  const int splits[] = {1, 2, 3, 4, 6, 8};
+  for (int c = 0; c < kNumCfgs; ++c) {
+    const TileCfg& tc = kCfgs[c];
+    if (tc.bn > 2 * N && tc.bn > 64) continue;
+    const long tiles = (long)((N + tc.bn - 1) / tc.bn) * ((M + tc.bm - 1) / tc.bm);
+    const int lds = 2 * (tc.bn + tc.bm) * 128;
+    int occ = 163840 / lds;
+    if (occ > tc.minw) occ = tc.minw;
+    if (occ < 1) occ = 1;
+    const double eff = fmin(1.0, (double)tc.bn * tc.bm / (tc.bn + tc.bm) / 64.0);
+    for (int si = 0; si < 6; ++si) {
+      const int sp = splits[si];
+      if (sp > 1 && sp > ktiles / 2) break;
+      const int per = (ktiles + sp - 1) / sp;
+      const long wgs = tiles * sp;
+      const long waves = (wgs + 256L * occ - 1) / (256L * occ);
+      double t = (double)waves * occ * tc.bn * tc.bm * per / eff;     // ~ cycles x const
+      t += (double)((N + tc.bn - 1) / tc.bn * tc.bn - N) * 0.0;        // masked columns already counted
+      if (sp > 1) t += (double)M * N * sp * 4.0 * 0.9 + 2.0e5;          // slab traffic + reduce launch
+      if (t < best) {
+        best = t;
+        bp = {c, (ktiles + per - 1) / per, per};
+      }
+    }
+  }
+  return bp;
 }
 
-ARB_API size_t arb_conv2d_workspace(int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample, int stride) {
-  const int Hl = upsample ? 2 * H : H, Wl = upsample ? 2 * W : W;
-  const int Ho = (Hl + 2 * pad - k) / stride + 1, Wo = (Wl + 2 * pad - k) / stride + 1;
-  const int M = B * Ho * Wo;
-  const int ktiles = k * k * Cin / 64;
-  const ConvPlan pl = conv_plan(M, Cout, ktiles);
-  return pl.split > 1 ? (size_t)pl.split * M * Cout * sizeof(float) : 0;
+static void conv_geom(ConvArgs& a, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
+                      int stride) {
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin;
+  a.Hl = upsample ? 2 * H : H; a.Wl = upsample ? 2 * W : W;
+  a.Ho = (a.Hl + 2 * pad - k) / stride + 1; a.Wo = (a.Wl + 2 * pad - k) / stride + 1;
+  a.N = Cout; a.K = k * k * Cin; a.M = B * a.Ho * a.Wo;
+  a.kw = k; a.pad = pad; a.stride = stride; a.upsample = upsample;
+  a.ktiles = a.K / 64; a.kt_per_split = a.ktiles;
 }
 
-template <int BN, int BM>
+ARB_API size_t arb_conv2d_workspace(int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample, int stride,
+                                    int cfg, int split) {
+  ConvArgs a;
+  conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
+  const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
+  return pl.split > 1 ? (size_t)pl.split * a.M * a.N * sizeof(float) : 0;
+}
+
+template <int BN, int BM, int WN, int WM, int MINW>
 static void launch_conv(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   ConvArgs p = a;
   p.tiles_n = (p.N + BN - 1) / BN;
@@ -264,42 +317,56 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
     dim3 grid(p.tiles_total, pl.split);
-    conv_igemm_kernel<BN, BM, true><<<grid, 256, 0, s>>>(p);
+    conv_igemm_kernel<BN, BM, WN, WM, MINW, true><<<grid, 256, 0, s>>>(p);
     long work = (long)p.M * (p.N / 8);
     long blocks = (work + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
   } else {
     dim3 grid(p.tiles_total, 1);
-    conv_igemm_kernel<BN, BM, false><<<grid, 256, 0, s>>>(p);
+    conv_igemm_kernel<BN, BM, WN, WM, MINW, false><<<grid, 256, 0, s>>>(p);
   }
 }
 
 // x [B,H,W,Cin] bf16, w [Cout, k, k, Cin], out [B,Ho,Wo,Cout]; Cin % 64 == 0, Cout % 8 == 0.
+// cfg/split = -1: planned; >= 0: forced (autotuning).
 ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* temb, const void* res,
                             void* out, void* ws, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
-                            int stride, hipStream_t stream) {
+                            int stride, int cfg, int split, hipStream_t stream) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3) || (stride != 1 && stride != 2)) return -1;
   ConvArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = (const bf16_t*)bias; a.temb = (const bf16_t*)temb;
   a.res = (const bf16_t*)res; a.out = (bf16_t*)out; a.ws = (float*)ws;
-  a.B = B; a.H = H; a.W = W; a.Cin = Cin;
-  a.Hl = upsample ? 2 * H : H; a.Wl = upsample ? 2 * W : W;
-  a.Ho = (a.Hl + 2 * pad - k) / stride + 1; a.Wo = (a.Wl + 2 * pad - k) / stride + 1;
-  a.N = Cout; a.K = k * k * Cin; a.M = B * a.Ho * a.Wo;
-  a.kw = k; a.pad = pad; a.stride = stride; a.upsample = upsample;
-  a.ktiles = a.K / 64; a.kt_per_split = a.ktiles;
-  const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles);
+  conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
+  const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
   if (pl.split > 1 && ws == nullptr) return -3;
-  if (pl.bn == 128 && pl.bm == 128) launch_conv<128, 128>(a, pl, stream);
-  else if (pl.bn == 64 && pl.bm == 128) launch_conv<64, 128>(a, pl, stream);
-  else if (pl.bn == 128 && pl.bm == 64) launch_conv<128, 64>(a, pl, stream);
-  else launch_conv<64, 64>(a, pl, stream);
+  switch (pl.cfg) {
+    case 0: launch_conv<128, 128, 2, 2, 2>(a, pl, stream); break;
+    case 1: launch_conv<64, 128, 2, 2, 2>(a, pl, stream); break;
+    case 2: launch_conv<128, 64, 2, 2, 2>(a, pl, stream); break;
+    case 3: launch_conv<64, 64, 2, 2, 2>(a, pl, stream); break;
+    case 4: launch_conv<160, 64, 2, 2, 2>(a, pl, stream); break;
+    case 5: launch_conv<160, 128, 2, 2, 1>(a, pl, stream); break;
+    case 6: launch_conv<320, 32, 4, 1, 1>(a, pl, stream); break;
+    case 7: launch_conv<256, 64, 4, 1, 1>(a, pl, stream); break;
+    case 8: launch_conv<128, 256, 2, 2, 1>(a, pl, stream); break;
+    default: launch_conv<64, 256, 1, 4, 1>(a, pl, stream); break;
+  }
   return (int)hipGetLastError();
+}
+
+ARB_API int arb_conv2d_plan(int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample, int stride,
+                            int* cfg_split) {
+  ConvArgs a;
+  conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
+  const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, -1, -1);
+  cfg_split[0] = pl.cfg;
+  cfg_split[1] = pl.split;
+  return 0;
 }
 
 // Plain GEMM with fused epilogue: out[M,N] = x[M,K] W[N,K]^T (+bias +residual); K % 64 == 0.
 ARB_API int arb_gemm_bias_res(const void* x, const void* w, const void* bias, const void* res, void* out, void* ws,
-                              int M, int N, int K, hipStream_t stream) {
-  return arb_conv2d_nhwc(x, w, bias, nullptr, res, out, ws, 1, 1, M, K, N, 1, 0, 0, 1, stream);
+                              int M, int N, int K, int cfg, int split, hipStream_t stream) {
+  return arb_conv2d_nhwc(x, w, bias, nullptr, res, out, ws, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, stream);
 }

@@ -1,0 +1,230 @@
+// GroupNorm (+SiLU) over channels-last activations [B, HW, C] bf16.
+//
+// The normalisation of every ResBlock / Transformer2D input of the SD1.5 UNet
+// and VAE.  Three short, wide kernels (each fills the chip;
+// hipGraph replay keeps the launch gaps at ~1 us):
+//   1. gn_stats    grid (chunks, B): every thread keeps RPT rows x 8 channels in
+//      registers (all loads in flight at once), computes EXACT per-channel
+//      (n, mean, M2) by two passes over registers, and the block combines them
+//      per group with the exact parallel-variance algebra
+//      (N = sum n, mu = sum n*mean / N, M2 = sum [M2_c + n_c (mean_c - mu)^2]).
+//   2. gn_finalize grid (G, B): one group per block, 256 threads combine the
+//      chunk stats (Chan) and a fixed-shape LDS tree -> mean, rstd.
+//   3. gn_apply    grid (blocks, B): normalise + gamma/beta (+SiLU), 16 B stores.
+// No atomics, fixed reduction order everywhere -> bitwise deterministic, and the
+// same partition for a given shape on every GPU.
+#include "common.h"
+
+#define GN_RPT 4  // rows per thread in the stats / apply kernels
+
+struct Stat {
+  float n, mean, m2, pad;
+};
+
+__device__ __forceinline__ Stat chan_combine(Stat a, Stat b) {
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float n = a.n + b.n;
+  const float d = b.mean - a.mean;
+  const float f = b.n / n;
+  Stat r;
+  r.n = n;
+  r.mean = a.mean + d * f;
+  r.m2 = a.m2 + b.m2 + d * d * a.n * f;
+  r.pad = 0.f;
+  return r;
+}
+
+// Thread geometry: NV = C/8 channel vectors.  NV < 256: k = 256/NV row lanes, thread
+// (v = t % NV, rl = t / NV).  NV >= 256: one row lane, thread owns vectors t, t+256 (VPT).
+template <int VPT>
+__global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict__ x, Stat* __restrict__ part,
+                                                       int HW, int C, int G) {
+  const int chunk = blockIdx.x, b = blockIdx.y, chunks = gridDim.x;
+  const int NV = C >> 3;
+  const int k = NV >= 256 ? 1 : 256 / NV;
+  const int t = threadIdx.x;
+  const int v = NV >= 256 ? t : t % NV, rl = NV >= 256 ? 0 : t / NV;
+  const int rows = k * GN_RPT;
+  const int r0 = chunk * rows;
+  __shared__ float sh_n[256];
+  __shared__ float sh_mean[256 * 8 * VPT];
+  __shared__ float sh_m2[256 * 8 * VPT];
+
+  float f[VPT][GN_RPT][8];
+  float n = 0.f;
+  const bf16_t* base = x + ((size_t)b * HW) * C;
+#pragma unroll
+  for (int i = 0; i < GN_RPT; ++i) {
+    const int r = r0 + rl + i * k;
+    const bool ok = rl < k && r < HW;
+    n += ok ? 1.f : 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int vv = v + 256 * j;
+      if (ok && vv < NV) {
+        unpack8(ld16(base + (size_t)r * C + vv * 8), f[j][i]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[j][i][e] = 0.f;
+      }
+    }
+  }
+  sh_n[t] = n;
+  const float inv_n = n > 0.f ? 1.f / n : 0.f;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < GN_RPT; ++i) s += f[j][i][e];
+      const float mean = s * inv_n;
+      float m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < GN_RPT; ++i) {
+        const int r = r0 + rl + i * k;
+        const float d = f[j][i][e] - mean;
+        m2 += (rl < k && r < HW) ? d * d : 0.f;
+      }
+      sh_mean[(t * VPT + j) * 8 + e] = mean;
+      sh_m2[(t * VPT + j) * 8 + e] = m2;
+    }
+  }
+  __syncthreads();
+  const int Cg = C / G;
+  if (t < G) {
+    float N = 0.f, sum = 0.f;
+    for (int c = t * Cg; c < (t + 1) * Cg; ++c) {
+      const int vv = c >> 3, e = c & 7;
+      for (int j = 0; j < k; ++j) {
+        const int tt = NV >= 256 ? (vv & 255) : j * NV + vv;
+        const int o = (tt * VPT + (NV >= 256 ? (vv >> 8) : 0)) * 8 + e;
+        N += sh_n[tt];
+        sum += sh_n[tt] * sh_mean[o];
+      }
+    }
+    const float mu = N > 0.f ? sum / N : 0.f;
+    float m2 = 0.f;
+    for (int c = t * Cg; c < (t + 1) * Cg; ++c) {
+      const int vv = c >> 3, e = c & 7;
+      for (int j = 0; j < k; ++j) {
+        const int tt = NV >= 256 ? (vv & 255) : j * NV + vv;
+        const int o = (tt * VPT + (NV >= 256 ? (vv >> 8) : 0)) * 8 + e;
+        const float d = sh_mean[o] - mu;
+        m2 += sh_m2[o] + sh_n[tt] * d * d;
+      }
+    }
+    Stat st = {N, mu, m2, 0.f};
+    part[((size_t)b * chunks + chunk) * G + t] = st;
+  }
+}
+
+__global__ void __launch_bounds__(256) gn_finalize_kernel(const Stat* __restrict__ part, float2* __restrict__ stats,
+                                                          int chunks, int G, float eps) {
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  __shared__ Stat sh[256];
+  Stat acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c = t; c < chunks; c += 256) acc = chan_combine(acc, part[((size_t)b * chunks + c) * G + g]);
+  sh[t] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) sh[t] = chan_combine(sh[t], sh[t + s]);
+    __syncthreads();
+  }
+  if (t == 0) {
+    const Stat r = sh[0];
+    stats[b * G + g] = make_float2(r.mean, rsqrtf(r.m2 / fmaxf(r.n, 1.f) + eps));
+  }
+}
+
+template <int VPT>
+__global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                       const float2* __restrict__ stats,
+                                                       const bf16_t* __restrict__ gamma,
+                                                       const bf16_t* __restrict__ beta, int HW, int C, int G,
+                                                       int silu) {
+  const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  __shared__ float2 sh_st[256];
+  if (t < G) sh_st[t] = stats[b * G + t];
+  __syncthreads();
+  const int NV = C >> 3;
+  const int k = NV >= 256 ? 1 : 256 / NV;
+  const int v = NV >= 256 ? t : t % NV, rl = NV >= 256 ? 0 : t / NV;
+  if (rl >= k) return;
+  const int Cg = C / G;
+  const int r0 = blk * k * GN_RPT;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int vv = v + 256 * j;
+    if (vv >= NV) continue;
+    float sc[8], sf[8];
+    {
+      float gm[8], bt[8];
+      unpack8(ld16(gamma + vv * 8), gm);
+      unpack8(ld16(beta + vv * 8), bt);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float2 st = sh_st[(vv * 8 + e) / Cg];
+        sc[e] = st.y * gm[e];
+        sf[e] = bt[e] - st.x * sc[e];
+      }
+    }
+    const size_t off = ((size_t)b * HW) * C + vv * 8;
+    uint4 raw[GN_RPT];
+#pragma unroll
+    for (int i = 0; i < GN_RPT; ++i) {
+      const int r = r0 + rl + i * k;
+      raw[i] = r < HW ? ld16(x + off + (size_t)r * C) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < GN_RPT; ++i) {
+      const int r = r0 + rl + i * k;
+      if (r >= HW) continue;
+      float f[8];
+      unpack8(raw[i], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float o = f[e] * sc[e] + sf[e];
+        f[e] = silu ? silu_f(o) : o;
+      }
+      st16(y + off + (size_t)r * C, pack8(f));
+    }
+  }
+}
+
+static int gn_chunks(int HW, int C) {
+  const int NV = C / 8;
+  const int k = NV >= 256 ? 1 : 256 / NV;
+  const int rows = k * GN_RPT;
+  return (HW + rows - 1) / rows;
+}
+
+ARB_API size_t arb_group_norm_workspace(int B, int HW, int C, int G) {
+  // partial stats + final (mean, rstd); 256-byte aligned split
+  const size_t part = (size_t)B * gn_chunks(HW, C) * G * sizeof(Stat);
+  return ((part + 255) / 256) * 256 + (size_t)B * G * sizeof(float2);
+}
+
+ARB_API int arb_group_norm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* workspace, int B,
+                                int HW, int C, int G, float eps, int silu, hipStream_t stream) {
+  if (C % 8 != 0 || C / 8 > 512 || C % G != 0 || G > 256) return -1;
+  const int chunks = gn_chunks(HW, C);
+  Stat* part = (Stat*)workspace;
+  const size_t part_bytes = ((size_t)B * chunks * G * sizeof(Stat) + 255) / 256 * 256;
+  float2* stats = (float2*)((char*)workspace + part_bytes);
+  dim3 g1(chunks, B);
+  if (C / 8 > 256)
+    gn_stats_kernel<2><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
+  else
+    gn_stats_kernel<1><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
+  gn_finalize_kernel<<<dim3(G, B), 256, 0, stream>>>(part, stats, chunks, G, eps);
+  if (C / 8 > 256)
+    gn_apply_kernel<2><<<g1, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, stats, (const bf16_t*)gamma,
+                                               (const bf16_t*)beta, HW, C, G, silu);
+  else
+    gn_apply_kernel<1><<<g1, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, stats, (const bf16_t*)gamma,
+                                               (const bf16_t*)beta, HW, C, G, silu);
+  return (int)hipGetLastError();
+}

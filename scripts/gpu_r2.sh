@@ -4,7 +4,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 python -m arbius_amd.ops.build > gpurun_out/build.log 2>&1 || exit 1
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python scripts/autotune_conv.py gpurun_out > gpurun_out/autotune.log 2>&1 || { tail -30 gpurun_out/autotune.log; exit 1; }
 timeout -k 10 300 python scripts/microbench.py gpurun_out/microbench.json > gpurun_out/microbench.log 2>&1 || { tail -30 gpurun_out/microbench.log; exit 1; }
 timeout -k 10 600 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_hip.log 2>&1 || { tail -30 gpurun_out/bench_hip.log; exit 1; }
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_hip2 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 > $GRAFT_REPO_ROOT/gpurun_out/prof_hip2.log 2>&1
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_hip3 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 > $GRAFT_REPO_ROOT/gpurun_out/prof_hip3.log 2>&1
 echo done
