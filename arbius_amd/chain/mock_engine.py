@@ -120,7 +120,7 @@ class MockToken:
             raise Revert("ERC20: transfer to the zero address")
         if self.balances.get(frm, 0) < amount:
             raise Revert("ERC20: transfer amount exceeds balance")
-        self.balances[frm] -= amount
+        self.balances[frm] = self.balances.get(frm, 0) - amount
         self.balances[to] = self.balances.get(to, 0) + amount
 
     def approve(self, owner, spender, amount):

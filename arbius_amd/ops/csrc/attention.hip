@@ -93,24 +93,50 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     kv_end = min(a.Nk, qmax + 1);
   }
 
-  for (int kv0 = 0; kv0 < kv_end; kv0 += KV_BLK) {
-    __syncthreads();
-    // ---- cooperative K / V tile load (16-byte chunks), zero fill outside (Nk, D)
-    constexpr int KCH = KV_BLK * KSTEPS * 4;
-    for (int c = tid; c < KCH; c += 256) {
+  // ---- register-staged K/V pipeline (T14): the next tile's global loads are in flight
+  //      while the current tile is consumed from LDS.
+  constexpr int KCH = KV_BLK * KSTEPS * 4;
+  constexpr int VCH = KV_BLK * DT * 2;
+  constexpr int KPT = (KCH + 255) / 256, VPT = (VCH + 255) / 256;
+  uint4 rk[KPT], rv[VPT];
+  auto load_kv = [&](int kv) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const int c = tid + 256 * i;
       const int r = c / (KSTEPS * 4), col = (c % (KSTEPS * 4)) * 8;
-      uint4 raw = make_uint4(0, 0, 0, 0);
-      if (kv0 + r < a.Nk && col < D) raw = ld16(kbase + (long)(kv0 + r) * a.k_sn + col);
-      st16(&sK[r * KROW + col], raw);
+      rk[i] = (c < KCH && kv + r < a.Nk && col < D) ? ld16(kbase + (long)(kv + r) * a.k_sn + col)
+                                                     : make_uint4(0, 0, 0, 0);
     }
-    constexpr int VCH = KV_BLK * DT * 2;
-    for (int c = tid; c < VCH; c += 256) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = tid + 256 * i;
       const int r = c / (DT * 2), col = (c % (DT * 2)) * 8;
-      uint4 raw = make_uint4(0, 0, 0, 0);
-      if (kv0 + r < a.Nk && col < D) raw = ld16(vbase + (long)(kv0 + r) * a.v_sn + col);
-      st16(&sV[r * VROW + col], raw);
+      rv[i] = (c < VCH && kv + r < a.Nk && col < D) ? ld16(vbase + (long)(kv + r) * a.v_sn + col)
+                                                     : make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
+  };
+  auto store_kv = [&]() {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const int c = tid + 256 * i;
+      if (c < KCH) st16(&sK[(c / (KSTEPS * 4)) * KROW + (c % (KSTEPS * 4)) * 8], rk[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = tid + 256 * i;
+      if (c < VCH) st16(&sV[(c / (DT * 2)) * VROW + (c % (DT * 2)) * 8], rv[i]);
+    }
+  };
+  if (kv_end > 0) {
+    load_kv(0);
+    store_kv();
+  }
+  __syncthreads();
+
+  for (int kv0 = 0; kv0 < kv_end; kv0 += KV_BLK) {
+    const bool more = kv0 + KV_BLK < kv_end;
+    if (more) load_kv(kv0 + KV_BLK);
+    const bool full = !a.causal && kv0 + KV_BLK <= a.Nk;  // no masking needed
 
     // ---- S^T tiles: 4 key tiles x QT query tiles
     f32x4 st[QT][4];
@@ -128,25 +154,27 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     }
 
     // ---- online softmax (per query column = lane&15)
+    // scores stay raw; scale (> 0) is applied inside one fma before exp2: max commutes with it.
     bf16x8 pf[QT][2];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
-      float mloc = -INFINITY;
+      if (!full) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kv0 + 16 * t + 4 * g + r;
-          float sv = st[qt][t][r] * a.scale_log2;
-          const bool masked = key >= a.Nk || (a.causal && key > qidx[qt]);
-          sv = masked ? -INFINITY : sv;
-          st[qt][t][r] = sv;
-          mloc = fmaxf(mloc, sv);
-        }
+          for (int r = 0; r < 4; ++r) {
+            const int key = kv0 + 16 * t + 4 * g + r;
+            const bool masked = key >= a.Nk || (a.causal && key > qidx[qt]);
+            st[qt][t][r] = masked ? -INFINITY : st[qt][t][r];
+          }
       }
+      float mloc = fmaxf(fmaxf(st[qt][0][0], st[qt][0][1]), fmaxf(st[qt][0][2], st[qt][0][3]));
+#pragma unroll
+      for (int t = 1; t < 4; ++t)
+        mloc = fmaxf(mloc, fmaxf(fmaxf(st[qt][t][0], st[qt][t][1]), fmaxf(st[qt][t][2], st[qt][t][3])));
       mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float m_new = fmaxf(m_run[qt], mloc);
+      const float m_new = fmaxf(m_run[qt], mloc * a.scale_log2);
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
       const float alpha = exp2f(m_run[qt] - m_use);
       m_run[qt] = m_new;
@@ -155,7 +183,7 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       for (int t = 0; t < 4; ++t) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(st[qt][t][r] - m_use);
+          const float p = exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
           st[qt][t][r] = p;
           lsum += p;
         }
@@ -192,6 +220,11 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
         for (int qt = 0; qt < QT; ++qt)
           o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][ks], o[qt][dt], 0, 0, 0);
       }
+    }
+    __syncthreads();          // every wave is done reading this tile
+    if (more) {
+      store_kv();             // the prefetched tile lands in LDS
+      __syncthreads();
     }
   }
 

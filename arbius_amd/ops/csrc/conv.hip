@@ -279,9 +279,10 @@ static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split
       const int per = (ktiles + sp - 1) / sp;
       const long wgs = tiles * sp;
       const long waves = (wgs + 256L * occ - 1) / (256L * occ);
-      double t = (double)waves * occ * tc.bn * tc.bm * per / eff;     // ~ cycles x const
-      t += (double)((N + tc.bn - 1) / tc.bn * tc.bn - N) * 0.0;        // masked columns already counted
-      if (sp > 1) t += (double)M * N * sp * 4.0 * 0.9 + 2.0e5;          // slab traffic + reduce launch
+      // seconds: each resident workgroup slot runs at (45% of 2 PF) * eff / slots
+      const double slot_rate = 2.0e15 * 0.45 * eff / (256.0 * occ);
+      double t = (double)waves * (2.0 * tc.bn * tc.bm * per * 64.0) / slot_rate;
+      if (sp > 1) t += (double)M * N * sp * 8.0 / 4.0e12 + 3.0e-6;  // fp32 slab write+read + reduce launch
       if (t < best) {
         best = t;
         bp = {c, (ktiles + per - 1) / per, per};

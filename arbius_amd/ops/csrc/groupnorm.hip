@@ -92,31 +92,45 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
     }
   }
   __syncthreads();
+  // Per-group combine, parallel: L = 256/G lanes per group (consecutive lanes of one wave),
+  // each takes every L-th (channel, row-lane) item; the L partials are merged by a fixed
+  // xor-shuffle butterfly -> deterministic.
   const int Cg = C / G;
-  if (t < G) {
-    float N = 0.f, sum = 0.f;
-    for (int c = t * Cg; c < (t + 1) * Cg; ++c) {
+  int L = 1;  // largest power of two with G * L <= 256, at most one wave
+  while (L < 64 && 2 * L * G <= 256) L *= 2;
+  const int g = t / L, sl = t % L;
+  const int items = Cg * k;
+  float N = 0.f, sum = 0.f;
+  if (g < G) {
+    for (int it = sl; it < items; it += L) {
+      const int c = g * Cg + it / k, j = it % k;
       const int vv = c >> 3, e = c & 7;
-      for (int j = 0; j < k; ++j) {
-        const int tt = NV >= 256 ? (vv & 255) : j * NV + vv;
-        const int o = (tt * VPT + (NV >= 256 ? (vv >> 8) : 0)) * 8 + e;
-        N += sh_n[tt];
-        sum += sh_n[tt] * sh_mean[o];
-      }
+      const int tt = NV >= 256 ? (vv & 255) : j * NV + vv;
+      const int o = (tt * VPT + (NV >= 256 ? (vv >> 8) : 0)) * 8 + e;
+      N += sh_n[tt];
+      sum += sh_n[tt] * sh_mean[o];
     }
-    const float mu = N > 0.f ? sum / N : 0.f;
-    float m2 = 0.f;
-    for (int c = t * Cg; c < (t + 1) * Cg; ++c) {
+  }
+  for (int o = 1; o < L; o <<= 1) {
+    N += __shfl_xor(N, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+  }
+  const float mu = N > 0.f ? sum / N : 0.f;
+  float m2 = 0.f;
+  if (g < G) {
+    for (int it = sl; it < items; it += L) {
+      const int c = g * Cg + it / k, j = it % k;
       const int vv = c >> 3, e = c & 7;
-      for (int j = 0; j < k; ++j) {
-        const int tt = NV >= 256 ? (vv & 255) : j * NV + vv;
-        const int o = (tt * VPT + (NV >= 256 ? (vv >> 8) : 0)) * 8 + e;
-        const float d = sh_mean[o] - mu;
-        m2 += sh_m2[o] + sh_n[tt] * d * d;
-      }
+      const int tt = NV >= 256 ? (vv & 255) : j * NV + vv;
+      const int o = (tt * VPT + (NV >= 256 ? (vv >> 8) : 0)) * 8 + e;
+      const float d = sh_mean[o] - mu;
+      m2 += sh_m2[o] + sh_n[tt] * d * d;
     }
+  }
+  for (int o = 1; o < L; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+  if (g < G && sl == 0) {
     Stat st = {N, mu, m2, 0.f};
-    part[((size_t)b * chunks + chunk) * G + t] = st;
+    part[((size_t)b * chunks + chunk) * G + g] = st;
   }
 }
 
