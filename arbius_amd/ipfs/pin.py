@@ -1,0 +1,130 @@
+"""IPFS pinning strategies (``miner/src/ipfs.ts``): kubo HTTP API, Pinata, and a
+local content-addressed store (MockIPFS, the CPU plumbing config).
+
+The node computes the CID itself (``unixfs.wrap_directory``) the moment the
+output bytes exist, so the commitment can be signalled while the pin is still
+in flight; the pin result is checked against the local CID.
+"""
+from __future__ import annotations
+
+import json
+import os
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from .unixfs import CHUNK, add_file, b58encode, wrap_directory
+
+KUBO_ADD_PARAMS = {"cid-version": "0", "hash": "sha2-256", "chunker": f"size-{CHUNK}", "raw-leaves": "false"}
+
+
+class Pinner:
+    async def pin_files(self, taskid: str, files: Sequence[Tuple[str, bytes]]) -> str:
+        """Wrap ``files`` in a directory, pin, return the base58 directory CID."""
+        raise NotImplementedError
+
+    async def pin_file(self, content: bytes, name: str) -> str:
+        raise NotImplementedError
+
+    async def close(self):
+        pass
+
+
+class LocalPinner(Pinner):
+    """MockIPFS: blocks kept in memory (and optionally mirrored to ``root`` on disk)."""
+
+    def __init__(self, root: Optional[str] = None):
+        self.blocks: Dict[bytes, bytes] = {}
+        self.pins: List[str] = []
+        self.root = Path(root) if root else None
+        if self.root:
+            self.root.mkdir(parents=True, exist_ok=True)
+
+    def _store(self, blocks):
+        self.blocks.update(blocks)
+        if self.root:
+            for mh, blk in blocks.items():
+                p = self.root / b58encode(mh)
+                if not p.exists():
+                    p.write_bytes(blk)
+
+    async def pin_files(self, taskid, files):
+        d = wrap_directory(list(files))
+        self._store(d.blocks)
+        self.pins.append(d.cid_str)
+        return d.cid_str
+
+    async def pin_file(self, content, name):
+        r = add_file(content)
+        self._store(r.blocks)
+        self.pins.append(r.cid_str)
+        return r.cid_str
+
+    def cat(self, cid_mh: bytes) -> bytes:
+        return self.blocks[cid_mh]
+
+
+class KuboPinner(Pinner):
+    """kubo ``/api/v0/add`` (ipfs-http-client addAll with wrapWithDirectory)."""
+
+    def __init__(self, url: str = "http://127.0.0.1:5001", timeout: float = 120.0):
+        import httpx
+        self.url = url.rstrip("/")
+        self.client = httpx.AsyncClient(timeout=timeout)
+
+    async def pin_files(self, taskid, files):
+        params = dict(KUBO_ADD_PARAMS, **{"wrap-with-directory": "true", "pin": "true"})
+        multipart = [("file", (name, data, "application/octet-stream")) for name, data in files]
+        r = await self.client.post(f"{self.url}/api/v0/add", params=params, files=multipart)
+        r.raise_for_status()
+        for line in r.text.strip().splitlines():
+            obj = json.loads(line)
+            if obj.get("Name", None) == "":
+                return obj["Hash"]
+        raise RuntimeError("ipfs cid extract failed")
+
+    async def pin_file(self, content, name):
+        r = await self.client.post(f"{self.url}/api/v0/add", params=dict(KUBO_ADD_PARAMS, pin="true"),
+                                   files=[("file", (name, content, "application/octet-stream"))])
+        r.raise_for_status()
+        return json.loads(r.text.strip().splitlines()[-1])["Hash"]
+
+    async def close(self):
+        await self.client.aclose()
+
+
+class PinataPinner(Pinner):
+    """Pinata ``pinFileToIPFS`` multipart upload (files under ``<taskid>/<name>``)."""
+
+    URL = "https://api.pinata.cloud/pinning/pinFileToIPFS"
+
+    def __init__(self, jwt: str, timeout: float = 120.0):
+        import httpx
+        self.jwt = jwt
+        self.client = httpx.AsyncClient(timeout=timeout)
+
+    async def _post(self, multipart):
+        data = {"pinataOptions": json.dumps({"cidVersion": 0})}
+        r = await self.client.post(self.URL, files=multipart, data=data,
+                                   headers={"Authorization": f"Bearer {self.jwt}"})
+        r.raise_for_status()
+        return r.json()["IpfsHash"]
+
+    async def pin_files(self, taskid, files):
+        return await self._post([("file", (f"{taskid}/{name}", data, "application/octet-stream"))
+                                 for name, data in files])
+
+    async def pin_file(self, content, name):
+        return await self._post([("file", (name, content, "application/octet-stream"))])
+
+    async def close(self):
+        await self.client.aclose()
+
+
+def make_pinner(cfg) -> Pinner:
+    """From ``MiningConfig.ipfs`` (strategy http_client | pinata | local)."""
+    s = cfg.ipfs.strategy
+    if s == "http_client":
+        return KuboPinner(cfg.ipfs.http_client.url)
+    if s == "pinata":
+        return PinataPinner(cfg.ipfs.pinata.jwt)
+    return LocalPinner(os.environ.get("ARBIUS_LOCAL_IPFS_DIR"))

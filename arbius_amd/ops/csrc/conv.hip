@@ -184,6 +184,178 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Multi-stage LDS-DMA variant.  Same tiling / fragment / epilogue as above, but the K-tile
+// stream is global_load_lds_dwordx4 (16 B per lane straight into LDS, no VGPR round trip)
+// into an NS-deep ring of LDS stages with NS-1 tiles in flight: at ~1 workgroup per CU the
+// HBM latency of a tile (~1-2 us) is longer than one tile's MFMA work (~0.3 us), so one-ahead
+// register staging leaves the MFMAs starved (cdna_hip_programming.md §5 "Pipelining across
+// barriers": counted vmcnt + raw s_barrier, never __syncthreads() while DMA is in flight).
+// The XOR swizzle moves to the per-lane SOURCE address (LDS image stays lane-linear, rule 21);
+// zero padding / masked rows read a zero page.
+__device__ __attribute__((aligned(16))) uint4 g_conv_zero_page[4];
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
+__global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
+  constexpr int BK = 64;
+  static_assert(WN * WM == 4, "4 waves");
+  constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
+  constexpr int WCH = BN * 8 / 256;  // glds per thread per tile (W)
+  constexpr int XCH = BM * 8 / 256;  // glds per thread per tile (X)
+  constexpr int LPT = WCH + XCH;     // vmcnt units per tile per wave
+  constexpr int STAGE = (BN + BM) * BK;  // bf16 elements per stage
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WM, wm = wave % WM;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int lin = xcd_remap(blockIdx.x, p.tiles_total);
+  const int n0 = (lin % p.tiles_n) * BN;
+  const int m0 = (lin / p.tiles_n) * BM;
+  const int kt0 = SPLIT ? blockIdx.y * p.kt_per_split : 0;
+  const int kt1 = SPLIT ? min(p.ktiles, kt0 + p.kt_per_split) : p.ktiles;
+  const int nk = kt1 - kt0;
+
+  // lane-linear LDS image: chunk c = tid + 256 i -> row c/8, position c%8 holds logical
+  // chunk (c%8) ^ (row & 7)  (the read side applies the same XOR).
+  const int pos = tid & 7;
+  int wrow[WCH], wcc[WCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) {
+    wrow[i] = (tid >> 3) + 32 * i;
+    wcc[i] = pos ^ (wrow[i] & 7);
+  }
+  int xb[XCH], xho[XCH], xwo[XCH], xcc[XCH];
+  bool xok[XCH];
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int row = (tid >> 3) + 32 * i;
+    xcc[i] = pos ^ (row & 7);
+    const int m = m0 + row;
+    xok[i] = m < p.M;
+    const int mm = xok[i] ? m : 0;
+    const int hw = p.Ho * p.Wo;
+    xb[i] = mm / hw;
+    const int rem = mm - xb[i] * hw;
+    xho[i] = (rem / p.Wo) * p.stride - p.pad;
+    xwo[i] = (rem % p.Wo) * p.stride - p.pad;
+  }
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * BK;
+    const int rs = k0 / p.Cin;
+    const int cbase = k0 - rs * p.Cin;
+    const int r = rs / p.kw, s = rs - (rs / p.kw) * p.kw;
+    bf16_t* sW = smem + stage * STAGE;
+    bf16_t* sX = sW + BN * BK;
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int n = n0 + wrow[i];
+      const void* src = n < p.N ? (const void*)(p.w + (size_t)n * p.K + k0 + wcc[i] * 8)
+                                : (const void*)g_conv_zero_page;
+      // wave-uniform destination: first row of this wave's 8-row slab
+      bf16_t* dst = sW + ((wave * 8) + 32 * i) * BK;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      int hi = xho[i] + r, wi = xwo[i] + s;
+      const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
+      if (p.upsample) { hi >>= 1; wi >>= 1; }
+      const void* src = ok ? (const void*)(p.x + (((size_t)xb[i] * p.H + hi) * p.W + wi) * p.Cin + cbase + xcc[i] * 8)
+                           : (const void*)g_conv_zero_page;
+      bf16_t* dst = sX + ((wave * 8) + 32 * i) * BK;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue: NS-1 tiles in flight
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(kt0 + s, s);
+
+  for (int i = 0; i < nk; ++i) {
+    // tile i has landed once at most (NS-2) newer tiles are outstanding
+    if (i + NS - 2 < nk) wait_vmcnt<(NS - 2) * LPT>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for tile i is visible
+    if (i + NS - 1 < nk) issue(kt0 + i + NS - 1, (i + NS - 1) % NS);  // that stage was read at i-1
+    const bf16_t* sW = smem + (i % NS) * STAGE;
+    const bf16_t* sX = sW + BN * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TN], bfr[TM];
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int row = wn * (BN / WN) + a * 16 + l16;
+        af[a] = __builtin_bit_cast(bf16x8, ld16(&sW[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+      }
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        const int row = wm * (BM / WM) + b * 16 + l16;
+        bfr[b] = __builtin_bit_cast(bf16x8, ld16(&sX[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+      }
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+    // WAR on stage i%NS is covered by the next iteration's barrier: its refill is issued
+    // only after every wave has arrived there, i.e. finished this tile's MFMAs (whose
+    // operands - these ds_reads - had to complete first).
+  }
+
+  const int hw = p.Ho * p.Wo;
+#pragma unroll
+  for (int b = 0; b < TM; ++b) {
+    const int m = m0 + wm * (BM / WM) + b * 16 + l16;
+    if (m >= p.M) continue;
+    const int bb = m / hw;
+#pragma unroll
+    for (int a = 0; a < TN; ++a) {
+      const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
+      if (n >= p.N) continue;
+      float v0 = acc[a][b][0], v1 = acc[a][b][1], v2 = acc[a][b][2], v3 = acc[a][b][3];
+      if (SPLIT) {
+        *reinterpret_cast<float4*>(p.ws + ((size_t)blockIdx.y * p.M + m) * p.N + n) = make_float4(v0, v1, v2, v3);
+        continue;
+      }
+      if (p.bias) {
+        const uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
+        v0 += __uint_as_float(bv.x << 16); v1 += __uint_as_float(bv.x & 0xffff0000u);
+        v2 += __uint_as_float(bv.y << 16); v3 += __uint_as_float(bv.y & 0xffff0000u);
+      }
+      if (p.temb) {
+        const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)bb * p.N + n);
+        v0 += __uint_as_float(tv.x << 16); v1 += __uint_as_float(tv.x & 0xffff0000u);
+        v2 += __uint_as_float(tv.y << 16); v3 += __uint_as_float(tv.y & 0xffff0000u);
+      }
+      if (p.res) {
+        const uint2 rv = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.N + n);
+        v0 += __uint_as_float(rv.x << 16); v1 += __uint_as_float(rv.x & 0xffff0000u);
+        v2 += __uint_as_float(rv.y << 16); v3 += __uint_as_float(rv.y & 0xffff0000u);
+      }
+      uint2 o;
+      o.x = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+      o.y = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
+      *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
+    }
+  }
+}
+
 // Ordered split-K reduction + epilogue: out[m, n..n+7] from S fp32 slabs.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
   const long total = (long)p.M * (p.N / 8);
@@ -248,7 +420,7 @@ struct PinnedPlan {
 
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
-  if (want_cfg >= 0 && want_cfg < kNumCfgs) {
+  if (want_cfg >= 0 && want_cfg < 2 * kNumCfgs) {
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
     const int per = (ktiles + split - 1) / split;
@@ -310,22 +482,39 @@ ARB_API size_t arb_conv2d_workspace(int B, int H, int W, int Cin, int Cout, int 
   return pl.split > 1 ? (size_t)pl.split * a.M * a.N * sizeof(float) : 0;
 }
 
+template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
+static void launch_glds(const ConvArgs& p, dim3 grid, hipStream_t s) {
+  constexpr size_t lds = (size_t)NS * (BN + BM) * 64 * sizeof(bf16_t);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT><<<grid, 256, lds, s>>>(p);
+}
+
 template <int BN, int BM, int WN, int WM, int MINW>
-static void launch_conv(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
+static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStream_t s) {
+  // stages of the LDS-DMA ring: as many as fit 160 KiB, at most 4
+  constexpr int STAGE_BYTES = (BN + BM) * 64 * 2;
+  constexpr int NS = (4 * STAGE_BYTES <= 160 * 1024) ? 4 : 3;
   ConvArgs p = a;
   p.tiles_n = (p.N + BN - 1) / BN;
   p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
     dim3 grid(p.tiles_total, pl.split);
-    conv_igemm_kernel<BN, BM, WN, WM, MINW, true><<<grid, 256, 0, s>>>(p);
+    if (glds) launch_glds<BN, BM, WN, WM, NS, true>(p, grid, s);
+    else conv_igemm_kernel<BN, BM, WN, WM, MINW, true><<<grid, 256, 0, s>>>(p);
     long work = (long)p.M * (p.N / 8);
     long blocks = (work + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
   } else {
     dim3 grid(p.tiles_total, 1);
-    conv_igemm_kernel<BN, BM, WN, WM, MINW, false><<<grid, 256, 0, s>>>(p);
+    if (glds) launch_glds<BN, BM, WN, WM, NS, false>(p, grid, s);
+    else conv_igemm_kernel<BN, BM, WN, WM, MINW, false><<<grid, 256, 0, s>>>(p);
   }
 }
 
@@ -341,17 +530,18 @@ ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, cons
   conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
   const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
   if (pl.split > 1 && ws == nullptr) return -3;
-  switch (pl.cfg) {
-    case 0: launch_conv<128, 128, 2, 2, 2>(a, pl, stream); break;
-    case 1: launch_conv<64, 128, 2, 2, 2>(a, pl, stream); break;
-    case 2: launch_conv<128, 64, 2, 2, 2>(a, pl, stream); break;
-    case 3: launch_conv<64, 64, 2, 2, 2>(a, pl, stream); break;
-    case 4: launch_conv<160, 64, 2, 2, 2>(a, pl, stream); break;
-    case 5: launch_conv<160, 128, 2, 2, 1>(a, pl, stream); break;
-    case 6: launch_conv<320, 32, 4, 1, 1>(a, pl, stream); break;
-    case 7: launch_conv<256, 64, 4, 1, 1>(a, pl, stream); break;
-    case 8: launch_conv<128, 256, 2, 2, 1>(a, pl, stream); break;
-    default: launch_conv<64, 256, 1, 4, 1>(a, pl, stream); break;
+  const bool glds = pl.cfg < kNumCfgs;  // cfg >= kNumCfgs: register-staged variant (A/B)
+  switch (pl.cfg % kNumCfgs) {
+    case 0: launch_conv<128, 128, 2, 2, 2>(a, pl, glds, stream); break;
+    case 1: launch_conv<64, 128, 2, 2, 2>(a, pl, glds, stream); break;
+    case 2: launch_conv<128, 64, 2, 2, 2>(a, pl, glds, stream); break;
+    case 3: launch_conv<64, 64, 2, 2, 2>(a, pl, glds, stream); break;
+    case 4: launch_conv<160, 64, 2, 2, 2>(a, pl, glds, stream); break;
+    case 5: launch_conv<160, 128, 2, 2, 1>(a, pl, glds, stream); break;
+    case 6: launch_conv<320, 32, 4, 1, 1>(a, pl, glds, stream); break;
+    case 7: launch_conv<256, 64, 4, 1, 1>(a, pl, glds, stream); break;
+    case 8: launch_conv<128, 256, 2, 2, 1>(a, pl, glds, stream); break;
+    default: launch_conv<64, 256, 1, 4, 1>(a, pl, glds, stream); break;
   }
   return (int)hipGetLastError();
 }

@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from arbius_amd import ops  # noqa: E402
 from arbius_amd.ops import _lib  # noqa: E402
 
-NCFG = 10
+NCFG = 20  # 0-9: LDS-DMA multi-stage, 10-19: register-staged
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 

@@ -119,3 +119,18 @@ def test_gemm(cuda, M, K, N):
     r = torch.randn(M, N, device=cuda).bfloat16()
     y = _lib.gemm(x, w, b, r)
     assert _rel(y, x.float() @ w.float().t() + b.float() + r.float()) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", list(range(20)))
+@pytest.mark.parametrize("split", [1, 3])
+def test_conv2d_all_tile_configs(cuda, cfg, split):
+    """Every tile config of both kernel variants (LDS-DMA ring / register staged) and split-K."""
+    torch.manual_seed(3)
+    B, H, W, Cin, Cout = 2, 12, 10, 128, 160
+    x = torch.randn(B, H, W, Cin, device=cuda).bfloat16()
+    w = (torch.randn(Cout, 3, 3, Cin, device=cuda) / math.sqrt(9 * Cin)).bfloat16()
+    b = torch.randn(Cout, device=cuda).bfloat16()
+    r = torch.randn(B, H, W, Cout, device=cuda).bfloat16()
+    y = _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg, split)
+    ref_y = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, 1, False) + r.float()
+    assert _rel(y, ref_y) < 1e-2, (cfg, split, _rel(y, ref_y))
