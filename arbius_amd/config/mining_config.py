@@ -85,6 +85,7 @@ class MI355XConfig(_Base):
     job_lease_seconds: float = 900.0
     poll_interval_ms: int = 100           # index.ts:1081
     min_model_filter_fee: str = "0"
+    verify_fraction: float = 0.0          # re-solve this fraction of others' solutions (Q10)
     chain_id: Optional[int] = None
     mock_chain: bool = False              # in-process MockEngine (testing / plumbing config)
 

@@ -1,0 +1,30 @@
+"""Template name -> in-process pipeline factory (replaces the per-model Cog
+containers referenced by ``templates/*.json`` ``meta.docker``)."""
+from __future__ import annotations
+
+from typing import Optional
+
+
+def build_pipeline(name: str, device="cpu", tiny: bool = False, weights_dir: Optional[str] = None,
+                   weight_seed: int = 0, **kw):
+    if name == "anythingv3":
+        from .sd15 import SD15Config, SD15Pipeline
+        cfg = SD15Config.tiny() if tiny else SD15Config()
+        pipe = SD15Pipeline(cfg, device=device, weight_seed=weight_seed, **kw)
+        if weights_dir:
+            from .weights import load_sd15
+            load_sd15(pipe, weights_dir)
+        return pipe
+    if name == "kandinsky2":
+        from .kandinsky2 import Kandinsky2Config, Kandinsky2Pipeline
+        cfg = Kandinsky2Config.tiny() if tiny else Kandinsky2Config()
+        return Kandinsky2Pipeline(cfg, device=device, weight_seed=weight_seed, **kw)
+    if name in ("zeroscopev2xl", "damo"):
+        from .video import VideoConfig, VideoPipeline
+        cfg = VideoConfig.tiny(name) if tiny else VideoConfig.for_model(name)
+        return VideoPipeline(cfg, device=device, weight_seed=weight_seed, **kw)
+    if name == "robust_video_matting":
+        from .rvm import RVMConfig, RVMPipeline
+        cfg = RVMConfig.tiny() if tiny else RVMConfig()
+        return RVMPipeline(cfg, device=device, weight_seed=weight_seed, **kw)
+    raise ValueError(f"unknown model template {name!r}")

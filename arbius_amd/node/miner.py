@@ -1,0 +1,499 @@
+"""The mining node orchestrator (the role of ``miner/src/index.ts``), asyncio-native.
+
+Chain events -> SQLite job queue -> job processors, with the reference's job
+methods, priorities and delays (index.ts:506-1101):
+
+  task (p10, concurrent) -> solve (p20) -> [commit, submit] -> claim (p50, +2120 s)
+  pinTaskInput (p10, concurrent), validatorStake (p30 boot / p100 every 600 s),
+  automine (p5, +delay), contestationVoteFinish (p30, +5010 s)
+
+MI355X-first differences (all behaviour-compatible on chain):
+  * ``solve`` jobs run on a pool of GPU task workers - up to one solve per GPU in
+    flight (the reference serialises solves, index.ts:555-563);
+  * the solution CID is computed locally from the output bytes, so the commitment
+    is signalled before the IPFS pin completes; the pin runs in the background and
+    its CID is checked against the local one;
+  * jobs are leased, not deleted up front (fixes Q4), and the event cursor is
+    persisted so missed events are back-filled after a restart (fixes Q8);
+  * ``contestationVoteFinish`` is implemented (the reference processor is a stub, Q11).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+from typing import Awaitable, Callable, Dict, Optional
+
+from ..chain.client import ChainClient, TxError
+from ..ipfs.pin import Pinner
+from ..ipfs.unixfs import cid_hex_to_str
+from ..store.db import DB
+from ..utils.protocol import expretry, generate_commitment, taskid2seed
+from .models import Model, check_model_filter, get_model_by_id, hydrate_input
+from .solver import EVIL_CID
+
+log = logging.getLogger("arbius.miner")
+ZERO_ADDR = "0x" + "00" * 20
+MAX_UINT256 = 2 ** 256 - 1
+MINER_VERSION = 0
+
+
+class Metrics:
+    """Counters / latency samples exported on the RPC server's /metrics route."""
+
+    def __init__(self):
+        self.counters: Dict[str, int] = {}
+        self.latencies: Dict[str, list] = {}
+
+    def inc(self, name, n=1):
+        self.counters[name] = self.counters.get(name, 0) + n
+
+    def observe(self, name, seconds):
+        self.latencies.setdefault(name, []).append(seconds)
+
+    def p50(self, name):
+        v = sorted(self.latencies.get(name, []))
+        return v[len(v) // 2] if v else None
+
+
+class Miner:
+    def __init__(self, cfg, db: DB, chain: ChainClient, pinner: Pinner, solver_pool, models: Dict[str, Model],
+                 clock: Callable[[], int] = None, sleep: Callable[[float], Awaitable] = None,
+                 retry_sleep: Callable[[float], Awaitable] = None):
+        self.c = cfg
+        self.db = db
+        self.chain = chain
+        self.pinner = pinner
+        self.pool = solver_pool
+        self.models = models
+        self.now = clock or (lambda: int(time.time()))
+        self.sleep = sleep or asyncio.sleep
+        self.retry_sleep = retry_sleep or asyncio.sleep
+        self.metrics = Metrics()
+        self.quirks = bool(getattr(cfg.mi355x, "reference_hydration_quirks", False))
+        self.lease_s = float(getattr(cfg.mi355x, "job_lease_seconds", 900.0))
+        self.poll_s = float(getattr(cfg.mi355x, "poll_interval_ms", 100)) / 1000.0
+        self._bg: set = set()
+        self._running_solves: Dict[int, asyncio.Task] = {}
+        self.stopped = False
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def wallet(self) -> str:
+        return self.chain.address
+
+    def _spawn(self, coro):
+        t = asyncio.ensure_future(coro)
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)
+        return t
+
+    async def _retry(self, fn, tries=10, base=1.5):
+        return await expretry(fn, tries, base, sleep=self.retry_sleep)
+
+    def queue(self, method, priority, waituntil, concurrent, data):
+        log.info("QueueJob %s %s %s %s", method, priority, waituntil, "concurrent" if concurrent else "blocking")
+        return self.db.queue_job(method, priority, waituntil, concurrent, data)
+
+    # ------------------------------------------------------------------ lookups (index.ts:82-189)
+    async def lookup_and_insert_task(self, taskid: str) -> dict:
+        existing = self.db.get_task(taskid)
+        if existing:
+            return {"model": existing["modelid"], "fee": int(existing["fee"]), "owner": existing["address"],
+                    "blocktime": int(existing["blocktime"]), "version": existing["version"], "cid": existing["cid"]}
+        t = await self._retry(lambda: self.chain.get_task(taskid))
+        if t is None:
+            raise RuntimeError(f"could not look up task {taskid}")
+        self.db.store_task(taskid, t["model"], t["fee"], t["owner"], t["blocktime"], t["version"], t["cid"])
+        return t
+
+    async def lookup_and_insert_task_input(self, taskid, cid, txid, template) -> Optional[dict]:
+        cached = self.db.get_task_input(taskid, cid)
+        if cached is not None:
+            return json.loads(cached["data"])
+        raw = await self._retry(lambda: self.chain.get_submit_task_input(txid))
+        if raw is None:
+            # reference Q9: non-submitTask calldata (task sent through a contract).  Do NOT mark
+            # invalid (that would contest a valid task); skip it.
+            log.warning("Task (%s) input could not be recovered from tx %s", taskid, txid)
+            return None
+        try:
+            pre_str = raw.decode("utf-8")
+            pre = json.loads(pre_str)
+        except Exception:  # noqa: BLE001
+            log.warning("Task (%s) request was unable to be parsed", taskid)
+            self.db.store_invalid_task(taskid)
+            return None
+        inp, err, msg = hydrate_input(pre, template, self.quirks)
+        if err:
+            log.warning("Task (%s) hydration error %s", taskid, msg)
+            self.db.store_invalid_task(taskid)
+            return None
+        inp["seed"] = taskid2seed(taskid)
+        self.db.store_task_input(taskid, cid, inp)
+        self.queue("pinTaskInput", 10, 0, True, {"taskid": taskid, "input": pre_str})
+        return inp
+
+    # ------------------------------------------------------------------ event handlers (index.ts:191-333)
+    async def on_event(self, ev):
+        a = ev.args
+        if ev.name == "TaskSubmitted":
+            await self.lookup_and_insert_task(a["id"])
+            self.queue("task", 10, 0, True, {"taskid": a["id"], "txid": ev.tx})
+            self.metrics.inc("tasks_seen")
+        elif ev.name == "TaskRetracted":
+            if not self.db.get_task(a["id"]):
+                await self.lookup_and_insert_task(a["id"])
+            self.db.update_task_set_retracted(a["id"])
+        elif ev.name == "SolutionSubmitted":
+            taskid = a["task"]
+            if self.db.get_solution(taskid):
+                return
+            s = await self._retry(lambda: self.chain.get_solution(taskid))
+            if self.db.get_invalid_task(taskid) is not None and s["validator"].lower() != self.wallet:
+                await self.contest_solution(taskid)
+            self.db.store_solution(taskid, s["validator"], s["blocktime"], s["claimed"], s["cid"])
+        elif ev.name == "ContestationSubmitted":
+            taskid = a["task"]
+            if self.db.get_contestation(taskid):
+                return
+            c = await self._retry(lambda: self.chain.get_contestation(taskid))
+            if self.db.get_invalid_task(taskid) is not None:
+                await self.vote_on_contestation(taskid, True)
+            elif c["validator"].lower() != self.wallet and self._should_verify(taskid):
+                # verify mode: re-run the task and vote by comparing CIDs
+                self._spawn(self._verify_and_vote(taskid))
+            self.db.store_contestation(taskid, c["validator"], c["blocktime"], c["finish_start_index"])
+        elif ev.name == "ContestationVote":
+            taskid, validator = a["task"], a["addr"]
+            if any(r["validator"] == validator for r in self.db.get_contestation_votes(taskid)):
+                return
+            self.db.store_contestation_vote(taskid, validator, a["yea"])
+        elif ev.name == "VersionChanged":
+            await self.version_check()
+
+    async def poll_events(self):
+        latest = await self.chain.block_number()
+        cur = self.db.get_cursor()
+        start = latest if cur is None else cur + 1  # first boot: only new events (reference .on semantics)
+        if cur is None:
+            self.db.set_cursor(latest)
+            return 0
+        if start > latest:
+            return 0
+        evs = await self.chain.get_events(start, latest)
+        for ev in evs:
+            try:
+                await self.on_event(ev)
+            except Exception as e:  # noqa: BLE001
+                log.error("event handler %s failed: %r", ev.name, e)
+        self.db.set_cursor(latest)
+        return len(evs)
+
+    # ------------------------------------------------------------------ processors (index.ts:379-750)
+    async def process_pin_task_input(self, taskid, input_str):
+        cid = await self._retry(lambda: self.pinner.pin_file(input_str.encode(), f"task-{taskid}.json"))
+        log.debug("Task input %s pinned with %s", taskid, cid)
+
+    async def process_validator_stake(self):
+        eth = await self.chain.eth_balance(self.wallet)
+        if eth < 10 ** 16:
+            log.warning("BCHK Low Ether balance")
+        staked = (await self.chain.get_validator(self.wallet))["staked"]
+        vmin = await self._retry(lambda: self.chain.get_validator_minimum())
+        self.queue("validatorStake", 100, self.now() + 600, False, {"validatorMinimum": str(vmin)})
+        min_topup = vmin * 100 // int(100 - self.c.stake_buffer_topup_percent)
+        if staked >= min_topup:
+            log.debug("BCHK Have sufficient stake")
+            return
+        min_buffer = vmin * 100 // int(100 - self.c.stake_buffer_percent)
+        deposit = min_buffer - staked
+        balance = await self._retry(lambda: self.chain.token_balance(self.wallet))
+        if balance < deposit:
+            log.error("BCHK Balance %s less than deposit amount %s", balance, deposit)
+            raise RuntimeError("unable to stake required balance")
+        allowance = await self._retry(lambda: self.chain.token_allowance(self.wallet, self.chain.engine_address))
+        if allowance < balance:
+            await self._retry(lambda: self.chain.token_approve(self.chain.engine_address, MAX_UINT256 - allowance))
+        await self._retry(lambda: self.chain.validator_deposit(self.wallet, deposit))
+        self.metrics.inc("stake_deposits")
+
+    async def process_automine(self):
+        a = self.c.automine
+        try:
+            await self.chain.submit_task(a.version, self.wallet, a.model, int(a.fee),
+                                         json.dumps(a.input, separators=(",", ":")).encode())
+        except Exception as e:  # noqa: BLE001
+            log.error("Automine submitTask failed %r", e)
+        if a.enabled:
+            self.queue("automine", 5, self.now() + a.delay, False, {})
+
+    async def process_task(self, taskid, txid):
+        t = await self.lookup_and_insert_task(taskid)
+        if int(t["version"]) != 0:
+            self.db.store_invalid_task(taskid)
+            return
+        enabled, passed, template = check_model_filter(self.models, t["model"], self.now(), int(t["fee"]),
+                                                       int(t["blocktime"]), t["owner"])
+        if not enabled or not passed:
+            return
+        inp = await self.lookup_and_insert_task_input(taskid, t["cid"], txid, template)
+        if inp is None:
+            return
+        self.queue("solve", 20, 0, False, {"taskid": taskid})
+
+    async def get_cid(self, model: Model, taskid: str, inp: dict) -> Optional[str]:
+        """default__getcid (models.ts:34-54) with local CID + background pin."""
+        if self.c.evilmode:
+            return EVIL_CID
+        t0 = time.perf_counter()
+        sol = await self._retry(lambda: self.pool.solve(model, taskid, inp))
+        if sol is None:
+            raise RuntimeError("cannot get files")
+        self.metrics.observe("gpu_solve_s", time.perf_counter() - t0)
+        self._spawn(self._pin_solution(taskid, sol))
+        return sol.cid
+
+    async def _pin_solution(self, taskid, sol):
+        cid58 = await self._retry(lambda: self.pinner.pin_files(taskid, sol.files))
+        if cid58 is None:
+            log.error("Task (%s) pin failed", taskid)
+            self.metrics.inc("pin_failures")
+        elif cid58 != cid_hex_to_str(sol.cid):
+            log.error("Task (%s) pinned CID %s != local CID %s", taskid, cid58, cid_hex_to_str(sol.cid))
+            self.metrics.inc("pin_cid_mismatch")
+
+    async def process_solve(self, taskid):
+        t_start = time.perf_counter()
+        s = await self._retry(lambda: self.chain.get_solution(taskid))
+        if s["validator"] != ZERO_ADDR:
+            if s["validator"].lower() != self.wallet and self._should_verify(taskid):
+                return await self.verify_solution(taskid, s)
+            log.debug("Task (%s) already has solution", taskid)
+            return
+        t = await self.lookup_and_insert_task(taskid)
+        m = get_model_by_id(self.models, t["model"])
+        if m is None:
+            log.error("Task (%s) could not find model (%s)", taskid, t["model"])
+            return
+        row = self.db.get_task_input(taskid, t["cid"])
+        if row is None:
+            log.warning("Task (%s) input not found in db", taskid)
+            return
+        inp = json.loads(row["data"])
+        cid = await self.get_cid(m, taskid, inp)
+        if not cid:
+            return
+        commitment = generate_commitment(self.wallet, taskid, cid)
+        try:
+            await self.chain.signal_commitment(commitment)
+        except Exception as e:  # noqa: BLE001
+            log.error("Commitment submission failed %r", e)
+            return
+
+        async def submit():
+            try:
+                await self.chain.submit_solution(taskid, cid)
+                self.queue("claim", 50, self.now() + 2000 + 120, False, {"taskid": taskid})
+                self.metrics.inc("solutions_submitted")
+                self.metrics.observe("task_latency_s", time.perf_counter() - t_start)
+                return True
+            except TxError as e:
+                ex = await self._retry(lambda: self.chain.get_solution(taskid))
+                if ex["validator"] == ZERO_ADDR:
+                    raise RuntimeError(f"unknown error submitting solution for {taskid}: {e.reason}")
+                if ex["cid"] == cid:
+                    log.info("Solution found for %s matches our cid %s", taskid, cid)
+                    return True
+                log.info("Solution found with cid %s does not match ours %s", ex["cid"], cid)
+                await self.contest_solution(taskid)
+                return True
+
+        await self._retry(submit, 3, 1.25)
+
+    def _should_verify(self, taskid) -> bool:
+        """Verify mode (reference defect Q10: solutions of others are never re-checked):
+        re-solve a deterministic fraction of already-solved tasks on spare GPU capacity."""
+        frac = float(getattr(self.c.mi355x, "verify_fraction", 0.0))
+        if frac <= 0.0:
+            return False
+        return (int(taskid, 16) % 10000) < frac * 10000
+
+    async def verify_solution(self, taskid, s):
+        t = await self.lookup_and_insert_task(taskid)
+        m = get_model_by_id(self.models, t["model"])
+        row = self.db.get_task_input(taskid, t["cid"])
+        if m is None or row is None or self.c.evilmode:
+            return
+        sol = await self._retry(lambda: self.pool.solve(m, taskid, json.loads(row["data"])))
+        if sol is None:
+            return
+        self.metrics.inc("verifications")
+        if sol.cid != s["cid"]:
+            log.info("Verify: task %s solution cid %s != ours %s -> contest", taskid, s["cid"], sol.cid)
+            await self.contest_solution(taskid)
+
+    async def _verify_and_vote(self, taskid):
+        s = await self._retry(lambda: self.chain.get_solution(taskid))
+        if s["validator"] == ZERO_ADDR or s["validator"].lower() == self.wallet:
+            return
+        try:
+            t = await self.lookup_and_insert_task(taskid)
+            m = get_model_by_id(self.models, t["model"])
+            row = self.db.get_task_input(taskid, t["cid"])
+            if m is None or row is None:
+                return
+            sol = await self._retry(lambda: self.pool.solve(m, taskid, json.loads(row["data"])))
+        except Exception as e:  # noqa: BLE001
+            log.error("verify %s failed: %r", taskid, e)
+            return
+        if sol is not None:
+            await self.vote_on_contestation(taskid, sol.cid != s["cid"])
+
+    async def contest_solution(self, taskid):
+        try:
+            await self.chain.submit_contestation(taskid)
+            self.queue("contestationVoteFinish", 30, self.now() + 5010, False, {"taskid": taskid})
+            self.metrics.inc("contestations_submitted")
+        except TxError:
+            c = await self._retry(lambda: self.chain.get_contestation(taskid))
+            if c["validator"] == ZERO_ADDR:
+                log.error("An unknown error occurred when we tried to contest %s", taskid)
+                return
+            await self.vote_on_contestation(taskid, True)
+
+    async def vote_on_contestation(self, taskid, yea):
+        if await self._retry(lambda: self.chain.contestation_voted(taskid, self.wallet)):
+            return
+        try:
+            await self.chain.vote_on_contestation(taskid, yea)
+            self.metrics.inc("contestation_votes")
+        except TxError as e:
+            log.error("Failed voting on contestation %s: %s", taskid, e.reason)
+
+    async def process_contestation_vote_finish(self, taskid):
+        """Implemented (reference stub, index.ts:392-395): finish in pages of 32 voters."""
+        c = await self._retry(lambda: self.chain.get_contestation(taskid))
+        if c["validator"] == ZERO_ADDR:
+            return
+        votes = self.db.get_contestation_votes(taskid)
+        total = max(len(votes), 1)
+        start = int(c["finish_start_index"])
+        while start < total:
+            try:
+                await self.chain.contestation_vote_finish(taskid, 32)
+            except TxError as e:
+                log.error("contestationVoteFinish %s failed: %s", taskid, e.reason)
+                return
+            start += 32
+
+    async def process_claim(self, taskid):
+        async def claim():
+            s = await self._retry(lambda: self.chain.get_solution(taskid))
+            if s["claimed"]:
+                return "already"
+            await self.chain.claim_solution(taskid)
+            return "ok"
+        r = await self._retry(claim)
+        if r is None:
+            log.error("Failed claiming (%s)", taskid)
+        elif r == "ok":
+            self.metrics.inc("claims")
+
+    # ------------------------------------------------------------------ boot / loop (index.ts:960-1101)
+    async def version_check(self):
+        v = await self.chain.version()
+        if v > MINER_VERSION:
+            raise SystemExit(f"version mismatch, have miner version {MINER_VERSION} and arbius is {v}")
+
+    async def boot(self):
+        self.db.clear_jobs_by_method("validatorStake")
+        self.db.clear_jobs_by_method("automine")
+        await self.version_check()
+        self.queue("validatorStake", 30, 0, False, {})
+        if self.c.automine.enabled:
+            self.queue("automine", 5, 0, False, {})
+
+    def _dispatch(self, method: str, data: dict):
+        if method == "automine":
+            return self.process_automine()
+        if method == "validatorStake":
+            return self.process_validator_stake()
+        if method == "task":
+            return self.process_task(data["taskid"], data["txid"])
+        if method == "solve":
+            return self.process_solve(data["taskid"])
+        if method == "claim":
+            return self.process_claim(data["taskid"])
+        if method == "pinTaskInput":
+            return self.process_pin_task_input(data["taskid"], data["input"])
+        if method == "contestationVoteFinish":
+            return self.process_contestation_vote_finish(data["taskid"])
+        raise SystemExit(f"method ({method}) has no implementation")  # index.ts:914-916
+
+    async def _run_job(self, job):
+        try:
+            await self._dispatch(job["method"], json.loads(job["data"]))
+            self.metrics.inc(f"jobs_ok_{job['method']}")
+        except SystemExit:
+            raise
+        except Exception as e:  # noqa: BLE001
+            log.error("Job (%s) [%s] failed: %r", job["id"], job["method"], e)
+            self.db.store_failed_job(job)
+            self.metrics.inc(f"jobs_failed_{job['method']}")
+        finally:
+            self.db.delete_job(job["id"])
+
+    async def process_jobs(self) -> int:
+        """One scheduler pass: concurrent jobs fire-and-forget, solves fill the GPU
+        pool, other blocking jobs run in priority order."""
+        jobs = self.db.runnable_jobs(self.now())
+        n = 0
+        for job in jobs:
+            if job["concurrent"]:
+                if self.db.lease_job(job["id"], "node", self.lease_s):
+                    self._spawn(self._run_job(job))
+                    n += 1
+        for job in jobs:
+            if job["concurrent"]:
+                continue
+            if job["method"] == "solve":
+                if len(self._running_solves) >= max(1, getattr(self.pool, "capacity", 1)):
+                    continue
+                if self.db.lease_job(job["id"], "gpu", self.lease_s):
+                    t = self._spawn(self._run_job(job))
+                    self._running_solves[job["id"]] = t
+                    t.add_done_callback(lambda _t, jid=job["id"]: self._running_solves.pop(jid, None))
+                    n += 1
+                continue
+            if self.db.lease_job(job["id"], "node", self.lease_s):
+                await self._run_job(job)
+                n += 1
+        return n
+
+    async def drain(self, max_rounds=10000):
+        """Run until no runnable job is left and no background work is pending (tests)."""
+        for _ in range(max_rounds):
+            n = await self.process_jobs()
+            if self._bg:
+                await asyncio.sleep(0)
+                await asyncio.gather(*list(self._bg), return_exceptions=True)
+                continue
+            if n == 0 and not self.db.runnable_jobs(self.now()):
+                return
+
+    async def run(self, stop: asyncio.Event = None):
+        await self.boot()
+        stop = stop or asyncio.Event()
+        last_poll = 0.0
+        while not stop.is_set():
+            if time.monotonic() - last_poll >= 1.0:
+                try:
+                    await self.poll_events()
+                except Exception as e:  # noqa: BLE001
+                    log.error("event poll failed: %r", e)
+                last_poll = time.monotonic()
+            n = await self.process_jobs()
+            if n == 0:
+                await self.sleep(self.poll_s)

@@ -1,0 +1,77 @@
+"""GPU task-worker pools behind the orchestrator's ``solve`` jobs.
+
+* ``LocalSolverPool``  - pipelines in this process on one device (CPU plumbing
+  config, single-GPU node); inference runs in a worker thread so the asyncio
+  control plane keeps polling events / serving RPC.
+* ``parallel.workers.MultiGPUSolverPool`` - one process per GPU (8 on a node).
+* ``FakeSolverPool``   - deterministic synthetic outputs (control-plane tests,
+  fault injection).
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import threading
+from typing import Callable, Dict, Optional
+
+import numpy as np
+
+from ..ipfs.unixfs import wrap_directory
+from ..utils.png import encode_png
+from .solver import Solution, solve_task
+
+
+class FakeSolverPool:
+    """Synthetic solver: a PNG derived from (model, input) only - deterministic like a real miner."""
+
+    def __init__(self, capacity: int = 1, delay: float = 0.0):
+        self.capacity = capacity
+        self.delay = delay
+        self.calls = []
+        self.fail_next = 0
+
+    async def solve(self, model, taskid, inp) -> Solution:
+        self.calls.append((model.id, taskid, dict(inp)))
+        if self.fail_next:
+            self.fail_next -= 1
+            raise RuntimeError("injected GPU worker failure")
+        if self.delay:
+            await asyncio.sleep(self.delay)
+        h = hashlib.sha256((model.id + repr(sorted(inp.items()))).encode()).digest()
+        img = np.frombuffer(h * 48, dtype=np.uint8)[: 16 * 16 * 3].reshape(16, 16, 3)
+        png = encode_png(img)
+        dag = wrap_directory([("out-1.png", png)])
+        return Solution([("out-1.png", png)], dag.cid_hex, dag, {})
+
+    async def close(self):
+        pass
+
+
+class LocalSolverPool:
+    """In-process pipelines (lazily built per model) on ``device``; one solve at a time."""
+
+    def __init__(self, device="cpu", pipeline_factory: Callable = None, capacity: int = 1, **factory_kw):
+        from ..models.registry import build_pipeline
+        self.device = device
+        self.capacity = capacity
+        self.factory = pipeline_factory or build_pipeline
+        self.factory_kw = factory_kw
+        self.pipes: Dict[str, object] = {}
+        self._lock = threading.Lock()
+
+    def _pipe(self, model):
+        with self._lock:
+            if model.name not in self.pipes:
+                self.pipes[model.name] = self.factory(model.name, device=self.device, **self.factory_kw)
+            return self.pipes[model.name]
+
+    def solve_sync(self, model, taskid, inp) -> Solution:
+        pipe = self._pipe(model)
+        return solve_task(model, pipe, inp)
+
+    async def solve(self, model, taskid, inp) -> Solution:
+        loop = asyncio.get_running_loop()
+        return await loop.run_in_executor(None, self.solve_sync, model, taskid, inp)
+
+    async def close(self):
+        self.pipes.clear()

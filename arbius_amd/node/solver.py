@@ -45,3 +45,17 @@ def solve_image(pipe, inp: dict, png_level: int = 6) -> Solution:
     tm = dict(getattr(pipe, "timings", {}))
     tm.update({"infer_s": t1 - t0, "encode_cid_s": t2 - t1})
     return Solution([("out-1.png", png)], dag.cid_hex, dag, tm)
+
+
+def solve_files(files, timings=None) -> Solution:
+    dag = wrap_directory(list(files))
+    return Solution(list(files), dag.cid_hex, dag, dict(timings or {}))
+
+
+def solve_task(model, pipe, inp: dict) -> Solution:
+    """Dispatch by template output kind: image -> out-1.png, video/matting -> out-1.mp4."""
+    if hasattr(pipe, "solve"):
+        return pipe.solve(inp)
+    if model.kind == "image":
+        return solve_image(pipe, inp)
+    raise ValueError(f"no solver for model kind {model.kind}")

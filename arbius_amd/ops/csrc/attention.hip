@@ -6,18 +6,23 @@
 // attention (seq = frames).  SURVEY.md §2.6 (a)-(c), §5.7.
 //
 // Structure (one workgroup = 4 waves, QT x 16 query rows per wave):
-//   * swapped product S^T = K Q^T on mfma_f32_16x16x32_bf16, so each lane
-//     owns ONE query column (q = lane&15) and 4 keys per 16-key tile:
-//     the softmax row statistics need only two cross-lane steps (xor 16/32)
-//     and the O^T accumulator rows are already lane-aligned with them.
+//   * swapped product S^T = K Q^T on mfma_f32_16x16x32_bf16, so each lane owns
+//     ONE query column (q = lane&15) and 4 keys per 16-key tile: softmax row
+//     statistics need only two cross-lane steps (xor 16/32) and the O^T
+//     accumulator rows are lane-aligned with them.
 //   * P^T goes straight from the S^T accumulators into the B operand of
 //     O^T = V^T P^T with a permuted k order (no LDS round-trip for P).
-//   * V^T fragments come from the row-major V tile in LDS through the CDNA4
-//     transposing read ds_read_b64_tr_b16 (two per 32-key step / 16-col tile),
-//     row stride 16*(odd) elements -> conflict-free (cdna_hip_programming T10).
-//   * K tile rows padded by 16 B; Q fragments live in registers.
-//   * head dim is padded to 32 (QK^T k-dim) / 16 (PV n-dim) with zero fill;
-//     key padding is masked with -inf, V padding rows are zeroed.
+//   * V^T fragments come from the row-major V tile through the CDNA4 transposing
+//     read ds_read_b64_tr_b16; row stride 16*(odd) elements -> conflict free (T10).
+//   * ROW SUMS ON THE MATRIX CORE: when D % 16 != 0 (d=40: the 4096-token SD
+//     self-attention, VALU-bound) the zero-padded V column D is set to 1.0, so
+//     O^T row D accumulates sum_k P[q,k] with the same rescaling as O - the
+//     per-score add of the softmax denominator disappears from the VALU.
+//   * scores stay raw; the scale is folded into the exp2 fma (max commutes).
+//   * K/V: register-staged prefetch of tile j+1 while tile j is consumed, LDS
+//     double buffer -> one barrier per 64-key tile (T14).
+//   * head dim padded to 32 (QK^T k-dim) / 16 (PV n-dim) with zero fill; key
+//     padding masked with -inf only on partial tiles; V padding rows zero.
 //   * 1-D XCD-aware block remap: the q-blocks of one (batch, head) share an L2.
 //   * no atomics, fixed reduction order -> bitwise deterministic.
 #include "common.h"
@@ -43,8 +48,11 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   constexpr int KROW = KSTEPS * 32 + 8;    // K tile row (elements): 16 B pad
   constexpr int VROW = 16 * (DT | 1);      // V tile row: 16*(odd) -> tr-read conflict free
   constexpr int QBLK = 4 * QT * 16;        // queries per workgroup
-  __shared__ __attribute__((aligned(16))) bf16_t sK[KV_BLK * KROW];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[KV_BLK * VROW];
+  constexpr int KCH = KV_BLK * KSTEPS * 4;
+  constexpr int VCH = KV_BLK * DT * 2;
+  constexpr int KPT = (KCH + 255) / 256, VPT = (VCH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t sK[2][KV_BLK * KROW];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[2][KV_BLK * VROW];
 
   const int nqb = (a.Nq + QBLK - 1) / QBLK;
   const int total = nqb * a.H * a.B;
@@ -57,6 +65,7 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   const int wave = tid >> 6, lane = tid & 63;
   const int lq = lane & 15, g = lane >> 4;
   const int D = a.D;
+  const bool ones = (D & 15) != 0;  // spare zero-padded V column D carries the row sum
 
   const bf16_t* qbase = a.q + b * a.q_sb + h * a.q_sh;
   const bf16_t* kbase = a.k + b * a.k_sb + h * a.k_sh;
@@ -93,12 +102,8 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     kv_end = min(a.Nk, qmax + 1);
   }
 
-  // ---- register-staged K/V pipeline (T14): the next tile's global loads are in flight
-  //      while the current tile is consumed from LDS.
-  constexpr int KCH = KV_BLK * KSTEPS * 4;
-  constexpr int VCH = KV_BLK * DT * 2;
-  constexpr int KPT = (KCH + 255) / 256, VPT = (VCH + 255) / 256;
   uint4 rk[KPT], rv[VPT];
+  const uint32_t one_bits = 0x3F80u;  // bf16 1.0
   auto load_kv = [&](int kv) {
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
@@ -111,32 +116,40 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     for (int i = 0; i < VPT; ++i) {
       const int c = tid + 256 * i;
       const int r = c / (DT * 2), col = (c % (DT * 2)) * 8;
-      rv[i] = (c < VCH && kv + r < a.Nk && col < D) ? ld16(vbase + (long)(kv + r) * a.v_sn + col)
-                                                     : make_uint4(0, 0, 0, 0);
+      uint4 val = (c < VCH && kv + r < a.Nk && col < D) ? ld16(vbase + (long)(kv + r) * a.v_sn + col)
+                                                         : make_uint4(0, 0, 0, 0);
+      if (ones && col == (D & ~7)) {
+        // column D is the first element of the first all-padding 8-chunk when D % 16 == 8
+        val.x = (val.x & 0xffff0000u) | one_bits;
+      }
+      rv[i] = val;
     }
   };
-  auto store_kv = [&]() {
+  auto store_kv = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
       const int c = tid + 256 * i;
-      if (c < KCH) st16(&sK[(c / (KSTEPS * 4)) * KROW + (c % (KSTEPS * 4)) * 8], rk[i]);
+      if (c < KCH) st16(&sK[buf][(c / (KSTEPS * 4)) * KROW + (c % (KSTEPS * 4)) * 8], rk[i]);
     }
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = tid + 256 * i;
-      if (c < VCH) st16(&sV[(c / (DT * 2)) * VROW + (c % (DT * 2)) * 8], rv[i]);
+      if (c < VCH) st16(&sV[buf][(c / (DT * 2)) * VROW + (c % (DT * 2)) * 8], rv[i]);
     }
   };
   if (kv_end > 0) {
     load_kv(0);
-    store_kv();
+    store_kv(0);
   }
   __syncthreads();
 
-  for (int kv0 = 0; kv0 < kv_end; kv0 += KV_BLK) {
+  int buf = 0;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += KV_BLK, buf ^= 1) {
     const bool more = kv0 + KV_BLK < kv_end;
     if (more) load_kv(kv0 + KV_BLK);
-    const bool full = !a.causal && kv0 + KV_BLK <= a.Nk;  // no masking needed
+    const bool full = !a.causal && kv0 + KV_BLK <= a.Nk;
+    const bf16_t* cK = sK[buf];
+    const bf16_t* cV = sV[buf];
 
     // ---- S^T tiles: 4 key tiles x QT query tiles
     f32x4 st[QT][4];
@@ -146,7 +159,7 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       for (int qt = 0; qt < QT; ++qt) st[qt][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
-        const bf16x8 kf = __builtin_bit_cast(bf16x8, ld16(&sK[(16 * t + lq) * KROW + 32 * s + 8 * g]));
+        const bf16x8 kf = __builtin_bit_cast(bf16x8, ld16(&cK[(16 * t + lq) * KROW + 32 * s + 8 * g]));
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
           st[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][s], st[qt][t], 0, 0, 0);
@@ -154,7 +167,6 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     }
 
     // ---- online softmax (per query column = lane&15)
-    // scores stay raw; scale (> 0) is applied inside one fma before exp2: max commutes with it.
     bf16x8 pf[QT][2];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
@@ -178,17 +190,23 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
       const float alpha = exp2f(m_run[qt] - m_use);
       m_run[qt] = m_new;
-      float lsum = 0.f;
+      if (ones) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
-          st[qt][t][r] = p;
-          lsum += p;
-        }
+          for (int r = 0; r < 4; ++r) st[qt][t][r] = exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
+      } else {
+        float lsum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
+            st[qt][t][r] = p;
+            lsum += p;
+          }
+        l_run[qt] = l_run[qt] * alpha + lsum;
       }
-      l_run[qt] = l_run[qt] * alpha + lsum;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[qt][dt] *= alpha;
 #pragma unroll
@@ -209,7 +227,7 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int qq = (lane & 15) >> 2, pp = lane & 3;
-        const bf16_t* a0 = &sV[(32 * ks + 4 * g + qq) * VROW + 16 * dt + 4 * pp];
+        const bf16_t* a0 = &cV[(32 * ks + 4 * g + qq) * VROW + 16 * dt + 4 * pp];
         const bf16_t* a1 = a0 + 16 * VROW;
         s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0));
         s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
@@ -221,20 +239,30 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
           o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][ks], o[qt][dt], 0, 0, 0);
       }
     }
-    __syncthreads();          // every wave is done reading this tile
-    if (more) {
-      store_kv();             // the prefetched tile lands in LDS
-      __syncthreads();
-    }
+    // the prefetched tile goes to the other buffer (last read one iteration ago, fenced by
+    // the previous barrier); this barrier publishes it and retires reads of `buf`.
+    if (more) store_kv(buf ^ 1);
+    __syncthreads();
   }
 
-  // ---- epilogue: combine l across the 4 lane groups, normalise, store O[q][d]
+  // ---- epilogue: denominator (MFMA ones-column or lane sums), normalise, store O[q][d]
   bf16_t* obase = a.o + b * a.o_sb + h * a.o_sh;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
-    float l = l_run[qt];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    float l;
+    if (ones) {
+      // O^T row D lives in d-tile D/16, lane group (D%16)/4, register (D%4) = 0 (D % 8 == 0)
+      const int dtl = D >> 4;
+      float cand = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        if (dt == dtl) cand = o[qt][dt][0];
+      l = __shfl(cand, ((D & 15) >> 2) * 16 + lq, 64);
+    } else {
+      l = l_run[qt];
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+    }
     const float inv = l > 0.f ? 1.f / l : 0.f;
     if (qidx[qt] < a.Nq) {
 #pragma unroll

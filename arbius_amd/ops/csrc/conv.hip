@@ -38,7 +38,29 @@ struct ConvArgs {
   int kw, pad, stride, upsample;
   int ktiles, kt_per_split;
   int tiles_n, tiles_total;
+  int nsplit, m_fastest;
 };
+
+// 1-D grid of tiles_total * nsplit blocks -> (split, n-tile, m-tile), XCD-aware: consecutive
+// logical ids share an XCD (L2).  When the weights outweigh the activations (small-M deep
+// levels: a 1280x11520 conv weight is 29 MB) the m-tiles of one weight panel run together
+// so the panel is fetched from HBM once per XCD instead of once per m-tile; otherwise the
+// n-tiles of one activation panel do.
+__device__ __forceinline__ void tile_coords(const ConvArgs& p, int BN, int BM, int& sp, int& n0, int& m0) {
+  const int lin = xcd_remap(blockIdx.x, p.tiles_total * p.nsplit);
+  const int tiles_m = p.tiles_total / p.tiles_n;
+  if (p.m_fastest) {
+    const int rest = lin / tiles_m;
+    m0 = (lin % tiles_m) * BM;
+    n0 = (rest % p.tiles_n) * BN;
+    sp = rest / p.tiles_n;
+  } else {
+    const int rest = lin / p.tiles_n;
+    n0 = (lin % p.tiles_n) * BN;
+    m0 = (rest % tiles_m) * BM;
+    sp = rest / tiles_m;
+  }
+}
 
 template <int BN, int BM, int WN, int WM, int MINW, bool SPLIT>
 __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
@@ -54,10 +76,9 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   const int wn = wave / WM, wm = wave % WM;
   const int g = lane >> 4, l16 = lane & 15;
 
-  const int lin = xcd_remap(blockIdx.x, p.tiles_total);
-  const int n0 = (lin % p.tiles_n) * BN;
-  const int m0 = (lin / p.tiles_n) * BM;
-  const int kt0 = SPLIT ? blockIdx.y * p.kt_per_split : 0;
+  int split_idx, n0, m0;
+  tile_coords(p, BN, BM, split_idx, n0, m0);
+  const int kt0 = SPLIT ? split_idx * p.kt_per_split : 0;
   const int kt1 = SPLIT ? min(p.ktiles, kt0 + p.kt_per_split) : p.ktiles;
 
   // ---- per-thread staging geometry (rows fixed across the K loop)
@@ -158,7 +179,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
       if (n >= p.N) continue;
       float v0 = acc[a][b][0], v1 = acc[a][b][1], v2 = acc[a][b][2], v3 = acc[a][b][3];
       if (SPLIT) {
-        *reinterpret_cast<float4*>(p.ws + ((size_t)blockIdx.y * p.M + m) * p.N + n) = make_float4(v0, v1, v2, v3);
+        *reinterpret_cast<float4*>(p.ws + ((size_t)split_idx * p.M + m) * p.N + n) = make_float4(v0, v1, v2, v3);
         continue;
       }
       if (p.bias) {
@@ -214,10 +235,9 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
   const int g = lane >> 4, l16 = lane & 15;
-  const int lin = xcd_remap(blockIdx.x, p.tiles_total);
-  const int n0 = (lin % p.tiles_n) * BN;
-  const int m0 = (lin / p.tiles_n) * BM;
-  const int kt0 = SPLIT ? blockIdx.y * p.kt_per_split : 0;
+  int split_idx, n0, m0;
+  tile_coords(p, BN, BM, split_idx, n0, m0);
+  const int kt0 = SPLIT ? split_idx * p.kt_per_split : 0;
   const int kt1 = SPLIT ? min(p.ktiles, kt0 + p.kt_per_split) : p.ktiles;
   const int nk = kt1 - kt0;
 
@@ -330,7 +350,7 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
       if (n >= p.N) continue;
       float v0 = acc[a][b][0], v1 = acc[a][b][1], v2 = acc[a][b][2], v3 = acc[a][b][3];
       if (SPLIT) {
-        *reinterpret_cast<float4*>(p.ws + ((size_t)blockIdx.y * p.M + m) * p.N + n) = make_float4(v0, v1, v2, v3);
+        *reinterpret_cast<float4*>(p.ws + ((size_t)split_idx * p.M + m) * p.N + n) = make_float4(v0, v1, v2, v3);
         continue;
       }
       if (p.bias) {
@@ -502,9 +522,11 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
   ConvArgs p = a;
   p.tiles_n = (p.N + BN - 1) / BN;
   p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
+  p.nsplit = pl.split > 1 ? pl.split : 1;
+  p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;  // weight bytes vs unique activation bytes
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
-    dim3 grid(p.tiles_total, pl.split);
+    dim3 grid(p.tiles_total * pl.split);
     if (glds) launch_glds<BN, BM, WN, WM, NS, true>(p, grid, s);
     else conv_igemm_kernel<BN, BM, WN, WM, MINW, true><<<grid, 256, 0, s>>>(p);
     long work = (long)p.M * (p.N / 8);
