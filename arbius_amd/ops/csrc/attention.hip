@@ -43,7 +43,7 @@ struct AttnArgs {
   int causal;
 };
 
-template <int KSTEPS, int DT, int QT>
+template <int KSTEPS, int DT, int QT, bool ONES>
 __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   constexpr int KROW = KSTEPS * 32 + 8;    // K tile row (elements): 16 B pad
   constexpr int VROW = 16 * (DT | 1);      // V tile row: 16*(odd) -> tr-read conflict free
@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   const int wave = tid >> 6, lane = tid & 63;
   const int lq = lane & 15, g = lane >> 4;
   const int D = a.D;
-  const bool ones = (D & 15) != 0;  // spare zero-padded V column D carries the row sum
+  // ONES: D % 16 != 0 -> the spare zero-padded V column D carries the row sum
 
   const bf16_t* qbase = a.q + b * a.q_sb + h * a.q_sh;
   const bf16_t* kbase = a.k + b * a.k_sb + h * a.k_sh;
@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       const int r = c / (DT * 2), col = (c % (DT * 2)) * 8;
       uint4 val = (c < VCH && kv + r < a.Nk && col < D) ? ld16(vbase + (long)(kv + r) * a.v_sn + col)
                                                          : make_uint4(0, 0, 0, 0);
-      if (ones && col == (D & ~7)) {
+      if (ONES && col == (D & ~7)) {
         // column D is the first element of the first all-padding 8-chunk when D % 16 == 8
         val.x = (val.x & 0xffff0000u) | one_bits;
       }
@@ -186,29 +186,38 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
         mloc = fmaxf(mloc, fmaxf(fmaxf(st[qt][t][0], st[qt][t][1]), fmaxf(st[qt][t][2], st[qt][t][3])));
       mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float m_new = fmaxf(m_run[qt], mloc * a.scale_log2);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_run[qt] - m_use);
-      m_run[qt] = m_new;
-      if (ones) {
+      // lazy rescale (T13): keep the running max unless it grew by > 8 (log2 units), so
+      // p <= 2^8; the O/l rescale then runs only on the (rare) tiles where some lane needs it.
+      const float m_cand = mloc * a.scale_log2;
+      const bool need = m_cand > m_run[qt] + 8.f;
+      float alpha = 1.f;
+      if (need) {
+        alpha = (m_run[qt] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run[qt] - m_cand);
+        m_run[qt] = m_cand;
+      }
+      const float m_use = (m_run[qt] == -INFINITY) ? 0.f : m_run[qt];
+      if (ONES) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) st[qt][t][r] = exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
+          for (int r = 0; r < 4; ++r)
+            st[qt][t][r] = __builtin_amdgcn_exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
       } else {
         float lsum = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
+            const float p = __builtin_amdgcn_exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
             st[qt][t][r] = p;
             lsum += p;
           }
         l_run[qt] = l_run[qt] * alpha + lsum;
       }
+      if (__any(need)) {
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[qt][dt] *= alpha;
+        for (int dt = 0; dt < DT; ++dt) o[qt][dt] *= alpha;
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8 p;
@@ -250,7 +259,7 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
     float l;
-    if (ones) {
+    if (ONES) {
       // O^T row D lives in d-tile D/16, lane group (D%16)/4, register (D%4) = 0 (D % 8 == 0)
       const int dtl = D >> 4;
       float cand = 0.f;
@@ -284,7 +293,8 @@ static void launch_fa(const AttnArgs& a, hipStream_t s) {
   constexpr int QBLK = 4 * QT * 16;
   const int nqb = (a.Nq + QBLK - 1) / QBLK;
   dim3 grid(nqb * a.H * a.B);
-  flash_attn_fwd_kernel<KSTEPS, DT, QT><<<grid, 256, 0, s>>>(a);
+  if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true><<<grid, 256, 0, s>>>(a);
+  else flash_attn_fwd_kernel<KSTEPS, DT, QT, false><<<grid, 256, 0, s>>>(a);
 }
 
 ARB_API int arb_flash_attention(const void* q, const void* k, const void* v, void* o, const long* strides, int B,
