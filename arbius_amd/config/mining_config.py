@@ -80,6 +80,7 @@ class MI355XConfig(_Base):
     gpus: Optional[int] = None            # default: all visible
     dtype: Literal["bf16", "fp16"] = "bf16"
     models: List[str] = Field(default_factory=lambda: ["kandinsky2"])  # enabled model names
+    model_ids: Dict[str, str] = Field(default_factory=dict)  # template name -> on-chain model id
     weights_dir: Optional[str] = None     # safetensors; None = random-init (benchmark only)
     reference_hydration_quirks: bool = False  # mirror models.ts:185-194 quirks Q2/Q3
     job_lease_seconds: float = 900.0

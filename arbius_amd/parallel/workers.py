@@ -1,0 +1,232 @@
+"""One process per GPU: the node-level task-parallel pool.
+
+    dispatcher (asyncio control plane, no GPU)
+        |-- mp.Queue --> worker 0 (cuda:0)  \
+        |-- mp.Queue --> worker 1 (cuda:1)   >  torch.distributed group over RCCL/xGMI:
+        ...                                  |  rank 0 materialises the weights, one
+        |-- mp.Queue --> worker N-1          /  bucketed broadcast fills every HBM
+        <-- result queue --------------------
+
+* every worker keeps ALL enabled models resident (288 GB HBM per GPU);
+* a solve goes to an idle worker; N solves run concurrently, no per-step collectives;
+* a worker that dies (HIP fault, OOM, kill) is detected by the watchdog, its in-flight
+  task fails over to the caller's retry (another worker), and the worker is respawned
+  standalone (deterministic init / safetensors load instead of the broken group) -
+  elastic N -> N-1 -> N.
+On CPU the same code runs with the gloo backend (tests, world size 2).
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import logging
+import multiprocessing as mp
+import os
+import queue as pyqueue
+import socket
+import time
+import traceback
+from typing import Dict, List, Optional
+
+log = logging.getLogger("arbius.workers")
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker_main(rank: int, world: int, port: int, device_type: str, models: List[str], tiny: bool,
+                 in_q, out_q, group: bool, weight_seed: int):
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch
+    import torch.distributed as dist
+
+    from ..models.registry import build_pipeline
+    from ..node.models import Model
+    from ..node.solver import solve_task
+    from . import dist as D
+
+    try:
+        if device_type == "cuda":
+            torch.cuda.set_device(rank)
+            dev = torch.device("cuda", rank)
+        else:
+            dev = torch.device("cpu")
+        if group and world > 1:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            backend = "nccl" if device_type == "cuda" else "gloo"
+            kw = {"device_id": dev} if device_type == "cuda" else {}
+            dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        pipes = {}
+        bstats = {"bytes": 0, "seconds": 0.0}
+        for name in models:
+            pipe = build_pipeline(name, device=dev, tiny=tiny, weight_seed=weight_seed,
+                                  init=(not group) or rank == 0)
+            if group and world > 1:
+                st = D.broadcast_modules(pipe.modules().values())
+                bstats["bytes"] += st["bytes"]
+                bstats["seconds"] += st["seconds"]
+            pipes[name] = pipe
+        out_q.put(("ready", rank, bstats))
+        while True:
+            msg = in_q.get()
+            if msg is None:
+                break
+            jid, mname, kind, mid, taskid, inp = msg
+            try:
+                t0 = time.perf_counter()
+                sol = solve_task(Model(mid, mname, {}, True, [], kind), pipes[mname], inp)
+                sol.dag = None  # blocks are recomputed by the pinner; keep the message small
+                sol.timings["worker_s"] = time.perf_counter() - t0
+                out_q.put(("ok", jid, rank, sol))
+            except Exception:  # noqa: BLE001
+                out_q.put(("err", jid, rank, traceback.format_exc()))
+    finally:
+        if group and world > 1 and dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:  # noqa: BLE001
+                pass
+
+
+class MultiGPUSolverPool:
+    def __init__(self, n: int, models: List[str], device_type: str = "cuda", tiny: bool = False,
+                 weight_seed: int = 0, start_timeout: float = 1800.0):
+        self.n = n
+        self.models = models
+        self.device_type = device_type
+        self.tiny = tiny
+        self.weight_seed = weight_seed
+        self.ctx = mp.get_context("spawn")
+        self.out_q = self.ctx.Queue()
+        self.in_qs = [self.ctx.Queue() for _ in range(n)]
+        self.procs: List[Optional[mp.Process]] = [None] * n
+        self.busy: Dict[int, int] = {}           # rank -> job id
+        self.idle: List[int] = []
+        self.futures: Dict[int, asyncio.Future] = {}
+        self._ids = itertools.count(1)
+        self.broadcast_stats = {}
+        self.restarts = 0
+        port = _free_port()
+        for r in range(n):
+            self._spawn(r, port, group=True)
+        ready = 0
+        t0 = time.time()
+        while ready < n:
+            if time.time() - t0 > start_timeout:
+                raise TimeoutError("GPU workers did not start")
+            try:
+                kind, rank, payload = self.out_q.get(timeout=1.0)
+            except pyqueue.Empty:
+                for r, p in enumerate(self.procs):
+                    if p is not None and not p.is_alive():
+                        raise RuntimeError(f"GPU worker {r} died during start (exit {p.exitcode})")
+                continue
+            if kind == "ready":
+                ready += 1
+                self.idle.append(rank)
+                self.broadcast_stats[rank] = payload
+        self.idle.sort()
+        self._pump_task = None
+
+    @property
+    def capacity(self) -> int:
+        return sum(1 for p in self.procs if p is not None and p.is_alive())
+
+    def _spawn(self, rank, port, group):
+        p = self.ctx.Process(target=_worker_main, daemon=True,
+                             args=(rank, self.n, port, self.device_type, self.models, self.tiny,
+                                   self.in_qs[rank], self.out_q, group, self.weight_seed))
+        p.start()
+        self.procs[rank] = p
+
+    def _ensure_pump(self):
+        if self._pump_task is None or self._pump_task.done():
+            self._pump_task = asyncio.ensure_future(self._pump())
+
+    def _handle(self, msg):
+        kind = msg[0]
+        if kind == "ready":
+            if msg[1] not in self.idle:
+                self.idle.append(msg[1])
+            return
+        _, jid, rank, payload = msg
+        self.busy.pop(rank, None)
+        if rank not in self.idle:
+            self.idle.append(rank)
+        fut = self.futures.pop(jid, None)
+        if fut is None or fut.done():
+            return
+        if kind == "ok":
+            fut.set_result(payload)
+        else:
+            fut.set_exception(RuntimeError(f"worker {rank} failed:\n{payload}"))
+
+    def _drain_nowait(self):
+        while True:
+            try:
+                self._handle(self.out_q.get_nowait())
+            except pyqueue.Empty:
+                return
+
+    async def _pump(self):
+        loop = asyncio.get_running_loop()
+        while self.futures:
+            try:
+                msg = await loop.run_in_executor(None, self.out_q.get, True, 0.5)
+            except pyqueue.Empty:
+                self._watchdog()
+                continue
+            self._handle(msg)
+
+    def _watchdog(self):
+        for r, p in enumerate(self.procs):
+            if p is not None and not p.is_alive():
+                log.error("GPU worker %d died (exit %s): failing its task over, respawning", r, p.exitcode)
+                jid = self.busy.pop(r, None)
+                if jid is not None and jid in self.futures:
+                    self.futures.pop(jid).set_exception(RuntimeError(f"worker {r} died"))
+                if r in self.idle:
+                    self.idle.remove(r)
+                self.restarts += 1
+                # a SIGKILLed reader can die holding its queue's lock: give the new process a fresh one
+                self.in_qs[r] = self.ctx.Queue()
+                self._spawn(r, _free_port(), group=False)   # standalone: deterministic init / load
+
+    async def solve(self, model, taskid, inp):
+        self._watchdog()
+        self._drain_nowait()
+        while not self.idle:
+            await asyncio.sleep(0.01)
+            self._watchdog()
+            self._drain_nowait()
+        rank = self.idle.pop(0)
+        jid = next(self._ids)
+        fut = asyncio.get_running_loop().create_future()
+        self.futures[jid] = fut
+        self.busy[rank] = jid
+        self.in_qs[rank].put((jid, model.name, model.kind, model.id, taskid, dict(inp)))
+        self._ensure_pump()
+        return await fut
+
+    def kill_worker(self, rank: int):
+        """Fault injection (tests): hard-kill one worker process."""
+        p = self.procs[rank]
+        if p is not None and p.is_alive():
+            p.kill()
+
+    async def close(self):
+        for q in self.in_qs:
+            try:
+                q.put(None)
+            except Exception:  # noqa: BLE001
+                pass
+        for p in self.procs:
+            if p is not None:
+                p.join(timeout=10)
+                if p.is_alive():
+                    p.kill()

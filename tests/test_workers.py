@@ -1,0 +1,40 @@
+"""One-process-per-device worker pool on CPU (gloo, world size 2): weight
+broadcast from rank 0, concurrent solves, cross-worker determinism, and
+elastic recovery after a worker is killed."""
+import asyncio
+
+import pytest
+
+from arbius_amd.node.models import Model, load_template
+from arbius_amd.node.pool import LocalSolverPool
+from arbius_amd.parallel.workers import MultiGPUSolverPool
+
+MODEL = Model("0x" + "ab" * 32, "anythingv3", load_template("anythingv3"), True, [], "image")
+INP = {"prompt": "a cat", "negative_prompt": "n", "width": 128, "height": 128, "num_inference_steps": 2,
+       "guidance_scale": 7.5, "scheduler": "DDIM", "seed": 1234}
+
+
+@pytest.mark.timeout(600)
+def test_two_workers_broadcast_determinism_and_failover():
+    ref = LocalSolverPool("cpu", tiny=True).solve_sync(MODEL, "t", INP)
+
+    async def go():
+        pool = MultiGPUSolverPool(2, ["anythingv3"], device_type="cpu", tiny=True)
+        try:
+            assert pool.capacity == 2
+            # rank 1 received its weights by broadcast (not initialised itself)
+            assert pool.broadcast_stats[1]["bytes"] > 0
+            a, b = await asyncio.gather(pool.solve(MODEL, "t1", INP), pool.solve(MODEL, "t2", INP))
+            assert a.cid == b.cid == ref.cid  # same bytes on every worker
+            pool.kill_worker(0)
+            pool.kill_worker(1)
+            with pytest.raises(RuntimeError):
+                await asyncio.wait_for(pool.solve(MODEL, "t3", INP), 300)
+            # respawned workers come back standalone and produce the same CID
+            c = await asyncio.wait_for(pool.solve(MODEL, "t4", INP), 300)
+            assert c.cid == ref.cid
+            assert pool.restarts >= 2
+        finally:
+            await pool.close()
+
+    asyncio.run(go())
