@@ -1,0 +1,99 @@
+"""Kandinsky 2.1 diffusion prior: text -> CLIP image embedding
+(SURVEY.md §2.6(b) [EXT]; DALL-E 2 style causal transformer).
+
+Token sequence (one per CFG branch):
+    [ CLIP text states (real tokens only) | pooled text | time | x_t | query ]
+with learned positional embeddings indexed by the ORIGINAL positions (text
+positions 0..76, then 77..80), causal attention, final LN and an output
+projection of the query token -> predicted x_0 in the normalised CLIP space.
+
+Padding keys of the reference's mask are removed from the sequence instead
+of masked: with causal attention and the pads masked as keys, the real
+tokens' outputs are identical, and the last token is the only one read.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .layers import LayerNorm, Linear, timestep_embedding
+
+
+@dataclass
+class PriorConfig:
+    width: int = 2048
+    layers: int = 20
+    heads: int = 32
+    clip_dim: int = 768
+    text_ctx: int = 77
+
+    @staticmethod
+    def kandinsky21():
+        return PriorConfig()
+
+    @staticmethod
+    def tiny():
+        return PriorConfig(width=64, layers=2, heads=2, clip_dim=32)
+
+
+class PriorBlock(nn.Module):
+    def __init__(self, cfg: PriorConfig):
+        super().__init__()
+        w = cfg.width
+        self.heads = cfg.heads
+        self.ln1 = LayerNorm(w)
+        self.qkv = Linear(w, 3 * w)
+        self.out = Linear(w, w)
+        self.ln2 = LayerNorm(w)
+        self.fc1 = Linear(w, 4 * w)
+        self.fc2 = Linear(4 * w, w)
+
+    def forward(self, x):
+        B, N, C = x.shape
+        H = self.heads
+        qkv = self.qkv(self.ln1(x)).view(B, N, 3, H, C // H)
+        o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
+        x = self.out(o.reshape(B, N, C), residual=x)
+        return self.fc2(torch.nn.functional.gelu(self.fc1(self.ln2(x))), residual=x)
+
+
+class PriorTransformer(nn.Module):
+    def __init__(self, cfg: PriorConfig = None):
+        super().__init__()
+        cfg = cfg or PriorConfig()
+        self.cfg = cfg
+        w, d = cfg.width, cfg.clip_dim
+        self.text_enc_proj = Linear(d, w)
+        self.text_emb_proj = Linear(d, w)
+        self.img_proj = Linear(d, w)
+        self.time1 = Linear(w, w)
+        self.time2 = Linear(w, w)
+        self.pos = nn.Parameter(torch.zeros(cfg.text_ctx + 4, w), requires_grad=False)
+        self.query = nn.Parameter(torch.zeros(w), requires_grad=False)
+        self.blocks = nn.ModuleList([PriorBlock(cfg) for _ in range(cfg.layers)])
+        self.final_ln = LayerNorm(w)
+        self.out_proj = Linear(w, d)
+        # CLIP image-embedding normalisation statistics (checkpoint buffers)
+        self.clip_mean = nn.Parameter(torch.zeros(d), requires_grad=False)
+        self.clip_std = nn.Parameter(torch.ones(d), requires_grad=False)
+
+    def reset(self, gen):
+        self.pos.data.normal_(0, 0.01, generator=gen)
+        self.query.data.normal_(0, 0.01, generator=gen)
+
+    def forward(self, x_t, t, text_states, text_pooled, n: int):
+        """x_t [1,d] (normalised), t scalar, text_states [1,77,d], text_pooled [1,d], n real tokens."""
+        w = self.cfg.width
+        tt = torch.tensor([float(t)], device=x_t.device)
+        temb = self.time2(ops.silu(self.time1(timestep_embedding(tt, w).to(x_t.dtype))))
+        seq = torch.cat([self.text_enc_proj(text_states[:, :n]), self.text_emb_proj(text_pooled)[:, None],
+                         temb[:, None], self.img_proj(x_t)[:, None], self.query.to(x_t.dtype)[None, None]], dim=1)
+        ctx = self.cfg.text_ctx
+        pos = torch.cat([self.pos[:n], self.pos[ctx:ctx + 4]], dim=0)
+        h = seq + pos[None].to(seq.dtype)
+        for blk in self.blocks:
+            h = blk(h)
+        return self.out_proj(self.final_ln(h[:, -1:]))[:, 0]

@@ -250,30 +250,68 @@ class PNDM(Scheduler):
         return self._prev(x, t, tp, e)
 
 
-class DDPMAncestral(Scheduler):
-    """Plain ancestral DDPM ``p_sample`` over respaced timesteps (Kandinsky2 p_sampler)."""
+def space_timesteps(n_train: int, steps: int) -> List[int]:
+    """Evenly strided subset of the training timesteps (guided-diffusion
+    ``space_timesteps(n, "K")`` with one section): round(i * (n-1)/(K-1))."""
+    if steps == 1:
+        return [0]
+    stride = (n_train - 1) / (steps - 1)
+    return sorted({int(round(i * stride)) for i in range(steps)})
+
+
+class GaussianDiffusion(Scheduler):
+    """Ancestral ``p_sample`` over a respaced DDPM (Kandinsky2 ``p_sampler``,
+    ``docs/src/pages/register-model.mdx:140-168``).
+
+    * ``predict``: "eps" (decoder UNet) or "x0" (diffusion prior);
+    * ``learned_var``: the model's extra channels are the learned-range
+      interpolation between log(beta_t) and the clipped posterior log-variance
+      (improved-DDPM); otherwise the fixed-small posterior variance;
+    * ``clamp``: pred_x0 clamp (Kandinsky decodes with clamp(-2, 2)).
+    The respaced chain recomputes betas from the kept alphas_cumprod.
+    ``step(out, i, x, generator, var=v)`` - ``v`` in [-1, 1] is the var head."""
     name = "p_sampler"
     needs_noise = True
 
-    def __init__(self, steps, n_train=1000, schedule="linear", beta_start=0.0001, beta_end=0.02):
-        ac = sd_alphas_cumprod(n_train, beta_start, beta_end, schedule)
-        super().__init__(steps, n_train, ac)
-        use = np.linspace(0, n_train - 1, steps).round().astype(np.int64)
+    def __init__(self, steps, n_train=1000, schedule="linear", beta_start=0.0001, beta_end=0.02,
+                 predict="eps", learned_var=True, clamp=None):
+        full = sd_alphas_cumprod(n_train, beta_start, beta_end, schedule)
+        use = space_timesteps(n_train, steps)
+        ac = full[use]
+        super().__init__(len(use), n_train, ac)
+        ac_prev = np.concatenate([[1.0], ac[:-1]])
+        self.betas = 1.0 - ac / ac_prev
+        pv = self.betas * (1.0 - ac_prev) / (1.0 - ac)
+        self.post_logvar = np.log(np.concatenate([[pv[1] if len(pv) > 1 else self.betas[0]], pv[1:]]))
+        self.ac_prev = ac_prev
+        self.use = use
         self.timesteps = [int(v) for v in use[::-1]]
+        self.predict, self.learned_var, self.clamp = predict, learned_var, clamp
 
-    def step(self, eps, i, x, generator=None):
-        t = self.timesteps[i]
-        tp = self.timesteps[i + 1] if i + 1 < len(self.timesteps) else -1
-        a_t = float(self.ac[t])
-        a_p = float(self.ac[tp]) if tp >= 0 else 1.0
-        beta = 1 - a_t / a_p
-        x0 = (x - math.sqrt(1 - a_t) * eps) / math.sqrt(a_t)
-        x0 = x0.clamp(-1, 1) if getattr(self, "clip", False) else x0
-        mean = (math.sqrt(a_p) * beta / (1 - a_t)) * x0 + (math.sqrt(1 - beta) * (1 - a_p) / (1 - a_t)) * x
-        if tp < 0:
+    def pred_x0(self, out, j, x):
+        a = float(self.ac[j])
+        if self.predict == "x0":
+            x0 = out
+        else:
+            x0 = math.sqrt(1.0 / a) * x - math.sqrt(1.0 / a - 1.0) * out
+        if self.clamp is not None:
+            x0 = x0.clamp(-self.clamp, self.clamp)
+        return x0
+
+    def step(self, out, i, x, generator=None, var=None):
+        j = len(self.use) - 1 - i              # respaced index, counting down
+        a, ap, b = float(self.ac[j]), float(self.ac_prev[j]), float(self.betas[j])
+        x0 = self.pred_x0(out.float(), j, x.float())
+        mean = (b * math.sqrt(ap) / (1 - a)) * x0 + ((1 - ap) * math.sqrt(1 - b) / (1 - a)) * x.float()
+        if j == 0:
             return mean
-        var = beta * (1 - a_p) / (1 - a_t)
-        return mean + math.sqrt(max(var, 1e-20)) * _randn_like(x, generator)
+        if self.learned_var and var is not None:
+            frac = (var.float() + 1.0) * 0.5
+            logv = frac * math.log(b) + (1.0 - frac) * float(self.post_logvar[j])
+            std = torch.exp(0.5 * logv)
+        else:
+            std = math.exp(0.5 * float(self.post_logvar[j]))
+        return mean + std * _randn_like(x, generator)
 
 
 SCHEDULERS = {
@@ -283,7 +321,7 @@ SCHEDULERS = {
     "DPMSolverMultistep": DPMSolverMultistep,
     "PNDM": PNDM,
     "KLMS": LMSDiscrete,
-    "p_sampler": DDPMAncestral,
+    "p_sampler": GaussianDiffusion,
 }
 
 

@@ -1,0 +1,120 @@
+"""XLM-RoBERTa text tower + M-CLIP pooling head (the Kandinsky 2.1 multilingual
+text encoder, SURVEY.md §2.6(b) [EXT]).
+
+Post-LN BERT layout: embeddings (word + position[offset 2] + type) -> LN ->
+L x {x = LN(x + Attn(x)); x = LN(x + FFN_gelu(x))}.  M-CLIP returns the full
+token states ``[77, 1024]`` (decoder context) and a masked-mean pooled vector
+projected 1024 -> 768.
+
+Padding: instead of an additive key mask, each sequence runs with its keys
+and values sliced to its real length (queries at pad positions still attend
+to the real tokens, exactly as a masked softmax does), so the shared flash
+kernel needs no mask support and pad keys cost nothing.
+"""
+from __future__ import annotations
+
+import hashlib
+import re
+from dataclasses import dataclass
+from pathlib import Path
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .layers import Embedding, LayerNorm, Linear
+
+
+@dataclass
+class XLMRConfig:
+    vocab: int = 250002
+    width: int = 1024
+    layers: int = 24
+    heads: int = 16
+    mlp: int = 4096
+    max_pos: int = 514
+    max_len: int = 77
+    proj_dim: int = 768           # M-CLIP LinearTransformation
+    eps: float = 1e-5
+
+    @staticmethod
+    def large():
+        return XLMRConfig()
+
+    @staticmethod
+    def tiny():
+        return XLMRConfig(vocab=1000, width=32, layers=2, heads=2, mlp=64, max_pos=100, proj_dim=32)
+
+
+class XLMRTokenizer:
+    """sentencepiece tokenizer when ``sentencepiece.bpe.model`` is available
+    locally; otherwise a deterministic hashed-word fallback with the same id
+    layout (<s>=0, <pad>=1, </s>=2, 77 positions)."""
+    BOS, PAD, EOS = 0, 1, 2
+    _WORD = re.compile(r"\w+|[^\w\s]+")
+
+    def __init__(self, vocab: int, max_len: int = 77, model_dir: Optional[str] = None):
+        self.vocab, self.max_len = vocab, max_len
+        self._sp = None
+        if model_dir and (Path(model_dir) / "sentencepiece.bpe.model").exists():
+            import sentencepiece as spm
+            self._sp = spm.SentencePieceProcessor(model_file=str(Path(model_dir) / "sentencepiece.bpe.model"))
+
+    def __call__(self, text: str) -> Tuple[List[int], int]:
+        if self._sp is not None:
+            ids = [i + 1 for i in self._sp.encode(text)]   # fairseq offset
+        else:
+            ids = []
+            for w in self._WORD.findall(text.lower()):
+                h = int.from_bytes(hashlib.blake2b(w.encode(), digest_size=8).digest(), "little")
+                ids.append(4 + h % (self.vocab - 4))
+        ids = [self.BOS] + ids[: self.max_len - 2] + [self.EOS]
+        n = len(ids)
+        return ids + [self.PAD] * (self.max_len - n), n
+
+
+class XLMRLayer(nn.Module):
+    def __init__(self, cfg: XLMRConfig):
+        super().__init__()
+        self.heads = cfg.heads
+        self.qkv = Linear(cfg.width, 3 * cfg.width)
+        self.out = Linear(cfg.width, cfg.width)
+        self.ln1 = LayerNorm(cfg.width, cfg.eps)
+        self.fc1 = Linear(cfg.width, cfg.mlp)
+        self.fc2 = Linear(cfg.mlp, cfg.width)
+        self.ln2 = LayerNorm(cfg.width, cfg.eps)
+
+    def forward(self, x, n: int):
+        B, N, C = x.shape
+        H = self.heads
+        qkv = self.qkv(x).view(B, N, 3, H, C // H)
+        o = ops.attention(qkv[:, :, 0], qkv[:, :n, 1], qkv[:, :n, 2])
+        x = self.ln1(self.out(o.reshape(B, N, C), residual=x))
+        h = torch.nn.functional.gelu(self.fc1(x))
+        return self.ln2(self.fc2(h, residual=x))
+
+
+class MCLIPText(nn.Module):
+    def __init__(self, cfg: XLMRConfig = None):
+        super().__init__()
+        cfg = cfg or XLMRConfig()
+        self.cfg = cfg
+        self.tok = Embedding(cfg.vocab, cfg.width)
+        self.pos = Embedding(cfg.max_pos, cfg.width)
+        self.tok_type = Embedding(1, cfg.width)
+        self.ln = LayerNorm(cfg.width, cfg.eps)
+        self.layers = nn.ModuleList([XLMRLayer(cfg) for _ in range(cfg.layers)])
+        self.proj = Linear(cfg.width, cfg.proj_dim)
+
+    def forward(self, ids: torch.Tensor, n: int):
+        """One sequence: ids [1, 77], n = real length -> (full [1,77,W], pooled [1,proj])."""
+        L = ids.shape[1]
+        pos = torch.arange(L, device=ids.device)
+        pos = torch.where(pos < n, pos + 2, torch.full_like(pos, 1))   # pad positions use padding_idx
+        x = self.tok(ids) + self.pos(pos)[None] + self.tok_type.weight[0]
+        x = self.ln(x)
+        for layer in self.layers:
+            x = layer(x, n)
+        pooled = x[:, :n].float().mean(dim=1).to(x.dtype)
+        return x, self.proj(pooled)

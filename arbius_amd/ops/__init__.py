@@ -90,6 +90,22 @@ def group_norm(x, gamma, beta, groups, eps, silu=False):
     return ref.group_norm_nhwc(x, gamma, beta, groups, eps, silu)
 
 
+def spatial_norm(x, yb, gamma, beta, groups, eps, silu=False):
+    """MoVQ SpatialNorm: GN(x) * y + b with ``yb`` = [y | b] [B, mh, mw, 2C] at a lower
+    (nearest-upsampled) resolution; one fused HIP pass after the GN statistics."""
+    if _hip(x):
+        return _lib.group_norm_mod_nhwc(x, gamma, beta, groups, eps, silu, yb, 0.0)
+    return ref.group_norm_mod_nhwc(x, gamma, beta, groups, eps, silu, yb, 0.0)
+
+
+def scale_shift_norm(x, ss, gamma, beta, groups, eps, silu=True):
+    """GLIDE ResBlock norm: GN(x) * (1 + scale) + shift (+ SiLU), ``ss`` = [scale | shift] [B, 2C]."""
+    mod = ss.reshape(ss.shape[0], 1, 1, ss.shape[-1])
+    if _hip(x):
+        return _lib.group_norm_mod_nhwc(x, gamma, beta, groups, eps, silu, mod, 1.0)
+    return ref.group_norm_mod_nhwc(x, gamma, beta, groups, eps, silu, mod, 1.0)
+
+
 def layer_norm(x, gamma, beta, eps):
     if _hip(x):
         return _lib.layer_norm(x, gamma, beta, eps)

@@ -24,6 +24,8 @@ c_void_p, c_int, c_long, c_float, c_size_t = (ctypes.c_void_p, ctypes.c_int, cty
 _SIGS = {
     "arb_group_norm_workspace": (c_size_t, [c_int, c_int, c_int, c_int]),
     "arb_group_norm_nhwc": (c_int, [c_void_p] * 5 + [c_int] * 4 + [c_float, c_int, c_void_p]),
+    "arb_group_norm_mod_nhwc": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_float, c_int, c_int, c_int, c_float,
+                                                                        c_void_p]),
     "arb_layer_norm": (c_int, [c_void_p] * 4 + [c_int, c_int, c_float, c_void_p]),
     "arb_flash_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_int, c_void_p]),
     "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
@@ -114,6 +116,25 @@ def group_norm_nhwc(x, gamma, beta, groups, eps, silu):
     y = torch.empty_like(x)
     _check(_fn("arb_group_norm_nhwc")(_p(x), _p(y), _p(gamma), _p(beta), _p(ws), B, HW, C, groups,
                                       float(eps), int(bool(silu)), _stream()), "group_norm")
+    return y
+
+
+def group_norm_mod_nhwc(x, gamma, beta, groups, eps, silu, mod, one_plus):
+    """GroupNorm whose output is modulated by ``mod`` [B, mh, mw, 2C] (nearest-upsampled):
+    out = GN(x) * (mod[..., :C] + one_plus) + mod[..., C:]  (+ SiLU)."""
+    _bf16(x, gamma, beta, mod)
+    x = x.contiguous()
+    mod = mod.contiguous()
+    B, H, W, C = x.shape
+    mh, mw = mod.shape[1], mod.shape[2]
+    if C % 8 or C // 8 > 512 or C % groups or groups > 256 or mod.shape[-1] != 2 * C or H % mh or W % mw:
+        raise ValueError(f"group_norm_mod: unsupported x={tuple(x.shape)} mod={tuple(mod.shape)} G={groups}")
+    ws_bytes = _fn("arb_group_norm_workspace")(B, H * W, C, groups)
+    ws = torch.empty(max(16, ws_bytes), dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(x)
+    _check(_fn("arb_group_norm_mod_nhwc")(_p(x), _p(y), _p(gamma), _p(beta), _p(ws), _p(mod), B, H, W, C, groups,
+                                          float(eps), int(bool(silu)), mh, mw, float(one_plus), _stream()),
+           "group_norm_mod")
     return y
 
 

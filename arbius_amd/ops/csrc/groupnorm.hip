@@ -153,12 +153,18 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const Stat* __restrict
   }
 }
 
-template <int VPT>
+// MOD: per-pixel modulation after the affine GN, read from a [B, mh, mw, 2C] map
+// at (nearest-)lower resolution:  out = gn * (y + one_plus) + b   (y = channels
+// [0,C), b = [C,2C)).  SpatialNorm of the MoVQ decoder (mh x mw = latent grid,
+// computed once per layer at latent resolution) and the scale-shift norm of the
+// GLIDE ResBlock (mh = mw = 1, one_plus = 1) both run as this one pass.
+template <int VPT, bool MOD>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                        const float2* __restrict__ stats,
                                                        const bf16_t* __restrict__ gamma,
                                                        const bf16_t* __restrict__ beta, int HW, int C, int G,
-                                                       int silu) {
+                                                       int silu, const bf16_t* __restrict__ mod, int W, int H,
+                                                       int mh, int mw, float one_plus) {
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   __shared__ float2 sh_st[256];
   if (t < G) sh_st[t] = stats[b * G + t];
@@ -198,10 +204,23 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict_
       if (r >= HW) continue;
       float f[8];
       unpack8(raw[i], f);
+      if constexpr (MOD) {
+        const int my = (r / W) * mh / H, mx = (r % W) * mw / W;
+        const bf16_t* mp = mod + (((size_t)b * mh + my) * mw + mx) * (2 * C) + vv * 8;
+        float my8[8], mb8[8];
+        unpack8(ld16(mp), my8);
+        unpack8(ld16(mp + C), mb8);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float o = f[e] * sc[e] + sf[e];
-        f[e] = silu ? silu_f(o) : o;
+        for (int e = 0; e < 8; ++e) {
+          const float o = (f[e] * sc[e] + sf[e]) * (my8[e] + one_plus) + mb8[e];
+          f[e] = silu ? silu_f(o) : o;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float o = f[e] * sc[e] + sf[e];
+          f[e] = silu ? silu_f(o) : o;
+        }
       }
       st16(y + off + (size_t)r * C, pack8(f));
     }
@@ -221,24 +240,43 @@ ARB_API size_t arb_group_norm_workspace(int B, int HW, int C, int G) {
   return ((part + 255) / 256) * 256 + (size_t)B * G * sizeof(float2);
 }
 
-ARB_API int arb_group_norm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* workspace, int B,
-                                int HW, int C, int G, float eps, int silu, hipStream_t stream) {
+static int gn_run(const void* x, void* y, const void* gamma, const void* beta, void* workspace, int B, int HW,
+                  int C, int G, float eps, int silu, const void* mod, int H, int W, int mh, int mw, float one_plus,
+                  hipStream_t stream) {
   if (C % 8 != 0 || C / 8 > 512 || C % G != 0 || G > 256) return -1;
   const int chunks = gn_chunks(HW, C);
   Stat* part = (Stat*)workspace;
   const size_t part_bytes = ((size_t)B * chunks * G * sizeof(Stat) + 255) / 256 * 256;
   float2* stats = (float2*)((char*)workspace + part_bytes);
   dim3 g1(chunks, B);
-  if (C / 8 > 256)
+  const bool wide = C / 8 > 256;
+  if (wide)
     gn_stats_kernel<2><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
   else
     gn_stats_kernel<1><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
   gn_finalize_kernel<<<dim3(G, B), 256, 0, stream>>>(part, stats, chunks, G, eps);
-  if (C / 8 > 256)
-    gn_apply_kernel<2><<<g1, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, stats, (const bf16_t*)gamma,
-                                               (const bf16_t*)beta, HW, C, G, silu);
-  else
-    gn_apply_kernel<1><<<g1, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, stats, (const bf16_t*)gamma,
-                                               (const bf16_t*)beta, HW, C, G, silu);
+#define GN_APPLY(VPT, MOD)                                                                                    \
+  gn_apply_kernel<VPT, MOD><<<g1, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, stats, (const bf16_t*)gamma, \
+                                                    (const bf16_t*)beta, HW, C, G, silu, (const bf16_t*)mod, W, H, \
+                                                    mh, mw, one_plus)
+  if (mod) {
+    if (wide) GN_APPLY(2, true); else GN_APPLY(1, true);
+  } else {
+    if (wide) GN_APPLY(2, false); else GN_APPLY(1, false);
+  }
+#undef GN_APPLY
   return (int)hipGetLastError();
+}
+
+ARB_API int arb_group_norm_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* workspace, int B,
+                                int HW, int C, int G, float eps, int silu, hipStream_t stream) {
+  return gn_run(x, y, gamma, beta, workspace, B, HW, C, G, eps, silu, nullptr, 1, HW, 1, 1, 0.f, stream);
+}
+
+// x [B, H, W, C]; mod [B, mh, mw, 2C] with H % mh == 0 and W % mw == 0.
+ARB_API int arb_group_norm_mod_nhwc(const void* x, void* y, const void* gamma, const void* beta, void* workspace,
+                                    const void* mod, int B, int H, int W, int C, int G, float eps, int silu, int mh,
+                                    int mw, float one_plus, hipStream_t stream) {
+  if (mh <= 0 || mw <= 0 || H % mh != 0 || W % mw != 0) return -1;
+  return gn_run(x, y, gamma, beta, workspace, B, H * W, C, G, eps, silu, mod, H, W, mh, mw, one_plus, stream);
 }

@@ -44,6 +44,22 @@ def group_norm_nhwc(x, gamma, beta, groups, eps, silu=False, residual=None):
     return y.to(x.dtype)
 
 
+def group_norm_mod_nhwc(x, gamma, beta, groups, eps, silu, mod, one_plus):
+    """GN(x) * (mod[..., :C] + one_plus) + mod[..., C:] with ``mod`` [B, mh, mw, 2C]
+    nearest-upsampled to x's grid (+ SiLU)."""
+    B, H, W, C = x.shape
+    xf = x.float().reshape(B, -1, groups, C // groups)
+    mean = xf.mean(dim=(1, 3), keepdim=True)
+    var = xf.var(dim=(1, 3), unbiased=False, keepdim=True)
+    y = ((xf - mean) * torch.rsqrt(var + eps)).reshape(x.shape) * gamma.float() + beta.float()
+    m = mod.float()
+    m = m.repeat_interleave(H // m.shape[1], dim=1).repeat_interleave(W // m.shape[2], dim=2)
+    y = y * (m[..., :C] + one_plus) + m[..., C:]
+    if silu:
+        y = F.silu(y)
+    return y.to(x.dtype)
+
+
 def layer_norm(x, gamma, beta, eps):
     return F.layer_norm(x.float(), (x.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)
 

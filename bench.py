@@ -33,8 +33,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--res", type=int, default=512)
-    ap.add_argument("--denoise-steps", type=int, default=50)
+    ap.add_argument("--model", default="anythingv3", choices=["anythingv3", "kandinsky2"],
+                    help="anythingv3 = BASELINE headline config; kandinsky2 = BASELINE config #3")
+    ap.add_argument("--res", type=int, default=None, help="default 512 (anythingv3) / 768 (kandinsky2)")
+    ap.add_argument("--denoise-steps", type=int, default=None, help="default 50 / 100")
     ap.add_argument("--scheduler", default="DPMSolverMultistep")
     ap.add_argument("--guidance", type=float, default=12.0)
     ap.add_argument("--reference-ops", action="store_true", help="A/B: PyTorch ops instead of HIP kernels")
@@ -42,9 +44,12 @@ def main():
     ap.add_argument("--tiny", action="store_true", help="tiny config (CPU plumbing check only)")
     ap.add_argument("--device", default=None)
     args = ap.parse_args()
+    k2 = args.model == "kandinsky2"
+    args.res = args.res or (768 if k2 else 512)
+    args.denoise_steps = args.denoise_steps or (100 if k2 else 50)
 
     from arbius_amd import ops
-    from arbius_amd.models.sd15 import SD15Config, SD15Pipeline
+    from arbius_amd.models.registry import build_pipeline
     from arbius_amd.node.solver import solve_image
     from arbius_amd.parallel import dist as D
     from arbius_amd.utils.protocol import generate_commitment, taskid2seed
@@ -56,9 +61,9 @@ def main():
     rank, local, world, dev = D.init(device_type=dev_type)
     n = world
 
-    cfg = SD15Config.tiny() if args.tiny else SD15Config()
     t_init = time.perf_counter()
-    pipe = SD15Pipeline(cfg, device=dev, init=(rank == 0), use_graphs=(dev.type == "cuda" and not args.no_graphs))
+    pipe = build_pipeline(args.model, device=dev, tiny=args.tiny, init=(rank == 0),
+                          use_graphs=(dev.type == "cuda" and not args.no_graphs))
     bstats = D.broadcast_modules(pipe.modules().values())
     t_init = time.perf_counter() - t_init
 
@@ -67,6 +72,15 @@ def main():
 
     def one_task(i):
         taskid = "0x" + keccak256(f"bench-task-{rank}-{i}".encode()).hex()
+        if k2:   # templates/kandinsky2.json inputs; hidden defaults 100 steps, guidance 4, prior 5 steps
+            pipe.cfg.num_steps = args.denoise_steps
+            inp = {"prompt": f"a red cat sitting on a castle wall, oil painting, task {i}",
+                   "width": args.res, "height": args.res, "seed": taskid2seed(taskid)}
+            t0 = time.perf_counter()
+            sol = pipe.solve(inp)
+            generate_commitment(wallet, taskid, sol.cid)
+            lat.append(time.perf_counter() - t0)
+            return sol
         inp = {
             "prompt": f"a detailed anime illustration of a castle on a hill, task {i}",
             "negative_prompt": "lowres, bad anatomy, bad hands, text, error",
@@ -114,14 +128,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
-            "data": "synthetic prompts, random-init weights (SD1.5 architecture)",
+            "data": "synthetic prompts, random-init weights (%s architecture)" % ("Kandinsky 2.1" if k2 else "SD1.5"),
             "config": {
-                "model": "anythingv3 (SD1.5 UNet + KL-VAE + CLIP ViT-L/14 text)" + (" TINY" if args.tiny else ""),
+                "model": ("kandinsky2 (Kandinsky 2.1: prior + GLIDE UNet + MoVQ + XLM-R/CLIP text)" if k2 else
+                          "anythingv3 (SD1.5 UNet + KL-VAE + CLIP ViT-L/14 text)") + (" TINY" if args.tiny else ""),
                 "global_batch": n,
                 "seq_len": (args.res // 8) ** 2,
                 "resolution": args.res,
                 "denoise_steps": args.denoise_steps,
-                "scheduler": args.scheduler,
+                "scheduler": "p_sampler" if k2 else args.scheduler,
                 "cfg_batch": 2,
                 "parallelism": f"task-dp{n}",
             },

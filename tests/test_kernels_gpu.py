@@ -135,3 +135,20 @@ def test_conv2d_all_tile_configs(cuda, cfg, split):
     y = _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg, split)
     ref_y = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, 1, False) + r.float()
     assert _rel(y, ref_y) < 1e-2, (cfg, split, _rel(y, ref_y))
+
+
+@pytest.mark.parametrize("B,H,W,C,G,mh,mw,one_plus,silu", [
+    (1, 96, 96, 512, 32, 96, 96, 0.0, True), (1, 192, 192, 256, 32, 96, 96, 0.0, True),
+    (1, 768, 768, 128, 32, 96, 96, 0.0, False), (2, 48, 48, 768, 32, 1, 1, 1.0, True),
+    (2, 12, 12, 3072, 32, 1, 1, 1.0, True), (2, 9, 15, 64, 8, 3, 5, 0.0, True)])
+def test_group_norm_modulated(cuda, B, H, W, C, G, mh, mw, one_plus, silu):
+    """SpatialNorm (MoVQ) / scale-shift norm (GLIDE) fused apply vs fp32 reference."""
+    torch.manual_seed(2)
+    x = (torch.randn(B, H, W, C, device=cuda) * 2 + 1).bfloat16()
+    g = (torch.rand(C, device=cuda) + 0.5).bfloat16()
+    b = torch.randn(C, device=cuda).bfloat16()
+    mod = torch.randn(B, mh, mw, 2 * C, device=cuda).bfloat16()
+    y = _lib.group_norm_mod_nhwc(x, g, b, G, 1e-6, silu, mod, one_plus)
+    r = ref.group_norm_mod_nhwc(x.float(), g.float(), b.float(), G, 1e-6, silu, mod.float(), one_plus)
+    assert _rel(y, r) < 1e-2
+    assert torch.equal(y, _lib.group_norm_mod_nhwc(x, g, b, G, 1e-6, silu, mod, one_plus))
