@@ -61,7 +61,8 @@ def _gemm_ok(K, N):
 def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, temb=None):
     """Channels-last conv. x [B,H,W,Cin], w [Cout,kh,kw,Cin]; fused epilogue
     (+bias, +temb[b, n] per-batch bias, +residual)."""
-    if _hip(x) and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0 and w.shape[1] in (1, 3):
+    if _hip(x) and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0 and (w.shape[1] in (1, 3) and w.shape[1] == w.shape[2]
+                                                                     or tuple(w.shape[1:3]) == (3, 1)):
         return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride)
     if x.is_cuda:
         # MIOpen NHWC path (channel counts the kernel does not tile: 3/4-channel
@@ -70,7 +71,8 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
         xc = x.permute(0, 3, 1, 2)
         if upsample:
             xc = F.interpolate(xc, scale_factor=2.0, mode="nearest")
-        y = F.conv2d(xc, w.permute(0, 3, 1, 2), b, stride=stride, padding=padding)
+        pad = (padding, 0) if w.shape[1] != w.shape[2] else padding
+        y = F.conv2d(xc, w.permute(0, 3, 1, 2), b, stride=stride, padding=pad)
         y = y.permute(0, 2, 3, 1)
         if not y.is_contiguous():
             y = y.contiguous()
@@ -120,6 +122,16 @@ def attention(q, k, v, scale=None, causal=False):
     if _hip(q):
         return _lib.flash_attention(q, k, v, scale, causal)
     return ref.attention(q, k, v, scale, causal)
+
+
+def temporal_attention(q, k, v, scale=None):
+    """Frame-axis attention, q/k/v [B, F, P, H, D] strided views of the frame-major
+    activation (P = pixels): one MFMA wave per (b, p, h) problem (HIP)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    if _hip(q):
+        return _lib.temporal_attention(q, k, v, scale)
+    return ref.temporal_attention(q, k, v, scale)
 
 
 # --------------------------------------------------------------------------- elementwise

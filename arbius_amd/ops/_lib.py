@@ -34,7 +34,7 @@ _SIGS = {
     "arb_conv2d_workspace": (c_size_t, [c_int] * 11),
     "arb_conv2d_plan": (c_int, [c_int] * 9 + [c_void_p]),
     "arb_gemm_bias_res": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p]),
-    "arb_temporal_attention": (c_int, [c_void_p] * 4 + [c_int] * 5 + [c_float, c_void_p]),
+    "arb_temporal_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_void_p]),
     "arb_convgru_gates": (c_int, [c_void_p] * 5 + [c_long, c_int, c_void_p]),
 }
 
@@ -172,6 +172,26 @@ def flash_attention(q, k, v, scale, causal):
     return o
 
 
+def temporal_attention(q, k, v, scale):
+    """Attention over the frame axis: q/k/v [B, F, P, H, D] views (any strides, last dim
+    contiguous) -> o [B, F, P, H, D] contiguous.  One wave per (b, p, h) problem."""
+    _bf16(q, k, v)
+    B, F, P, H, D = q.shape
+    for t in (q, k, v):
+        if t.stride(-1) != 1 or any(s % 8 for s in t.stride()[:4]) or t.data_ptr() % 16:
+            raise ValueError("temporal_attention: last dim must be contiguous, strides/base 16B aligned")
+    if F > 96 or D not in (32, 64, 128):
+        raise ValueError(f"temporal_attention: unsupported F={F} D={D}")
+    o = torch.empty(B, F, P, H, D, dtype=q.dtype, device=q.device)
+    st = []
+    for t in (q, k, v, o):
+        st += [t.stride(0), t.stride(1), t.stride(2), t.stride(3)]
+    strides = (ctypes.c_long * 16)(*st)
+    _check(_fn("arb_temporal_attention")(_p(q), _p(k), _p(v), _p(o), strides, B, F, P, H, D, float(scale),
+                                         _stream()), "temporal_attention")
+    return o
+
+
 def _large_head_attention(q, k, v, scale):
     """Head dims > 160 (the single-head d=512 VAE mid-block attention): two
     hipBLASLt GEMMs around an fp32 softmax.  Runs once per task."""
@@ -220,11 +240,13 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     w = w.contiguous()
     B, H, W, Cin = x.shape
     Cout, kh, kw, Cin2 = w.shape
-    if Cin != Cin2 or kh != kw or kh not in (1, 3) or Cin % 64 or Cout % 8 or stride not in (1, 2):
+    temporal = (kh, kw) == (3, 1)      # (3,1,1) Conv3d over a [B, F, HW, C] view
+    if Cin != Cin2 or not (kh == kw and kh in (1, 3) or temporal) or Cin % 64 or Cout % 8 or stride not in (1, 2):
         raise ValueError(f"conv2d: unsupported shape x={tuple(x.shape)} w={tuple(w.shape)} stride={stride}")
     Hl, Wl = (2 * H, 2 * W) if upsample else (H, W)
+    padw = 0 if temporal else padding
     Ho = (Hl + 2 * padding - kh) // stride + 1
-    Wo = (Wl + 2 * padding - kw) // stride + 1
+    Wo = (Wl + 2 * padw - kw) // stride + 1
     y = torch.empty(B, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     if residual is not None:
         residual = residual.contiguous()
@@ -236,7 +258,7 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
             raise ValueError("conv2d temb must be [B, Cout]")
     if b is not None and b.numel() != Cout:
         raise ValueError("conv2d bias size")
-    args = (B, H, W, Cin, Cout, kh, padding, int(bool(upsample)), stride, int(cfg), int(split))
+    args = (B, H, W, Cin, Cout, 31 if temporal else kh, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
     _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), *args, _stream()),

@@ -35,7 +35,7 @@ struct ConvArgs {
   int Hl, Wl;           // logical input dims (after upsample)
   int Ho, Wo;
   int N, K, M;
-  int kw, pad, stride, upsample;
+  int kw, pad, padw, stride, upsample;
   int ktiles, kt_per_split;
   int tiles_n, tiles_total;
   int nsplit, m_fastest;
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     xb[i] = mm / hw;
     const int rem = mm - xb[i] * hw;
     xho[i] = (rem / p.Wo) * p.stride - p.pad;
-    xwo[i] = (rem % p.Wo) * p.stride - p.pad;
+    xwo[i] = (rem % p.Wo) * p.stride - p.padw;
   }
 
   uint4 rw[WCH], rx[XCH];
@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
     xb[i] = mm / hw;
     const int rem = mm - xb[i] * hw;
     xho[i] = (rem / p.Wo) * p.stride - p.pad;
-    xwo[i] = (rem % p.Wo) * p.stride - p.pad;
+    xwo[i] = (rem % p.Wo) * p.stride - p.padw;
   }
   typedef __attribute__((address_space(1))) const void* gptr_t;
   typedef __attribute__((address_space(3))) void* lptr_t;
@@ -481,16 +481,21 @@ static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split
       }
     }
   }
+  bp.cfg += kNumCfgs;  // register-staged variant: faster than the LDS-DMA ring on every tuned shape
   return bp;
 }
 
+// k = 1 / 3: square kernel, padding `pad` on both axes.  k = 31: a 3x1 kernel
+// (padding pad x 0) - the (3,1,1) temporal Conv3d of the UNet3D run over the
+// frame-major [B, F, H*W, C] activation viewed as an F x HW image.
 static void conv_geom(ConvArgs& a, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
                       int stride) {
+  const int kh = k == 31 ? 3 : k, kw = k == 31 ? 1 : k, padw = k == 31 ? 0 : pad;
   a.B = B; a.H = H; a.W = W; a.Cin = Cin;
   a.Hl = upsample ? 2 * H : H; a.Wl = upsample ? 2 * W : W;
-  a.Ho = (a.Hl + 2 * pad - k) / stride + 1; a.Wo = (a.Wl + 2 * pad - k) / stride + 1;
-  a.N = Cout; a.K = k * k * Cin; a.M = B * a.Ho * a.Wo;
-  a.kw = k; a.pad = pad; a.stride = stride; a.upsample = upsample;
+  a.Ho = (a.Hl + 2 * pad - kh) / stride + 1; a.Wo = (a.Wl + 2 * padw - kw) / stride + 1;
+  a.N = Cout; a.K = kh * kw * Cin; a.M = B * a.Ho * a.Wo;
+  a.kw = kw; a.pad = pad; a.padw = padw; a.stride = stride; a.upsample = upsample;
   a.ktiles = a.K / 64; a.kt_per_split = a.ktiles;
 }
 
@@ -545,7 +550,7 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
 ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* temb, const void* res,
                             void* out, void* ws, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
                             int stride, int cfg, int split, hipStream_t stream) {
-  if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3) || (stride != 1 && stride != 2)) return -1;
+  if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
   ConvArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = (const bf16_t*)bias; a.temb = (const bf16_t*)temb;
   a.res = (const bf16_t*)res; a.out = (bf16_t*)out; a.ws = (float*)ws;

@@ -1,0 +1,172 @@
+// Temporal self-attention over the frames axis (UNet3D of zeroscopev2xl / damo,
+// SURVEY.md §2.6(c), §5.7): a SHORT sequence (F = 1..96 frames) for a HUGE batch
+// (every latent pixel x head x CFG branch: 2 x 2880 x 5 = 28800 problems at the
+// 576x320x24f level-0 blocks).  The generic flash kernel tiles 64+ queries per
+// wave and would idle >60% of every MFMA here, so this kernel gives each wave
+// ONE (video, pixel, head) problem and keeps the whole frame axis in registers:
+//
+//   S^T = K Q^T  on mfma_f32_16x16x32_bf16 (K rows / Q rows are 16-byte loads
+//                straight from the activation - no LDS, no transposes)
+//   softmax over keys: in-lane over the 4 C rows x key tiles, then xor 16/32
+//   O^T = V^T P^T: P^T is consumed from the S^T accumulators in place through
+//                a permuted key order (slot 8g+j <-> key tile/row held by lane
+//                group g), V^T gathered with the same permutation.
+//
+// Activations stay in the UNet's frame-major channels-last layout
+// [B*F, H, W, C] (fused QKV adds a 3x): element (b, f, p, h, d) is at
+// b*sb + f*sf + p*sp + h*sh + d, so no permute/copy exists on either side.
+// Deterministic: fixed reduction order, no atomics.
+#include "common.h"
+
+struct TAArgs {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  bf16_t* o;
+  long q_sb, q_sf, q_sp, q_sh;
+  long k_sb, k_sf, k_sp, k_sh;
+  long v_sb, v_sf, v_sp, v_sh;
+  long o_sb, o_sf, o_sp, o_sh;
+  int B, F, P, H;
+  long items;
+  float scale_log2;
+};
+
+template <int KT32, int DD>
+__global__ void __launch_bounds__(256) temporal_attn_kernel(TAArgs a) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long item = (long)blockIdx.x * 4 + wave;
+  if (item >= a.items) return;
+  const int h = (int)(item % a.H);
+  const long t = item / a.H;
+  const int p = (int)(t % a.P);
+  const int b = (int)(t / a.P);
+  const bf16_t* qb = a.q + b * a.q_sb + p * a.q_sp + h * a.q_sh;
+  const bf16_t* kb = a.k + b * a.k_sb + p * a.k_sp + h * a.k_sh;
+  const bf16_t* vb = a.v + b * a.v_sb + p * a.v_sp + h * a.v_sh;
+  bf16_t* ob = a.o + b * a.o_sb + p * a.o_sp + h * a.o_sh;
+  const int F = a.F;
+  const int r16 = lane & 15, g = lane >> 4;
+  constexpr int KS = DD / 32;     // contraction steps of S
+  constexpr int NKT = 2 * KT32;   // 16-key tiles
+  constexpr int DT = DD / 16;     // 16-row d tiles of O^T
+  const bf16x8 zero8 = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+
+  // K as the A operand of S^T: lane holds K[kt*16 + r16][ks*32 + 8g .. +7]
+  bf16x8 kf[NKT][KS];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int key = kt * 16 + r16;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      kf[kt][ks] = key < F ? __builtin_bit_cast(bf16x8, ld16(kb + key * a.k_sf + ks * 32 + 8 * g)) : zero8;
+  }
+  // V^T as the A operand of O^T, permuted key slots: slot 8g+j <-> key
+  //   j < 4: tile 2s, row 4g+j      j >= 4: tile 2s+1, row 4g+j-4
+  bf16x8 vf[KT32][DT];
+#pragma unroll
+  for (int s = 0; s < KT32; ++s) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x8 u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int key = (j < 4) ? (2 * s) * 16 + 4 * g + j : (2 * s + 1) * 16 + 4 * g + (j - 4);
+        u[j] = key < F ? vb[key * a.v_sf + dt * 16 + r16] : (unsigned short)0;
+      }
+      vf[s][dt] = __builtin_bit_cast(bf16x8, u);
+    }
+  }
+
+  const int QT = (F + 15) >> 4;
+  for (int qt = 0; qt < QT; ++qt) {
+    const int qrow = qt * 16 + r16;
+    bf16x8 qf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      qf[ks] = qrow < F ? __builtin_bit_cast(bf16x8, ld16(qb + qrow * a.q_sf + ks * 32 + 8 * g)) : zero8;
+    f32x4 sc[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      sc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][ks], qf[ks], sc[kt], 0, 0, 0);
+    }
+    // sc[kt][r] = S^T[key = kt*16 + 4g + r][query = qt*16 + r16]
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 16 + 4 * g + r;
+        const float v = key < F ? sc[kt][r] * a.scale_log2 : -INFINITY;
+        sc[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __builtin_amdgcn_exp2f(sc[kt][r] - mx);
+        sc[kt][r] = e;
+        sum += e;
+      }
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    f32x4 oc[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) oc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KT32; ++s) {
+      u16x8 pu;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pu[j] = f2bf(sc[2 * s][j]);
+        pu[4 + j] = f2bf(sc[2 * s + 1][j]);
+      }
+      const bf16x8 pb = __builtin_bit_cast(bf16x8, pu);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][dt], pb, oc[dt], 0, 0, 0);
+    }
+    // oc[dt][r] = O^T[d = dt*16 + 4g + r][query = qrow]
+    if (qrow < F) {
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const uint32_t w0 = (uint32_t)f2bf(oc[dt][0] * inv) | ((uint32_t)f2bf(oc[dt][1] * inv) << 16);
+        const uint32_t w1 = (uint32_t)f2bf(oc[dt][2] * inv) | ((uint32_t)f2bf(oc[dt][3] * inv) << 16);
+        *reinterpret_cast<uint2*>(ob + qrow * a.o_sf + dt * 16 + 4 * g) = make_uint2(w0, w1);
+      }
+    }
+  }
+}
+
+// strides: 16 longs (q, k, v, o) x (sb, sf, sp, sh) in elements.  F <= 96, D in {32, 64, 128}.
+ARB_API int arb_temporal_attention(const void* q, const void* k, const void* v, void* o, const long* st, int B, int F,
+                                   int P, int H, int D, float scale, hipStream_t stream) {
+  if (F < 1 || F > 96 || (D != 32 && D != 64 && D != 128)) return -1;
+  TAArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
+  a.q_sb = st[0]; a.q_sf = st[1]; a.q_sp = st[2]; a.q_sh = st[3];
+  a.k_sb = st[4]; a.k_sf = st[5]; a.k_sp = st[6]; a.k_sh = st[7];
+  a.v_sb = st[8]; a.v_sf = st[9]; a.v_sp = st[10]; a.v_sh = st[11];
+  a.o_sb = st[12]; a.o_sf = st[13]; a.o_sp = st[14]; a.o_sh = st[15];
+  a.B = B; a.F = F; a.P = P; a.H = H;
+  a.items = (long)B * P * H;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  const long blocks = (a.items + 3) / 4;
+  if (blocks > 0x7fffffffL) return -2;
+  const int kt32 = (F + 31) / 32;
+#define TA_CASE(KT, DDV) \
+  if (kt32 == KT && D == DDV) { temporal_attn_kernel<KT, DDV><<<(unsigned)blocks, 256, 0, stream>>>(a); return (int)hipGetLastError(); }
+  TA_CASE(1, 64) TA_CASE(2, 64) TA_CASE(3, 64)
+  TA_CASE(1, 32) TA_CASE(2, 32) TA_CASE(3, 32)
+  TA_CASE(1, 128) TA_CASE(2, 128) TA_CASE(3, 128)
+#undef TA_CASE
+  return -3;
+}

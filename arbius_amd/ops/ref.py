@@ -25,7 +25,8 @@ def conv2d_nhwc(x, w, b=None, stride=1, padding=1, upsample=False):
     xc = x.permute(0, 3, 1, 2)
     if upsample:
         xc = F.interpolate(xc, scale_factor=2.0, mode="nearest")
-    y = F.conv2d(xc, w.permute(0, 3, 1, 2), b, stride=stride, padding=padding)
+    pad = (padding, 0) if w.shape[1] != w.shape[2] else padding   # (3,1) temporal kernel
+    y = F.conv2d(xc, w.permute(0, 3, 1, 2), b, stride=stride, padding=pad)
     return y.permute(0, 2, 3, 1).contiguous()
 
 
@@ -98,17 +99,9 @@ def cfg_combine(eps, scale):
     return u + scale * (c - u)
 
 
-def temporal_attention(x, wq, wk, wv, wo, bo, heads, scale=None):
-    """Attention along the frame axis. x [B, F, N, C] -> [B, F, N, C] (fp32 ref)."""
-    B, Fr, N, C = x.shape
-    D = C // heads
-    xf = x.float()
-    q = (xf @ wq.float().t()).reshape(B, Fr, N, heads, D)
-    k = (xf @ wk.float().t()).reshape(B, Fr, N, heads, D)
-    v = (xf @ wv.float().t()).reshape(B, Fr, N, heads, D)
-    # [B, N, F, H, D] so frames become the sequence axis
-    q, k, v = (t.permute(0, 2, 1, 3, 4).reshape(B * N, Fr, heads, D) for t in (q, k, v))
-    o = attention(q, k, v, scale)
-    o = o.reshape(B, N, Fr, C).permute(0, 2, 1, 3)
-    o = o @ wo.float().t() + bo.float()
-    return o.to(x.dtype)
+def temporal_attention(q, k, v, scale=None):
+    """Attention along the frame axis: q/k/v [B, F, P, H, D] -> [B, F, P, H, D]."""
+    B, Fr, P, H, D = q.shape
+    qs, ks, vs = (t.permute(0, 2, 1, 3, 4).reshape(B * P, Fr, H, D) for t in (q, k, v))
+    o = attention(qs, ks, vs, scale)
+    return o.reshape(B, P, Fr, H, D).permute(0, 2, 1, 3, 4).contiguous()

@@ -1,0 +1,278 @@
+"""Deterministic MP4 (H.264) writer for the video models' ``out-1.mp4``
+(templates zeroscopev2xl / damo / robust_video_matting, SURVEY.md §2.6(c,d)).
+
+There is no ffmpeg/libx264 in the image and a solution CID must be a pure
+function of the frames, so the encoder is self-contained and bit-exact:
+
+* colour: RGB -> BT.601 limited-range YCbCr 4:2:0 in integer arithmetic
+  (chroma = rounded 2x2 mean of the RGB samples, then the integer matrix);
+* bitstream: H.264 Constrained Baseline, every picture one IDR slice made of
+  I_PCM macroblocks (mb_type 25: raw samples, lossless w.r.t. the YCbCr
+  planes, decodable by every H.264 decoder).  Samples are clamped to
+  [1, 254], so the macroblock payload can never contain a start-code prefix
+  (``00 00 0x``) and only the slice header needs emulation prevention;
+* container: ftyp + moov (faststart) + mdat, fixed zero timestamps, AVCC
+  4-byte NAL lengths, avcC with the SPS/PPS.
+
+The whole frame -> bytes path is numpy-vectorised (one concatenate per
+picture, no per-macroblock Python); odd sizes are padded to whole macroblocks
+with edge replication and cropped back in the SPS.
+"""
+from __future__ import annotations
+
+import struct
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+PROFILE_IDC, CONSTRAINT_FLAGS, LEVEL_IDC = 66, 0xC0, 51
+
+
+class _Bits:
+    def __init__(self):
+        self.bits: List[int] = []
+
+    def u(self, n: int, v: int):
+        self.bits.extend((v >> (n - 1 - i)) & 1 for i in range(n))
+
+    def ue(self, v: int):
+        v += 1
+        n = v.bit_length()
+        self.u(n - 1, 0)
+        self.u(n, v)
+
+    def se(self, v: int):
+        self.ue(2 * v - 1 if v > 0 else -2 * v)
+
+    def align_zero(self):
+        while len(self.bits) % 8:
+            self.bits.append(0)
+
+    def trailing(self):
+        self.bits.append(1)
+        self.align_zero()
+
+    def bytes(self) -> bytes:
+        assert len(self.bits) % 8 == 0
+        out = bytearray()
+        for i in range(0, len(self.bits), 8):
+            b = 0
+            for bit in self.bits[i:i + 8]:
+                b = (b << 1) | bit
+            out.append(b)
+        return bytes(out)
+
+
+def _ep(rbsp: bytes) -> bytes:
+    """Emulation prevention (insert 0x03 after 00 00 when the next byte is <= 3)."""
+    out = bytearray()
+    zeros = 0
+    for b in rbsp:
+        if zeros >= 2 and b <= 3:
+            out.append(3)
+            zeros = 0
+        out.append(b)
+        zeros = zeros + 1 if b == 0 else 0
+    return bytes(out)
+
+
+def _nal(ref_idc: int, typ: int, payload: bytes) -> bytes:
+    return bytes([(ref_idc << 5) | typ]) + payload
+
+
+def sps_pps(width: int, height: int) -> Tuple[bytes, bytes]:
+    mbw, mbh = (width + 15) // 16, (height + 15) // 16
+    s = _Bits()
+    s.u(8, PROFILE_IDC); s.u(8, CONSTRAINT_FLAGS); s.u(8, LEVEL_IDC)
+    s.ue(0)               # seq_parameter_set_id
+    s.ue(0)               # log2_max_frame_num_minus4
+    s.ue(2)               # pic_order_cnt_type
+    s.ue(1)               # max_num_ref_frames
+    s.u(1, 0)             # gaps_in_frame_num_value_allowed_flag
+    s.ue(mbw - 1); s.ue(mbh - 1)
+    s.u(1, 1)             # frame_mbs_only_flag
+    s.u(1, 1)             # direct_8x8_inference_flag
+    crop_r, crop_b = (mbw * 16 - width) // 2, (mbh * 16 - height) // 2
+    if crop_r or crop_b:
+        s.u(1, 1); s.ue(0); s.ue(crop_r); s.ue(0); s.ue(crop_b)
+    else:
+        s.u(1, 0)
+    s.u(1, 0)             # vui_parameters_present_flag
+    s.trailing()
+    p = _Bits()
+    p.ue(0); p.ue(0)      # pps id, sps id
+    p.u(1, 0)             # entropy_coding_mode_flag (CAVLC)
+    p.u(1, 0)             # bottom_field_pic_order_in_frame_present_flag
+    p.ue(0)               # num_slice_groups_minus1
+    p.ue(0); p.ue(0)      # num_ref_idx_l0/l1_default_active_minus1
+    p.u(1, 0); p.u(2, 0)  # weighted_pred_flag, weighted_bipred_idc
+    p.se(0); p.se(0); p.se(0)   # pic_init_qp/qs_minus26, chroma_qp_index_offset
+    p.u(1, 1)             # deblocking_filter_control_present_flag
+    p.u(1, 0); p.u(1, 0)  # constrained_intra_pred_flag, redundant_pic_cnt_present_flag
+    p.trailing()
+    return _nal(3, 7, _ep(s.bytes())), _nal(3, 8, _ep(p.bytes()))
+
+
+def rgb_to_yuv420(frame: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """uint8 [H, W, 3] (H, W multiples of 16) -> Y [H, W], Cb/Cr [H/2, W/2], BT.601 limited range."""
+    f = frame.astype(np.int32)
+    r, g, b = f[..., 0], f[..., 1], f[..., 2]
+    y = ((66 * r + 129 * g + 25 * b + 128) >> 8) + 16
+    H, W = r.shape
+    q = f.reshape(H // 2, 2, W // 2, 2, 3).sum(axis=(1, 3))
+    r2, g2, b2 = q[..., 0], q[..., 1], q[..., 2]          # 4 x mean
+    cb = ((-38 * r2 - 74 * g2 + 112 * b2 + 512) >> 10) + 128
+    cr = ((112 * r2 - 94 * g2 - 18 * b2 + 512) >> 10) + 128
+    clip = lambda a: np.clip(a, 1, 254).astype(np.uint8)
+    return clip(y), clip(cb), clip(cr)
+
+
+def _pad16(frame: np.ndarray) -> np.ndarray:
+    H, W = frame.shape[:2]
+    ph, pw = (-H) % 16, (-W) % 16
+    if ph or pw:
+        frame = np.pad(frame, ((0, ph), (0, pw), (0, 0)), mode="edge")
+    return frame
+
+
+def encode_idr_pcm(frame: np.ndarray, idr_pic_id: int) -> bytes:
+    """One RGB frame -> one IDR slice NAL of I_PCM macroblocks."""
+    y, cb, cr = rgb_to_yuv420(_pad16(frame))
+    H, W = y.shape
+    mbh, mbw = H // 16, W // 16
+    n = mbh * mbw
+    ymb = y.reshape(mbh, 16, mbw, 16).transpose(0, 2, 1, 3).reshape(n, 256)
+    cbm = cb.reshape(mbh, 8, mbw, 8).transpose(0, 2, 1, 3).reshape(n, 64)
+    crm = cr.reshape(mbh, 8, mbw, 8).transpose(0, 2, 1, 3).reshape(n, 64)
+    hdr = _Bits()
+    hdr.ue(0)             # first_mb_in_slice
+    hdr.ue(7)             # slice_type: I (all slices)
+    hdr.ue(0)             # pic_parameter_set_id
+    hdr.u(4, 0)           # frame_num
+    hdr.ue(idr_pic_id & 1)
+    hdr.u(1, 0); hdr.u(1, 0)   # no_output_of_prior_pics_flag, long_term_reference_flag
+    hdr.se(0)             # slice_qp_delta
+    hdr.ue(1)             # disable_deblocking_filter_idc
+    hdr.ue(25)            # mb_type I_PCM (first macroblock)
+    hdr.align_zero()      # pcm_alignment_zero_bits
+    body = np.empty((n, 386), dtype=np.uint8)
+    body[:, 0], body[:, 1] = 0x0D, 0x00   # ue(25) + 7 alignment zeros, byte aligned
+    body[:, 2:258], body[:, 258:322], body[:, 322:386] = ymb, cbm, crm
+    payload = _ep(hdr.bytes()) + body[0, 2:].tobytes() + body[1:].tobytes() + b"\x80"
+    return _nal(3, 5, payload)
+
+
+# ------------------------------------------------------------------------------------ container
+def _box(typ: bytes, *parts: bytes) -> bytes:
+    data = b"".join(parts)
+    return struct.pack(">I", 8 + len(data)) + typ + data
+
+
+def _full(typ: bytes, version: int, flags: int, *parts: bytes) -> bytes:
+    return _box(typ, struct.pack(">I", (version << 24) | flags), *parts)
+
+
+_MATRIX = struct.pack(">9I", 0x10000, 0, 0, 0, 0x10000, 0, 0, 0, 0x40000000)
+
+
+def _moov(width, height, fps, sizes, sps, pps, mdat_offset) -> bytes:
+    F = len(sizes)
+    dur_ms = int(round(F * 1000 / fps))
+    mvhd = _full(b"mvhd", 0, 0, struct.pack(">IIII", 0, 0, 1000, dur_ms), struct.pack(">IH", 0x10000, 0x100),
+                 b"\0" * 10, _MATRIX, b"\0" * 24, struct.pack(">I", 2))
+    tkhd = _full(b"tkhd", 0, 3, struct.pack(">IIIII", 0, 0, 1, 0, dur_ms), b"\0" * 8,
+                 struct.pack(">hhhH", 0, 0, 0, 0), _MATRIX, struct.pack(">II", width << 16, height << 16))
+    mdhd = _full(b"mdhd", 0, 0, struct.pack(">IIIIHH", 0, 0, fps, F, 0x55C4, 0))
+    hdlr = _full(b"hdlr", 0, 0, struct.pack(">I", 0), b"vide", b"\0" * 12, b"VideoHandler\0")
+    vmhd = _full(b"vmhd", 0, 1, b"\0" * 8)
+    dinf = _box(b"dinf", _full(b"dref", 0, 0, struct.pack(">I", 1), _full(b"url ", 0, 1)))
+    avcc = _box(b"avcC", bytes([1, PROFILE_IDC, CONSTRAINT_FLAGS, LEVEL_IDC, 0xFF, 0xE1]),
+                struct.pack(">H", len(sps)), sps, b"\x01", struct.pack(">H", len(pps)), pps)
+    name = b"\x0bI_PCM H.264".ljust(32, b"\0")
+    avc1 = _box(b"avc1", b"\0" * 6, struct.pack(">H", 1), b"\0" * 16, struct.pack(">HH", width, height),
+                struct.pack(">III", 0x480000, 0x480000, 0), struct.pack(">H", 1), name,
+                struct.pack(">Hh", 0x18, -1), avcc)
+    stsd = _full(b"stsd", 0, 0, struct.pack(">I", 1), avc1)
+    stts = _full(b"stts", 0, 0, struct.pack(">III", 1, F, 1))
+    stsc = _full(b"stsc", 0, 0, struct.pack(">IIII", 1, 1, F, 1))
+    stsz = _full(b"stsz", 0, 0, struct.pack(">II", 0, F), struct.pack(">%dI" % F, *sizes))
+    stco = _full(b"stco", 0, 0, struct.pack(">II", 1, mdat_offset))
+    stbl = _box(b"stbl", stsd, stts, stsc, stsz, stco)
+    minf = _box(b"minf", vmhd, dinf, stbl)
+    mdia = _box(b"mdia", mdhd, hdlr, minf)
+    return _box(b"moov", mvhd, _box(b"trak", tkhd, mdia))
+
+
+def encode_mp4(frames: Sequence[np.ndarray], fps: int) -> bytes:
+    """uint8 RGB frames [H, W, 3] (all the same size) -> MP4 bytes (deterministic)."""
+    frames = list(frames)
+    if not frames:
+        raise ValueError("encode_mp4: no frames")
+    H, W = frames[0].shape[:2]
+    fps = max(1, int(fps))
+    sps, pps = sps_pps(W, H)
+    samples = []
+    for i, f in enumerate(frames):
+        if f.shape != (H, W, 3) or f.dtype != np.uint8:
+            raise ValueError("encode_mp4: frames must be uint8 [H, W, 3] of one size")
+        nal = encode_idr_pcm(f, i)
+        samples.append(struct.pack(">I", len(nal)) + nal)
+    sizes = [len(s) for s in samples]
+    ftyp = _box(b"ftyp", b"isom", struct.pack(">I", 512), b"isomiso2avc1mp41")
+    moov_len = len(_moov(W, H, fps, sizes, sps, pps, 0))
+    mdat_payload = sum(sizes)
+    offset = len(ftyp) + moov_len + 8
+    moov = _moov(W, H, fps, sizes, sps, pps, offset)
+    if 8 + mdat_payload > 0xFFFFFFFF:
+        raise ValueError("encode_mp4: output above 4 GiB")
+    return ftyp + moov + struct.pack(">I", 8 + mdat_payload) + b"mdat" + b"".join(samples)
+
+
+# ------------------------------------------------------------------------------------ reader (tests)
+def _boxes(data: bytes, start: int = 0, end: int = None):
+    end = len(data) if end is None else end
+    i = start
+    while i < end:
+        size, typ = struct.unpack(">I4s", data[i:i + 8])
+        yield typ, i + 8, i + size
+        i += size
+
+
+def read_mp4_pcm(data: bytes):
+    """Parse an MP4 written by ``encode_mp4`` back into (fps, [(Y, Cb, Cr)])."""
+    top = {t: (a, b) for t, a, b in _boxes(data)}
+    ma, mb = top[b"moov"]
+
+    def find(path, a, b):
+        for t, x, y in _boxes(data, a, b):
+            if t == path[0]:
+                if len(path) == 1:
+                    return x, y
+                skip = {b"stsd": 8, b"avc1": 78, b"dref": 8}.get(path[0], 0)
+                return find(path[1:], x + skip, y)
+        raise KeyError(path)
+
+    ha, hb = find([b"trak", b"mdia", b"mdhd"], ma, mb)
+    fps = struct.unpack(">I", data[ha + 12:ha + 16])[0]
+    sa, sb = find([b"trak", b"mdia", b"minf", b"stbl", b"stsz"], ma, mb)
+    n = struct.unpack(">I", data[sa + 8:sa + 12])[0]
+    sizes = struct.unpack(">%dI" % n, data[sa + 12:sa + 12 + 4 * n])
+    ca, cb = find([b"trak", b"mdia", b"minf", b"stbl", b"stco"], ma, mb)
+    off = struct.unpack(">I", data[ca + 8:ca + 12])[0]
+    va, vb = find([b"trak", b"mdia", b"minf", b"stbl", b"stsd", b"avc1"], ma, mb)
+    W, H = struct.unpack(">HH", data[va + 24:va + 28])
+    W16, H16 = (W + 15) // 16 * 16, (H + 15) // 16 * 16
+    mbw, mbh = W16 // 16, H16 // 16
+    out = []
+    for s in sizes:
+        nal = data[off + 4:off + s]
+        off += s
+        assert nal[0] & 0x1F == 5
+        nmb = mbw * mbh
+        body = np.frombuffer(nal[len(nal) - 1 - (nmb * 386 - 2):len(nal) - 1], dtype=np.uint8)
+        body = np.concatenate([np.zeros(2, np.uint8), body]).reshape(nmb, 386)
+        y = body[:, 2:258].reshape(mbh, mbw, 16, 16).transpose(0, 2, 1, 3).reshape(H16, W16)
+        cbp = body[:, 258:322].reshape(mbh, mbw, 8, 8).transpose(0, 2, 1, 3).reshape(H16 // 2, W16 // 2)
+        crp = body[:, 322:386].reshape(mbh, mbw, 8, 8).transpose(0, 2, 1, 3).reshape(H16 // 2, W16 // 2)
+        out.append((y, cbp, crp))
+    return fps, out

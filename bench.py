@@ -33,8 +33,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--model", default="anythingv3", choices=["anythingv3", "kandinsky2"],
-                    help="anythingv3 = BASELINE headline config; kandinsky2 = BASELINE config #3")
+    ap.add_argument("--model", default="anythingv3", choices=["anythingv3", "kandinsky2", "zeroscopev2xl", "damo"],
+                    help="anythingv3 = BASELINE headline config; kandinsky2 = config #3; zeroscopev2xl = #4")
+    ap.add_argument("--frames", type=int, default=24, help="video models: frames (config #4: 24)")
     ap.add_argument("--res", type=int, default=None, help="default 512 (anythingv3) / 768 (kandinsky2)")
     ap.add_argument("--denoise-steps", type=int, default=None, help="default 50 / 100")
     ap.add_argument("--scheduler", default="DPMSolverMultistep")
@@ -45,7 +46,9 @@ def main():
     ap.add_argument("--device", default=None)
     args = ap.parse_args()
     k2 = args.model == "kandinsky2"
-    args.res = args.res or (768 if k2 else 512)
+    vid = args.model in ("zeroscopev2xl", "damo")
+    args.res = args.res or (768 if k2 else 576 if args.model == "zeroscopev2xl" else 256 if vid else 512)
+    args.height = 320 if args.model == "zeroscopev2xl" else args.res
     args.denoise_steps = args.denoise_steps or (100 if k2 else 50)
 
     from arbius_amd import ops
@@ -72,6 +75,15 @@ def main():
 
     def one_task(i):
         taskid = "0x" + keccak256(f"bench-task-{rank}-{i}".encode()).hex()
+        if vid:  # BASELINE config #4: 576x320x24f text-to-video
+            inp = {"prompt": f"a red cat walking on a castle wall, cinematic, task {i}", "num_frames": args.frames,
+                   "width": args.res, "height": args.height, "num_inference_steps": args.denoise_steps,
+                   "seed": taskid2seed(taskid), "fps": 24}
+            t0 = time.perf_counter()
+            sol = pipe.solve(inp)
+            generate_commitment(wallet, taskid, sol.cid)
+            lat.append(time.perf_counter() - t0)
+            return sol
         if k2:   # templates/kandinsky2.json inputs; hidden defaults 100 steps, guidance 4, prior 5 steps
             pipe.cfg.num_steps = args.denoise_steps
             inp = {"prompt": f"a red cat sitting on a castle wall, oil painting, task {i}",
@@ -128,15 +140,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
-            "data": "synthetic prompts, random-init weights (%s architecture)" % ("Kandinsky 2.1" if k2 else "SD1.5"),
+            "data": "synthetic prompts, random-init weights (%s architecture)" % (
+                "Kandinsky 2.1" if k2 else "UNet3D text-to-video" if vid else "SD1.5"),
             "config": {
                 "model": ("kandinsky2 (Kandinsky 2.1: prior + GLIDE UNet + MoVQ + XLM-R/CLIP text)" if k2 else
+                          f"{args.model} (UNet3D + KL-VAE + OpenCLIP ViT-H text), {args.frames} frames" if vid else
                           "anythingv3 (SD1.5 UNet + KL-VAE + CLIP ViT-L/14 text)") + (" TINY" if args.tiny else ""),
                 "global_batch": n,
-                "seq_len": (args.res // 8) ** 2,
-                "resolution": args.res,
+                "seq_len": (args.res // 8) * (args.height // 8),
+                "resolution": args.res if not vid else f"{args.res}x{args.height}",
                 "denoise_steps": args.denoise_steps,
-                "scheduler": "p_sampler" if k2 else args.scheduler,
+                "scheduler": "p_sampler" if k2 else "DPMSolverMultistep" if vid else args.scheduler,
                 "cfg_batch": 2,
                 "parallelism": f"task-dp{n}",
             },

@@ -25,16 +25,36 @@ NCFG = 20  # 0-9: LDS-DMA multi-stage, 10-19: register-staged
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
-def collect_shapes(res=512):
-    from arbius_amd.models.unet2d import UNet2DCondition, UNetConfig
-    from arbius_amd.models.vae import VAEDecoder
+def _run_meta(models, res):
+    """Run the selected model families on the meta device (shapes only)."""
+    with torch.device("meta"):
+        if "sd15" in models:
+            from arbius_amd.models.unet2d import UNet2DCondition, UNetConfig
+            from arbius_amd.models.vae import VAEDecoder
+            UNet2DCondition(UNetConfig())(torch.zeros(2, res // 8, res // 8, 4), torch.tensor([500.0]),
+                                          torch.zeros(2, 77, 768))
+            VAEDecoder()(torch.zeros(1, res // 8, res // 8, 4))
+        if "kandinsky2" in models:
+            from arbius_amd.models.glide_unet import GlideUNet
+            from arbius_amd.models.movq import MoVQDecoder
+            GlideUNet()(torch.zeros(2, 96, 96, 4), torch.tensor([500.0]), torch.zeros(2, 77, 1024),
+                        torch.zeros(2, 768), torch.zeros(2, 768))
+            MoVQDecoder()(torch.zeros(1, 96, 96, 4))
+        if "video" in models:   # BASELINE config #4: zeroscope 576x320x24f; VAE in chunks of 8 frames
+            from arbius_amd.models.unet3d import UNet3DCondition
+            from arbius_amd.models.vae import VAEDecoder
+            UNet3DCondition()(torch.zeros(48, 40, 72, 4), torch.tensor([500.0]), torch.zeros(2, 77, 1024), frames=24)
+            VAEDecoder()(torch.zeros(8, 40, 72, 4))
+
+
+def collect_shapes(models=("sd15",), res=512):
     convs, gemms = set(), set()
     orig_conv, orig_lin = ops.conv2d, ops.linear
 
     def conv(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, temb=None):
         if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
             B, H, W, C = x.shape
-            convs.add((B, H, W, C, w.shape[0], w.shape[1], padding, int(bool(upsample)), stride))
+            convs.add((B, H, W, C, w.shape[0], w.shape[1], w.shape[2], padding, int(bool(upsample)), stride))
         return orig_conv(x, w, b, stride, padding, upsample, residual, temb)
 
     def lin(x, w, b=None, residual=None):
@@ -44,14 +64,38 @@ def collect_shapes(res=512):
 
     ops.conv2d, ops.linear = conv, lin
     try:
-        with torch.device("meta"):
-            u = UNet2DCondition(UNetConfig())
-            u(torch.zeros(2, res // 8, res // 8, 4), torch.tensor([500.0]), torch.zeros(2, 77, 768))
-            d = VAEDecoder()
-            d(torch.zeros(1, res // 8, res // 8, 4))
+        _run_meta(models, res)
     finally:
         ops.conv2d, ops.linear = orig_conv, orig_lin
     return sorted(convs), sorted(gemms)
+
+
+def read_table(path):
+    """Existing conv_plans.inc -> {(M, N, K): (cfg, split)}."""
+    out = {}
+    if not os.path.exists(path):
+        return out
+    for line in open(path):
+        line = line.strip()
+        if line.startswith("{") and line.endswith("},"):
+            M, N, K, c, sp = (int(v) for v in line[1:-2].split(","))
+            out[(M, N, K)] = (c, sp)
+    return out
+
+
+def candidates(M, N, K, legacy_only):
+    """(cfg, split) pairs worth timing: split-K only when the grid is short of 2 waves."""
+    cfgs = range(10, NCFG) if legacy_only else range(NCFG)
+    for cfg in cfgs:
+        bn, bm = KCFG[cfg % 10]
+        tiles = -(-N // bn) * -(-M // bm)
+        for sp in SPLITS:
+            if sp > 1 and (sp > (K // 64) // 2 or tiles >= 512):
+                continue
+            yield cfg, sp
+
+
+KCFG = [(128, 128), (64, 128), (128, 64), (64, 64), (160, 64), (160, 128), (320, 32), (256, 64), (128, 256), (64, 256)]
 
 
 def graph_time(fn, reps=10, rounds=5):
@@ -80,24 +124,32 @@ def graph_time(fn, reps=10, rounds=5):
 
 
 def main():
-    out_dir = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out_dir", nargs="?", default="gpurun_out")
+    ap.add_argument("--models", default="sd15", help="comma list: sd15,kandinsky2,video")
+    ap.add_argument("--legacy-only", action="store_true", help="time only the register-staged cfgs (10-19)")
+    ap.add_argument("--merge", default=None, help="existing conv_plans.inc to keep entries from")
+    args = ap.parse_args()
+    out_dir = args.out_dir
     os.makedirs(out_dir, exist_ok=True)
     dev = torch.device("cuda")
-    convs, gemms = collect_shapes()
-    results, pinned = [], {}
-    for (B, H, W, C, Co, k, pad, up, st) in convs:
+    convs, gemms = collect_shapes(tuple(args.models.split(",")))
+    results = []
+    pinned = read_table(args.merge) if args.merge else {}
+    print(f"{len(convs)} conv shapes, {len(gemms)} gemm shapes, {len(pinned)} pinned kept", flush=True)
+    for (B, H, W, C, Co, kh, kw, pad, up, st) in convs:
         x = torch.randn(B, H, W, C, device=dev).bfloat16()
-        w = (torch.randn(Co, k, k, C, device=dev) / math.sqrt(k * k * C)).bfloat16()
+        w = (torch.randn(Co, kh, kw, C, device=dev) / math.sqrt(kh * kw * C)).bfloat16()
         b = torch.randn(Co, device=dev).bfloat16()
         Hl, Wl = (2 * H, 2 * W) if up else (H, W)
-        Ho, Wo = (Hl + 2 * pad - k) // st + 1, (Wl + 2 * pad - k) // st + 1
-        M, K = B * Ho * Wo, k * k * C
-        auto = _lib.conv_plan(B, H, W, C, Co, k, pad, up, st)
+        padw = 0 if kw != kh else pad
+        Ho, Wo = (Hl + 2 * pad - kh) // st + 1, (Wl + 2 * padw - kw) // st + 1
+        M, K = B * Ho * Wo, kh * kw * C
+        auto = _lib.conv_plan(B, H, W, C, Co, 31 if kw != kh else kh, pad, up, st)
         best = None
-        for cfg in range(NCFG):
-            for sp in SPLITS:
-                if sp > 1 and sp > (K // 64) // 2:
-                    continue
+        for cfg, sp in candidates(M, Co, K, args.legacy_only):
+            if True:
                 try:
                     t = graph_time(lambda: _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st, cfg, sp))
                 except Exception as e:  # noqa: BLE001
@@ -107,7 +159,7 @@ def main():
                     best = (t, cfg, sp)
         t_auto = graph_time(lambda: _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st))
         fl = 2.0 * M * Co * K
-        rec = {"kind": "conv", "shape": [B, H, W, C, Co, k, pad, up, st], "MNK": [M, Co, K], "best_us": round(best[0], 2),
+        rec = {"kind": "conv", "shape": [B, H, W, C, Co, kh, kw, pad, up, st], "MNK": [M, Co, K], "best_us": round(best[0], 2),
                "best_cfg": best[1], "best_split": best[2], "best_tflops": round(fl / best[0] / 1e6, 1),
                "auto_cfg": auto, "auto_us": round(t_auto, 2)}
         results.append(rec)
@@ -119,10 +171,8 @@ def main():
         b = torch.randn(N, device=dev).bfloat16()
         r = torch.randn(M, N, device=dev).bfloat16()
         best = None
-        for cfg in range(NCFG):
-            for sp in SPLITS:
-                if sp > 1 and sp > (K // 64) // 2:
-                    continue
+        for cfg, sp in candidates(M, N, K, args.legacy_only):
+            if True:
                 try:
                     t = graph_time(lambda: _lib.gemm(x, w, b, r, cfg, sp))
                 except Exception as e:  # noqa: BLE001
@@ -134,7 +184,7 @@ def main():
         rec = {"kind": "gemm_res", "MNK": [M, N, K], "best_us": round(best[0], 2), "best_cfg": best[1],
                "best_split": best[2], "best_tflops": round(fl / best[0] / 1e6, 1), "hipblaslt_addmm_add_us": round(t_blas, 2)}
         results.append(rec)
-        if (M, N, K) not in pinned:
+        if (M, N, K) not in {tuple(r["MNK"]) for r in results if r["kind"] == "conv"}:
             pinned[(M, N, K)] = (best[1], best[2])
         print(json.dumps(rec), flush=True)
     json.dump(results, open(os.path.join(out_dir, "autotune_conv.json"), "w"), indent=1)

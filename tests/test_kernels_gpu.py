@@ -152,3 +152,30 @@ def test_group_norm_modulated(cuda, B, H, W, C, G, mh, mw, one_plus, silu):
     r = ref.group_norm_mod_nhwc(x.float(), g.float(), b.float(), G, 1e-6, silu, mod.float(), one_plus)
     assert _rel(y, r) < 1e-2
     assert torch.equal(y, _lib.group_norm_mod_nhwc(x, g, b, G, 1e-6, silu, mod, one_plus))
+
+
+@pytest.mark.parametrize("B,F,P,H,D", [(2, 24, 2880, 5, 64), (2, 16, 64, 2, 64), (1, 1, 10, 1, 64),
+                                       (2, 33, 17, 3, 64), (1, 96, 9, 2, 64), (2, 24, 40, 4, 32),
+                                       (1, 24, 30, 2, 128), (1, 70, 5, 1, 128)])
+def test_temporal_attention(cuda, B, F, P, H, D):
+    """Frame-axis attention on strided views of a fused-QKV frame-major activation."""
+    torch.manual_seed(3)
+    qkv = torch.randn(B, F, P, 3, H, D, device=cuda).bfloat16()
+    q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
+    o = _lib.temporal_attention(q, k, v, 1 / math.sqrt(D))
+    r = ref.temporal_attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D))
+    assert _rel(o, r) < 2e-2
+    assert torch.equal(o, _lib.temporal_attention(q, k, v, 1 / math.sqrt(D)))
+
+
+@pytest.mark.parametrize("B,F,P,C,Co", [(2, 24, 2880, 320, 320), (1, 16, 64, 128, 64), (2, 5, 33, 64, 128)])
+def test_temporal_conv3x1(cuda, B, F, P, C, Co):
+    """(3,1,1) Conv3d over [B, F, HW, C] as a 3x1 implicit-GEMM conv (+ fused residual)."""
+    torch.manual_seed(4)
+    x = torch.randn(B, F, P, C, device=cuda).bfloat16()
+    w = (torch.randn(Co, 3, 1, C, device=cuda) / math.sqrt(3 * C)).bfloat16()
+    b = torch.randn(Co, device=cuda).bfloat16()
+    res = torch.randn(B, F, P, Co, device=cuda).bfloat16()
+    y = _lib.conv2d_nhwc(x, w, b, 1, False, res)
+    r = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, 1) + res.float()
+    assert y.shape == r.shape and _rel(y, r) < 1e-2

@@ -72,3 +72,33 @@ def test_sd15_unet_hip_vs_reference(cuda):
         finally:
             ops.set_reference_ops(False)
     assert _rel(y, r) < 5e-2
+
+
+def test_unet3d_hip_vs_reference(cuda):
+    from arbius_amd.models.layers import init_weights
+    from arbius_amd.models.unet3d import UNet3DCondition, UNet3DConfig
+    cfg = UNet3DConfig(block_channels=(64, 128, 128, 128), layers_per_block=1, head_dim=64, in_heads=2,
+                       cross_dim=64, groups=32, time_dim=64)
+    m = init_weights(torch.nn.ModuleDict({"u": UNet3DCondition(cfg)}), 5)["u"].to(cuda, torch.bfloat16).eval()
+    g = torch.Generator().manual_seed(0)
+    F = 6
+    x = torch.randn(2 * F, 16, 16, 4, generator=g).to(cuda, torch.bfloat16)
+    ctx = torch.randn(2, 77, 64, generator=g).to(cuda, torch.bfloat16)
+    t = torch.tensor([300.0], device=cuda)
+    with torch.no_grad():
+        y = m(x, t, ctx, frames=F)
+        ops.set_reference_ops(True)
+        try:
+            r = m(x, t, ctx, frames=F)
+        finally:
+            ops.set_reference_ops(False)
+    assert _rel(y, r) < 5e-2
+
+
+def test_zeroscope_full_arch_small_mp4(cuda):
+    pipe = build_pipeline("zeroscopev2xl", device=cuda)
+    inp = {"prompt": "arbius test cat", "num_frames": 8, "width": 256, "height": 256, "num_inference_steps": 2,
+           "seed": 11, "fps": 8}
+    a, b = pipe.solve(inp), pipe.solve(inp)
+    assert ops.native_loaded()
+    assert a.files[0][0] == "out-1.mp4" and a.cid == b.cid, "video solutions must be deterministic"
