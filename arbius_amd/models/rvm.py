@@ -1,0 +1,348 @@
+"""Robust Video Matting (``templates/robust_video_matting.json``; SURVEY.md §2.6(d),
+BASELINE config #5: 1080p stream, recurrent ConvGRU as CDNA4 HIP, fp16).
+
+    frames -> (downsample to <= 512 px, ratio ~0.27 at 1080p)
+    MobileNetV3-Large encoder (dilated last stage) -> LR-ASPP        [time-batched]
+    recurrent decoder: 4 x {upsample, concat skip + pooled source, conv, ConvGRU
+                            on half the channels}                      [GRU sequential]
+    projection -> (fgr residual, alpha) -> Deep Guided Filter -> full resolution
+    output_type: "" / green-screen (composite on RVM's green), alpha-mask,
+                 foreground-mask -> deterministic MP4 (utils/mp4.py)
+
+MI355X mapping: fp16 channels-last throughout.  Everything that is not
+recurrent runs on a CHUNK of T frames at once (batch = T), so the encoder and
+the per-stage convs are wide launches; only the ConvGRU state update walks the
+time axis, as two library 3x3 convs around the fused HIP gate kernels
+(csrc/convgru.hip) - the concat(x, r*h) input of the second conv is written in
+place by the gate kernel.  BatchNorm is folded into conv biases (inference).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+CL = torch.channels_last
+GREEN = (120 / 255, 255 / 255, 155 / 255)     # RVM's green-screen background
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+# MobileNetV3-Large inverted residual table: kernel, expand, out, SE, hardswish, stride, dilation
+MBV3_LARGE = [
+    (3, 16, 16, False, False, 1, 1), (3, 64, 24, False, False, 2, 1), (3, 72, 24, False, False, 1, 1),
+    (5, 72, 40, True, False, 2, 1), (5, 120, 40, True, False, 1, 1), (5, 120, 40, True, False, 1, 1),
+    (3, 240, 80, False, True, 2, 1), (3, 200, 80, False, True, 1, 1), (3, 184, 80, False, True, 1, 1),
+    (3, 184, 80, False, True, 1, 1), (3, 480, 112, True, True, 1, 1), (3, 672, 112, True, True, 1, 1),
+    (5, 672, 160, True, True, 1, 2), (5, 960, 160, True, True, 1, 2), (5, 960, 160, True, True, 1, 2),
+]
+
+
+def _div8(v):
+    return max(8, int(v + 4) // 8 * 8)
+
+
+@dataclass
+class RVMConfig:
+    width_mult: float = 1.0
+    decoder_channels: Tuple[int, ...] = (80, 40, 32, 16)
+    aspp_channels: int = 128
+    max_side: int = 512              # auto downsample ratio = min(1, max_side / max(H, W))
+    chunk: int = 12                  # frames per time-batched chunk
+    dgf_hidden: int = 16
+
+    @staticmethod
+    def tiny():
+        return RVMConfig(width_mult=0.5, decoder_channels=(32, 16, 16, 16), aspp_channels=32, max_side=64, chunk=4)
+
+
+class ConvAct(nn.Module):
+    def __init__(self, cin, cout, k=1, stride=1, groups=1, act="relu", dilation=1, bias=True):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, k, stride, dilation * (k // 2), dilation=dilation, groups=groups, bias=bias)
+        self.act = act
+
+    def forward(self, x):
+        x = self.conv(x)
+        if self.act == "relu":
+            return F.relu(x)
+        if self.act == "hs":
+            return F.hardswish(x)
+        return x
+
+
+class SE(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        s = _div8(c // 4)
+        self.fc1 = nn.Conv2d(c, s, 1)
+        self.fc2 = nn.Conv2d(s, c, 1)
+
+    def forward(self, x):
+        w = F.adaptive_avg_pool2d(x, 1)
+        return x * F.hardsigmoid(self.fc2(F.relu(self.fc1(w))))
+
+
+class InvertedResidual(nn.Module):
+    def __init__(self, cin, k, exp, cout, se, hs, stride, dil):
+        super().__init__()
+        act = "hs" if hs else "relu"
+        self.expand = ConvAct(cin, exp, 1, act=act) if exp != cin else None
+        self.dw = ConvAct(exp, exp, k, stride, groups=exp, act=act, dilation=dil)
+        self.se = SE(exp) if se else None
+        self.project = ConvAct(exp, cout, 1, act=None)
+        self.res = stride == 1 and cin == cout
+
+    def forward(self, x):
+        h = self.expand(x) if self.expand is not None else x
+        h = self.dw(h)
+        if self.se is not None:
+            h = self.se(h)
+        h = self.project(h)
+        return x + h if self.res else h
+
+
+class MobileNetV3Encoder(nn.Module):
+    def __init__(self, width_mult=1.0):
+        super().__init__()
+        c = lambda v: _div8(v * width_mult)
+        layers: List[nn.Module] = [ConvAct(3, c(16), 3, 2, act="hs")]
+        cin = c(16)
+        for (k, e, o, se, hs, s, d) in MBV3_LARGE:
+            layers.append(InvertedResidual(cin, k, c(e), c(o), se, hs, s, d))
+            cin = c(o)
+        layers.append(ConvAct(cin, c(960) if width_mult != 1.0 else 960, 1, act="hs"))
+        self.features = nn.ModuleList(layers)
+        self.out_channels = (c(16), c(24), c(40), c(960) if width_mult != 1.0 else 960)
+
+    def forward(self, x):
+        f = self.features
+        for i in range(0, 2):
+            x = f[i](x)
+        f1 = x
+        for i in range(2, 4):
+            x = f[i](x)
+        f2 = x
+        for i in range(4, 7):
+            x = f[i](x)
+        f3 = x
+        for i in range(7, 17):
+            x = f[i](x)
+        return f1, f2, f3, x
+
+
+class LRASPP(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.aspp1 = ConvAct(cin, cout, 1, act="relu")
+        self.aspp2 = nn.Conv2d(cin, cout, 1, bias=False)
+
+    def forward(self, x):
+        return self.aspp1(x) * torch.sigmoid(self.aspp2(F.adaptive_avg_pool2d(x, 1)))
+
+
+class ConvGRU(nn.Module):
+    """h' = (1-z) h + z tanh(W_hh * [x, r h]);  [r, z] = sigmoid(W_ih * [x, h])."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.c = c
+        self.ih = nn.Conv2d(2 * c, 2 * c, 3, padding=1)
+        self.hh = nn.Conv2d(2 * c, c, 3, padding=1)
+
+    def forward(self, x, h):
+        """x [B, T, C, H, W] (time-batched chunk), h [B, C, H, W] or None -> (out [B,T,C,H,W], h)."""
+        B, T, C, H, W = x.shape
+        if h is None:
+            h = torch.zeros(B, C, H, W, dtype=x.dtype, device=x.device).contiguous(memory_format=CL)
+        outs = []
+        for t in range(T):
+            buf = torch.cat([x[:, t], h], dim=1).contiguous(memory_format=CL)   # [x | h]
+            z = ops.convgru_gates1(self.ih(buf).contiguous(memory_format=CL), h, buf, C)   # buf -> [x | r h]
+            h = ops.convgru_gates2(self.hh(buf).contiguous(memory_format=CL), h, z)
+            outs.append(h)
+        return torch.stack(outs, dim=1), h
+
+
+class _GRUHalf(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.half = c // 2
+        self.gru = ConvGRU(c // 2)
+
+    def forward(self, x, h):          # x [B, T, C, H, W]
+        a, b = x[:, :, : self.half], x[:, :, self.half:]
+        b, h = self.gru(b, h)
+        return torch.cat([a, b], dim=2), h
+
+
+def _bt(x):    # [B, T, C, H, W] -> [B*T, C, H, W] channels-last
+    B, T = x.shape[:2]
+    return x.reshape(B * T, *x.shape[2:]).contiguous(memory_format=CL)
+
+
+def _ubt(x, B):
+    return x.reshape(B, x.shape[0] // B, *x.shape[1:])
+
+
+class UpBlock(nn.Module):
+    def __init__(self, cin, cskip, csrc, cout):
+        super().__init__()
+        self.conv = ConvAct(cin + cskip + csrc, cout, 3, act="relu")
+        self.gru = _GRUHalf(cout)
+
+    def forward(self, x, f, s, h, B):
+        x = F.interpolate(x, scale_factor=2.0, mode="bilinear", align_corners=False)
+        x = x[:, :, : s.shape[2], : s.shape[3]]
+        x = self.conv(torch.cat([x, f, s], dim=1).contiguous(memory_format=CL))
+        x, h = self.gru(_ubt(x, B), h)
+        return _bt(x), h
+
+
+class RecurrentDecoder(nn.Module):
+    def __init__(self, feat: Tuple[int, ...], aspp: int, dec: Tuple[int, ...]):
+        super().__init__()
+        self.decode4 = _GRUHalf(aspp)
+        self.decode3 = UpBlock(aspp, feat[2], 3, dec[0])
+        self.decode2 = UpBlock(dec[0], feat[1], 3, dec[1])
+        self.decode1 = UpBlock(dec[1], feat[0], 3, dec[2])
+        self.out0 = ConvAct(dec[2] + 3, dec[3], 3, act="relu")
+        self.out1 = ConvAct(dec[3], dec[3], 3, act="relu")
+
+    def forward(self, s0, f1, f2, f3, f4, rec, B):
+        s1 = F.avg_pool2d(s0, 2, 2, ceil_mode=True)
+        s2 = F.avg_pool2d(s1, 2, 2, ceil_mode=True)
+        s3 = F.avg_pool2d(s2, 2, 2, ceil_mode=True)
+        x4, r4 = self.decode4(_ubt(f4, B), rec[0])
+        x3, r3 = self.decode3(_bt(x4), f3, s3, rec[1], B)
+        x2, r2 = self.decode2(x3, f2, s2, rec[2], B)
+        x1, r1 = self.decode1(x2, f1, s1, rec[3], B)
+        x = F.interpolate(x1, scale_factor=2.0, mode="bilinear", align_corners=False)
+        x = x[:, :, : s0.shape[2], : s0.shape[3]]
+        x = self.out1(self.out0(torch.cat([x, s0], dim=1).contiguous(memory_format=CL)))
+        return x, [r4, r3, r2, r1]
+
+
+class DeepGuidedFilter(nn.Module):
+    def __init__(self, hid=16):
+        super().__init__()
+        self.register_buffer("box", torch.full((4, 1, 3, 3), 1.0 / 9.0))
+        self.c1 = ConvAct(4 * 2 + hid, hid, 1, act="relu", bias=True)
+        self.c2 = ConvAct(hid, hid, 1, act="relu", bias=True)
+        self.c3 = nn.Conv2d(hid, 4, 1)
+
+    def _boxf(self, x):
+        return F.conv2d(x, self.box.to(x.dtype), padding=1, groups=4)
+
+    def forward(self, fine_src, base_src, base_fgr, base_pha, base_hid):
+        fine_x = torch.cat([fine_src, fine_src.mean(1, keepdim=True)], dim=1)
+        base_x = torch.cat([base_src, base_src.mean(1, keepdim=True)], dim=1)
+        base_y = torch.cat([base_fgr, base_pha], dim=1)
+        mean_x, mean_y = self._boxf(base_x), self._boxf(base_y)
+        cov_xy = self._boxf(base_x * base_y) - mean_x * mean_y
+        var_x = self._boxf(base_x * base_x) - mean_x * mean_x
+        A = self.c3(self.c2(self.c1(torch.cat([cov_xy, var_x, base_hid], dim=1))))
+        b = mean_y - A * mean_x
+        H, W = fine_src.shape[2:]
+        A = F.interpolate(A, (H, W), mode="bilinear", align_corners=False)
+        b = F.interpolate(b, (H, W), mode="bilinear", align_corners=False)
+        out = A * fine_x + b
+        return out[:, :3], out[:, 3:]
+
+
+class MattingNetwork(nn.Module):
+    def __init__(self, cfg: RVMConfig):
+        super().__init__()
+        self.backbone = MobileNetV3Encoder(cfg.width_mult)
+        feat = self.backbone.out_channels
+        self.aspp = LRASPP(feat[3], cfg.aspp_channels)
+        self.decoder = RecurrentDecoder(feat, cfg.aspp_channels, cfg.decoder_channels)
+        self.project = nn.Conv2d(cfg.decoder_channels[3], 4, 1)
+        self.refiner = DeepGuidedFilter(cfg.decoder_channels[3])
+        self.register_buffer("mean", torch.tensor(IMAGENET_MEAN).view(1, 3, 1, 1))
+        self.register_buffer("std", torch.tensor(IMAGENET_STD).view(1, 3, 1, 1))
+
+    def forward(self, src, rec, ratio: float):
+        """src [B, T, 3, H, W] in [0,1] -> fgr, pha [B, T, *, H, W], new recurrent state."""
+        B, T = src.shape[:2]
+        fine = _bt(src)
+        if ratio < 1.0:
+            H, W = fine.shape[2:]
+            small = F.interpolate(fine, (int(round(H * ratio)), int(round(W * ratio))), mode="bilinear",
+                                  align_corners=False, antialias=False).contiguous(memory_format=CL)
+        else:
+            small = fine
+        x = ((small - self.mean.to(small.dtype)) / self.std.to(small.dtype)).contiguous(memory_format=CL)
+        f1, f2, f3, f4 = self.backbone(x)
+        f4 = self.aspp(f4)
+        hid, rec = self.decoder(small, f1, f2, f3, f4, rec, B)
+        proj = self.project(hid)
+        fgr_res, pha = proj[:, :3], proj[:, 3:]
+        if ratio < 1.0:
+            fgr_res, pha = self.refiner(fine, small, fgr_res, pha, hid)
+        fgr = (fgr_res + fine).clamp(0.0, 1.0)
+        pha = pha.clamp(0.0, 1.0)
+        return _ubt(fgr, B), _ubt(pha, B), rec
+
+
+class RVMPipeline:
+    def __init__(self, cfg: RVMConfig = None, device="cpu", dtype=None, weight_seed: int = 0, init=True, **_):
+        self.cfg = cfg = cfg or RVMConfig()
+        self.device = torch.device(device)
+        if dtype is None:
+            dtype = torch.float16 if self.device.type == "cuda" else torch.float32
+        self.dtype = dtype
+        with torch.random.fork_rng(devices=[]):
+            torch.manual_seed(weight_seed + 7)
+            self.net = MattingNetwork(cfg)
+        self.net.requires_grad_(False)
+        self.net.to(device=self.device, dtype=dtype, memory_format=CL).eval()
+        self.timings = {}
+
+    def modules(self):
+        return {"net": self.net}
+
+    @torch.no_grad()
+    def __call__(self, frames: np.ndarray, output_type: str = "green-screen") -> np.ndarray:
+        """frames uint8 [T, H, W, 3] -> uint8 [T, H, W, 3] (composite / alpha / foreground)."""
+        t0 = time.perf_counter()
+        T, H, W, _ = frames.shape
+        ratio = min(1.0, self.cfg.max_side / max(H, W))
+        rec = [None] * 4
+        out = []
+        green = torch.tensor(GREEN, dtype=self.dtype, device=self.device).view(1, 3, 1, 1)
+        for i in range(0, T, self.cfg.chunk):
+            chunk = torch.from_numpy(np.ascontiguousarray(frames[i:i + self.cfg.chunk])).to(self.device)
+            src = (chunk.permute(0, 3, 1, 2).to(self.dtype) / 255.0)[None]     # [1, t, 3, H, W]
+            fgr, pha, rec = self.net(src, rec, ratio)
+            fgr, pha = fgr[0], pha[0]
+            if output_type == "alpha-mask":
+                img = pha.expand(-1, 3, -1, -1)
+            elif output_type == "foreground-mask":
+                img = fgr
+            else:                                   # "" and "green-screen"
+                img = fgr * pha + green * (1 - pha)
+            out.append((img.float() * 255).round().clamp(0, 255).to(torch.uint8).permute(0, 2, 3, 1).cpu())
+        res = torch.cat(out).numpy()
+        self.timings = {"matting_s": time.perf_counter() - t0}
+        return res
+
+    def solve(self, inp: dict):
+        from ..node.solver import solve_files
+        from ..utils.mp4 import encode_mp4
+        from ..utils.video_io import load_video
+        t0 = time.perf_counter()
+        frames, fps = load_video(inp["input_video"])
+        out = self(frames, inp.get("output_type") or "green-screen")
+        t1 = time.perf_counter()
+        mp4 = encode_mp4(list(out), fps)
+        tm = dict(self.timings)
+        tm.update({"infer_s": t1 - t0, "encode_cid_s": time.perf_counter() - t1})
+        return solve_files([("out-1.mp4", mp4)], tm)

@@ -134,6 +134,21 @@ def temporal_attention(q, k, v, scale=None):
     return ref.temporal_attention(q, k, v, scale)
 
 
+# --------------------------------------------------------------------------- ConvGRU
+def convgru_gates1(ih, h, cat_buf, cx):
+    """RVM ConvGRU: [r|z] = sigmoid(ih); z returned, r*h written into cat_buf[:, cx:] (fp16 HIP)."""
+    if _hip(ih):
+        return _lib.convgru_gates1(ih, h, cat_buf, cx)
+    return ref.convgru_gates1(ih, h, cat_buf, cx)
+
+
+def convgru_gates2(c, h, z):
+    """RVM ConvGRU state update h' = (1-z) h + z tanh(c) (fp16 HIP)."""
+    if _hip(c):
+        return _lib.convgru_gates2(c, h, z)
+    return ref.convgru_gates2(c, h, z)
+
+
 # --------------------------------------------------------------------------- elementwise
 def geglu(h):
     if _hip(h):

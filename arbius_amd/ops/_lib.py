@@ -35,7 +35,7 @@ _SIGS = {
     "arb_conv2d_plan": (c_int, [c_int] * 9 + [c_void_p]),
     "arb_gemm_bias_res": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p]),
     "arb_temporal_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_void_p]),
-    "arb_convgru_gates": (c_int, [c_void_p] * 5 + [c_long, c_int, c_void_p]),
+    "arb_convgru_gates": (c_int, [c_int] + [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_void_p]),
 }
 
 
@@ -201,6 +201,34 @@ def _large_head_attention(q, k, v, scale):
     s = torch.matmul(qf, kf.transpose(-1, -2)).float() * scale
     p = torch.softmax(s, dim=-1).to(q.dtype)
     return torch.matmul(p, vf).transpose(1, 2).contiguous()
+
+
+# --------------------------------------------------------------------------- ConvGRU (fp16)
+def _cl_fp16(*ts):
+    for t in ts:
+        if t.dtype != torch.float16 or not t.is_contiguous(memory_format=torch.channels_last):
+            raise TypeError("convgru kernels take fp16 channels_last NCHW tensors")
+
+
+def convgru_gates1(ih, h, cat_buf, cx):
+    """ih [N,2C,H,W] -> z [N,C,H,W]; writes sigmoid(r)*h into cat_buf[:, cx:cx+C] (in place)."""
+    _cl_fp16(ih, h, cat_buf)
+    N, C2, H, W = ih.shape
+    C = C2 // 2
+    z = torch.empty_like(h, memory_format=torch.channels_last)
+    _check(_fn("arb_convgru_gates")(1, _p(ih), _p(h), _p(z), _p(cat_buf), N * H * W, C, cat_buf.shape[1], cx,
+                                    _stream()), "convgru_gates1")
+    return z
+
+
+def convgru_gates2(c, h, z):
+    """h' = (1 - z) * h + z * tanh(c)."""
+    _cl_fp16(c, h, z)
+    N, C, H, W = c.shape
+    out = torch.empty_like(h, memory_format=torch.channels_last)
+    _check(_fn("arb_convgru_gates")(2, _p(c), _p(h), _p(z), _p(out), N * H * W, C, 0, 0, _stream()),
+           "convgru_gates2")
+    return out
 
 
 # --------------------------------------------------------------------------- elementwise

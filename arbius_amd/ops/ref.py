@@ -105,3 +105,15 @@ def temporal_attention(q, k, v, scale=None):
     qs, ks, vs = (t.permute(0, 2, 1, 3, 4).reshape(B * P, Fr, H, D) for t in (q, k, v))
     o = attention(qs, ks, vs, scale)
     return o.reshape(B, P, Fr, H, D).permute(0, 2, 1, 3, 4).contiguous()
+
+
+def convgru_gates1(ih, h, cat_buf, cx):
+    C = h.shape[1]
+    r, z = torch.sigmoid(ih[:, :C].float()), torch.sigmoid(ih[:, C:].float())
+    cat_buf[:, cx:cx + C] = (r * h.float()).to(cat_buf.dtype)
+    return z.to(h.dtype)
+
+
+def convgru_gates2(c, h, z):
+    zf = z.float()
+    return ((1 - zf) * h.float() + zf * torch.tanh(c.float())).to(h.dtype)

@@ -238,8 +238,8 @@ def _boxes(data: bytes, start: int = 0, end: int = None):
         i += size
 
 
-def read_mp4_pcm(data: bytes):
-    """Parse an MP4 written by ``encode_mp4`` back into (fps, [(Y, Cb, Cr)])."""
+def read_mp4_pcm(data: bytes, with_size: bool = False):
+    """Parse an MP4 written by ``encode_mp4`` back into (fps, [(Y, Cb, Cr)]) (+ (W, H))."""
     top = {t: (a, b) for t, a, b in _boxes(data)}
     ma, mb = top[b"moov"]
 
@@ -275,4 +275,4 @@ def read_mp4_pcm(data: bytes):
         cbp = body[:, 258:322].reshape(mbh, mbw, 8, 8).transpose(0, 2, 1, 3).reshape(H16 // 2, W16 // 2)
         crp = body[:, 322:386].reshape(mbh, mbw, 8, 8).transpose(0, 2, 1, 3).reshape(H16 // 2, W16 // 2)
         out.append((y, cbp, crp))
-    return fps, out
+    return (fps, out, (W, H)) if with_size else (fps, out)

@@ -179,3 +179,20 @@ def test_temporal_conv3x1(cuda, B, F, P, C, Co):
     y = _lib.conv2d_nhwc(x, w, b, 1, False, res)
     r = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, 1) + res.float()
     assert y.shape == r.shape and _rel(y, r) < 1e-2
+
+
+@pytest.mark.parametrize("N,C,H,W", [(1, 64, 18, 32), (2, 20, 36, 64), (1, 16, 144, 256), (3, 40, 9, 16)])
+def test_convgru_gates(cuda, N, C, H, W):
+    """RVM ConvGRU fused gates (fp16 channels-last) vs fp32 reference."""
+    torch.manual_seed(5)
+    cl = torch.channels_last
+    ih = torch.randn(N, 2 * C, H, W, device=cuda).half().contiguous(memory_format=cl)
+    h = torch.rand(N, C, H, W, device=cuda).half().contiguous(memory_format=cl)
+    buf = torch.randn(N, 2 * C, H, W, device=cuda).half().contiguous(memory_format=cl)
+    buf_r = buf.clone()
+    z = _lib.convgru_gates1(ih, h, buf, C)
+    zr = ref.convgru_gates1(ih, h, buf_r, C)
+    assert _rel(z, zr) < 2e-3 and _rel(buf, buf_r) < 2e-3
+    c = torch.randn(N, C, H, W, device=cuda).half().contiguous(memory_format=cl)
+    hn = _lib.convgru_gates2(c, h, z)
+    assert _rel(hn, ref.convgru_gates2(c, h, z)) < 2e-3

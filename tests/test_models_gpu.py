@@ -102,3 +102,13 @@ def test_zeroscope_full_arch_small_mp4(cuda):
     a, b = pipe.solve(inp), pipe.solve(inp)
     assert ops.native_loaded()
     assert a.files[0][0] == "out-1.mp4" and a.cid == b.cid, "video solutions must be deterministic"
+
+
+def test_rvm_1080p_fp16_deterministic(cuda):
+    import numpy as np
+    pipe = build_pipeline("robust_video_matting", device=cuda)
+    frames = np.random.default_rng(0).integers(0, 256, (6, 1080, 1920, 3), dtype=np.uint8)
+    a = pipe(frames, "green-screen")
+    b = pipe(frames, "green-screen")
+    assert a.shape == frames.shape and (a == b).all()
+    assert ops.native_loaded()

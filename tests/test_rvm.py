@@ -1,0 +1,65 @@
+"""Robust video matting (BASELINE config #5) on CPU: recurrence semantics,
+time-batched chunks == frame-by-frame, output types, MP4 input/output, node run."""
+import asyncio
+import json
+
+import numpy as np
+import torch
+
+from arbius_amd.models.rvm import ConvGRU, RVMConfig, RVMPipeline
+from arbius_amd.utils.mp4 import encode_mp4
+from arbius_amd.utils.video_io import load_video
+from arbius_amd.node.pool import LocalSolverPool
+
+from test_node_e2e import _full_cycle, make_miner, make_world
+
+
+def test_convgru_matches_formula():
+    torch.manual_seed(0)
+    g = ConvGRU(8).eval()
+    x = torch.randn(1, 3, 8, 5, 6)
+    out, h = g(x, None)
+    hh = torch.zeros(1, 8, 5, 6)
+    for t in range(3):
+        rz = torch.sigmoid(g.ih(torch.cat([x[:, t], hh], 1)))
+        r, z = rz[:, :8], rz[:, 8:]
+        c = torch.tanh(g.hh(torch.cat([x[:, t], r * hh], 1)))
+        hh = (1 - z) * hh + z * c
+        assert torch.allclose(out[:, t], hh, atol=1e-5)
+    assert torch.allclose(h, hh, atol=1e-5)
+
+
+def test_chunking_does_not_change_output():
+    frames = np.random.default_rng(1).integers(0, 256, (7, 72, 128, 3), dtype=np.uint8)
+    a = RVMPipeline(RVMConfig.tiny())
+    b = RVMPipeline(RVMConfig.tiny())
+    b.cfg.chunk = 1
+    oa, ob = a(frames), b(frames)
+    assert oa.shape == frames.shape
+    assert np.abs(oa.astype(int) - ob.astype(int)).max() <= 1
+
+
+def test_output_types_and_mp4_io(tmp_path):
+    frames = np.random.default_rng(2).integers(0, 256, (3, 64, 96, 3), dtype=np.uint8)
+    p = tmp_path / "in.mp4"
+    p.write_bytes(encode_mp4(list(frames), 10))
+    dec, fps = load_video(str(p))
+    assert dec.shape == frames.shape and fps == 10
+    pipe = RVMPipeline(RVMConfig.tiny())
+    alpha = pipe(dec, "alpha-mask")
+    assert (alpha[..., 0] == alpha[..., 1]).all()
+    sol = pipe.solve({"input_video": str(p), "output_type": "green-screen"})
+    sol2 = pipe.solve({"input_video": str(p), "output_type": "green-screen"})
+    assert sol.files[0][0] == "out-1.mp4" and sol.cid == sol2.cid
+
+
+def test_rvm_through_node(tmp_path):
+    frames = np.random.default_rng(3).integers(0, 256, (2, 48, 64, 3), dtype=np.uint8)
+    p = tmp_path / "v.mp4"
+    p.write_bytes(encode_mp4(list(frames), 5))
+    e, tok, mid = make_world("robust_video_matting")
+    pool = LocalSolverPool("cpu", tiny=True)
+    m = make_miner(e, mid, pool, model="robust_video_matting")
+    tid = asyncio.run(_full_cycle(e, mid, m, {"input_video": str(p), "output_type": "alpha-mask"}))
+    row = json.loads(m.db.get_task_input(tid, e.tasks[tid].cid)["data"])
+    assert pool.solve_sync(m.models[mid.lower()], tid, row).cid == e.solutions[tid].cid
