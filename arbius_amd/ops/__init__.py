@@ -25,6 +25,11 @@ from . import _lib
 
 _FORCE_REF = os.environ.get("ARBIUS_REFERENCE_OPS", "0") == "1"
 
+# Library convolutions (MIOpen: depthwise / 3-4 channel / fp16 RVM convs) must pick the
+# same deterministic solver on every call and every GPU: a solution CID is consensus.
+torch.backends.cudnn.deterministic = True
+torch.backends.cudnn.benchmark = False
+
 
 def set_reference_ops(flag: bool) -> None:
     global _FORCE_REF

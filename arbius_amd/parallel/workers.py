@@ -13,6 +13,9 @@
   task fails over to the caller's retry (another worker), and the worker is respawned
   standalone (deterministic init / safetensors load instead of the broken group) -
   elastic N -> N-1 -> N.
+* every worker has its OWN request and result queue: a process killed in the middle of
+  a queue operation can leave that queue's lock held or a truncated message in its
+  pipe, so both queues are replaced on respawn and no other worker's traffic shares them.
 On CPU the same code runs with the gloo backend (tests, world size 2).
 """
 from __future__ import annotations
@@ -102,8 +105,8 @@ class MultiGPUSolverPool:
         self.tiny = tiny
         self.weight_seed = weight_seed
         self.ctx = mp.get_context("spawn")
-        self.out_q = self.ctx.Queue()
         self.in_qs = [self.ctx.Queue() for _ in range(n)]
+        self.out_qs = [self.ctx.Queue() for _ in range(n)]
         self.procs: List[Optional[mp.Process]] = [None] * n
         self.busy: Dict[int, int] = {}           # rank -> job id
         self.idle: List[int] = []
@@ -116,20 +119,22 @@ class MultiGPUSolverPool:
             self._spawn(r, port, group=True)
         ready = 0
         t0 = time.time()
-        while ready < n:
+        pending = set(range(n))
+        while pending:
             if time.time() - t0 > start_timeout:
                 raise TimeoutError("GPU workers did not start")
-            try:
-                kind, rank, payload = self.out_q.get(timeout=1.0)
-            except pyqueue.Empty:
-                for r, p in enumerate(self.procs):
+            for r in sorted(pending):
+                try:
+                    kind, rank, payload = self.out_qs[r].get(timeout=0.2)
+                except pyqueue.Empty:
+                    p = self.procs[r]
                     if p is not None and not p.is_alive():
                         raise RuntimeError(f"GPU worker {r} died during start (exit {p.exitcode})")
-                continue
-            if kind == "ready":
-                ready += 1
-                self.idle.append(rank)
-                self.broadcast_stats[rank] = payload
+                    continue
+                if kind == "ready":
+                    pending.discard(rank)
+                    self.idle.append(rank)
+                    self.broadcast_stats[rank] = payload
         self.idle.sort()
         self._pump_task = None
 
@@ -140,7 +145,7 @@ class MultiGPUSolverPool:
     def _spawn(self, rank, port, group):
         p = self.ctx.Process(target=_worker_main, daemon=True,
                              args=(rank, self.n, port, self.device_type, self.models, self.tiny,
-                                   self.in_qs[rank], self.out_q, group, self.weight_seed))
+                                   self.in_qs[rank], self.out_qs[rank], group, self.weight_seed))
         p.start()
         self.procs[rank] = p
 
@@ -166,22 +171,23 @@ class MultiGPUSolverPool:
         else:
             fut.set_exception(RuntimeError(f"worker {rank} failed:\n{payload}"))
 
-    def _drain_nowait(self):
-        while True:
-            try:
-                self._handle(self.out_q.get_nowait())
-            except pyqueue.Empty:
-                return
+    def _drain_nowait(self) -> int:
+        n = 0
+        for q in list(self.out_qs):
+            while True:
+                try:
+                    msg = q.get_nowait()
+                except pyqueue.Empty:
+                    break
+                self._handle(msg)
+                n += 1
+        return n
 
     async def _pump(self):
-        loop = asyncio.get_running_loop()
         while self.futures:
-            try:
-                msg = await loop.run_in_executor(None, self.out_q.get, True, 0.5)
-            except pyqueue.Empty:
+            if not self._drain_nowait():
                 self._watchdog()
-                continue
-            self._handle(msg)
+                await asyncio.sleep(0.005)
 
     def _watchdog(self):
         for r, p in enumerate(self.procs):
@@ -193,8 +199,9 @@ class MultiGPUSolverPool:
                 if r in self.idle:
                     self.idle.remove(r)
                 self.restarts += 1
-                # a SIGKILLed reader can die holding its queue's lock: give the new process a fresh one
+                # a SIGKILLed process can die holding a queue lock or mid-message: fresh queues
                 self.in_qs[r] = self.ctx.Queue()
+                self.out_qs[r] = self.ctx.Queue()
                 self._spawn(r, _free_port(), group=False)   # standalone: deterministic init / load
 
     async def solve(self, model, taskid, inp):
