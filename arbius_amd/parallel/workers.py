@@ -225,6 +225,7 @@ class MultiGPUSolverPool:
         p = self.procs[rank]
         if p is not None and p.is_alive():
             p.kill()
+            p.join(30)   # deterministic injection: the worker is gone when this returns
 
     async def close(self):
         for q in self.in_qs:

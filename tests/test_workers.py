@@ -28,12 +28,20 @@ def test_two_workers_broadcast_determinism_and_failover():
             assert a.cid == b.cid == ref.cid  # same bytes on every worker
             pool.kill_worker(0)
             pool.kill_worker(1)
-            with pytest.raises(RuntimeError):
-                await asyncio.wait_for(pool.solve(MODEL, "t3", INP), 300)
-            # respawned workers come back standalone and produce the same CID
-            c = await asyncio.wait_for(pool.solve(MODEL, "t4", INP), 300)
+            # both respawn standalone (deterministic init) and produce the same CID
+            c = await asyncio.wait_for(pool.solve(MODEL, "t3", INP), 300)
             assert c.cid == ref.cid
             assert pool.restarts >= 2
+            # a worker killed while it holds a task: that task fails (caller retries elsewhere)
+            slow = dict(INP, num_inference_steps=200)
+            task = asyncio.ensure_future(pool.solve(MODEL, "t4", slow))
+            while not pool.busy:
+                await asyncio.sleep(0.005)
+            pool.kill_worker(next(iter(pool.busy)))
+            with pytest.raises(RuntimeError):
+                await asyncio.wait_for(task, 300)
+            d = await asyncio.wait_for(pool.solve(MODEL, "t5", INP), 300)
+            assert d.cid == ref.cid
         finally:
             await pool.close()
 
