@@ -1,0 +1,32 @@
+"""Build the native CPU runtime extension in-tree (``arbius_amd/native/_native*.so``).
+
+    python -m arbius_amd.native.build
+"""
+from __future__ import annotations
+
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+SRC = HERE / "src" / "native.cpp"
+
+
+def target() -> Path:
+    return HERE / ("_native" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build(force: bool = False) -> Path:
+    out = target()
+    if out.exists() and not force and out.stat().st_mtime >= SRC.stat().st_mtime:
+        return out
+    import pybind11
+    cmd = ["g++", "-O3", "-shared", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-pthread",
+           "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], str(SRC), "-lz", "-o", str(out)]
+    subprocess.run(cmd, check=True)
+    return out
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,213 @@
+// arbius_amd._native: CPU-side hot paths of the node runtime.
+//
+//  * keccak256          - Ethereum keccak (padding 0x01), used for task ids,
+//                         commitments, selectors, tx hashes (hashlib has none);
+//  * png_encode         - deterministic PNG (filter 0 rows + zlib at a fixed level):
+//                         byte-identical to utils/png.py (same zlib, same params),
+//                         without the Python-side row copy;
+//  * pcm_slice_body     - the H.264 I_PCM macroblock payload of one picture for
+//                         utils/mp4.py: RGB -> BT.601 YCbCr 4:2:0 (integer) and the
+//                         macroblock raster, multi-threaded over macroblock rows
+//                         (zeroscope 1024x576x24f: ~1 s in numpy, ~20 ms here).
+//
+// Everything is a pure function of its input (no time, no thread-count dependence:
+// each thread writes a disjoint, precomputed byte range).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace py = pybind11;
+
+// ------------------------------------------------------------------------------------ keccak
+static const uint64_t RC[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+    0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+    0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+    0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+    0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+    0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+static const int ROTC[25] = {0, 36, 3, 41, 18, 1, 44, 10, 45, 2, 62, 6, 43, 15, 61, 28, 55, 25, 21, 56, 27, 20, 39, 8, 14};  // [x*5+y]
+
+static inline uint64_t rol(uint64_t x, int n) { return n ? (x << n) | (x >> (64 - n)) : x; }
+
+static void keccak_f(uint64_t s[25]) {  // s[x + 5y]
+  for (int round = 0; round < 24; ++round) {
+    uint64_t c[5], d[5], b[25];
+    for (int x = 0; x < 5; ++x) c[x] = s[x] ^ s[x + 5] ^ s[x + 10] ^ s[x + 15] ^ s[x + 20];
+    for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ rol(c[(x + 1) % 5], 1);
+    for (int i = 0; i < 25; ++i) s[i] ^= d[i % 5];
+    for (int x = 0; x < 5; ++x)
+      for (int y = 0; y < 5; ++y) b[y + 5 * ((2 * x + 3 * y) % 5)] = rol(s[x + 5 * y], ROTC[x * 5 + y]);
+    for (int x = 0; x < 5; ++x)
+      for (int y = 0; y < 5; ++y) s[x + 5 * y] = b[x + 5 * y] ^ ((~b[(x + 1) % 5 + 5 * y]) & b[(x + 2) % 5 + 5 * y]);
+    s[0] ^= RC[round];
+  }
+}
+
+static std::string keccak256_raw(const uint8_t* p, size_t n) {
+  const size_t rate = 136;
+  uint64_t s[25] = {0};
+  std::vector<uint8_t> blk(rate);
+  size_t off = 0;
+  bool done = false;
+  while (!done) {
+    size_t take = std::min(rate, n - off);
+    std::memset(blk.data(), 0, rate);
+    std::memcpy(blk.data(), p + off, take);
+    off += take;
+    if (take < rate) {  // final (padded) block
+      blk[take] ^= 0x01;
+      blk[rate - 1] ^= 0x80;
+      done = true;
+    }
+    for (size_t i = 0; i < rate / 8; ++i) {
+      uint64_t w;
+      std::memcpy(&w, blk.data() + 8 * i, 8);
+      s[i] ^= w;
+    }
+    keccak_f(s);
+  }
+  std::string out(32, '\0');
+  std::memcpy(&out[0], s, 32);
+  return out;
+}
+
+static py::bytes keccak256(py::bytes data) {
+  std::string d = data;
+  std::string h;
+  {
+    py::gil_scoped_release nogil;
+    h = keccak256_raw(reinterpret_cast<const uint8_t*>(d.data()), d.size());
+  }
+  return py::bytes(h);
+}
+
+// ------------------------------------------------------------------------------------ PNG
+static void put_be32(std::string& s, uint32_t v) {
+  char b[4] = {char(v >> 24), char(v >> 16), char(v >> 8), char(v)};
+  s.append(b, 4);
+}
+
+static void png_chunk(std::string& out, const char* tag, const std::string& body) {
+  put_be32(out, (uint32_t)body.size());
+  std::string tb(tag, 4);
+  tb += body;
+  out += tb;
+  put_be32(out, (uint32_t)crc32(0L, reinterpret_cast<const Bytef*>(tb.data()), (uInt)tb.size()));
+}
+
+static py::bytes png_encode(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> img, int level) {
+  auto b = img.request();
+  if (b.ndim != 2 && b.ndim != 3) throw std::invalid_argument("png_encode: [H, W] or [H, W, C]");
+  const size_t h = b.shape[0], w = b.shape[1], c = b.ndim == 3 ? b.shape[2] : 1;
+  int color;
+  switch (c) {
+    case 1: color = 0; break;
+    case 3: color = 2; break;
+    case 4: color = 6; break;
+    default: throw std::invalid_argument("png_encode: C must be 1, 3 or 4");
+  }
+  const uint8_t* src = static_cast<const uint8_t*>(b.ptr);
+  std::string out;
+  {
+    py::gil_scoped_release nogil;
+    const size_t row = 1 + w * c;
+    std::vector<uint8_t> raw(h * row);
+    for (size_t y = 0; y < h; ++y) {
+      raw[y * row] = 0;  // filter type 0
+      std::memcpy(&raw[y * row + 1], src + y * w * c, w * c);
+    }
+    uLongf zn = compressBound(raw.size());
+    std::string z(zn, '\0');
+    if (compress2(reinterpret_cast<Bytef*>(&z[0]), &zn, raw.data(), raw.size(), level) != Z_OK)
+      throw std::runtime_error("zlib compress2 failed");
+    z.resize(zn);
+    out = "\x89PNG\r\n\x1a\n";
+    std::string ihdr;
+    put_be32(ihdr, (uint32_t)w);
+    put_be32(ihdr, (uint32_t)h);
+    ihdr.push_back(8);
+    ihdr.push_back((char)color);
+    ihdr.append(3, '\0');
+    png_chunk(out, "IHDR", ihdr);
+    png_chunk(out, "IDAT", z);
+    png_chunk(out, "IEND", std::string());
+  }
+  return py::bytes(out);
+}
+
+// ------------------------------------------------------------------------------------ H.264 I_PCM
+static inline uint8_t clip1(int v) { return (uint8_t)std::min(254, std::max(1, v)); }
+
+// frame: uint8 [H, W, 3] with H, W multiples of 16.  Returns the macroblock payload of the
+// slice: MB0 samples (its mb_type/alignment are in the Python-built header) followed by
+// (0x0D 0x00 + samples) for every later macroblock; 386 bytes per macroblock minus 2.
+static py::bytes pcm_slice_body(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> frame, int threads) {
+  auto b = frame.request();
+  if (b.ndim != 3 || b.shape[2] != 3) throw std::invalid_argument("pcm_slice_body: [H, W, 3]");
+  const int H = (int)b.shape[0], W = (int)b.shape[1];
+  if (H % 16 || W % 16) throw std::invalid_argument("pcm_slice_body: H, W must be multiples of 16");
+  const uint8_t* src = static_cast<const uint8_t*>(b.ptr);
+  const int mbw = W / 16, mbh = H / 16;
+  const size_t nmb = (size_t)mbw * mbh;
+  std::string out(nmb * 386 - 2, '\0');
+  {
+    py::gil_scoped_release nogil;
+    auto work = [&](int r0, int r1) {
+      for (int my = r0; my < r1; ++my) {
+        for (int mx = 0; mx < mbw; ++mx) {
+          const size_t idx = (size_t)my * mbw + mx;
+          uint8_t* dst = reinterpret_cast<uint8_t*>(&out[0]) + (idx == 0 ? 0 : idx * 386 - 2);
+          if (idx != 0) {
+            *dst++ = 0x0D;
+            *dst++ = 0x00;
+          }
+          for (int y = 0; y < 16; ++y) {
+            const uint8_t* p = src + ((size_t)(my * 16 + y) * W + mx * 16) * 3;
+            for (int x = 0; x < 16; ++x) {
+              const int r = p[3 * x], g = p[3 * x + 1], bl = p[3 * x + 2];
+              dst[y * 16 + x] = clip1(((66 * r + 129 * g + 25 * bl + 128) >> 8) + 16);
+            }
+          }
+          uint8_t* cb = dst + 256;
+          uint8_t* cr = dst + 320;
+          for (int y = 0; y < 8; ++y) {
+            const uint8_t* p0 = src + ((size_t)(my * 16 + 2 * y) * W + mx * 16) * 3;
+            const uint8_t* p1 = p0 + (size_t)W * 3;
+            for (int x = 0; x < 8; ++x) {
+              const int r = p0[6 * x] + p0[6 * x + 3] + p1[6 * x] + p1[6 * x + 3];
+              const int g = p0[6 * x + 1] + p0[6 * x + 4] + p1[6 * x + 1] + p1[6 * x + 4];
+              const int bl = p0[6 * x + 2] + p0[6 * x + 5] + p1[6 * x + 2] + p1[6 * x + 5];
+              cb[y * 8 + x] = clip1(((-38 * r - 74 * g + 112 * bl + 512) >> 10) + 128);
+              cr[y * 8 + x] = clip1(((112 * r - 94 * g - 18 * bl + 512) >> 10) + 128);
+            }
+          }
+        }
+      }
+    };
+    int nt = std::max(1, std::min(threads, mbh));
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t) {
+      const int r0 = mbh * t / nt, r1 = mbh * (t + 1) / nt;
+      pool.emplace_back(work, r0, r1);
+    }
+    for (auto& th : pool) th.join();
+  }
+  return py::bytes(out);
+}
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "arbius_amd native CPU runtime (keccak256, PNG, H.264 I_PCM payload)";
+  m.def("keccak256", &keccak256, "Ethereum keccak-256");
+  m.def("png_encode", &png_encode, py::arg("img"), py::arg("level") = 6, "deterministic filter-0 PNG");
+  m.def("pcm_slice_body", &pcm_slice_body, py::arg("frame"), py::arg("threads") = 8,
+        "H.264 I_PCM macroblock payload of one RGB frame");
+}

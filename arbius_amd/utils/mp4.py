@@ -137,13 +137,6 @@ def _pad16(frame: np.ndarray) -> np.ndarray:
 
 def encode_idr_pcm(frame: np.ndarray, idr_pic_id: int) -> bytes:
     """One RGB frame -> one IDR slice NAL of I_PCM macroblocks."""
-    y, cb, cr = rgb_to_yuv420(_pad16(frame))
-    H, W = y.shape
-    mbh, mbw = H // 16, W // 16
-    n = mbh * mbw
-    ymb = y.reshape(mbh, 16, mbw, 16).transpose(0, 2, 1, 3).reshape(n, 256)
-    cbm = cb.reshape(mbh, 8, mbw, 8).transpose(0, 2, 1, 3).reshape(n, 64)
-    crm = cr.reshape(mbh, 8, mbw, 8).transpose(0, 2, 1, 3).reshape(n, 64)
     hdr = _Bits()
     hdr.ue(0)             # first_mb_in_slice
     hdr.ue(7)             # slice_type: I (all slices)
@@ -155,11 +148,25 @@ def encode_idr_pcm(frame: np.ndarray, idr_pic_id: int) -> bytes:
     hdr.ue(1)             # disable_deblocking_filter_idc
     hdr.ue(25)            # mb_type I_PCM (first macroblock)
     hdr.align_zero()      # pcm_alignment_zero_bits
+    from .. import native
+    f16 = _pad16(frame)
+    body = native.pcm_slice_body(f16) if native.loaded else pcm_slice_body_py(f16)
+    return _nal(3, 5, _ep(hdr.bytes()) + body + b"\x80")
+
+
+def pcm_slice_body_py(frame: np.ndarray) -> bytes:
+    """Macroblock payload of one picture (reference of ``native.pcm_slice_body``):
+    MB0 samples, then ``0x0D 0x00`` (ue(25) + 7 alignment zeros) + samples per MB."""
+    y, cb, cr = rgb_to_yuv420(frame)
+    H, W = y.shape
+    mbh, mbw = H // 16, W // 16
+    n = mbh * mbw
     body = np.empty((n, 386), dtype=np.uint8)
-    body[:, 0], body[:, 1] = 0x0D, 0x00   # ue(25) + 7 alignment zeros, byte aligned
-    body[:, 2:258], body[:, 258:322], body[:, 322:386] = ymb, cbm, crm
-    payload = _ep(hdr.bytes()) + body[0, 2:].tobytes() + body[1:].tobytes() + b"\x80"
-    return _nal(3, 5, payload)
+    body[:, 0], body[:, 1] = 0x0D, 0x00
+    body[:, 2:258] = y.reshape(mbh, 16, mbw, 16).transpose(0, 2, 1, 3).reshape(n, 256)
+    body[:, 258:322] = cb.reshape(mbh, 8, mbw, 8).transpose(0, 2, 1, 3).reshape(n, 64)
+    body[:, 322:386] = cr.reshape(mbh, 8, mbw, 8).transpose(0, 2, 1, 3).reshape(n, 64)
+    return body.tobytes()[2:]
 
 
 # ------------------------------------------------------------------------------------ container

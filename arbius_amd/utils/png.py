@@ -19,7 +19,16 @@ def _chunk(tag: bytes, data: bytes) -> bytes:
 
 
 def encode_png(img: np.ndarray, level: int = 6) -> bytes:
-    """img: uint8 [H, W, 3] (RGB) or [H, W, 4] (RGBA) or [H, W] (gray)."""
+    """img: uint8 [H, W, 3] (RGB) or [H, W, 4] (RGBA) or [H, W] (gray).  Native C++
+    encoder when built (byte-identical: same zlib, same parameters)."""
+    from .. import native
+    if native.loaded and isinstance(img, np.ndarray) and img.dtype == np.uint8 and img.ndim in (2, 3):
+        return native.png_encode(img, level)
+    return encode_png_py(img, level)
+
+
+def encode_png_py(img: np.ndarray, level: int = 6) -> bytes:
+    """Python reference of ``encode_png``."""
     img = np.ascontiguousarray(img)
     if img.dtype != np.uint8:
         raise TypeError("encode_png expects uint8")

@@ -1,0 +1,34 @@
+"""Native C++ runtime (arbius_amd/native) == its Python references, byte for byte."""
+import os
+
+import numpy as np
+import pytest
+
+from arbius_amd import native
+from arbius_amd.utils.keccak import keccak256_py
+from arbius_amd.utils.mp4 import _pad16, pcm_slice_body_py
+from arbius_amd.utils.png import encode_png_py
+
+pytestmark = pytest.mark.skipif(not native.loaded, reason="native extension not built")
+
+
+def test_keccak_matches_python():
+    for n in (0, 1, 31, 135, 136, 137, 271, 272, 1000):
+        d = os.urandom(n)
+        assert native.keccak256(d) == keccak256_py(d)
+    assert native.keccak256(b"").hex() == "c5d2460186f7233c927e7db2dcc703c0e500b653ca82273b7bfad8045d85a470"
+
+
+@pytest.mark.parametrize("shape", [(64, 48, 3), (17, 5, 4), (9, 9), (512, 512, 3)])
+def test_png_matches_python(shape):
+    img = np.random.default_rng(0).integers(0, 256, shape, dtype=np.uint8)
+    for level in (1, 6, 9):
+        assert native.png_encode(img, level) == encode_png_py(img, level)
+
+
+@pytest.mark.parametrize("hw", [(16, 16), (320, 576), (90, 160), (1080, 1920)])
+def test_pcm_body_matches_python(hw):
+    f = _pad16(np.random.default_rng(1).integers(0, 256, (*hw, 3), dtype=np.uint8))
+    a = native.pcm_slice_body(f)
+    assert a == pcm_slice_body_py(f)
+    assert a == native.pcm_slice_body(f, threads=3)      # thread count never changes bytes
