@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils.trace import span
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .layers import init_weights
 from .schedulers import make_scheduler
@@ -120,25 +121,22 @@ class SD15Pipeline:
                  num_inference_steps: int = 50, guidance_scale: float = 7.5, scheduler: str = "DDIM",
                  seed: int = 0, output: str = "uint8"):
         sync = torch.cuda.synchronize if self.device.type == "cuda" else (lambda: None)
-        t0 = time.perf_counter()
-        ctx = self.encode_prompt(prompt, negative_prompt)
-        h, w = height // 8, width // 8
-        x, gen = self.initial_noise(seed, h, w, self.cfg.unet.in_channels)
-        sched = make_scheduler(scheduler, num_inference_steps)
-        x = (x * sched.init_noise_sigma).to(self.device)
-        sync()
-        t1 = time.perf_counter()
-        for i, t in enumerate(sched.timesteps):
-            xin = sched.scale_model_input(x, i).to(self.dtype)
-            eps2 = self._unet_eval(torch.cat([xin, xin]), t, ctx)
-            eps = ops.ref.cfg_combine(eps2, guidance_scale)
-            x = sched.step(eps, i, x, gen)
-        sync()
-        t2 = time.perf_counter()
-        img = self.decode(x)
-        sync()
-        t3 = time.perf_counter()
-        self.timings = {"text_s": t1 - t0, "denoise_s": t2 - t1, "vae_s": t3 - t2}
+        tm: Dict[str, float] = {}
+        with span("text_s", tm, sync):
+            ctx = self.encode_prompt(prompt, negative_prompt)
+            h, w = height // 8, width // 8
+            x, gen = self.initial_noise(seed, h, w, self.cfg.unet.in_channels)
+            sched = make_scheduler(scheduler, num_inference_steps)
+            x = (x * sched.init_noise_sigma).to(self.device)
+        with span("denoise_s", tm, sync):
+            for i, t in enumerate(sched.timesteps):
+                xin = sched.scale_model_input(x, i).to(self.dtype)
+                eps2 = self._unet_eval(torch.cat([xin, xin]), t, ctx)
+                eps = ops.ref.cfg_combine(eps2, guidance_scale)
+                x = sched.step(eps, i, x, gen)
+        with span("vae_s", tm, sync):
+            img = self.decode(x)
+        self.timings = tm
         return img
 
     @torch.no_grad()

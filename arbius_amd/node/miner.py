@@ -49,8 +49,11 @@ class Metrics:
     def inc(self, name, n=1):
         self.counters[name] = self.counters.get(name, 0) + n
 
-    def observe(self, name, seconds):
-        self.latencies.setdefault(name, []).append(seconds)
+    def observe(self, name, seconds, keep: int = 10000):
+        v = self.latencies.setdefault(name, [])
+        v.append(seconds)
+        if len(v) > keep:          # bounded window for the p50/p99 export
+            del v[: len(v) - keep]
 
     def p50(self, name):
         v = sorted(self.latencies.get(name, []))
@@ -252,6 +255,9 @@ class Miner:
         if sol is None:
             raise RuntimeError("cannot get files")
         self.metrics.observe("gpu_solve_s", time.perf_counter() - t0)
+        for k, v in (sol.timings or {}).items():       # per-stage spans from the worker
+            if isinstance(v, (int, float)):
+                self.metrics.observe(f"stage_{k}", float(v))
         self._spawn(self._pin_solution(taskid, sol))
         return sol.cid
 
@@ -286,20 +292,26 @@ class Miner:
         if not cid:
             return
         commitment = generate_commitment(self.wallet, taskid, cid)
+        t_c = time.perf_counter()
         try:
             await self.chain.signal_commitment(commitment)
         except Exception as e:  # noqa: BLE001
             log.error("Commitment submission failed %r", e)
+            self.metrics.inc("tx_failures")
             return
+        self.metrics.observe("commit_tx_s", time.perf_counter() - t_c)
 
         async def submit():
             try:
+                t_s = time.perf_counter()
                 await self.chain.submit_solution(taskid, cid)
+                self.metrics.observe("submit_tx_s", time.perf_counter() - t_s)
                 self.queue("claim", 50, self.now() + 2000 + 120, False, {"taskid": taskid})
                 self.metrics.inc("solutions_submitted")
                 self.metrics.observe("task_latency_s", time.perf_counter() - t_start)
                 return True
             except TxError as e:
+                self.metrics.inc("tx_failures")
                 ex = await self._retry(lambda: self.chain.get_solution(taskid))
                 if ex["validator"] == ZERO_ADDR:
                     raise RuntimeError(f"unknown error submitting solution for {taskid}: {e.reason}")

@@ -115,6 +115,11 @@ def make_app(db, miner=None) -> web.Application:
                     lines.append(f"arbius_{k}_p99 {vals[min(len(vals) - 1, int(len(vals) * 0.99))]:.6f}")
                     lines.append(f"arbius_{k}_count {len(vals)}")
         lines.append(f"arbius_jobs_queued {len(db.get_jobs())}")
+        if miner is not None:
+            pool = getattr(miner, "pool", None)
+            lines.append(f"arbius_gpu_workers {int(getattr(pool, 'capacity', 0) or 0)}")
+            lines.append(f"arbius_gpu_workers_busy {len(getattr(pool, 'busy', {}) or {})}")
+            lines.append(f"arbius_gpu_worker_restarts {int(getattr(pool, 'restarts', 0) or 0)}")
         return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
 
     async def health(_req):

@@ -66,9 +66,15 @@ def _gemm_ok(K, N):
 def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, temb=None):
     """Channels-last conv. x [B,H,W,Cin], w [Cout,kh,kw,Cin]; fused epilogue
     (+bias, +temb[b, n] per-batch bias, +residual)."""
-    if _hip(x) and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0 and (w.shape[1] in (1, 3) and w.shape[1] == w.shape[2]
-                                                                     or tuple(w.shape[1:3]) == (3, 1)):
-        return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride)
+    kern_ok = (w.shape[1] in (1, 3) and w.shape[1] == w.shape[2]) or tuple(w.shape[1:3]) == (3, 1)
+    if _hip(x) and kern_ok:
+        if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
+            return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride)
+        if x.shape[-1] <= 64 or w.shape[0] % 8:
+            # 3/4-channel conv_in / conv_out / SpatialNorm maps: zero-pad channels onto the MFMA
+            # kernel (a few wasted FLOPs on tiny layers) instead of a library fallback - MIOpen's
+            # deterministic mode would pick its naive direct kernel for these shapes.
+            return _padded_conv(x, w, b, padding, upsample, residual, temb, stride)
     if x.is_cuda:
         # MIOpen NHWC path (channel counts the kernel does not tile: 3/4-channel
         # conv_in / conv_out).  A permuted view of a contiguous NHWC tensor is an
@@ -88,6 +94,40 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
     if residual is not None:
         y = y + residual
     return y
+
+
+_PAD_W = {}
+
+
+def _padded_weights(w, b):
+    key = (w.data_ptr(), w._version, None if b is None else b.data_ptr())
+    hit = _PAD_W.get(key)
+    if hit is None:
+        cout, kh, kw, cin = w.shape
+        ci, co = -(-cin // 64) * 64, -(-cout // 8) * 8
+        wp = torch.zeros(co, kh, kw, ci, dtype=w.dtype, device=w.device)
+        wp[:cout, :, :, :cin] = w
+        bp = None
+        if b is not None:
+            bp = torch.zeros(co, dtype=b.dtype, device=b.device)
+            bp[:cout] = b
+        hit = _PAD_W[key] = (wp, bp)
+    return hit
+
+
+def _padded_conv(x, w, b, padding, upsample, residual, temb, stride):
+    cout, cin = w.shape[0], w.shape[-1]
+    wp, bp = _padded_weights(w, b)
+    if wp.shape[-1] != cin:
+        x = F.pad(x, (0, wp.shape[-1] - cin))
+    if wp.shape[0] != cout:
+        y = _lib.conv2d_nhwc(x, wp, bp, padding, upsample, None, None, stride)[..., :cout]
+        if temb is not None:
+            y = y + temb[:, None, None, :].to(y.dtype)
+        if residual is not None:
+            y = y + residual
+        return y.contiguous()
+    return _lib.conv2d_nhwc(x, wp, bp, padding, upsample, residual, temb, stride)
 
 
 # --------------------------------------------------------------------------- normalisation

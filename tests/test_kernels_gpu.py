@@ -196,3 +196,17 @@ def test_convgru_gates(cuda, N, C, H, W):
     c = torch.randn(N, C, H, W, device=cuda).half().contiguous(memory_format=cl)
     hn = _lib.convgru_gates2(c, h, z)
     assert _rel(hn, ref.convgru_gates2(c, h, z)) < 2e-3
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k", [(2, 64, 64, 4, 320, 3), (2, 64, 64, 320, 4, 3), (1, 96, 96, 4, 1024, 1),
+                                              (1, 128, 128, 128, 3, 3), (1, 96, 96, 4, 512, 3)])
+def test_small_channel_conv_padded_onto_mfma(cuda, B, H, W, Cin, Cout, k):
+    """conv_in / conv_out / SpatialNorm maps run on the HIP kernel via channel padding."""
+    from arbius_amd import ops
+    torch.manual_seed(6)
+    x = torch.randn(B, H, W, Cin, device=cuda).bfloat16()
+    w = (torch.randn(Cout, k, k, Cin, device=cuda) / math.sqrt(k * k * Cin)).bfloat16()
+    b = torch.randn(Cout, device=cuda).bfloat16()
+    y = ops.conv2d(x, w, b, padding=k // 2)
+    r = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, k // 2)
+    assert y.shape == r.shape and y.is_contiguous() and _rel(y, r) < 1e-2
