@@ -7,9 +7,16 @@ when the caller passes the static buffer itself).
 """
 from __future__ import annotations
 
+import contextlib
+import copy
+import threading
 from typing import Callable, Sequence
 
 import torch
+
+# Captures are serialised process-wide; "thread_local" capture mode lets other threads keep
+# launching work on their own streams while one thread captures (concurrent task streams).
+CAPTURE_LOCK = threading.Lock()
 
 
 class GraphedCall:
@@ -17,15 +24,16 @@ class GraphedCall:
         dev = example_args[0].device
         self.fn = fn
         self.inputs = [a.detach().clone() for a in example_args]
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            for _ in range(warmup):   # allocator + kernel-library load outside capture
+        with CAPTURE_LOCK:
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for _ in range(warmup):   # allocator + kernel-library load outside capture
+                    self.out = fn(*self.inputs)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self.out = fn(*self.inputs)
-        torch.cuda.current_stream(dev).wait_stream(s)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = fn(*self.inputs)
 
     def __call__(self, *args):
         for dst, src in zip(self.inputs, args):
@@ -50,3 +58,31 @@ class GraphCache:
         if g is None:
             g = self.graphs[key] = GraphedCall(self.fn, args)
         return g(*args)
+
+
+class PipelineBase:
+    """Stream-aware pipeline plumbing shared by every model family.
+
+    ``fork()`` returns a clone that SHARES the weights but owns its hipGraphs and a
+    private HIP stream: N forks solve N tasks concurrently on one GPU (their kernels
+    overlap and fill CUs a single small-latent task leaves idle).  Outputs are bitwise
+    identical to a solo run - the same kernels and plans run, only interleaved."""
+
+    stream = None
+
+    def _reset_graphs(self):
+        raise NotImplementedError
+
+    def fork(self):
+        c = copy.copy(self)
+        c._reset_graphs()
+        c.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        c.timings = {}
+        return c
+
+    def _stream_ctx(self):
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()

@@ -29,7 +29,7 @@ import torch.nn as nn
 from ..utils.png import encode_png
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .glide_unet import GlideUNet, GlideUNetConfig
-from .graphs import GraphCache
+from .graphs import GraphCache, PipelineBase
 from .layers import Linear, init_weights
 from .movq import MoVQConfig, MoVQDecoder
 from .prior import PriorConfig, PriorTransformer
@@ -66,7 +66,7 @@ class _Buffers(nn.Module):
         self.zero_img_emb.data.normal_(0.0, 0.5, generator=gen)
 
 
-class Kandinsky2Pipeline:
+class Kandinsky2Pipeline(PipelineBase):
     def __init__(self, cfg: Kandinsky2Config = None, device="cpu", dtype=None, weight_seed: int = 0,
                  use_graphs: Optional[bool] = None, tokenizer_dir: Optional[str] = None, init=True):
         self.cfg = cfg = cfg or Kandinsky2Config()
@@ -93,6 +93,9 @@ class Kandinsky2Pipeline:
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
         self._unet = GraphCache(self.unet, self.use_graphs)
         self.timings: Dict[str, float] = {}
+
+    def _reset_graphs(self):
+        self._unet = GraphCache(self.unet, self.use_graphs)
 
     def modules(self) -> Dict[str, nn.Module]:
         return {"unet": self.unet, "movq": self.movq, "prior": self.prior, "clip": self.clip,
@@ -136,10 +139,15 @@ class Kandinsky2Pipeline:
     def __call__(self, prompt: str, width: int = 768, height: int = 768, seed: int = 0,
                  num_inference_steps: Optional[int] = None, guidance_scale: Optional[float] = None,
                  prior_cf_scale: Optional[float] = None, prior_steps: Optional[int] = None):
+        with self._stream_ctx():
+            return self._run(prompt, width, height, seed, num_inference_steps, guidance_scale, prior_cf_scale,
+                             prior_steps)
+
+    def _run(self, prompt, width, height, seed, num_inference_steps, guidance_scale, prior_cf_scale, prior_steps):
         cfg = self.cfg
         steps = num_inference_steps or cfg.num_steps
         g = cfg.guidance_scale if guidance_scale is None else guidance_scale
-        sync = torch.cuda.synchronize if self.device.type == "cuda" else (lambda: None)
+        sync = self._sync
         t0 = time.perf_counter()
         gen = torch.Generator(device="cpu").manual_seed(int(seed))
         hidden, pooled, lens = self.encode_clip(prompt)

@@ -23,6 +23,7 @@ import torch
 from .. import ops
 from ..utils.trace import span
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
+from .graphs import CAPTURE_LOCK, PipelineBase
 from .layers import init_weights
 from .schedulers import make_scheduler
 from .tokenizer import CLIPTokenizer
@@ -50,6 +51,13 @@ class _GraphedUNet:
         self.x = torch.zeros(x_shape, dtype=dtype, device=dev)
         self.t = torch.zeros(1, dtype=torch.float32, device=dev)
         self.ctx = ctx.clone()
+        CAPTURE_LOCK.acquire()
+        try:
+            self._capture(unet, dev)
+        finally:
+            CAPTURE_LOCK.release()
+
+    def _capture(self, unet, dev):
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
@@ -57,7 +65,7 @@ class _GraphedUNet:
                 self.out = unet(self.x, self.t, self.ctx)
         torch.cuda.current_stream(dev).wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = unet(self.x, self.t, self.ctx)
 
     def __call__(self, x, t, ctx):
@@ -69,7 +77,7 @@ class _GraphedUNet:
         return self.out
 
 
-class SD15Pipeline:
+class SD15Pipeline(PipelineBase):
     def __init__(self, cfg: SD15Config = None, device="cpu", dtype=None, weight_seed: int = 0,
                  use_graphs: Optional[bool] = None, tokenizer_dir: Optional[str] = None, init=True):
         self.cfg = cfg or SD15Config()
@@ -93,6 +101,9 @@ class SD15Pipeline:
 
     def modules(self):
         return {"unet": self.unet, "vae": self.vae, "text": self.text}
+
+    def _reset_graphs(self):
+        self._graphs = {}
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -120,7 +131,12 @@ class SD15Pipeline:
     def __call__(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
                  num_inference_steps: int = 50, guidance_scale: float = 7.5, scheduler: str = "DDIM",
                  seed: int = 0, output: str = "uint8"):
-        sync = torch.cuda.synchronize if self.device.type == "cuda" else (lambda: None)
+        with self._stream_ctx():
+            return self._run(prompt, negative_prompt, width, height, num_inference_steps, guidance_scale,
+                             scheduler, seed)
+
+    def _run(self, prompt, negative_prompt, width, height, num_inference_steps, guidance_scale, scheduler, seed):
+        sync = self._sync
         tm: Dict[str, float] = {}
         with span("text_s", tm, sync):
             ctx = self.encode_prompt(prompt, negative_prompt)

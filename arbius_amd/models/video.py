@@ -22,7 +22,7 @@ import torch
 
 from ..utils.mp4 import encode_mp4
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
-from .graphs import GraphCache
+from .graphs import GraphCache, PipelineBase
 from .layers import init_weights
 from .schedulers import make_scheduler
 from .tokenizer import CLIPTokenizer
@@ -63,7 +63,7 @@ class VideoConfig:
         return c
 
 
-class VideoPipeline:
+class VideoPipeline(PipelineBase):
     def __init__(self, cfg: VideoConfig = None, device="cpu", dtype=None, weight_seed: int = 0,
                  use_graphs: Optional[bool] = None, tokenizer_dir: Optional[str] = None, init=True):
         self.cfg = cfg = cfg or VideoConfig()
@@ -88,6 +88,9 @@ class VideoPipeline:
     def modules(self):
         return {"unet": self.unet, "vae": self.vae, "text": self.text}
 
+    def _reset_graphs(self):
+        self._graphs = {}
+
     def _unet(self, frames):
         if frames not in self._graphs:
             self._graphs[frames] = GraphCache(functools.partial(self.unet, frames=frames), self.use_graphs)
@@ -98,13 +101,18 @@ class VideoPipeline:
                  width: Optional[int] = None, height: Optional[int] = None,
                  num_inference_steps: Optional[int] = None, guidance_scale: Optional[float] = None,
                  seed: int = 0):
+        with self._stream_ctx():
+            return self._run(prompt, negative_prompt, num_frames, width, height, num_inference_steps,
+                             guidance_scale, seed)
+
+    def _run(self, prompt, negative_prompt, num_frames, width, height, num_inference_steps, guidance_scale, seed):
         cfg = self.cfg
         F = int(num_frames or cfg.num_frames)
         W, H = int(width or cfg.width), int(height or cfg.height)
         steps = int(num_inference_steps or cfg.num_inference_steps)
         g = cfg.guidance_scale if guidance_scale is None else float(guidance_scale)
         neg = cfg.negative_prompt if negative_prompt is None else negative_prompt
-        sync = torch.cuda.synchronize if self.device.type == "cuda" else (lambda: None)
+        sync = self._sync
         t0 = time.perf_counter()
         ids = torch.tensor([self.tokenizer(neg), self.tokenizer(prompt)], dtype=torch.long, device=self.device)
         ctx, _ = self.text(ids)                                   # [2, 77, 1024]: (uncond, cond)

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--model", default="anythingv3", choices=["anythingv3", "kandinsky2", "zeroscopev2xl", "damo"],
                     help="anythingv3 = BASELINE headline config; kandinsky2 = config #3; zeroscopev2xl = #4")
     ap.add_argument("--frames", type=int, default=24, help="video models: frames (config #4: 24)")
+    ap.add_argument("--concurrent", type=int, default=1,
+                    help="tasks solved concurrently per GPU (pipeline forks on private HIP streams)")
     ap.add_argument("--res", type=int, default=None, help="default 512 (anythingv3) / 768 (kandinsky2)")
     ap.add_argument("--denoise-steps", type=int, default=None, help="default 50 / 100")
     ap.add_argument("--scheduler", default="DPMSolverMultistep")
@@ -72,8 +74,10 @@ def main():
 
     wallet = "0x" + "11" * 20
     lat = []
+    C = max(1, args.concurrent)
+    forks = [pipe.fork() for _ in range(C)] if C > 1 else [pipe]
 
-    def one_task(i):
+    def one_task(i, pipe=pipe):
         taskid = "0x" + keccak256(f"bench-task-{rank}-{i}".encode()).hex()
         if vid:  # BASELINE config #4: 576x320x24f text-to-video
             inp = {"prompt": f"a red cat walking on a castle wall, cinematic, task {i}", "num_frames": args.frames,
@@ -108,8 +112,22 @@ def main():
         lat.append(time.perf_counter() - t0)
         return sol
 
+    from concurrent.futures import ThreadPoolExecutor
+    ex = ThreadPoolExecutor(C) if C > 1 else None
+
+    def one_step(i):
+        """One bench step = C tasks, concurrently on C pipeline forks (C = 1: one task)."""
+        if ex is None:
+            return one_task(i)
+        futs = [ex.submit(one_task, i * C + j, forks[j]) for j in range(C)]
+        return [f.result() for f in futs][-1]
+
     for i in range(args.warmup):
-        one_task(-1 - i)
+        if ex is None:
+            one_task(-1 - i)
+        else:               # capture every fork's graphs once, one after the other
+            for j in range(C):
+                one_task(-1 - i * C - j, forks[j])
     lat.clear()
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     D.barrier(dev)
@@ -117,7 +135,7 @@ def main():
     t0 = time.perf_counter()
     last = None
     for i in range(args.steps):
-        last = one_task(i)
+        last = one_step(i)
     sync()
     D.barrier(dev)
     elapsed = time.perf_counter() - t0
@@ -127,7 +145,7 @@ def main():
     p50 = statistics.median(flat) * 1000.0 if flat else float("nan")
 
     if rank == 0:
-        tasks_per_hour = n * 3600.0 * 1000.0 / ms_per_step
+        tasks_per_hour = n * C * 3600.0 * 1000.0 / ms_per_step
         out = {
             "metric": "tasks_solved_per_hour",
             "value": round(tasks_per_hour, 2),
@@ -146,7 +164,8 @@ def main():
                 "model": ("kandinsky2 (Kandinsky 2.1: prior + GLIDE UNet + MoVQ + XLM-R/CLIP text)" if k2 else
                           f"{args.model} (UNet3D + KL-VAE + OpenCLIP ViT-H text), {args.frames} frames" if vid else
                           "anythingv3 (SD1.5 UNet + KL-VAE + CLIP ViT-L/14 text)") + (" TINY" if args.tiny else ""),
-                "global_batch": n,
+                "global_batch": n * C,
+                "concurrent_tasks_per_gpu": C,
                 "seq_len": (args.res // 8) * (args.height // 8),
                 "resolution": args.res if not vid else f"{args.res}x{args.height}",
                 "denoise_steps": args.denoise_steps,

@@ -112,3 +112,21 @@ def test_rvm_1080p_fp16_deterministic(cuda):
     b = pipe(frames, "green-screen")
     assert a.shape == frames.shape and (a == b).all()
     assert ops.native_loaded()
+
+
+def test_concurrent_streams_bitwise_equal_solo(cuda):
+    """Two pipeline forks on private HIP streams, solving concurrently from two threads,
+    produce exactly the solo CIDs (hipGraph capture is thread-local and serialised)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from arbius_amd.node.solver import solve_image
+    pipe = build_pipeline("anythingv3", device=cuda)
+    inps = [{"prompt": f"cat {i}", "negative_prompt": "", "width": 256, "height": 256, "num_inference_steps": 4,
+             "guidance_scale": 7.5, "scheduler": "DPMSolverMultistep", "seed": 100 + i} for i in range(2)]
+    solo = [solve_image(pipe, inp).cid for inp in inps]
+    forks = [pipe.fork() for _ in range(2)]
+    for f, inp in zip(forks, inps):          # capture each fork's graph first
+        solve_image(f, inp)
+    with ThreadPoolExecutor(2) as ex:
+        for _ in range(3):
+            conc = list(ex.map(lambda a: solve_image(a[0], a[1]).cid, zip(forks, inps)))
+            assert conc == solo

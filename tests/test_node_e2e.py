@@ -171,3 +171,19 @@ def test_config1_full_arch_64px_2step_ddim_cpu():
            "num_inference_steps": 2, "scheduler": "DDIM"}
     # template enum has no 64 -> smallest legal 128x128 image (latent 16x16)
     asyncio.run(_full_cycle(e, mid, m, inp))
+
+
+def test_concurrent_forks_match_solo():
+    """Pipeline forks solving tasks concurrently (threads; private streams on GPU) give the
+    same bytes as a solo solve - concurrency never changes a CID."""
+    from concurrent.futures import ThreadPoolExecutor
+    from arbius_amd.models.registry import build_pipeline
+    from arbius_amd.node.solver import solve_image
+    pipe = build_pipeline("anythingv3", tiny=True)
+    inps = [{"prompt": f"cat {i}", "negative_prompt": "", "width": 128, "height": 128, "num_inference_steps": 2,
+             "guidance_scale": 7.5, "scheduler": "DDIM", "seed": 10 + i} for i in range(3)]
+    solo = [solve_image(pipe, inp).cid for inp in inps]
+    forks = [pipe.fork() for _ in range(3)]
+    with ThreadPoolExecutor(3) as ex:
+        conc = list(ex.map(lambda a: solve_image(a[0], a[1]).cid, zip(forks, inps)))
+    assert conc == solo
