@@ -39,12 +39,29 @@ FUNCS: Dict[str, Tuple[str, List[str]]] = {
     "setPaused": ("setPaused(bool)", []),
     "initiateValidatorWithdraw": ("initiateValidatorWithdraw(uint256)", ["uint256"]),
     "validatorWithdraw": ("validatorWithdraw(uint256,address)", []),
+    "cancelValidatorWithdraw": ("cancelValidatorWithdraw(uint256)", []),
+    # owner / admin (EngineV1.sol:264-383; contract/tasks/index.ts admin:* tasks)
+    "transferOwnership": ("transferOwnership(address)", []),
+    "transferTreasury": ("transferTreasury(address)", []),
+    "transferPauser": ("transferPauser(address)", []),
+    "setSolutionMineableRate": ("setSolutionMineableRate(bytes32,uint256)", []),
+    "setVersion": ("setVersion(uint256)", []),
+    "owner": ("owner()", ["address"]),
+    "treasury": ("treasury()", ["address"]),
+    "pauser": ("pauser()", ["address"]),
     # ERC20 (base token)
     "balanceOf": ("balanceOf(address)", ["uint256"]),
     "allowance": ("allowance(address,address)", ["uint256"]),
     "approve": ("approve(address,uint256)", ["bool"]),
     "transfer": ("transfer(address,uint256)", ["bool"]),
 }
+
+
+# the 10 uint256 parameter setters / getters (EngineV1.sol:313-383)
+ENGINE_PARAMS = ['validatorMinimumPercentage', 'slashAmountPercentage', 'solutionFeePercentage', 'retractionFeePercentage', 'treasuryRewardPercentage', 'minClaimSolutionTime', 'minRetractionWaitTime', 'minContestationVotePeriodTime', 'maxContestationValidatorStakeSince', 'exitValidatorMinUnlockTime']
+for _p in ENGINE_PARAMS:
+    FUNCS["set" + _p[0].upper() + _p[1:]] = ("set" + _p[0].upper() + _p[1:] + "(uint256)", [])
+    FUNCS[_p] = (_p + "()", ["uint256"])
 
 # event -> (signature, [(name, type, indexed)])
 EVENTS: Dict[str, Tuple[str, List[Tuple[str, str, bool]]]] = {

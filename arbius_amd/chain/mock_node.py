@@ -17,11 +17,18 @@ from typing import Dict
 from aiohttp import web
 
 from . import abi
-from .engine_abi import FUNCS, encode_log
+import re
+
+from .engine_abi import ENGINE_PARAMS, FUNCS, encode_log
 from .mock_engine import MockEngine, MockToken, Revert
 from .tx import decode_raw_tx
 
 TOKEN_ADDRESS = "0xe3dbc4f88eaa632ddf9708732e2832eeaa6688ab"
+DEFAULT_ETH = 10 * 10 ** 18      # every account starts funded (hardhat-node style)
+
+
+def _snake(name: str) -> str:
+    return re.sub(r"(?<!^)(?=[A-Z])", "_", name).lower()
 
 
 def _h(b: bytes) -> str:
@@ -33,6 +40,7 @@ class MockNode:
         self.engine = engine or MockEngine(MockToken())
         self.token_address = token_address.lower()
         self.nonces: Dict[str, int] = {}
+        self.eth: Dict[str, int] = {}
         self.receipts: Dict[str, dict] = {}
         self.txs: Dict[str, dict] = {}
         self.by_selector = {abi.selector(sig): (name, sig, rets) for name, (sig, rets) in FUNCS.items()}
@@ -81,6 +89,10 @@ class MockNode:
             return abi.encode(rets, [e.generate_ipfs_cid(bytes.fromhex(args[0][2:]))])
         if name == "validatorCanVote":
             return abi.encode(rets, [e.validator_can_vote(args[0], args[1])])
+        if name in ("owner", "treasury", "pauser"):
+            return abi.encode(rets, [getattr(e, name)])
+        if name in ENGINE_PARAMS:
+            return abi.encode(rets, [int(getattr(e, _snake(name)))])
         if name == "models":
             m = e.models.get(args[0].lower())
             return abi.encode(rets, [m.fee, m.addr, m.rate, m.cid] if m else [0, "0x" + "00" * 20, 0, b""])
@@ -117,7 +129,16 @@ class MockNode:
             "setPaused": lambda: e.set_paused(sender, args[0]),
             "initiateValidatorWithdraw": lambda: e.initiate_validator_withdraw(sender, args[0]),
             "validatorWithdraw": lambda: e.validator_withdraw(sender, args[0], args[1]),
+            "cancelValidatorWithdraw": lambda: e.cancel_validator_withdraw(sender, args[0]),
+            "transferOwnership": lambda: e.transfer_ownership(sender, args[0]),
+            "transferTreasury": lambda: e.transfer_treasury(sender, args[0]),
+            "transferPauser": lambda: e.transfer_pauser(sender, args[0]),
+            "setSolutionMineableRate": lambda: e.set_solution_mineable_rate(sender, args[0], args[1]),
+            "setVersion": lambda: e.set_version(sender, args[0]),
         }
+        for p in ENGINE_PARAMS:
+            setter = "set" + p[0].upper() + p[1:]
+            dispatch[setter] = (lambda p=p: e.set_param(sender, _snake(p), args[0]))
         if name not in dispatch:
             raise Revert(f"unsupported method {name}")
         dispatch[name]()
@@ -125,6 +146,8 @@ class MockNode:
     def send_raw(self, raw_hex: str) -> str:
         raw = bytes.fromhex(raw_hex[2:])
         f, sender = decode_raw_tx(raw)
+        if not f["data"]:                      # plain value transfer (send-eth)
+            return self._value_transfer(f, sender)
         if f["chain_id"] != self.engine.chain_id:
             raise ValueError("invalid chain id")
         expected = self.nonces.get(sender, 0)
@@ -155,6 +178,25 @@ class MockNode:
                          "nonce": hex(f["nonce"]), "blockNumber": hex(blk)}
         return txh
 
+    def _value_transfer(self, f, sender):
+        expected = self.nonces.get(sender, 0)
+        if f["nonce"] != expected:
+            raise ValueError("nonce mismatch")
+        self.nonces[sender] = expected + 1
+        bal = self.eth.get(sender, DEFAULT_ETH)
+        if bal < f["value"]:
+            raise ValueError("insufficient funds")
+        to = f["to"].lower()
+        self.eth[sender] = bal - f["value"]
+        self.eth[to] = self.eth.get(to, DEFAULT_ETH) + f["value"]
+        self.engine.mine(1)
+        txh = f["hash"]
+        self.receipts[txh] = {"transactionHash": txh, "status": "0x1", "blockNumber": hex(self.engine.block_number),
+                              "logs": [], "revertReason": None}
+        self.txs[txh] = {"hash": txh, "from": sender, "to": f["to"], "input": "0x", "value": hex(f["value"]),
+                         "nonce": hex(f["nonce"]), "blockNumber": hex(self.engine.block_number)}
+        return txh
+
     def get_logs(self, flt: dict):
         lo = int(flt.get("fromBlock", "0x0"), 16)
         hi_raw = flt.get("toBlock", "latest")
@@ -177,7 +219,7 @@ class MockNode:
         if method == "eth_blockNumber":
             return hex(e.block_number)
         if method == "eth_getBalance":
-            return hex(10 * 10 ** 18)
+            return hex(self.eth.get(params[0].lower(), DEFAULT_ETH))
         if method == "eth_getTransactionCount":
             return hex(self.nonces.get(params[0].lower(), 0))
         if method == "eth_gasPrice":
@@ -227,12 +269,35 @@ _LOGGABLE = {"TaskSubmitted", "TaskRetracted", "SignalCommitment", "SolutionSubm
              "ModelRegistered", "ValidatorDeposit"}
 
 
+def deploy_basic(node: "MockNode", deployer: str, engine_supply: int = 597_000 * 10 ** 18) -> dict:
+    """``scripts/003-deploy-core-basic.ts`` on the mock chain: the deployer owns the
+    engine and is treasury, the engine holds the mining supply, and kandinsky2 is
+    registered as a FREE mineable model (addr 0x..01, fee 0) with rate 1e18."""
+    from ..node.models import template_bytes
+    e, tok = node.engine, node.engine.token
+    deployer = deployer.lower()
+    e.owner = e.treasury = e.pauser = deployer
+    tok.mint(e.address, engine_supply)
+    addr = "0x" + "00" * 19 + "01"
+    mid = e.register_model(deployer, addr, 0, template_bytes("kandinsky2"))
+    e.set_solution_mineable_rate(deployer, mid, 10 ** 18)
+    return {"engineAddress": e.address, "baseTokenAddress": node.token_address,
+            "models": {"kandinsky2": {"id": mid, "mineable": True,
+                                      "params": {"addr": addr, "fee": "0", "rate": str(10 ** 18)}}}}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="local mock Arbius chain (JSON-RPC)")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8545)
+    ap.add_argument("--deploy", default=None, metavar="DEPLOYER",
+                    help="run the 003-deploy-core-basic equivalent for this deployer address")
     a = ap.parse_args(argv)
-    web.run_app(MockNode().app(), host=a.host, port=a.port)
+    node = MockNode()
+    if a.deploy:
+        import json
+        print(json.dumps(deploy_basic(node, a.deploy), indent=2), flush=True)
+    web.run_app(node.app(), host=a.host, port=a.port)
 
 
 if __name__ == "__main__":

@@ -52,6 +52,10 @@ class RpcChainClient(ChainClient):
     def engine_address(self) -> str:
         return self._engine
 
+    @property
+    def token_address(self) -> str:
+        return self.token
+
     async def rpc(self, method: str, params: list):
         r = await self.http.post(self.url, json={"jsonrpc": "2.0", "id": next(self._ids), "method": method,
                                                  "params": params})
@@ -117,9 +121,23 @@ class RpcChainClient(ChainClient):
         return bytes.fromhex(abi.decode_call(sig, data)[4][2:])
 
     # ------------------------------------------------------------------ transactions
+    async def call_sig(self, to: str, sig: str, rets: List[str], *args):
+        """Generic eth_call by signature string (operator CLI: admin/governance reads)."""
+        out = await self.rpc("eth_call", [{"to": to, "data": "0x" + abi.encode_call(sig, *args).hex()}, "latest"])
+        raw = bytes.fromhex(out[2:])
+        return abi.decode(rets, raw) if rets else []
+
+    async def send_sig(self, to: str, sig: str, *args, value: int = 0, gas: int = 1_000_000, wait: bool = True):
+        """Generic signed transaction by signature string ("" = plain value transfer)."""
+        data = abi.encode_call(sig, *args) if sig else b""
+        return await self._send_raw(to, data, gas, value, wait)
+
     async def _send(self, to: str, name: str, *args, wait: bool = True) -> str:
         sig, _ = FUNCS[name]
         data = abi.encode_call(sig, *args)
+        return await self._send_raw(to, data, GAS.get(name, 1_000_000), 0, wait)
+
+    async def _send_raw(self, to: str, data: bytes, gas: int, value: int, wait: bool) -> str:
         async with self._nonce_lock:
             if self.chain_id is None:
                 self.chain_id = int(await self.rpc("eth_chainId", []), 16)
@@ -127,10 +145,9 @@ class RpcChainClient(ChainClient):
                 self._nonce = int(await self.rpc("eth_getTransactionCount", [self.address, "pending"]), 16)
             gas_price = int(await self.rpc("eth_gasPrice", []), 16)
             if self.eip1559:
-                tx = Tx(self._nonce, to, data, GAS.get(name, 1_000_000), self.chain_id, 0, None, gas_price * 2,
-                        0)
+                tx = Tx(self._nonce, to, data, gas, self.chain_id, value, None, gas_price * 2, 0)
             else:
-                tx = Tx(self._nonce, to, data, GAS.get(name, 1_000_000), self.chain_id, 0, gas_price)
+                tx = Tx(self._nonce, to, data, gas, self.chain_id, value, gas_price)
             raw = tx.sign(self.priv)
             try:
                 txh = await self.rpc("eth_sendRawTransaction", ["0x" + raw.hex()])

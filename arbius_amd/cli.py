@@ -14,6 +14,15 @@ the operator tasks of ``contract/tasks/index.ts`` that a miner needs.
     python -m arbius_amd signal-support MODEL true -c cfg.json
     python -m arbius_amd is-paused -c cfg.json
     python -m arbius_amd submit-task MODEL '{"prompt":"..."}' --fee 0 -c cfg.json
+    python -m arbius_amd accounts | mine [N] | timetravel SECONDS -c cfg.json
+    python -m arbius_amd send-eth TO AMOUNT | transfer TO AMOUNT -c cfg.json
+    python -m arbius_amd engine-pause true|false | withdraw-fees | params -c cfg.json
+    python -m arbius_amd admin setVersion 1 | admin setSolutionMineableRate MODEL RATE -c cfg.json
+    python -m arbius_amd validator-withdraw initiate AMOUNT | cancel COUNT | withdraw COUNT -c cfg.json
+    python -m arbius_amd governance delegate|propose|vote|cancel|queue|execute|proposal ... --governor ADDR
+    python -m arbius_amd call TO 'sig(types)' 'ret,types' ARGS... | send TO 'sig(types)' ARGS... [--value ETH]
+    python -m arbius_amd explorer [--blocks 128] | task TASKID -c cfg.json
+    python -m arbius_amd pinata-gc -c cfg.json          # unpin Pinata files older than 2 h
 """
 from __future__ import annotations
 
@@ -111,6 +120,106 @@ async def _start(path: str):
         await runner.cleanup()
 
 
+def _arg(v: str):
+    """CLI argument -> ABI value: JSON for arrays/numbers/bools, else the string itself."""
+    try:
+        return json.loads(v)
+    except ValueError:
+        return v
+
+
+GOV = {  # GovernorV1 (OZ Governor + Bravo) / token votes: contract/tasks/index.ts:234-465
+    "delegate": ("token", "delegate(address)"),
+    "propose": ("governor", "propose(address[],uint256[],bytes[],string)"),
+    "vote": ("governor", "castVote(uint256,uint8)"),
+    "cancel": ("governor", "cancel(uint256)"),
+    "queue": ("governor", "queue(uint256)"),
+    "execute": ("governor", "execute(uint256)"),
+}
+
+
+async def _operator(a, c):
+    """contract/tasks/index.ts operator tasks beyond the miner's own needs."""
+    from .chain.engine_abi import ENGINE_PARAMS, FUNCS
+    eng = c.engine_address
+    if a.cmd == "accounts":
+        print(json.dumps({"address": c.address, "eth": _fmt(await c.eth_balance(c.address)),
+                          "aius": _fmt(await c.token_balance(c.address))}))
+    elif a.cmd == "mine":
+        for _ in range(a.n):
+            await c.rpc("evm_mine", [])
+        print(await c.block_number())
+    elif a.cmd == "timetravel":
+        await c.rpc("evm_increaseTime", [int(a.seconds)])
+        await c.rpc("evm_mine", [])
+        print(await c.block_number())
+    elif a.cmd == "send-eth":
+        print(await c.send_sig(a.to, "", value=int(float(a.amount) * E18), gas=21000))
+    elif a.cmd == "transfer":
+        print(await c.send_sig(c.token_address, "transfer(address,uint256)", a.to, int(float(a.amount) * E18)))
+    elif a.cmd == "engine-pause":
+        print(await c.send_sig(eng, "setPaused(bool)", a.paused.lower() in ("1", "true", "yes")))
+    elif a.cmd == "withdraw-fees":
+        print(await c.send_sig(eng, "withdrawAccruedFees()"))
+    elif a.cmd == "params":
+        out = {}
+        for p in ENGINE_PARAMS + ["version", "owner", "treasury", "pauser", "paused", "accruedFees"]:
+            sig, rets = FUNCS[p]
+            out[p] = str((await c.call_sig(eng, sig, rets))[0])
+        print(json.dumps(out, indent=1))
+    elif a.cmd == "admin":
+        if a.setter not in FUNCS:
+            raise SystemExit(f"unknown admin function {a.setter}")
+        print(await c.send_sig(eng, FUNCS[a.setter][0], *[_arg(x) for x in a.args]))
+    elif a.cmd == "validator-withdraw":
+        sig = {"initiate": "initiateValidatorWithdraw(uint256)", "cancel": "cancelValidatorWithdraw(uint256)",
+               "withdraw": "validatorWithdraw(uint256,address)"}[a.action]
+        args = [int(float(a.args[0]) * E18)] if a.action == "initiate" else [int(a.args[0])]
+        if a.action == "withdraw":
+            args.append(a.args[1] if len(a.args) > 1 else c.address)
+        print(await c.send_sig(eng, sig, *args))
+    elif a.cmd == "governance":
+        if a.action == "proposal":
+            gov = a.governor or _need_gov()
+            st = await c.call_sig(gov, "state(uint256)", ["uint8"], int(a.args[0]))
+            names = ["Pending", "Active", "Canceled", "Defeated", "Succeeded", "Queued", "Expired", "Executed"]
+            print(json.dumps({"id": a.args[0], "state": names[st[0]] if st[0] < len(names) else st[0]}))
+            return
+        target, sig = GOV[a.action]
+        to = c.token_address if target == "token" else (a.governor or _need_gov())
+        print(await c.send_sig(to, sig, *[_arg(x) for x in a.args]))
+    elif a.cmd == "call":
+        rets = [t for t in a.rets.split(",") if t]
+        print(json.dumps([str(v) for v in await c.call_sig(a.to, a.sig, rets, *[_arg(x) for x in a.args])]))
+    elif a.cmd == "send":
+        print(await c.send_sig(a.to, a.sig, *[_arg(x) for x in a.args], value=int(float(a.value) * E18)))
+    elif a.cmd == "explorer":
+        head = await c.block_number()
+        for ev in await c.get_events(max(0, head - a.n), head):
+            print(json.dumps({"block": ev.block, "event": ev.name, **{k: str(v) for k, v in ev.args.items()}}))
+    elif a.cmd == "task":
+        from .ipfs.unixfs import cid_hex_to_str
+        t = await c.get_task(a.taskid)
+        s = await c.get_solution(a.taskid)
+        k = await c.get_contestation(a.taskid)
+        out = {"task": {k2: str(v) for k2, v in t.items()}, "solution": {k2: str(v) for k2, v in s.items()},
+               "contestation": {k2: str(v) for k2, v in k.items()}}
+        cid = s.get("cid")
+        if cid and cid not in ("0x", b""):
+            h = cid if isinstance(cid, str) else "0x" + cid.hex()
+            out["solution_cid"] = cid_hex_to_str(h)
+        print(json.dumps(out, indent=1))
+    elif a.cmd == "pinata-gc":
+        from .ipfs.pin import pinata_gc
+        print(json.dumps(await pinata_gc(_cfg(a.config).ipfs.pinata.jwt)))
+    else:
+        raise SystemExit(f"unknown command {a.cmd}")
+
+
+def _need_gov():
+    raise SystemExit("--governor ADDRESS is required for governance commands")
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="arbius_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -121,13 +230,33 @@ def main(argv=None):
     p = sub.add_parser("decode-calldata"); p.add_argument("data")
     for name, extra in [("decode-tx", ["txid"]), ("model-register", ["template"]), ("validator-stake", ["amount"]),
                         ("balance", []), ("claim", ["taskid"]), ("signal-support", ["model", "support"]),
-                        ("is-paused", []), ("submit-task", ["model", "input"])]:
+                        ("is-paused", []), ("submit-task", ["model", "input"]), ("accounts", []),
+                        ("timetravel", ["seconds"]), ("send-eth", ["to", "amount"]), ("transfer", ["to", "amount"]),
+                        ("engine-pause", ["paused"]), ("withdraw-fees", []), ("params", []),
+                        ("task", ["taskid"]), ("pinata-gc", [])]:
         p = sub.add_parser(name)
         for e in extra:
             p.add_argument(e)
         p.add_argument("-c", "--config", default="MiningConfig.json")
         if name in ("model-register", "submit-task"):
             p.add_argument("--fee", default="0")
+    for name in ("mine", "explorer"):
+        p = sub.add_parser(name)
+        p.add_argument("n", nargs="?", type=int, default=1 if name == "mine" else 128)
+        p.add_argument("-c", "--config", default="MiningConfig.json")
+    for name, first in (("admin", "setter"), ("validator-withdraw", "action"), ("governance", "action")):
+        p = sub.add_parser(name)
+        p.add_argument(first)
+        p.add_argument("args", nargs="*")
+        p.add_argument("-c", "--config", default="MiningConfig.json")
+        p.add_argument("--governor", default=None)
+    p = sub.add_parser("call")
+    p.add_argument("to"); p.add_argument("sig"); p.add_argument("rets"); p.add_argument("args", nargs="*")
+    p.add_argument("-c", "--config", default="MiningConfig.json")
+    p = sub.add_parser("send")
+    p.add_argument("to"); p.add_argument("sig"); p.add_argument("args", nargs="*")
+    p.add_argument("--value", default="0")
+    p.add_argument("-c", "--config", default="MiningConfig.json")
     a = ap.parse_args(argv)
 
     if a.cmd == "start":
@@ -187,6 +316,8 @@ def main(argv=None):
                 print((await c._call(c.engine_address, "paused"))[0])
             elif a.cmd == "submit-task":
                 print(await c.submit_task(0, c.address, a.model, int(a.fee), a.input.encode()))
+            else:
+                await _operator(a, c)
         finally:
             await c.close()
 

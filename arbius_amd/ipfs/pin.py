@@ -120,6 +120,43 @@ class PinataPinner(Pinner):
         await self.client.aclose()
 
 
+async def pinata_gc(jwt: str, max_age_s: float = 7200.0, base: str = "https://api.pinata.cloud", client=None,
+                    now: float = None) -> dict:
+    """Unpin Pinata pins older than ``max_age_s`` (2 h) - the reference's (disabled)
+    ``miner/src/scripts/pinata_unpin_old_files.ts`` as one pass (run it from cron /
+    a loop).  Pages through ``/data/pinList?status=pinned`` and ``DELETE /pinning/unpin/<cid>``."""
+    import datetime
+    import time as _time
+
+    import httpx
+    own = client is None
+    client = client or httpx.AsyncClient(timeout=60.0)
+    hdr = {"Authorization": f"Bearer {jwt}"}
+    now = _time.time() if now is None else now
+    removed, kept, offset = [], 0, 0
+    try:
+        while True:
+            r = await client.get(f"{base}/data/pinList", params={"status": "pinned", "pageLimit": 1000,
+                                                                 "pageOffset": offset}, headers=hdr)
+            r.raise_for_status()
+            rows = r.json().get("rows", [])
+            if not rows:
+                break
+            for row in rows:
+                ts = datetime.datetime.fromisoformat(row["date_pinned"].replace("Z", "+00:00")).timestamp()
+                if now - ts > max_age_s:
+                    d = await client.delete(f"{base}/pinning/unpin/{row['ipfs_pin_hash']}", headers=hdr)
+                    d.raise_for_status()
+                    removed.append(row["ipfs_pin_hash"])
+                else:
+                    kept += 1
+            offset += len(rows)
+    finally:
+        if own:
+            await client.aclose()
+    return {"unpinned": len(removed), "kept": kept, "cids": removed}
+
+
 def make_pinner(cfg) -> Pinner:
     """From ``MiningConfig.ipfs`` (strategy http_client | pinata | local)."""
     s = cfg.ipfs.strategy

@@ -83,3 +83,81 @@ def test_miner_over_jsonrpc():
             await server.close()
 
     asyncio.run(go())
+
+
+def test_operator_cli_against_mock_node(tmp_path, capsys):
+    """contract/tasks/index.ts operator tasks over JSON-RPC: deploy, accounts, params,
+    admin setters, pause, send-eth, transfer, timetravel, explorer, task."""
+    import json as _json
+    import threading
+    import time as _time
+
+    from aiohttp import web as _web
+
+    from arbius_amd import cli
+    from arbius_amd.chain.mock_node import MockNode, deploy_basic
+    from arbius_amd.chain.secp256k1 import address_from_priv
+
+    key = "0x" + "42" * 32
+    me = address_from_priv(key)
+    node = MockNode()
+    info = deploy_basic(node, me)
+    node.engine.token.mint(me, 100 * 10 ** 18)
+    port = _free()
+    loop = asyncio.new_event_loop()
+    runner = _web.AppRunner(node.app())
+
+    def serve():
+        asyncio.set_event_loop(loop)
+        loop.run_until_complete(runner.setup())
+        loop.run_until_complete(_web.TCPSite(runner, "127.0.0.1", port).start())
+        loop.run_forever()
+
+    th = threading.Thread(target=serve, daemon=True)
+    th.start()
+    _time.sleep(0.5)
+    cfgp = tmp_path / "cfg.json"
+    cfgp.write_text(_json.dumps({"blockchain": {"private_key": key, "rpc_url": f"http://127.0.0.1:{port}"},
+                                 "mi355x": {"chain_id": node.engine.chain_id}}))
+    import arbius_amd.node.models as nm
+    old = dict(nm.CHAIN_CONFIG)
+    nm.CHAIN_CONFIG["engineAddress"] = node.engine.address
+    nm.CHAIN_CONFIG["baseTokenAddress"] = node.token_address
+    try:
+        c = ["-c", str(cfgp)]
+        cli.main(["params"] + c)
+        params = _json.loads(capsys.readouterr().out)
+        assert params["minClaimSolutionTime"] == "2000" and params["owner"].lower() == me.lower()
+        cli.main(["admin", "setMinClaimSolutionTime", "1500"] + c)
+        cli.main(["admin", "setVersion", "3"] + c)
+        assert node.engine.min_claim_solution_time == 1500 and node.engine.version == 3
+        cli.main(["engine-pause", "true"] + c)
+        assert node.engine.paused
+        cli.main(["engine-pause", "false"] + c)
+        other = "0x" + "99" * 20
+        cli.main(["send-eth", other, "1.5"] + c)
+        assert node.eth[other] == 10 * 10 ** 18 + 15 * 10 ** 17
+        cli.main(["transfer", other, "2"] + c)
+        assert node.engine.token.balance_of(other) == 2 * 10 ** 18
+        t0 = node.engine.timestamp
+        cli.main(["timetravel", "100"] + c)
+        assert node.engine.timestamp >= t0 + 100
+        capsys.readouterr()
+        cli.main(["explorer", "1000"] + c)
+        evs = [_json.loads(x) for x in capsys.readouterr().out.splitlines()]
+        assert any(e["event"] == "VersionChanged" for e in evs)
+        mid = info["models"]["kandinsky2"]["id"]
+        assert node.engine.models[mid.lower()].rate == 10 ** 18
+    finally:
+        nm.CHAIN_CONFIG.clear()
+        nm.CHAIN_CONFIG.update(old)
+        loop.call_soon_threadsafe(loop.stop)
+
+
+def _free():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
