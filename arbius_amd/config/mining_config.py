@@ -89,6 +89,9 @@ class MI355XConfig(_Base):
     verify_fraction: float = 0.0          # re-solve this fraction of others' solutions (Q10)
     chain_id: Optional[int] = None
     mock_chain: bool = False              # in-process MockEngine (testing / plumbing config)
+    selftest: bool = True                 # boot CID self-test (index.ts:981-1001)
+    selftest_table: Optional[str] = None  # override of config/selftest.json
+    workers_per_gpu: int = 1              # concurrent task streams per GPU (pipeline forks)
 
 
 class MiningConfig(_Base):

@@ -24,6 +24,9 @@ def _filename(model) -> str:
 class CogSolverPool:
     """``axios.post(c.ml.cog[modelid].url, {input})`` -> ``output[0]`` base64 data URI."""
 
+    hardware = "cog"
+    weights_id = "container"
+
     def __init__(self, urls: Dict[str, str], capacity: int = 1, timeout: float = 600.0):
         import httpx
         self.urls = {k.lower(): v for k, v in urls.items()}
@@ -51,6 +54,8 @@ class ReplicateSolverPool:
     """``replicate.run(owner/model:hash, {input})`` then download the output URL."""
 
     API = "https://api.replicate.com/v1/predictions"
+    hardware = "replicate"
+    weights_id = "container"
 
     def __init__(self, api_token: str, capacity: int = 1, timeout: float = 600.0, poll: float = 1.0):
         import httpx

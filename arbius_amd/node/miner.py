@@ -419,10 +419,46 @@ class Miner:
         if v > MINER_VERSION:
             raise SystemExit(f"version mismatch, have miner version {MINER_VERSION} and arbius is {v}")
 
+    def _selftest_key(self) -> str:
+        arch = getattr(self.pool, "hardware", None)
+        arch = arch() if callable(arch) else (arch or "unknown")
+        weights = getattr(self.pool, "weights_id", None)
+        weights = weights() if callable(weights) else (weights or "unknown")
+        return f"{arch}/{weights}"
+
+    async def self_test(self):
+        """Boot CID self-test (miner/src/index.ts:981-1001) against a per-hardware table."""
+        from pathlib import Path
+        path = getattr(self.c.mi355x, "selftest_table", None) or str(Path(__file__).resolve().parents[1]
+                                                                       / "config" / "selftest.json")
+        table = json.loads(Path(path).read_text())
+        key = self._selftest_key()
+        for m in self.models.values():
+            entry = table.get(m.name)
+            if entry is None or not isinstance(entry, dict):
+                continue
+            inp, err, msg = hydrate_input(dict(entry["input"]), m.template)
+            if err:
+                raise SystemExit(f"self test input invalid for {m.name}: {msg}")
+            inp["seed"] = entry["input"]["seed"]
+            sol = await self.pool.solve(m, "selftest", inp)
+            want = entry.get("expected", {}).get(key)
+            if want is None:
+                log.warning("Self test %s on %s: cid %s (no pinned value for this hardware/weights)", m.name, key,
+                            sol.cid)
+            elif want.lower() != sol.cid.lower():
+                log.error("Self test %s on %s FAILED: expected %s got %s", m.name, key, want, sol.cid)
+                raise SystemExit("boot self test cid mismatch")
+            else:
+                log.info("Self test %s on %s passed (%s)", m.name, key, sol.cid)
+            self.metrics.inc("selftests_run")
+
     async def boot(self):
         self.db.clear_jobs_by_method("validatorStake")
         self.db.clear_jobs_by_method("automine")
         await self.version_check()
+        if getattr(self.c.mi355x, "selftest", False) and not self.c.evilmode:
+            await self.self_test()
         self.queue("validatorStake", 30, 0, False, {})
         if self.c.automine.enabled:
             self.queue("automine", 5, 0, False, {})

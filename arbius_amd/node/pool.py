@@ -24,6 +24,9 @@ from .solver import Solution, solve_task
 class FakeSolverPool:
     """Synthetic solver: a PNG derived from (model, input) only - deterministic like a real miner."""
 
+    hardware = "fake"
+    weights_id = "synthetic"
+
     def __init__(self, capacity: int = 1, delay: float = 0.0):
         self.capacity = capacity
         self.delay = delay
@@ -47,6 +50,16 @@ class FakeSolverPool:
         pass
 
 
+def hardware_id(device) -> str:
+    """'gfx950' for an MI355X, 'cpu' for the plumbing config (self-test table key)."""
+    import torch
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        name = getattr(torch.cuda.get_device_properties(dev), "gcnArchName", "") or "cuda"
+        return name.split(":")[0]
+    return "cpu"
+
+
 class LocalSolverPool:
     """In-process pipelines (lazily built per model) on ``device``; one solve at a time."""
 
@@ -64,6 +77,15 @@ class LocalSolverPool:
             if model.name not in self.pipes:
                 self.pipes[model.name] = self.factory(model.name, device=self.device, **self.factory_kw)
             return self.pipes[model.name]
+
+    def hardware(self) -> str:
+        return hardware_id(self.device)
+
+    def weights_id(self) -> str:
+        wd = self.factory_kw.get("weights_dir")
+        base = f"safetensors:{wd.rstrip('/').split('/')[-1]}" if wd else \
+            f"random-init-seed{self.factory_kw.get('weight_seed', 0)}"
+        return base + ("-tiny" if self.factory_kw.get("tiny") else "")
 
     def solve_sync(self, model, taskid, inp) -> Solution:
         pipe = self._pipe(model)

@@ -138,6 +138,13 @@ class MultiGPUSolverPool:
         self.idle.sort()
         self._pump_task = None
 
+    def hardware(self) -> str:
+        from ..node.pool import hardware_id
+        return hardware_id("cuda:0" if self.device_type == "cuda" else "cpu")
+
+    def weights_id(self) -> str:
+        return f"random-init-seed{self.weight_seed}" + ("-tiny" if self.tiny else "")
+
     @property
     def capacity(self) -> int:
         return sum(1 for p in self.procs if p is not None and p.is_alive())

@@ -32,6 +32,7 @@ def make_world(model="anythingv3", supply_engine=597000):
 
 
 def make_miner(e, mid, pool, addr=MINER, model="anythingv3", **cfg_over):
+    cfg_over.setdefault("mi355x", {"selftest": False})
     cfg = MiningConfig.from_dict({"db_path": ":memory:", "evilmode": False, **cfg_over})
     m = Miner(cfg, DB(":memory:"), MockChainClient(e, addr), LocalPinner(), pool,
               default_models({model: mid}), clock=lambda: e.timestamp, retry_sleep=lambda s: asyncio.sleep(0))
@@ -187,3 +188,23 @@ def test_concurrent_forks_match_solo():
     with ThreadPoolExecutor(3) as ex:
         conc = list(ex.map(lambda a: solve_image(a[0], a[1]).cid, zip(forks, inps)))
     assert conc == solo
+
+
+def test_boot_selftest_pins_per_hardware_cid(tmp_path):
+    """Boot self-test: unknown hardware/weights key -> computed CID logged; pinned key with a
+    wrong CID -> the node refuses to start (miner/src/index.ts:995-1000)."""
+    e, tok, mid = make_world("kandinsky2")
+    pool = FakeSolverPool()
+    m = make_miner(e, mid, pool, model="kandinsky2", mi355x={"selftest": True})
+    asyncio.run(m.boot())
+    assert m.metrics.counters["selftests_run"] == 1
+    got = pool.calls[-1]
+    assert got[2]["prompt"] == "arbius test cat" and got[2]["seed"] == 1337 and got[2]["width"] == 768
+    table = {"kandinsky2": {"input": {"prompt": "arbius test cat", "seed": 1337},
+                            "expected": {"fake/synthetic": "0x1220" + "00" * 32}}}
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(table))
+    m2 = make_miner(e, mid, FakeSolverPool(), model="kandinsky2",
+                    mi355x={"selftest": True, "selftest_table": str(p)})
+    with pytest.raises(SystemExit):
+        asyncio.run(m2.boot())
