@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import asyncio
 import hashlib
+import queue
 import threading
 from typing import Callable, Dict, Optional
 
@@ -61,22 +62,30 @@ def hardware_id(device) -> str:
 
 
 class LocalSolverPool:
-    """In-process pipelines (lazily built per model) on ``device``; one solve at a time."""
+    """In-process pipelines (lazily built per model) on ``device``.  ``capacity`` > 1 runs
+    that many solves concurrently on pipeline forks (shared weights, private HIP stream
+    and hipGraphs each) - concurrency never changes a solution's bytes."""
 
     def __init__(self, device="cpu", pipeline_factory: Callable = None, capacity: int = 1, **factory_kw):
         from ..models.registry import build_pipeline
         self.device = device
-        self.capacity = capacity
+        self.capacity = max(1, int(capacity))
         self.factory = pipeline_factory or build_pipeline
         self.factory_kw = factory_kw
         self.pipes: Dict[str, object] = {}
+        self._free: Dict[str, "queue.Queue"] = {}
         self._lock = threading.Lock()
 
     def _pipe(self, model):
         with self._lock:
             if model.name not in self.pipes:
-                self.pipes[model.name] = self.factory(model.name, device=self.device, **self.factory_kw)
-            return self.pipes[model.name]
+                base = self.factory(model.name, device=self.device, **self.factory_kw)
+                self.pipes[model.name] = base
+                q = queue.Queue()
+                for _ in range(self.capacity):
+                    q.put(base if self.capacity == 1 or not hasattr(base, "fork") else base.fork())
+                self._free[model.name] = q
+            return self._free[model.name]
 
     def hardware(self) -> str:
         return hardware_id(self.device)
@@ -88,8 +97,12 @@ class LocalSolverPool:
         return base + ("-tiny" if self.factory_kw.get("tiny") else "")
 
     def solve_sync(self, model, taskid, inp) -> Solution:
-        pipe = self._pipe(model)
-        return solve_task(model, pipe, inp)
+        free = self._pipe(model)
+        pipe = free.get()
+        try:
+            return solve_task(model, pipe, inp)
+        finally:
+            free.put(pipe)
 
     async def solve(self, model, taskid, inp) -> Solution:
         loop = asyncio.get_running_loop()

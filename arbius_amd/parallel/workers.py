@@ -43,8 +43,11 @@ def _free_port() -> int:
 
 
 def _worker_main(rank: int, world: int, port: int, device_type: str, models: List[str], tiny: bool,
-                 in_q, out_q, group: bool, weight_seed: int):
+                 in_q, out_q, group: bool, weight_seed: int, streams: int = 1):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import queue as _queue
+    import threading
+
     import torch
     import torch.distributed as dist
 
@@ -74,20 +77,38 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 bstats["bytes"] += st["bytes"]
                 bstats["seconds"] += st["seconds"]
             pipes[name] = pipe
+        # `streams` task slots: slot k solves on its own pipeline forks (private HIP stream + graphs)
+        slots = [{n: (p if streams == 1 else p.fork()) for n, p in pipes.items()} for _ in range(streams)]
+        jobs: "_queue.Queue" = _queue.Queue()
+
+        def slot_loop(k):
+            while True:
+                msg = jobs.get()
+                if msg is None:
+                    return
+                jid, mname, kind, mid, taskid, inp = msg
+                try:
+                    t0 = time.perf_counter()
+                    sol = solve_task(Model(mid, mname, {}, True, [], kind), slots[k][mname], inp)
+                    sol.dag = None  # blocks are recomputed by the pinner; keep the message small
+                    sol.timings["worker_s"] = time.perf_counter() - t0
+                    out_q.put(("ok", jid, rank, sol))
+                except Exception:  # noqa: BLE001
+                    out_q.put(("err", jid, rank, traceback.format_exc()))
+
+        threads = [threading.Thread(target=slot_loop, args=(k,), daemon=True) for k in range(streams)]
+        for t in threads:
+            t.start()
         out_q.put(("ready", rank, bstats))
         while True:
             msg = in_q.get()
             if msg is None:
                 break
-            jid, mname, kind, mid, taskid, inp = msg
-            try:
-                t0 = time.perf_counter()
-                sol = solve_task(Model(mid, mname, {}, True, [], kind), pipes[mname], inp)
-                sol.dag = None  # blocks are recomputed by the pinner; keep the message small
-                sol.timings["worker_s"] = time.perf_counter() - t0
-                out_q.put(("ok", jid, rank, sol))
-            except Exception:  # noqa: BLE001
-                out_q.put(("err", jid, rank, traceback.format_exc()))
+            jobs.put(msg)
+        for _ in threads:
+            jobs.put(None)
+        for t in threads:
+            t.join()
     finally:
         if group and world > 1 and dist.is_initialized():
             try:
@@ -98,7 +119,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
 
 class MultiGPUSolverPool:
     def __init__(self, n: int, models: List[str], device_type: str = "cuda", tiny: bool = False,
-                 weight_seed: int = 0, start_timeout: float = 1800.0):
+                 weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1):
         self.n = n
         self.models = models
         self.device_type = device_type
@@ -108,8 +129,9 @@ class MultiGPUSolverPool:
         self.in_qs = [self.ctx.Queue() for _ in range(n)]
         self.out_qs = [self.ctx.Queue() for _ in range(n)]
         self.procs: List[Optional[mp.Process]] = [None] * n
-        self.busy: Dict[int, int] = {}           # rank -> job id
-        self.idle: List[int] = []
+        self.streams = max(1, int(streams_per_gpu))
+        self.busy: Dict[int, int] = {}           # job id -> rank
+        self.idle: List[int] = []                # one entry per free task slot (rank repeated)
         self.futures: Dict[int, asyncio.Future] = {}
         self._ids = itertools.count(1)
         self.broadcast_stats = {}
@@ -133,7 +155,7 @@ class MultiGPUSolverPool:
                     continue
                 if kind == "ready":
                     pending.discard(rank)
-                    self.idle.append(rank)
+                    self.idle.extend([rank] * self.streams)
                     self.broadcast_stats[rank] = payload
         self.idle.sort()
         self._pump_task = None
@@ -147,12 +169,12 @@ class MultiGPUSolverPool:
 
     @property
     def capacity(self) -> int:
-        return sum(1 for p in self.procs if p is not None and p.is_alive())
+        return self.streams * sum(1 for p in self.procs if p is not None and p.is_alive())
 
     def _spawn(self, rank, port, group):
         p = self.ctx.Process(target=_worker_main, daemon=True,
                              args=(rank, self.n, port, self.device_type, self.models, self.tiny,
-                                   self.in_qs[rank], self.out_qs[rank], group, self.weight_seed))
+                                   self.in_qs[rank], self.out_qs[rank], group, self.weight_seed, self.streams))
         p.start()
         self.procs[rank] = p
 
@@ -163,12 +185,11 @@ class MultiGPUSolverPool:
     def _handle(self, msg):
         kind = msg[0]
         if kind == "ready":
-            if msg[1] not in self.idle:
-                self.idle.append(msg[1])
+            rank = msg[1]
+            self.idle = [r for r in self.idle if r != rank] + [rank] * self.streams
             return
         _, jid, rank, payload = msg
-        self.busy.pop(rank, None)
-        if rank not in self.idle:
+        if self.busy.pop(jid, None) is not None:
             self.idle.append(rank)
         fut = self.futures.pop(jid, None)
         if fut is None or fut.done():
@@ -199,12 +220,12 @@ class MultiGPUSolverPool:
     def _watchdog(self):
         for r, p in enumerate(self.procs):
             if p is not None and not p.is_alive():
-                log.error("GPU worker %d died (exit %s): failing its task over, respawning", r, p.exitcode)
-                jid = self.busy.pop(r, None)
-                if jid is not None and jid in self.futures:
-                    self.futures.pop(jid).set_exception(RuntimeError(f"worker {r} died"))
-                if r in self.idle:
-                    self.idle.remove(r)
+                log.error("GPU worker %d died (exit %s): failing its tasks over, respawning", r, p.exitcode)
+                for jid in [j for j, rr in self.busy.items() if rr == r]:
+                    del self.busy[jid]
+                    if jid in self.futures:
+                        self.futures.pop(jid).set_exception(RuntimeError(f"worker {r} died"))
+                self.idle = [x for x in self.idle if x != r]
                 self.restarts += 1
                 # a SIGKILLed process can die holding a queue lock or mid-message: fresh queues
                 self.in_qs[r] = self.ctx.Queue()
@@ -218,11 +239,14 @@ class MultiGPUSolverPool:
             await asyncio.sleep(0.01)
             self._watchdog()
             self._drain_nowait()
-        rank = self.idle.pop(0)
+        # least-loaded GPU first: spread concurrent tasks over GPUs before doubling up on one
+        load = {r: sum(1 for rr in self.busy.values() if rr == r) for r in set(self.idle)}
+        rank = min(set(self.idle), key=lambda r: (load[r], r))
+        self.idle.remove(rank)
         jid = next(self._ids)
         fut = asyncio.get_running_loop().create_future()
         self.futures[jid] = fut
-        self.busy[rank] = jid
+        self.busy[jid] = rank
         self.in_qs[rank].put((jid, model.name, model.kind, model.id, taskid, dict(inp)))
         self._ensure_pump()
         return await fut

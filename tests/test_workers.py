@@ -37,11 +37,29 @@ def test_two_workers_broadcast_determinism_and_failover():
             task = asyncio.ensure_future(pool.solve(MODEL, "t4", slow))
             while not pool.busy:
                 await asyncio.sleep(0.005)
-            pool.kill_worker(next(iter(pool.busy)))
+            pool.kill_worker(next(iter(pool.busy.values())))
             with pytest.raises(RuntimeError):
                 await asyncio.wait_for(task, 300)
             d = await asyncio.wait_for(pool.solve(MODEL, "t5", INP), 300)
             assert d.cid == ref.cid
+        finally:
+            await pool.close()
+
+    asyncio.run(go())
+
+
+@pytest.mark.timeout(600)
+def test_two_task_streams_per_worker():
+    """streams_per_gpu=2: one worker process serves two tasks at once on pipeline forks,
+    with the same CIDs as a solo solve."""
+    ref = [LocalSolverPool("cpu", tiny=True).solve_sync(MODEL, "t", dict(INP, seed=s)).cid for s in (1, 2)]
+
+    async def go():
+        pool = MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, streams_per_gpu=2)
+        try:
+            assert pool.capacity == 2
+            a, b = await asyncio.gather(pool.solve(MODEL, "a", dict(INP, seed=1)), pool.solve(MODEL, "b", dict(INP, seed=2)))
+            assert [a.cid, b.cid] == ref
         finally:
             await pool.close()
 
