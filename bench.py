@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--model", default="anythingv3", choices=["anythingv3", "kandinsky2", "zeroscopev2xl", "damo"],
                     help="anythingv3 = BASELINE headline config; kandinsky2 = config #3; zeroscopev2xl = #4")
     ap.add_argument("--frames", type=int, default=24, help="video models: frames (config #4: 24)")
-    ap.add_argument("--concurrent", type=int, default=1,
+    ap.add_argument("--concurrent", type=int, default=2,
                     help="tasks solved concurrently per GPU (pipeline forks on private HIP streams)")
     ap.add_argument("--res", type=int, default=None, help="default 512 (anythingv3) / 768 (kandinsky2)")
     ap.add_argument("--denoise-steps", type=int, default=None, help="default 50 / 100")
