@@ -72,16 +72,19 @@ class SSResBlock(nn.Module):
         return x
 
     def forward(self, x, emb_act):
-        h = self.norm1(x)
-        if self.up or self.down:
-            h = self._resample(h, self.up, self.down)
-            x = self._resample(x, self.up, self.down)
-        h = self.conv1(h)
-        ss = self.emb(emb_act)                                  # [B, 2C] = [scale | shift]
-        n2 = self.norm2
-        h = ops.scale_shift_norm(h, ss, n2.weight, n2.bias, n2.groups, n2.eps, silu=True)
+        if self.down:                                   # avg-pool does not commute with SiLU
+            h = self._resample(self.norm1(x), False, True)
+            x = self._resample(x, False, True)
+            h = self.conv1(h)
+        else:                                           # GN+SiLU (and nearest-up) fused into conv1
+            h = self.conv1(x, upsample=self.up, norm=self.norm1.table(x))
+            if self.up:
+                x = self._resample(x, True, False)
+        ss = self.emb(emb_act)                          # [B, 2C] = [scale | shift]
+        # scale-shift norm + SiLU folded into one per-(b, c) affine table: conv2's prologue
+        norm = self.norm2.table(h, mod=ss, one_plus=1.0, silu=True)
         skip = self.skip(x) if self.skip is not None else x
-        return self.conv2(h, residual=skip)
+        return self.conv2(h, residual=skip, norm=norm)
 
 
 class JointAttention(nn.Module):
@@ -98,7 +101,7 @@ class JointAttention(nn.Module):
     def forward(self, x, ctx):
         B, H, W, C = x.shape
         N, Hh = H * W, self.heads
-        qkv = self.qkv(self.norm(x).view(B, N, C)).view(B, N, 3, Hh, C // Hh)
+        qkv = self.qkv.forward_norm(x.view(B, N, C), self.norm.table(x)).view(B, N, 3, Hh, C // Hh)
         ckv = self.ctx_kv(ctx).view(B, ctx.shape[1], 2, Hh, C // Hh)
         k = torch.cat([ckv[:, :, 0], qkv[:, :, 1]], dim=1)
         v = torch.cat([ckv[:, :, 1], qkv[:, :, 2]], dim=1)
@@ -189,4 +192,4 @@ class GlideUNet(nn.Module):
                 h = blk.attn(h, ctx)
             if blk.upsample is not None:
                 h = blk.upsample(h, emb_act)
-        return self.conv_out(self.norm_out(h))
+        return self.conv_out(h, norm=self.norm_out.table(h))

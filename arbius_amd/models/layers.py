@@ -35,6 +35,14 @@ class Linear(nn.Module):
     def forward(self, x, residual=None):
         return ops.linear(x, self.weight, self.bias, residual=residual)
 
+    def forward_norm(self, x, norm):
+        """x [B, ..., Cin] with a GroupNorm(+SiLU) prologue from ``norm = (table, silu)`` (table per
+        batch row b): run as a 1x1 implicit-GEMM conv over the [B, 1, N, Cin] view."""
+        B, C = x.shape[0], x.shape[-1]
+        y = ops.conv2d(x.reshape(B, 1, -1, C), self.weight.view(self.cout, 1, 1, self.cin), self.bias,
+                       padding=0, norm=norm)
+        return y.view(*x.shape[:-1], self.cout)
+
 
 class Conv2d(nn.Module):
     """kxk conv, stride 1 or 2, channels-last; weight [Cout, k, k, Cin]."""
@@ -52,9 +60,10 @@ class Conv2d(nn.Module):
         if self.bias is not None:
             self.bias.data.uniform_(-bound, bound, generator=gen)
 
-    def forward(self, x, upsample=False, residual=None, temb=None):
+    def forward(self, x, upsample=False, residual=None, temb=None, norm=None):
+        """``norm = (table, silu)``: GroupNorm(+SiLU) prologue fused into the conv."""
         return ops.conv2d(x, self.weight, self.bias, stride=self.stride, padding=self.padding,
-                          upsample=upsample, residual=residual, temb=temb)
+                          upsample=upsample, residual=residual, temb=temb, norm=norm)
 
 
 class GroupNorm(nn.Module):
@@ -71,6 +80,11 @@ class GroupNorm(nn.Module):
     def forward(self, x, silu=None):
         return ops.group_norm(x, self.weight, self.bias, self.groups, self.eps,
                               self.silu if silu is None else silu)
+
+    def table(self, x, mod=None, one_plus=0.0, silu=None):
+        """(affine table, silu) for a consumer's fused GroupNorm prologue."""
+        return (ops.group_norm_table(x, self.weight, self.bias, self.groups, self.eps, mod, one_plus),
+                self.silu if silu is None else silu)
 
 
 class LayerNorm(nn.Module):

@@ -122,8 +122,7 @@ class Transformer2D(nn.Module):
 
     def forward(self, x, ctx):
         B, H, W, C = x.shape
-        h = self.norm(x).view(B, H * W, C)
-        h = self.proj_in(h)
+        h = self.proj_in.forward_norm(x.view(B, H * W, C), self.norm.table(x))  # GN fused into proj_in
         h = self.block(h, ctx)
         return self.proj_out(h, residual=x.view(B, H * W, C)).view(B, H, W, C)
 
@@ -141,10 +140,11 @@ class ResBlock(nn.Module):
 
     def forward(self, x, temb_out=None):
         """temb_out: this block's projected time embedding [B, cout] (batched GEMM)."""
-        h = self.conv1(self.norm1(x), temb=temb_out)  # time-embedding add fused in the epilogue
-        h = self.norm2(h)
+        # GroupNorm+SiLU run as the convs' operand prologue (table of per-(b, c) affines);
+        # time-embedding add and residual are fused into the epilogues.
+        h = self.conv1(x, temb=temb_out, norm=self.norm1.table(x))
         skip = self.shortcut(x) if self.shortcut is not None else x
-        return self.conv2(h, residual=skip)
+        return self.conv2(h, residual=skip, norm=self.norm2.table(h))
 
 
 class Downsample(nn.Module):
@@ -273,4 +273,4 @@ class UNet2DCondition(nn.Module):
                     h = blk.attns[i](h, ctx)
             if blk.upsample is not None:
                 h = blk.upsample(h)
-        return self.conv_out(self.norm_out(h))
+        return self.conv_out(h, norm=self.norm_out.table(h))

@@ -70,9 +70,8 @@ class TemporalConv(nn.Module):
         BF, H, W, C = x.shape
         v = x.view(BF // frames, frames, H * W, C)
         h = v
-        for i in range(4):
-            h = self.norms[i](h.reshape(BF // frames, frames * H * W, C)).view_as(v)
-            h = self.convs[i](h, residual=v if i == 3 else None)
+        for i in range(4):   # GN (per video) + SiLU fused into each (3,1,1) conv's prologue
+            h = self.convs[i](h, residual=v if i == 3 else None, norm=self.norms[i].table(h))
         return h.view(BF, H, W, C)
 
 
@@ -101,8 +100,8 @@ class TemporalTransformer(nn.Module):
     def forward(self, x, frames: int):
         BF, H, W, C = x.shape
         B, P = BF // frames, H * W
-        h = self.norm(x.view(B, frames * P, C)).view(BF * P, C)
-        h = self.proj_in(h)
+        h = self.proj_in.forward_norm(x.view(B, frames * P, C), self.norm.table(x.view(B, frames * P, C)))
+        h = h.view(BF * P, -1)
         h = self.out1(self._attn(self.norm1(h), self.qkv1, self.out1, B, frames, P), residual=h)
         h = self.out2(self._attn(self.norm2(h), self.qkv2, self.out2, B, frames, P), residual=h)
         h = self.ff(self.norm3(h), residual=h)
@@ -209,4 +208,4 @@ class UNet3DCondition(nn.Module):
                 h = self._layer(m, torch.cat([h, skips.pop()], dim=-1), temb, ctx_f, frames)
             if blk.upsample is not None:
                 h = blk.upsample(h)
-        return self.conv_out(self.norm_out(h))
+        return self.conv_out(h, norm=self.norm_out.table(h))

@@ -45,8 +45,7 @@ class VAEAttention(nn.Module):
 
     def forward(self, x):
         B, H, W, C = x.shape
-        h = self.norm(x).view(B, H * W, C)
-        qkv = self.to_qkv(h).view(B, H * W, 3, 1, C)
+        qkv = self.to_qkv.forward_norm(x.view(B, H * W, C), self.norm.table(x)).view(B, H * W, 3, 1, C)
         o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])
         return self.to_out(o.reshape(B, H * W, C), residual=x.view(B, H * W, C)).view(B, H, W, C)
 
@@ -86,4 +85,4 @@ class VAEDecoder(nn.Module):
                 h = rb(h)
             if blk.upsample is not None:
                 h = blk.upsample(h, upsample=True)
-        return self.conv_out(self.norm_out(h))
+        return self.conv_out(h, norm=self.norm_out.table(h))

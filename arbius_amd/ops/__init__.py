@@ -63,18 +63,23 @@ def _gemm_ok(K, N):
     return K % 64 == 0 and N % 8 == 0
 
 
-def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, temb=None):
+def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, temb=None, norm=None):
     """Channels-last conv. x [B,H,W,Cin], w [Cout,kh,kw,Cin]; fused epilogue
-    (+bias, +temb[b, n] per-batch bias, +residual)."""
+    (+bias, +temb[b, n] per-batch bias, +residual); ``norm = (table, silu)`` applies a
+    GroupNorm(+SiLU) prologue from ``group_norm_table`` inside the conv's operand load."""
     kern_ok = (w.shape[1] in (1, 3) and w.shape[1] == w.shape[2]) or tuple(w.shape[1:3]) == (3, 1)
     if _hip(x) and kern_ok:
+        table, nsilu = norm if norm is not None else (None, False)
         if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
-            return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride)
-        if x.shape[-1] <= 64 or w.shape[0] % 8:
+            return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride, norm=table,
+                                    norm_silu=nsilu)
+        if (x.shape[-1] <= 64 or w.shape[0] % 8) and (table is None or x.shape[-1] % 64 == 0):
             # 3/4-channel conv_in / conv_out / SpatialNorm maps: zero-pad channels onto the MFMA
             # kernel (a few wasted FLOPs on tiny layers) instead of a library fallback - MIOpen's
             # deterministic mode would pick its naive direct kernel for these shapes.
-            return _padded_conv(x, w, b, padding, upsample, residual, temb, stride)
+            return _padded_conv(x, w, b, padding, upsample, residual, temb, stride, table, nsilu)
+    if norm is not None:
+        x = apply_norm_table(x, *norm)
     if x.is_cuda:
         # MIOpen NHWC path (channel counts the kernel does not tile: 3/4-channel
         # conv_in / conv_out).  A permuted view of a contiguous NHWC tensor is an
@@ -115,22 +120,40 @@ def _padded_weights(w, b):
     return hit
 
 
-def _padded_conv(x, w, b, padding, upsample, residual, temb, stride):
+def _padded_conv(x, w, b, padding, upsample, residual, temb, stride, table=None, nsilu=False):
     cout, cin = w.shape[0], w.shape[-1]
     wp, bp = _padded_weights(w, b)
     if wp.shape[-1] != cin:
         x = F.pad(x, (0, wp.shape[-1] - cin))
     if wp.shape[0] != cout:
-        y = _lib.conv2d_nhwc(x, wp, bp, padding, upsample, None, None, stride)[..., :cout]
+        y = _lib.conv2d_nhwc(x, wp, bp, padding, upsample, None, None, stride, norm=table,
+                             norm_silu=nsilu)[..., :cout]
         if temb is not None:
             y = y + temb[:, None, None, :].to(y.dtype)
         if residual is not None:
             y = y + residual
         return y.contiguous()
-    return _lib.conv2d_nhwc(x, wp, bp, padding, upsample, residual, temb, stride)
+    return _lib.conv2d_nhwc(x, wp, bp, padding, upsample, residual, temb, stride, norm=table, norm_silu=nsilu)
 
 
 # --------------------------------------------------------------------------- normalisation
+def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
+    """GroupNorm of x as a per-(batch, channel) affine table [B, C, 2] fp32 (scale, shift) for a
+    consumer prologue (conv/GEMM); ``mod`` [B, 2C] folds the GLIDE scale-shift modulation
+    (out = GN(x) * (mod[:, :C] + one_plus) + mod[:, C:])."""
+    if _hip(x):
+        return _lib.group_norm_table(x, gamma, beta, groups, eps, mod, one_plus)
+    return ref.group_norm_table(x, gamma, beta, groups, eps, mod, one_plus)
+
+
+def apply_norm_table(x, table, silu=False):
+    """x * scale + shift (+SiLU) per (batch, channel) - the unfused form of a norm prologue."""
+    B, C = x.shape[0], x.shape[-1]
+    shape = (B,) + (1,) * (x.dim() - 2) + (C,)
+    y = x.float() * table[..., 0].reshape(shape) + table[..., 1].reshape(shape)
+    if silu:
+        y = F.silu(y)
+    return y.to(x.dtype)
 def group_norm(x, gamma, beta, groups, eps, silu=False):
     if _hip(x):
         return _lib.group_norm_nhwc(x, gamma, beta, groups, eps, silu)

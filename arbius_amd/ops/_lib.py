@@ -30,7 +30,8 @@ _SIGS = {
     "arb_flash_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_int, c_void_p]),
     "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
-    "arb_conv2d_nhwc": (c_int, [c_void_p] * 7 + [c_int] * 11 + [c_void_p]),
+    "arb_conv2d_nhwc": (c_int, [c_void_p] * 8 + [c_int] * 12 + [c_void_p]),
+    "arb_group_norm_table": (c_int, [c_void_p] * 4 + [c_float] + [c_void_p] * 2 + [c_int] * 4 + [c_float, c_void_p]),
     "arb_conv2d_workspace": (c_size_t, [c_int] * 11),
     "arb_conv2d_plan": (c_int, [c_int] * 9 + [c_void_p]),
     "arb_gemm_bias_res": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p]),
@@ -260,9 +261,31 @@ def conv_plan(B, H, W, Cin, Cout, k, pad, upsample, stride):
     return out[0], out[1]
 
 
-def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-1, split=-1):
+def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
+    """GroupNorm of x [B, *, C] as a per-(batch, channel) affine table [B, C, 2] fp32
+    (scale, shift) for a consumer prologue; ``mod`` [B, 2C] folds a scale-shift modulation."""
+    _bf16(x, gamma, beta, mod)
+    x = x.contiguous()
+    B, C = x.shape[0], x.shape[-1]
+    HW = x.numel() // (B * C)
+    if C % 8 or C // 8 > 512 or C % groups or groups > 256:
+        raise ValueError(f"group_norm_table: unsupported C={C} G={groups}")
+    if mod is not None:
+        mod = mod.contiguous()
+        if tuple(mod.shape) != (B, 2 * C):
+            raise ValueError("group_norm_table: mod must be [B, 2C]")
+    ws = torch.empty(max(16, _fn("arb_group_norm_workspace")(B, HW, C, groups)), dtype=torch.uint8, device=x.device)
+    table = torch.empty(B, C, 2, dtype=torch.float32, device=x.device)
+    _check(_fn("arb_group_norm_table")(_p(x), _p(gamma), _p(beta), _p(mod), float(one_plus), _p(ws), _p(table), B,
+                                       HW, C, groups, float(eps), _stream()), "group_norm_table")
+    return table
+
+
+def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-1, split=-1, norm=None,
+                norm_silu=False):
     """Implicit-GEMM conv (csrc/conv.hip).  x [B,H,W,Cin], w [Cout,k,k,Cin] -> [B,Ho,Wo,Cout].
-    Fused epilogue: + bias[n] + temb[b, n] + residual[m, n]."""
+    Fused epilogue: + bias[n] + temb[b, n] + residual[m, n]; optional GroupNorm(+SiLU)
+    prologue from a ``group_norm_table`` (the normalised x never hits HBM)."""
     _bf16(x, w, b, residual, temb)
     x = x.contiguous()
     w = w.contiguous()
@@ -286,11 +309,14 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
             raise ValueError("conv2d temb must be [B, Cout]")
     if b is not None and b.numel() != Cout:
         raise ValueError("conv2d bias size")
+    if norm is not None:
+        if norm.dtype != torch.float32 or tuple(norm.shape) != (B, Cin, 2) or not norm.is_contiguous():
+            raise ValueError("conv2d norm table must be contiguous fp32 [B, Cin, 2]")
     args = (B, H, W, Cin, Cout, 31 if temporal else kh, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
-    _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), *args, _stream()),
-           "conv2d")
+    _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), _p(norm), *args,
+                                  int(bool(norm_silu)), _stream()), "conv2d")
     return y
 
 

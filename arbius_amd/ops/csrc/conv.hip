@@ -31,6 +31,8 @@ struct ConvArgs {
   const bf16_t* res;    // [M, N] or null
   bf16_t* out;          // [M, N]
   float* ws;            // split-K slabs [S, M, N]
+  const float* norm;    // [B, Cin, 2] (scale, shift) GroupNorm prologue or null
+  int norm_silu;
   int B, H, W, Cin;     // input (pre-upsample)
   int Hl, Wl;           // logical input dims (after upsample)
   int Ho, Wo;
@@ -62,7 +64,11 @@ __device__ __forceinline__ void tile_coords(const ConvArgs& p, int BN, int BM, i
   }
 }
 
-template <int BN, int BM, int WN, int WM, int MINW, bool SPLIT>
+// NORM: the A operand is GroupNorm(+SiLU)(x) computed on the fly from a per-(batch, channel)
+// affine table (scale, shift) - the normalised activation is never written to HBM.  Zero
+// padding stays zero (the reference pads the NORMALISED tensor), so only in-bounds chunks
+// are transformed.
+template <int BN, int BM, int WN, int WM, int MINW, bool SPLIT, bool NORM>
 __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   constexpr int BK = 64;
   static_assert(WN * WM == 4, "4 waves");
@@ -98,10 +104,13 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   }
 
   uint4 rw[WCH], rx[XCH];
+  bool xv[XCH];
+  int lc0 = 0;
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
     const int rs = k0 / p.Cin;
     const int c0 = k0 - rs * p.Cin + cc * 8;
+    lc0 = c0;
     const int r = rs / p.kw, s = rs - (rs / p.kw) * p.kw;
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
@@ -114,9 +123,29 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
       const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
       if (p.upsample) { hi >>= 1; wi >>= 1; }
       rx[i] = ok ? ld16(p.x + (((size_t)xb[i] * p.H + hi) * p.W + wi) * p.Cin + c0) : make_uint4(0, 0, 0, 0);
+      xv[i] = ok;
+    }
+  };
+  auto norm_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      if (!xv[i]) continue;
+      const float4* t = reinterpret_cast<const float4*>(p.norm + ((size_t)xb[i] * p.Cin + lc0) * 2);
+      const float4 t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
+      const float sc[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
+      const float sh[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
+      float f[8];
+      unpack8(rx[i], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = fmaf(f[e], sc[e], sh[e]);
+        f[e] = p.norm_silu ? silu_f(v) : v;
+      }
+      rx[i] = pack8(f);
     }
   };
   auto store_tile = [&](int buf) {
+    if constexpr (NORM) norm_tile();
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       const int row = (tid >> 3) + 32 * i;
@@ -532,28 +561,34 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
     dim3 grid(p.tiles_total * pl.split);
-    if (glds) launch_glds<BN, BM, WN, WM, NS, true>(p, grid, s);
-    else conv_igemm_kernel<BN, BM, WN, WM, MINW, true><<<grid, 256, 0, s>>>(p);
+    if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, true, true><<<grid, 256, 0, s>>>(p);
+    else if (glds) launch_glds<BN, BM, WN, WM, NS, true>(p, grid, s);
+    else conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false><<<grid, 256, 0, s>>>(p);
     long work = (long)p.M * (p.N / 8);
     long blocks = (work + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
   } else {
     dim3 grid(p.tiles_total, 1);
-    if (glds) launch_glds<BN, BM, WN, WM, NS, false>(p, grid, s);
-    else conv_igemm_kernel<BN, BM, WN, WM, MINW, false><<<grid, 256, 0, s>>>(p);
+    if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, false, true><<<grid, 256, 0, s>>>(p);
+    else if (glds) launch_glds<BN, BM, WN, WM, NS, false>(p, grid, s);
+    else conv_igemm_kernel<BN, BM, WN, WM, MINW, false, false><<<grid, 256, 0, s>>>(p);
   }
 }
 
 // x [B,H,W,Cin] bf16, w [Cout, k, k, Cin], out [B,Ho,Wo,Cout]; Cin % 64 == 0, Cout % 8 == 0.
 // cfg/split = -1: planned; >= 0: forced (autotuning).
+// norm: optional [B, Cin, 2] fp32 (scale, shift) GroupNorm table applied to x in the prologue
+// (+ SiLU when norm_silu) - see arb_group_norm_table.  Register-staged kernels only.
 ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* temb, const void* res,
-                            void* out, void* ws, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
-                            int stride, int cfg, int split, hipStream_t stream) {
+                            void* out, void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k,
+                            int pad, int upsample, int stride, int cfg, int split, int norm_silu,
+                            hipStream_t stream) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
   ConvArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = (const bf16_t*)bias; a.temb = (const bf16_t*)temb;
   a.res = (const bf16_t*)res; a.out = (bf16_t*)out; a.ws = (float*)ws;
+  a.norm = (const float*)norm; a.norm_silu = norm_silu;
   conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
   const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
   if (pl.split > 1 && ws == nullptr) return -3;
@@ -586,5 +621,5 @@ ARB_API int arb_conv2d_plan(int B, int H, int W, int Cin, int Cout, int k, int p
 // Plain GEMM with fused epilogue: out[M,N] = x[M,K] W[N,K]^T (+bias +residual); K % 64 == 0.
 ARB_API int arb_gemm_bias_res(const void* x, const void* w, const void* bias, const void* res, void* out, void* ws,
                               int M, int N, int K, int cfg, int split, hipStream_t stream) {
-  return arb_conv2d_nhwc(x, w, bias, nullptr, res, out, ws, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, stream);
+  return arb_conv2d_nhwc(x, w, bias, nullptr, res, out, ws, nullptr, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, 0, stream);
 }

@@ -280,3 +280,57 @@ ARB_API int arb_group_norm_mod_nhwc(const void* x, void* y, const void* gamma, c
   if (mh <= 0 || mw <= 0 || H % mh != 0 || W % mw != 0) return -1;
   return gn_run(x, y, gamma, beta, workspace, B, H * W, C, G, eps, silu, mod, H, W, mh, mw, one_plus, stream);
 }
+
+// ---------------------------------------------------------------------------------------------
+// GroupNorm as an affine TABLE for a consumer's prologue (conv / GEMM A-operand transform):
+//   table[b, c] = (scale, shift),  GN(x)[b, p, c] = x * scale + shift
+// with an optional per-(b, c) modulation folded in (GLIDE scale-shift norm):
+//   out = GN(x) * (mod[b, c] + one_plus) + mod[b, C + c]  ->  scale *= m, shift = shift * m + t
+// Grid (G, B): the exact Chan combine of gn_finalize, then Cg threads write the group's channels.
+__global__ void __launch_bounds__(256) gn_table_kernel(const Stat* __restrict__ part, float2* __restrict__ table,
+                                                       const bf16_t* __restrict__ gamma,
+                                                       const bf16_t* __restrict__ beta,
+                                                       const bf16_t* __restrict__ mod, float one_plus, int chunks,
+                                                       int C, int G, float eps) {
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  __shared__ Stat sh[256];
+  Stat acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c = t; c < chunks; c += 256) acc = chan_combine(acc, part[((size_t)b * chunks + c) * G + g]);
+  sh[t] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) sh[t] = chan_combine(sh[t], sh[t + s]);
+    __syncthreads();
+  }
+  const Stat r = sh[0];
+  const float mean = r.mean, rstd = rsqrtf(r.m2 / fmaxf(r.n, 1.f) + eps);
+  const int Cg = C / G;
+  for (int i = t; i < Cg; i += 256) {
+    const int c = g * Cg + i;
+    float sc = rstd * bf2f(gamma[c]);
+    float sf = bf2f(beta[c]) - mean * sc;
+    if (mod) {
+      const float m = bf2f(mod[(size_t)b * 2 * C + c]) + one_plus, a = bf2f(mod[(size_t)b * 2 * C + C + c]);
+      sc *= m;
+      sf = fmaf(sf, m, a);
+    }
+    table[(size_t)b * C + c] = make_float2(sc, sf);
+  }
+}
+
+ARB_API int arb_group_norm_table(const void* x, const void* gamma, const void* beta, const void* mod, float one_plus,
+                                 void* workspace, void* table, int B, int HW, int C, int G, float eps,
+                                 hipStream_t stream) {
+  if (C % 8 != 0 || C / 8 > 512 || C % G != 0 || G > 256) return -1;
+  const int chunks = gn_chunks(HW, C);
+  Stat* part = (Stat*)workspace;
+  dim3 g1(chunks, B);
+  if (C / 8 > 256)
+    gn_stats_kernel<2><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
+  else
+    gn_stats_kernel<1><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
+  gn_table_kernel<<<dim3(G, B), 256, 0, stream>>>(part, (float2*)table, (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                  (const bf16_t*)mod, one_plus, chunks, C, G, eps);
+  return (int)hipGetLastError();
+}

@@ -61,6 +61,22 @@ def group_norm_mod_nhwc(x, gamma, beta, groups, eps, silu, mod, one_plus):
     return y.to(x.dtype)
 
 
+def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
+    """Reference of the GroupNorm affine table [B, C, 2] (scale, shift)."""
+    B, C = x.shape[0], x.shape[-1]
+    xf = x.float().reshape(B, -1, groups, C // groups)
+    mean = xf.mean(dim=(1, 3))
+    var = xf.var(dim=(1, 3), unbiased=False)
+    rstd = torch.rsqrt(var + eps)
+    cg = C // groups
+    sc = rstd.repeat_interleave(cg, dim=1) * gamma.float()[None]
+    sf = beta.float()[None] - mean.repeat_interleave(cg, dim=1) * sc
+    if mod is not None:
+        m = mod[:, :C].float() + one_plus
+        sc, sf = sc * m, sf * m + mod[:, C:].float()
+    return torch.stack([sc, sf], dim=-1).contiguous()
+
+
 def layer_norm(x, gamma, beta, eps):
     return F.layer_norm(x.float(), (x.shape[-1],), gamma.float(), beta.float(), eps).to(x.dtype)
 

@@ -210,3 +210,30 @@ def test_small_channel_conv_padded_onto_mfma(cuda, B, H, W, Cin, Cout, k):
     y = ops.conv2d(x, w, b, padding=k // 2)
     r = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, k // 2)
     assert y.shape == r.shape and y.is_contiguous() and _rel(y, r) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,k,silu,up,mod", [
+    (2, 64, 64, 320, 320, 3, True, False, False), (2, 32, 32, 640, 1280, 3, True, False, False),
+    (2, 16, 16, 2560, 1280, 3, True, False, False), (1, 48, 48, 384, 384, 3, True, True, False),
+    (2, 24, 24, 768, 768, 3, True, False, True), (2, 1, 4096, 320, 320, 1, False, False, False),
+    (2, 24, 2880, 320, 320, 31, True, False, False)])
+def test_conv_groupnorm_prologue(cuda, B, H, W, C, Co, k, silu, up, mod):
+    """GroupNorm(+SiLU, +scale-shift) fused into the conv operand load == GN then conv."""
+    from arbius_amd import ops
+    torch.manual_seed(7)
+    x = (torch.randn(B, H, W, C, device=cuda) * 2 + 0.5).bfloat16()
+    kh, kw = (3, 1) if k == 31 else (k, k)
+    w = (torch.randn(Co, kh, kw, C, device=cuda) / math.sqrt(kh * kw * C)).bfloat16()
+    b = torch.randn(Co, device=cuda).bfloat16()
+    g = (torch.rand(C, device=cuda) + 0.5).bfloat16()
+    bt = torch.randn(C, device=cuda).bfloat16()
+    m = torch.randn(B, 2 * C, device=cuda).bfloat16() if mod else None
+    table = _lib.group_norm_table(x, g, bt, 32, 1e-5, m, 1.0)
+    rt = ref.group_norm_table(x.float(), g.float(), bt.float(), 32, 1e-5, None if m is None else m.float(), 1.0)
+    assert _rel(table, rt) < 1e-4
+    pad = 0 if k == 1 else 1
+    y = _lib.conv2d_nhwc(x, w, b, pad, up, None, None, 1, norm=table, norm_silu=silu)
+    xn = ops.apply_norm_table(x.float(), rt, silu)
+    r = ref.conv2d_nhwc(xn, w.float(), b.float(), 1, pad, up)
+    assert _rel(y, r) < 1.5e-2
+    assert torch.equal(y, _lib.conv2d_nhwc(x, w, b, pad, up, None, None, 1, norm=table, norm_silu=silu))
