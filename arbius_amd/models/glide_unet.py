@@ -103,9 +103,9 @@ class JointAttention(nn.Module):
         N, Hh = H * W, self.heads
         qkv = self.qkv.forward_norm(x.view(B, N, C), self.norm.table(x)).view(B, N, 3, Hh, C // Hh)
         ckv = self.ctx_kv(ctx).view(B, ctx.shape[1], 2, Hh, C // Hh)
-        k = torch.cat([ckv[:, :, 0], qkv[:, :, 1]], dim=1)
-        v = torch.cat([ckv[:, :, 1], qkv[:, :, 2]], dim=1)
-        o = ops.attention(qkv[:, :, 0], k, v)
+        # joint softmax over [context tokens | spatial tokens]: the context K/V are a prefix
+        # segment read in place by the flash kernel (encoder_kv attention, no concat copy)
+        o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], kv_prefix=(ckv[:, :, 0], ckv[:, :, 1]))
         return self.out(o.reshape(B, N, C), residual=x.view(B, N, C)).view(B, H, W, C)
 
 

@@ -183,12 +183,16 @@ def layer_norm(x, gamma, beta, eps):
 
 
 # --------------------------------------------------------------------------- attention
-def attention(q, k, v, scale=None, causal=False):
-    """q [B,Nq,H,D], k/v [B,Nk,H,D] (last dim contiguous) -> [B,Nq,H,D]."""
+def attention(q, k, v, scale=None, causal=False, kv_prefix=None):
+    """q [B,Nq,H,D], k/v [B,Nk,H,D] (last dim contiguous) -> [B,Nq,H,D].
+    ``kv_prefix = (kp, vp)``: extra keys/values placed AHEAD of k/v (joint attention over
+    context + spatial tokens) read in place by the kernel - no concatenated copy."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     if _hip(q):
-        return _lib.flash_attention(q, k, v, scale, causal)
+        return _lib.flash_attention(q, k, v, scale, causal, kv_prefix)
+    if kv_prefix is not None:
+        k, v = torch.cat([kv_prefix[0], k], 1), torch.cat([kv_prefix[1], v], 1)
     return ref.attention(q, k, v, scale, causal)
 
 

@@ -27,7 +27,8 @@ _SIGS = {
     "arb_group_norm_mod_nhwc": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_float, c_int, c_int, c_int, c_float,
                                                                         c_void_p]),
     "arb_layer_norm": (c_int, [c_void_p] * 4 + [c_int, c_int, c_float, c_void_p]),
-    "arb_flash_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_int, c_void_p]),
+    "arb_flash_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 3
+                            + [c_int, c_void_p]),
     "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
     "arb_conv2d_nhwc": (c_int, [c_void_p] * 8 + [c_int] * 12 + [c_void_p]),
@@ -152,14 +153,27 @@ def layer_norm(x, gamma, beta, eps):
 
 
 # --------------------------------------------------------------------------- attention
-def flash_attention(q, k, v, scale, causal):
-    """q [B,Nq,H,D], k/v [B,Nk,H,D] (last dim contiguous, strides multiple of 8)."""
+def flash_attention(q, k, v, scale, causal, kv_prefix=None):
+    """q [B,Nq,H,D], k/v [B,Nk,H,D] (last dim contiguous, strides multiple of 8).
+    ``kv_prefix = (kp, vp)`` [B,Np,H,D]: extra keys/values ahead of k/v (joint attention)."""
     _bf16(q, k, v)
     B, Nq, H, D = q.shape
     Nk = k.shape[1]
     if D > 160:
-        from . import ref
+        if kv_prefix is not None:
+            k, v = torch.cat([kv_prefix[0], k], 1), torch.cat([kv_prefix[1], v], 1)
         return _large_head_attention(q, k, v, scale)
+    Np, kp, vp, pst = 0, None, None, None
+    if kv_prefix is not None:
+        kp, vp = kv_prefix
+        _bf16(kp, vp)
+        Np = kp.shape[1]
+        if kp.stride(2) != k.stride(2) or vp.stride(2) != v.stride(2) or causal:
+            raise ValueError("flash_attention: prefix K/V must share the head stride (and no causal mask)")
+        for t in (kp, vp):
+            if t.stride(-1) != 1 or any(s % 8 for s in t.stride()[:3]) or t.data_ptr() % 16:
+                raise ValueError("flash_attention: prefix last dim contiguous, strides/base 16B aligned")
+        pst = (ctypes.c_long * 4)(kp.stride(0), kp.stride(1), vp.stride(0), vp.stride(1))
     for t in (q, k, v):
         if t.stride(-1) != 1 or any(s % 8 for s in t.stride()[:3]) or t.data_ptr() % 16:
             raise ValueError("flash_attention: last dim must be contiguous, strides/base 16B aligned")
@@ -168,8 +182,8 @@ def flash_attention(q, k, v, scale, causal):
     o = torch.empty(B, Nq, H, D, dtype=q.dtype, device=q.device)
     strides = (ctypes.c_long * 12)(q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
                                    v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2))
-    _check(_fn("arb_flash_attention")(_p(q), _p(k), _p(v), _p(o), strides, B, H, Nq, Nk, D, float(scale),
-                                      int(bool(causal)), _stream()), "flash_attention")
+    _check(_fn("arb_flash_attention")(_p(q), _p(k), _p(v), _p(o), strides, B, H, Nq, Nk + Np, D, float(scale),
+                                      int(bool(causal)), _p(kp), _p(vp), pst, Np, _stream()), "flash_attention")
     return o
 
 

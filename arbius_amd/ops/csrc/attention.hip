@@ -41,6 +41,13 @@ struct AttnArgs {
   int B, H, Nq, Nk, D;
   float scale_log2;
   int causal;
+  // optional K/V PREFIX segment (keys [0, Np) read from kp/vp, keys [Np, Nk) from k/v at
+  // j - Np): the Kandinsky joint attention's text+image context tokens ahead of the spatial
+  // tokens, without materialising cat(ctx_kv, kv) every layer and step.
+  const bf16_t* kp;
+  const bf16_t* vp;
+  long kp_sb, kp_sn, vp_sb, vp_sn;
+  int Np;
 };
 
 template <int KSTEPS, int DT, int QT, bool ONES>
@@ -70,6 +77,10 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   const bf16_t* qbase = a.q + b * a.q_sb + h * a.q_sh;
   const bf16_t* kbase = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vbase = a.v + b * a.v_sb + h * a.v_sh;
+  const bf16_t* kpbase = a.Np ? a.kp + b * a.kp_sb + h * a.k_sh : nullptr;
+  const bf16_t* vpbase = a.Np ? a.vp + b * a.vp_sb + h * a.v_sh : nullptr;
+  auto krow = [&](int j) { return j < a.Np ? kpbase + (long)j * a.kp_sn : kbase + (long)(j - a.Np) * a.k_sn; };
+  auto vrow = [&](int j) { return j < a.Np ? vpbase + (long)j * a.vp_sn : vbase + (long)(j - a.Np) * a.v_sn; };
 
   // ---- Q fragments (B operand of S^T = K Q^T): lane holds Q[q][32s + 8g .. +7]
   bf16x8 qf[QT][KSTEPS];
@@ -109,15 +120,13 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     for (int i = 0; i < KPT; ++i) {
       const int c = tid + 256 * i;
       const int r = c / (KSTEPS * 4), col = (c % (KSTEPS * 4)) * 8;
-      rk[i] = (c < KCH && kv + r < a.Nk && col < D) ? ld16(kbase + (long)(kv + r) * a.k_sn + col)
-                                                     : make_uint4(0, 0, 0, 0);
+      rk[i] = (c < KCH && kv + r < a.Nk && col < D) ? ld16(krow(kv + r) + col) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = tid + 256 * i;
       const int r = c / (DT * 2), col = (c % (DT * 2)) * 8;
-      uint4 val = (c < VCH && kv + r < a.Nk && col < D) ? ld16(vbase + (long)(kv + r) * a.v_sn + col)
-                                                         : make_uint4(0, 0, 0, 0);
+      uint4 val = (c < VCH && kv + r < a.Nk && col < D) ? ld16(vrow(kv + r) + col) : make_uint4(0, 0, 0, 0);
       if (ONES && col == (D & ~7)) {
         // column D is the first element of the first all-padding 8-chunk when D % 16 == 8
         val.x = (val.x & 0xffff0000u) | one_bits;
@@ -297,10 +306,18 @@ static void launch_fa(const AttnArgs& a, hipStream_t s) {
   else flash_attn_fwd_kernel<KSTEPS, DT, QT, false><<<grid, 256, 0, s>>>(a);
 }
 
+// kp/vp (may be null): prefix K/V segment of Np keys with strides pstrides = {kp_sb, kp_sn, vp_sb, vp_sn}
+// (head stride shared with k/v); Nk counts prefix + main keys.
 ARB_API int arb_flash_attention(const void* q, const void* k, const void* v, void* o, const long* strides, int B,
-                                int H, int Nq, int Nk, int D, float scale, int causal, hipStream_t stream) {
-  if (D % 8 != 0 || D > 160) return -1;
+                                int H, int Nq, int Nk, int D, float scale, int causal, const void* kp,
+                                const void* vp, const long* pstrides, int Np, hipStream_t stream) {
+  if (D % 8 != 0 || D > 160 || (Np > 0 && (kp == nullptr || vp == nullptr || causal))) return -1;
   AttnArgs a;
+  a.kp = (const bf16_t*)kp;
+  a.vp = (const bf16_t*)vp;
+  a.Np = Np;
+  a.kp_sb = Np ? pstrides[0] : 0; a.kp_sn = Np ? pstrides[1] : 0;
+  a.vp_sb = Np ? pstrides[2] : 0; a.vp_sn = Np ? pstrides[3] : 0;
   a.q = (const bf16_t*)q;
   a.k = (const bf16_t*)k;
   a.v = (const bf16_t*)v;

@@ -237,3 +237,19 @@ def test_conv_groupnorm_prologue(cuda, B, H, W, C, Co, k, silu, up, mod):
     r = ref.conv2d_nhwc(xn, w.float(), b.float(), 1, pad, up)
     assert _rel(y, r) < 1.5e-2
     assert torch.equal(y, _lib.conv2d_nhwc(x, w, b, pad, up, None, None, 1, norm=table, norm_silu=silu))
+
+
+@pytest.mark.parametrize("B,Nq,Np,H,D", [(2, 2304, 87, 12, 64), (2, 576, 87, 18, 64), (1, 100, 5, 2, 64),
+                                         (2, 144, 64, 4, 40)])
+def test_flash_attention_kv_prefix(cuda, B, Nq, Np, H, D):
+    """Joint attention: prefix K/V segment read in place == attention over the concatenation."""
+    torch.manual_seed(8)
+    qkv = torch.randn(B, Nq, 3, H, D, device=cuda).bfloat16()
+    ckv = torch.randn(B, Np, 2, H, D, device=cuda).bfloat16()
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    kp, vp = ckv[:, :, 0], ckv[:, :, 1]
+    o = _lib.flash_attention(q, k, v, 1 / math.sqrt(D), False, (kp, vp))
+    r = ref.attention(q.float(), torch.cat([kp, k], 1).float(), torch.cat([vp, v], 1).float(), 1 / math.sqrt(D))
+    assert _rel(o, r) < 2e-2
+    oc = _lib.flash_attention(q, torch.cat([kp, k], 1), torch.cat([vp, v], 1), 1 / math.sqrt(D), False)
+    assert torch.equal(o, oc), "prefix segment must be bitwise identical to the concatenated keys"
