@@ -33,6 +33,7 @@ struct ConvArgs {
   float* ws;            // split-K slabs [S, M, N]
   const float* norm;    // [B, Cin, 2] (scale, shift) GroupNorm prologue or null
   int norm_silu;
+  int* counters;        // split-K tile tickets (in-launch reduction) or null
   int B, H, W, Cin;     // input (pre-upsample)
   int Hl, Wl;           // logical input dims (after upsample)
   int Ho, Wo;
@@ -197,39 +198,89 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
 
   // ---- epilogue: lane holds out[m][n .. n+3]
   const int hw = p.Ho * p.Wo;
+  auto emit = [&](int m, int n, float v0, float v1, float v2, float v3) {
+    if (p.bias) {
+      const uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
+      v0 += __uint_as_float(bv.x << 16); v1 += __uint_as_float(bv.x & 0xffff0000u);
+      v2 += __uint_as_float(bv.y << 16); v3 += __uint_as_float(bv.y & 0xffff0000u);
+    }
+    if (p.temb) {
+      const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)(m / hw) * p.N + n);
+      v0 += __uint_as_float(tv.x << 16); v1 += __uint_as_float(tv.x & 0xffff0000u);
+      v2 += __uint_as_float(tv.y << 16); v3 += __uint_as_float(tv.y & 0xffff0000u);
+    }
+    if (p.res) {
+      const uint2 rv = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.N + n);
+      v0 += __uint_as_float(rv.x << 16); v1 += __uint_as_float(rv.x & 0xffff0000u);
+      v2 += __uint_as_float(rv.y << 16); v3 += __uint_as_float(rv.y & 0xffff0000u);
+    }
+    uint2 o;
+    o.x = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+    o.y = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
+    *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
+  };
+  if constexpr (!SPLIT) {
 #pragma unroll
-  for (int b = 0; b < TM; ++b) {
-    const int m = m0 + wm * (BM / WM) + b * 16 + l16;
-    if (m >= p.M) continue;
-    const int bb = m / hw;
+    for (int b = 0; b < TM; ++b) {
+      const int m = m0 + wm * (BM / WM) + b * 16 + l16;
+      if (m >= p.M) continue;
 #pragma unroll
-    for (int a = 0; a < TN; ++a) {
-      const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
-      if (n >= p.N) continue;
-      float v0 = acc[a][b][0], v1 = acc[a][b][1], v2 = acc[a][b][2], v3 = acc[a][b][3];
-      if (SPLIT) {
-        *reinterpret_cast<float4*>(p.ws + ((size_t)split_idx * p.M + m) * p.N + n) = make_float4(v0, v1, v2, v3);
-        continue;
+      for (int a = 0; a < TN; ++a) {
+        const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
+        if (n >= p.N) continue;
+        emit(m, n, acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
       }
-      if (p.bias) {
-        const uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
-        v0 += __uint_as_float(bv.x << 16); v1 += __uint_as_float(bv.x & 0xffff0000u);
-        v2 += __uint_as_float(bv.y << 16); v3 += __uint_as_float(bv.y & 0xffff0000u);
+    }
+    return;
+  } else {
+    // ---- split-K: fp32 slab, then IN-LAUNCH ordered reduction by the tile's last arriving
+    // block (cdna_hip_programming.md "In-launch split-K reduction": agent-scope release before
+    // the ticket, acquire in the reducer, counters zeroed by a memset node per call).  The
+    // reducer sums slabs 0..S-1 in order - the same arithmetic as splitk_reduce_kernel, so
+    // results are bitwise identical and independent of which block arrives last.
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int m = m0 + wm * (BM / WM) + b * 16 + l16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
+        if (n >= p.N) continue;
+        *reinterpret_cast<float4*>(p.ws + ((size_t)split_idx * p.M + m) * p.N + n) =
+            make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
       }
-      if (p.temb) {
-        const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)bb * p.N + n);
-        v0 += __uint_as_float(tv.x << 16); v1 += __uint_as_float(tv.x & 0xffff0000u);
-        v2 += __uint_as_float(tv.y << 16); v3 += __uint_as_float(tv.y & 0xffff0000u);
+    }
+    if (p.counters == nullptr) return;            // separate reduce kernel (A/B path)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(&sX[0][0]);  // the existing LDS array (no 2nd __shared__)
+    const int tile = (m0 / BM) * p.tiles_n + n0 / BN;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(&p.counters[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (t == p.nsplit - 1);
+    }
+    __syncthreads();
+    if (!*flag) return;
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int m = m0 + wm * (BM / WM) + b * 16 + l16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
+        if (n >= p.N) continue;
+        float4 v = *reinterpret_cast<const float4*>(p.ws + (size_t)m * p.N + n);
+        for (int sp = 1; sp < p.nsplit; ++sp) {
+          const float4 w4 = *reinterpret_cast<const float4*>(p.ws + ((size_t)sp * p.M + m) * p.N + n);
+          v.x += w4.x; v.y += w4.y; v.z += w4.z; v.w += w4.w;
+        }
+        emit(m, n, v.x, v.y, v.z, v.w);
       }
-      if (p.res) {
-        const uint2 rv = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.N + n);
-        v0 += __uint_as_float(rv.x << 16); v1 += __uint_as_float(rv.x & 0xffff0000u);
-        v2 += __uint_as_float(rv.y << 16); v3 += __uint_as_float(rv.y & 0xffff0000u);
-      }
-      uint2 o;
-      o.x = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
-      o.y = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
-      *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
     }
   }
 }
@@ -514,6 +565,10 @@ static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split
   return bp;
 }
 
+static size_t slab_bytes(int split, int M, int N) {
+  return ((size_t)split * M * N * sizeof(float) + 255) / 256 * 256;
+}
+
 // k = 1 / 3: square kernel, padding `pad` on both axes.  k = 31: a 3x1 kernel
 // (padding pad x 0) - the (3,1,1) temporal Conv3d of the UNet3D run over the
 // frame-major [B, F, H*W, C] activation viewed as an F x HW image.
@@ -533,7 +588,10 @@ ARB_API size_t arb_conv2d_workspace(int B, int H, int W, int Cin, int Cout, int 
   ConvArgs a;
   conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
   const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
-  return pl.split > 1 ? (size_t)pl.split * a.M * a.N * sizeof(float) : 0;
+  if (pl.split <= 1) return 0;
+  const TileCfg& tc = kCfgs[pl.cfg % kNumCfgs];
+  const size_t tiles = (size_t)((a.N + tc.bn - 1) / tc.bn) * ((a.M + tc.bm - 1) / tc.bm);
+  return slab_bytes(pl.split, a.M, a.N) + tiles * sizeof(int);   // slabs + split-K tile tickets
 }
 
 template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
@@ -561,13 +619,20 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
     dim3 grid(p.tiles_total * pl.split);
-    if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, true, true><<<grid, 256, 0, s>>>(p);
-    else if (glds) launch_glds<BN, BM, WN, WM, NS, true>(p, grid, s);
-    else conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false><<<grid, 256, 0, s>>>(p);
-    long work = (long)p.M * (p.N / 8);
-    long blocks = (work + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
+    if (glds && !p.norm) {
+      p.counters = nullptr;
+      launch_glds<BN, BM, WN, WM, NS, true>(p, grid, s);
+      long work = (long)p.M * (p.N / 8);
+      long blocks = (work + 255) / 256;
+      if (blocks > 2048) blocks = 2048;
+      splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
+    } else {
+      // register-staged kernel: in-launch reduction by each tile's last block
+      p.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(p.ws) + slab_bytes(pl.split, p.M, p.N));
+      hipMemsetAsync(p.counters, 0, (size_t)p.tiles_total * sizeof(int), s);
+      if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, true, true><<<grid, 256, 0, s>>>(p);
+      else conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false><<<grid, 256, 0, s>>>(p);
+    }
   } else {
     dim3 grid(p.tiles_total, 1);
     if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, false, true><<<grid, 256, 0, s>>>(p);

@@ -253,3 +253,18 @@ def test_flash_attention_kv_prefix(cuda, B, Nq, Np, H, D):
     assert _rel(o, r) < 2e-2
     oc = _lib.flash_attention(q, torch.cat([kp, k], 1), torch.cat([vp, v], 1), 1 / math.sqrt(D), False)
     assert torch.equal(o, oc), "prefix segment must be bitwise identical to the concatenated keys"
+
+
+@pytest.mark.parametrize("cfg", [0, 3, 5])
+def test_splitk_inlaunch_reduce_bitwise_equals_reduce_kernel(cuda, cfg):
+    """In-launch split-K reduction (register-staged kernels) sums slabs in the same order as the
+    separate reduce kernel (LDS-DMA kernels): identical bits."""
+    torch.manual_seed(9)
+    x = torch.randn(2, 16, 16, 640, device=cuda).bfloat16()
+    w = (torch.randn(1280, 3, 3, 640, device=cuda) / 76).bfloat16()
+    b = torch.randn(1280, device=cuda).bfloat16()
+    r = torch.randn(2, 16, 16, 1280, device=cuda).bfloat16()
+    a = _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg + 10, 4)
+    g = _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg, 4)
+    assert torch.equal(a, g)
+    assert torch.equal(a, _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg + 10, 4))
