@@ -51,11 +51,11 @@ def collect_shapes(models=("sd15",), res=512):
     convs, gemms = set(), set()
     orig_conv, orig_lin = ops.conv2d, ops.linear
 
-    def conv(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, temb=None):
+    def conv(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, temb=None, norm=None):
         if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
             B, H, W, C = x.shape
             convs.add((B, H, W, C, w.shape[0], w.shape[1], w.shape[2], padding, int(bool(upsample)), stride))
-        return orig_conv(x, w, b, stride, padding, upsample, residual, temb)
+        return orig_conv(x, w, b, stride, padding, upsample, residual, temb, norm)
 
     def lin(x, w, b=None, residual=None):
         if residual is not None and x.shape[-1] % 64 == 0:
