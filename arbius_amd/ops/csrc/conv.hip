@@ -23,6 +23,9 @@
 //     kernel that applies the epilogue (no atomics -> bitwise reproducible).
 #include "common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 struct ConvArgs {
   const bf16_t* x;      // [B, H, W, Cin]
   const bf16_t* w;      // [N, K]
@@ -235,7 +238,8 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   } else {
     // ---- split-K: fp32 slab, then IN-LAUNCH ordered reduction by the tile's last arriving
     // block (cdna_hip_programming.md "In-launch split-K reduction": agent-scope release before
-    // the ticket, acquire in the reducer, counters zeroed by a memset node per call).  The
+    // the ticket, acquire in the reducer).  Tickets live in a persistent zero-initialised pool;
+    // the reducer re-arms its counter to 0, so no memset node is needed per call.  The
     // reducer sums slabs 0..S-1 in order - the same arithmetic as splitk_reduce_kernel, so
     // results are bitwise identical and independent of which block arrives last.
 #pragma unroll
@@ -282,6 +286,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
         emit(m, n, v.x, v.y, v.z, v.w);
       }
     }
+    if (tid == 0) p.counters[tile] = 0;   // re-arm for the next launch on this region
   }
 }
 
@@ -565,6 +570,54 @@ static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split
   return bp;
 }
 
+// Split-K ticket regions.  A pool of zero-initialised int counters per device, allocated once
+// (eagerly, never during stream capture).  Every launch recorded into a hipGraph gets its OWN
+// region (graph nodes may replay concurrently on different streams); eager launches share one
+// region per stream (same-stream kernels are serialised).  Reducers re-arm counters to 0.
+struct CounterPool {
+  int* base = nullptr;
+  size_t cap = 0, used = 0;
+  std::unordered_map<hipStream_t, int*> eager;
+};
+static std::mutex g_cnt_mu;
+static std::unordered_map<int, CounterPool> g_cnt_pools;
+static constexpr size_t kCounterPoolInts = size_t(8) << 20;   // 32 MB per device
+static constexpr int kEagerRegionInts = 1 << 16;
+
+static int* split_counters(hipStream_t s, int tiles) {
+  std::lock_guard<std::mutex> lk(g_cnt_mu);
+  int dev = 0;
+  hipGetDevice(&dev);
+  CounterPool& pool = g_cnt_pools[dev];
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  hipStreamIsCapturing(s, &st);
+  const bool capturing = st != hipStreamCaptureStatusNone;
+  if (pool.base == nullptr) {
+    if (capturing) return nullptr;   // no allocation inside a capture: use the reduce kernel
+    if (hipMalloc(&pool.base, kCounterPoolInts * sizeof(int)) != hipSuccess) {
+      pool.base = nullptr;
+      return nullptr;
+    }
+    hipMemset(pool.base, 0, kCounterPoolInts * sizeof(int));
+    hipDeviceSynchronize();
+    pool.cap = kCounterPoolInts;
+  }
+  if (capturing) {
+    if (pool.used + tiles > pool.cap) return nullptr;
+    int* r = pool.base + pool.used;
+    pool.used += ((size_t)tiles + 63) / 64 * 64;
+    return r;
+  }
+  if (tiles > kEagerRegionInts) return nullptr;
+  auto it = pool.eager.find(s);
+  if (it != pool.eager.end()) return it->second;
+  if (pool.used + kEagerRegionInts > pool.cap) return nullptr;
+  int* r = pool.base + pool.used;
+  pool.used += kEagerRegionInts;
+  pool.eager[s] = r;
+  return r;
+}
+
 static size_t slab_bytes(int split, int M, int N) {
   return ((size_t)split * M * N * sizeof(float) + 255) / 256 * 256;
 }
@@ -588,10 +641,7 @@ ARB_API size_t arb_conv2d_workspace(int B, int H, int W, int Cin, int Cout, int 
   ConvArgs a;
   conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
   const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
-  if (pl.split <= 1) return 0;
-  const TileCfg& tc = kCfgs[pl.cfg % kNumCfgs];
-  const size_t tiles = (size_t)((a.N + tc.bn - 1) / tc.bn) * ((a.M + tc.bm - 1) / tc.bm);
-  return slab_bytes(pl.split, a.M, a.N) + tiles * sizeof(int);   // slabs + split-K tile tickets
+  return pl.split > 1 ? slab_bytes(pl.split, a.M, a.N) : 0;
 }
 
 template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
@@ -628,10 +678,15 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
       splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
     } else {
       // register-staged kernel: in-launch reduction by each tile's last block
-      p.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(p.ws) + slab_bytes(pl.split, p.M, p.N));
-      hipMemsetAsync(p.counters, 0, (size_t)p.tiles_total * sizeof(int), s);
+      p.counters = split_counters(s, p.tiles_total);
       if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, true, true><<<grid, 256, 0, s>>>(p);
       else conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false><<<grid, 256, 0, s>>>(p);
+      if (p.counters == nullptr) {     // no ticket region available: separate ordered reduce
+        long work = (long)p.M * (p.N / 8);
+        long blocks = (work + 255) / 256;
+        if (blocks > 2048) blocks = 2048;
+        splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
+      }
     }
   } else {
     dim3 grid(p.tiles_total, 1);
