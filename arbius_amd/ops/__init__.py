@@ -24,6 +24,11 @@ from . import ref
 from . import _lib
 
 _FORCE_REF = os.environ.get("ARBIUS_REFERENCE_OPS", "0") == "1"
+# GroupNorm-table prologue fused into the conv operand load (1) or applied by a separate
+# elementwise kernel in front of the LDS-DMA conv variant (0, default: measured 9098 vs 7925
+# tasks/h on SD1.5 512^2 - the register-staged kernel that can take the prologue is slower than
+# the LDS-DMA one by more than the extra elementwise pass costs).
+_NORM_PROLOGUE = os.environ.get("ARBIUS_NORM_PROLOGUE", "0") == "1"
 
 # Library convolutions (MIOpen: depthwise / 3-4 channel / fp16 RVM convs) must pick the
 # same deterministic solver on every call and every GPU: a solution CID is consensus.
@@ -70,6 +75,8 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
     kern_ok = (w.shape[1] in (1, 3) and w.shape[1] == w.shape[2]) or tuple(w.shape[1:3]) == (3, 1)
     if _hip(x) and kern_ok:
         table, nsilu = norm if norm is not None else (None, False)
+        if table is not None and not _NORM_PROLOGUE and x.shape[-1] % 8 == 0:
+            x, table, nsilu = _lib.norm_table_apply(x, table, nsilu), None, False
         if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
             return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride, norm=table,
                                     norm_silu=nsilu)
@@ -148,6 +155,8 @@ def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
 
 def apply_norm_table(x, table, silu=False):
     """x * scale + shift (+SiLU) per (batch, channel) - the unfused form of a norm prologue."""
+    if _hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+        return _lib.norm_table_apply(x, table, silu)
     B, C = x.shape[0], x.shape[-1]
     shape = (B,) + (1,) * (x.dim() - 2) + (C,)
     y = x.float() * table[..., 0].reshape(shape) + table[..., 1].reshape(shape)

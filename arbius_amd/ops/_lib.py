@@ -31,6 +31,7 @@ _SIGS = {
                             + [c_int, c_void_p]),
     "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
+    "arb_norm_table_apply": (c_int, [c_void_p] * 3 + [c_int, c_long, c_int, c_int, c_void_p]),
     "arb_conv2d_nhwc": (c_int, [c_void_p] * 8 + [c_int] * 12 + [c_void_p]),
     "arb_group_norm_table": (c_int, [c_void_p] * 4 + [c_float] + [c_void_p] * 2 + [c_int] * 4 + [c_float, c_void_p]),
     "arb_conv2d_workspace": (c_size_t, [c_int] * 11),
@@ -266,6 +267,20 @@ def silu(x):
         return ref.silu(x)
     y = torch.empty_like(x)
     _check(_fn("arb_silu")(_p(x), _p(y), x.numel(), _stream()), "silu")
+    return y
+
+
+def norm_table_apply(x, table, silu=False):
+    """x [B, *, C] * table[b, c].scale + .shift (+SiLU) - the unfused GroupNorm-table prologue."""
+    _bf16(x)
+    x = x.contiguous()
+    B, C = x.shape[0], x.shape[-1]
+    if C % 8 or tuple(table.shape) != (B, C, 2) or table.dtype != torch.float32:
+        raise ValueError(f"norm_table_apply: bad shapes x={tuple(x.shape)} table={tuple(table.shape)}")
+    table = table.contiguous()
+    y = torch.empty_like(x)
+    _check(_fn("arb_norm_table_apply")(_p(x), _p(y), _p(table), B, x.numel() // (B * C), C, int(bool(silu)),
+                                       _stream()), "norm_table_apply")
     return y
 
 

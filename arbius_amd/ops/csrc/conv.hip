@@ -23,6 +23,7 @@
 //     kernel that applies the epilogue (no atomics -> bitwise reproducible).
 #include "common.h"
 
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
@@ -618,6 +619,14 @@ static int* split_counters(hipStream_t s, int tiles) {
   return r;
 }
 
+static bool splitk_inlaunch() {
+  static const bool on = [] {
+    const char* e = std::getenv("ARB_SPLITK_INLAUNCH");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 static size_t slab_bytes(int split, int M, int N) {
   return ((size_t)split * M * N * sizeof(float) + 255) / 256 * 256;
 }
@@ -678,7 +687,10 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
       splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
     } else {
       // register-staged kernel: in-launch reduction by each tile's last block
-      p.counters = split_counters(s, p.tiles_total);
+      // In-launch reduction is opt-in (ARB_SPLITK_INLAUNCH=1): the agent-scope release/acquire
+      // pair writes back / invalidates the XCD's L2 per block, which measured 2-3x slower than
+      // the separate ordered reduce on SD1.5 shapes (profiles/rocprof_r1_v10_*).
+      p.counters = splitk_inlaunch() ? split_counters(s, p.tiles_total) : nullptr;
       if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, true, true><<<grid, 256, 0, s>>>(p);
       else conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false><<<grid, 256, 0, s>>>(p);
       if (p.counters == nullptr) {     // no ticket region available: separate ordered reduce

@@ -30,6 +30,31 @@ __global__ void __launch_bounds__(256) silu_kernel(const bf16_t* __restrict__ x,
   }
 }
 
+
+// Unfused form of a GroupNorm-table prologue: y[b, p, c] = x * table[b, c].x + table[b, c].y
+// (+SiLU).  Used in front of the LDS-DMA conv variant, which stages operands straight into
+// LDS and so cannot transform them on the way in.
+__global__ void __launch_bounds__(256) norm_table_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                               const float2* __restrict__ table, long HW, int C,
+                                                               long total8, int silu) {
+  const int CV = C >> 3;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
+    const long pix = i / CV;
+    const int c = (int)(i - pix * CV) * 8;
+    const long b = pix / HW;
+    const float2* t = table + b * C + c;
+    float f[8];
+    unpack8(ld16(x + i * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float2 ss = t[e];
+      const float o = fmaf(f[e], ss.x, ss.y);
+      f[e] = silu ? silu_f(o) : o;
+    }
+    st16(y + i * 8, pack8(f));
+  }
+}
+
 static int grid_for(long work) {
   long g = (work + 255) / 256;
   if (g > 2048) g = 2048;
@@ -46,5 +71,14 @@ ARB_API int arb_geglu(const void* h, void* out, long M, int F, hipStream_t strea
 ARB_API int arb_silu(const void* x, void* y, long n, hipStream_t stream) {
   if (n % 8 != 0) return -1;
   silu_kernel<<<grid_for(n / 8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, n / 8);
+  return (int)hipGetLastError();
+}
+
+ARB_API int arb_norm_table_apply(const void* x, void* y, const void* table, int B, long HW, int C, int silu,
+                                 hipStream_t stream) {
+  if (C % 8 != 0) return -1;
+  const long total8 = (long)B * HW * (C / 8);
+  norm_table_apply_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
+                                                                HW, C, total8, silu);
   return (int)hipGetLastError();
 }

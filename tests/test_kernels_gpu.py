@@ -268,3 +268,15 @@ def test_splitk_inlaunch_reduce_bitwise_equals_reduce_kernel(cuda, cfg):
     g = _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg, 4)
     assert torch.equal(a, g)
     assert torch.equal(a, _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg + 10, 4))
+
+
+@pytest.mark.parametrize("B,H,W,C,silu", [(2, 16, 16, 320, True), (1, 8, 24, 1280, False), (3, 5, 7, 64, True)])
+def test_norm_table_apply(cuda, B, H, W, C, silu):
+    """Unfused GroupNorm-table prologue kernel == fp32 x*scale+shift(+SiLU)."""
+    from arbius_amd import ops
+    torch.manual_seed(11)
+    x = torch.randn(B, H, W, C, device=cuda).bfloat16()
+    table = torch.randn(B, C, 2, device=cuda)
+    y = _lib.norm_table_apply(x, table, silu)
+    r = ops.apply_norm_table(x.float(), table, silu)
+    assert _rel(y, r) < 1e-2
