@@ -48,6 +48,11 @@ def _to_bytes(v) -> bytes:
 
 
 def _enc_single(t: str, v: Any) -> bytes:
+    if t.endswith("[]"):
+        return len(v).to_bytes(32, "big") + encode([t[:-2]] * len(v), list(v))
+    m = re.match(r"(.*)\[(\d+)\]$", t)
+    if m:
+        return encode([m.group(1)] * int(m.group(2)), list(v))
     if t.startswith("uint"):
         v = int(v)
         if v < 0:

@@ -37,17 +37,26 @@ def _h(b: bytes) -> str:
 
 class MockNode:
     def __init__(self, engine: MockEngine = None, token_address: str = TOKEN_ADDRESS):
-        self.engine = engine or MockEngine(MockToken())
+        from .mock_governance import MockBaseToken
+        self.engine = engine or MockEngine(MockBaseToken(address=token_address))
+        if getattr(self.engine.token, "clock", False) is None:
+            self.engine.token.clock = self.engine
         self.token_address = token_address.lower()
         self.nonces: Dict[str, int] = {}
         self.eth: Dict[str, int] = {}
         self.receipts: Dict[str, dict] = {}
         self.txs: Dict[str, dict] = {}
         self.by_selector = {abi.selector(sig): (name, sig, rets) for name, (sig, rets) in FUNCS.items()}
+        self.contracts: Dict[str, object] = {}     # extra twins by address (governance: deploy_basic)
 
     # ------------------------------------------------------------------ views
     def _view(self, to: str, data: bytes) -> bytes:
         e, tok = self.engine, self.engine.token
+        from .mock_governance import call_view
+        if to in self.contracts:
+            return call_view(self.contracts[to], data)
+        if to == self.token_address and hasattr(tok, "VIEWS") and data[:4] not in self.by_selector:
+            return call_view(tok, data)
         name, sig, rets = self.by_selector[data[:4]]
         args = abi.decode_call(sig, data)
         b32 = lambda x: x  # noqa: E731
@@ -101,6 +110,13 @@ class MockNode:
     # ------------------------------------------------------------------ transactions
     def _exec(self, sender: str, to: str, data: bytes):
         e, tok = self.engine, self.engine.token
+        from .mock_governance import dispatch
+        if to in self.contracts:
+            dispatch(self.contracts[to], sender, data)
+            return
+        if to == self.token_address and hasattr(tok, "ABI") and data[:4] not in self.by_selector:
+            dispatch(tok, sender, data)             # delegate / bridgeMint / ... (BaseTokenV1)
+            return
         name, sig, rets = self.by_selector[data[:4]]
         args = abi.decode_call(sig, data)
         raw = lambda x: bytes.fromhex(x[2:])  # noqa: E731
@@ -269,7 +285,8 @@ _LOGGABLE = {"TaskSubmitted", "TaskRetracted", "SignalCommitment", "SolutionSubm
              "ModelRegistered", "ValidatorDeposit"}
 
 
-def deploy_basic(node: "MockNode", deployer: str, engine_supply: int = 597_000 * 10 ** 18) -> dict:
+def deploy_basic(node: "MockNode", deployer: str, engine_supply: int = 597_000 * 10 ** 18,
+                 governance: bool = False) -> dict:
     """``scripts/003-deploy-core-basic.ts`` on the mock chain: the deployer owns the
     engine and is treasury, the engine holds the mining supply, and kandinsky2 is
     registered as a FREE mineable model (addr 0x..01, fee 0) with rate 1e18."""
@@ -281,9 +298,16 @@ def deploy_basic(node: "MockNode", deployer: str, engine_supply: int = 597_000 *
     addr = "0x" + "00" * 19 + "01"
     mid = e.register_model(deployer, addr, 0, template_bytes("kandinsky2"))
     e.set_solution_mineable_rate(deployer, mid, 10 ** 18)
-    return {"engineAddress": e.address, "baseTokenAddress": node.token_address,
-            "models": {"kandinsky2": {"id": mid, "mineable": True,
-                                      "params": {"addr": addr, "fee": "0", "rate": str(10 ** 18)}}}}
+    out = {"engineAddress": e.address, "baseTokenAddress": node.token_address,
+           "models": {"kandinsky2": {"id": mid, "mineable": True,
+                                     "params": {"addr": addr, "fee": "0", "rate": str(10 ** 18)}}}}
+    if governance:      # governance.test.ts fixture: Timelock (3 days) owns the Engine, Governor proposes
+        from .mock_governance import deploy_governance
+        tok.l2_gateway = deployer
+        _, tl, gov, reg = deploy_governance(e, deployer)
+        node.contracts.update({tl.address: tl, gov.address: gov})
+        out.update(timelockAddress=tl.address, governorAddress=gov.address)
+    return out
 
 
 def main(argv=None):
@@ -292,11 +316,13 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=8545)
     ap.add_argument("--deploy", default=None, metavar="DEPLOYER",
                     help="run the 003-deploy-core-basic equivalent for this deployer address")
+    ap.add_argument("--governance", action="store_true",
+                    help="with --deploy: also deploy Timelock + Governor (the engine's owner becomes the timelock)")
     a = ap.parse_args(argv)
     node = MockNode()
     if a.deploy:
         import json
-        print(json.dumps(deploy_basic(node, a.deploy), indent=2), flush=True)
+        print(json.dumps(deploy_basic(node, a.deploy, governance=a.governance), indent=2), flush=True)
     web.run_app(node.app(), host=a.host, port=a.port)
 
 

@@ -1,0 +1,480 @@
+"""Scenario port of contract/test/base.test.ts (84 ``it`` blocks, :166-3070) onto the MockEngine
+twin: validator / admin / model / task sections, and the two contestation sections (before
+slashing, :989-2121, and with slashing reached, :2123-3070) with the reference's golden
+balances and stakes (e.g. 2.10072 / 0.29928 / 0.14964 / 0.07476 AIUS)."""
+from decimal import Decimal
+
+import pytest
+
+from arbius_amd.chain.mock_engine import E18, MockEngine, MockToken, Revert
+from arbius_amd.utils.protocol import generate_commitment, hash_model
+
+TESTBUF = bytes.fromhex("746573740a")                                        # base.test.ts:10
+TESTCID = "0x1220f4ad8a3bd3189da2ad909ee41148d6893d8c629c410f7f2c7e3fae75aade79c8"
+ZERO32 = "0x" + "00" * 32
+
+
+def A(n):
+    return "0x" + f"{n:040x}"
+
+
+DEPLOYER, USER1, USER2, V1, V2, V3, V4, TREASURY = (A(i) for i in range(1, 9))
+
+
+def eth(x):
+    return int(Decimal(str(x)) * E18)
+
+
+def events(e, name):
+    return [ev for ev in e.events if ev.name == name]
+
+
+@pytest.fixture
+def env():
+    """beforeEach (base.test.ts:29-79): token + engine, 2000 AIUS to the deployer, approvals."""
+    tok = MockToken()
+    e = MockEngine(tok, treasury=TREASURY, owner=DEPLOYER)
+    tok.mint(DEPLOYER, eth(2000))
+    for a in (USER1, USER2, V1, V2, V3, V4):
+        tok.approve(a, e.address, 2 ** 256 - 1)
+    return e, tok
+
+
+def model(e):
+    return e.register_model(USER1, USER1, 0, TESTBUF)                   # deployBootstrapModel :83-101
+
+
+def task(e, mid, fee=0):
+    return e.submit_task(USER1, 0, USER1, mid, fee, TESTBUF)            # deployBootstrapTask :147-163
+
+
+def deposit(e, tok, v, amount=eth(2.4)):
+    tok.transfer(DEPLOYER, v, amount)
+    e.validator_deposit(v, v, amount)
+
+
+def bootstrap_validator(e, tok):                                          # :115-131
+    tok.mint(e.address, eth(599990))
+    deposit(e, tok, V1)
+
+
+def solve(e, v, tid, cid=TESTCID):
+    e.signal_commitment(v, generate_commitment(v, tid, cid))
+    e.submit_solution(v, tid, cid)
+
+
+# ----------------------------------------------------------------------------------- meta
+def test_meta_name_symbol(env):
+    e, tok = env
+    assert (tok.name, tok.symbol) == ("Arbius", "AIUS")                  # :172-179
+
+
+# ----------------------------------------------------------------------------------- validator
+def test_cannot_become_validator_when_paused(env):
+    e, tok = env
+    tok.mint(e.address, eth(599990))
+    tok.transfer(DEPLOYER, V1, eth(2.4))
+    e.set_paused(DEPLOYER, True)
+    with pytest.raises(Revert, match="paused"):
+        e.validator_deposit(V1, V1, eth(2.4))
+
+
+def test_become_validator(env):
+    e, tok = env
+    bootstrap_validator(e, tok)
+    ev = events(e, "ValidatorDeposit")[-1]
+    assert ev.args == {"addr": V1, "validator": V1, "amount": eth(2.4)}
+    v = e.get_validator(V1)
+    assert v.addr == V1 and v.staked == eth(2.4)
+
+
+def test_cannot_exit_validator_when_paused(env):
+    e, tok = env
+    bootstrap_validator(e, tok)
+    cnt = e.initiate_validator_withdraw(V1, eth(2.4))
+    assert events(e, "ValidatorWithdrawInitiated")
+    e.increase_time(86400)
+    e.set_paused(DEPLOYER, True)
+    with pytest.raises(Revert, match="paused"):
+        e.validator_withdraw(V1, cnt, V1)
+
+
+def test_exit_validator(env):
+    e, tok = env
+    bootstrap_validator(e, tok)
+    cnt = e.initiate_validator_withdraw(V1, eth(2.4))
+    with pytest.raises(Revert, match="wait longer"):
+        e.validator_withdraw(V1, cnt, V1)
+    e.increase_time(86400)
+    e.validator_withdraw(V1, cnt, V1)
+    assert events(e, "ValidatorWithdraw")[-1].args == {"addr": V1, "to": V1, "count": cnt, "amount": eth(2.4)}
+    assert e.get_validator(V1).staked == 0 and tok.balance_of(V1) == eth(2.4)
+    with pytest.raises(Revert, match="request not exist"):
+        e.validator_withdraw(V1, cnt, V1)
+
+
+def test_cancel_validator_withdraw(env):
+    e, tok = env
+    bootstrap_validator(e, tok)
+    cnt = e.initiate_validator_withdraw(V1, eth(1))
+    e.cancel_validator_withdraw(V1, cnt)
+    assert e.withdraw_pending_amount[V1] == 0
+    with pytest.raises(Revert, match="request not exist"):
+        e.cancel_validator_withdraw(V1, cnt)
+
+
+def test_cannot_solve_task_while_exiting(env):
+    """base.test.ts:286-320 (no engine pre-funding: the 2.4 stake is below the 0.08 % minimum
+    of the ~600k pseudo supply once the withdraw is pending)."""
+    e, tok = env
+    tid = task(e, model(e))
+    deposit(e, tok, V1)
+    e.initiate_validator_withdraw(V1, eth(2.4))
+    e.signal_commitment(V1, generate_commitment(V1, tid, TESTCID))
+    with pytest.raises(Revert, match="min staked too low"):
+        e.submit_solution(V1, tid, TESTCID)
+
+
+def test_signal_support(env):
+    e, tok = env
+    bootstrap_validator(e, tok)
+    mid = model(e)
+    e.signal_support(V1, mid, True)
+    assert events(e, "SignalSupport")[-1].args == {"addr": V1, "model": mid, "supported": True}
+
+
+# ----------------------------------------------------------------------------------- admin
+def test_add_mineable_model_set_rate(env):
+    e, tok = env
+    mid = model(e)
+    e.set_solution_mineable_rate(DEPLOYER, mid, eth(1))
+    assert e.models[mid].rate == eth(1)
+    with pytest.raises(Revert, match="Ownable: caller is not the owner"):
+        e.set_solution_mineable_rate(USER1, mid, eth(1))
+
+
+def test_can_change_model_rate_when_paused(env):
+    e, tok = env
+    mid = model(e)
+    e.set_paused(DEPLOYER, True)
+    e.set_solution_mineable_rate(DEPLOYER, mid, eth(2))
+    assert e.models[mid].rate == eth(2)
+
+
+@pytest.mark.parametrize("fn,evname", [("transfer_ownership", "OwnershipTransferred"),
+                                       ("transfer_pauser", "PauserTransferred"),
+                                       ("transfer_treasury", "TreasuryTransferred")])
+def test_transfer_roles(env, fn, evname):
+    e, tok = env
+    with pytest.raises(Revert, match="Ownable: caller is not the owner"):
+        getattr(e, fn)(USER1, USER1)
+    getattr(e, fn)(DEPLOYER, USER1)
+    assert events(e, evname)
+    attr = {"transfer_ownership": "owner", "transfer_pauser": "pauser", "transfer_treasury": "treasury"}[fn]
+    assert getattr(e, attr) == USER1
+
+
+def test_pause_unpause_and_non_pauser(env):
+    e, tok = env
+    with pytest.raises(Revert, match="not pauser"):
+        e.set_paused(USER1, True)
+    e.set_paused(DEPLOYER, True)
+    assert e.paused and events(e, "PausedChanged")[-1].args == {"paused": True}
+    e.set_paused(DEPLOYER, False)
+    assert not e.paused
+
+
+def test_set_version(env):
+    e, tok = env
+    with pytest.raises(Revert, match="Ownable"):
+        e.set_version(USER1, 1)
+    e.set_version(DEPLOYER, 1)
+    assert e.version == 1 and events(e, "VersionChanged")[-1].args == {"version": 1}
+
+
+@pytest.mark.parametrize("param,value", [
+    ("validator_minimum_percentage", eth(0.0009)), ("slash_amount_percentage", eth(0.0002)),
+    ("solution_fee_percentage", eth(0.2)), ("retraction_fee_percentage", eth(0.2)),
+    ("treasury_reward_percentage", eth(0.2)), ("min_claim_solution_time", 1000),
+    ("min_retraction_wait_time", 1000), ("min_contestation_vote_period_time", 1000),
+    ("max_contestation_validator_stake_since", 1000), ("exit_validator_min_unlock_time", 1000)])
+def test_param_setters(env, param, value):
+    """The ten owner setters and their non-owner reverts (base.test.ts:450-620)."""
+    e, tok = env
+    with pytest.raises(Revert, match="Ownable: caller is not the owner"):
+        e.set_param(USER1, param, value)
+    e.set_param(DEPLOYER, param, value)
+    assert getattr(e, param) == value
+    assert e.events[-1].args == {"amount": value}
+
+
+# ----------------------------------------------------------------------------------- model
+def test_cannot_register_model_when_paused(env):
+    e, tok = env
+    e.set_paused(DEPLOYER, True)
+    with pytest.raises(Revert, match="paused"):
+        model(e)
+
+
+def test_register_model(env):
+    e, tok = env
+    mid = model(e)
+    assert mid == hash_model(USER1, USER1, 0, TESTCID)
+    m = e.models[mid]
+    assert (m.addr, m.fee, m.rate, m.cid) == (USER1, 0, 0, TESTCID)
+    assert events(e, "ModelRegistered")[-1].args == {"id": mid}
+    with pytest.raises(Revert, match="model already registered"):
+        model(e)
+
+
+# ----------------------------------------------------------------------------------- task
+def test_task_paused_guards(env):
+    e, tok = env
+    bootstrap_validator(e, tok)
+    mid = model(e)
+    tid = task(e, mid)
+    e.set_paused(DEPLOYER, True)
+    for call in (lambda: task(e, mid), lambda: e.retract_task(USER1, tid),
+                 lambda: e.signal_commitment(V1, generate_commitment(V1, tid, TESTCID)),
+                 lambda: e.submit_solution(V1, tid, TESTCID), lambda: e.claim_solution(V1, tid)):
+        with pytest.raises(Revert, match="paused"):
+            call()
+
+
+def test_submit_and_retract_bootstrap_task(env):
+    e, tok = env
+    mid = model(e)
+    tid = task(e, mid)
+    ev = events(e, "TaskSubmitted")[-1]
+    assert ev.args == {"id": tid, "model": mid, "fee": 0, "sender": USER1}
+    t = e.get_task(tid)
+    assert (t.model, t.owner, t.fee, t.cid) == (mid, USER1, 0, TESTCID)
+    with pytest.raises(Revert, match="did not wait long enough"):
+        e.retract_task(USER1, tid)
+    e.increase_time(10001)
+    with pytest.raises(Revert, match="not owner"):
+        e.retract_task(USER2, tid)
+    e.retract_task(USER1, tid)
+    assert events(e, "TaskRetracted")[-1].args == {"id": tid}
+
+
+def test_commitment_solution_claim(env):
+    e, tok = env
+    bootstrap_validator(e, tok)
+    tid = task(e, model(e))
+    c = generate_commitment(V1, tid, TESTCID)
+    with pytest.raises(Revert, match="non existent commitment"):
+        e.submit_solution(V1, tid, TESTCID)
+    e.signal_commitment(V1, c)
+    assert events(e, "SignalCommitment")[-1].args == {"addr": V1, "commitment": c}
+    with pytest.raises(Revert, match="commitment exists"):
+        e.signal_commitment(V1, c)
+    e.submit_solution(V1, tid, TESTCID)
+    assert events(e, "SolutionSubmitted")[-1].args == {"addr": V1, "task": tid}
+    with pytest.raises(Revert, match="solution already submitted"):
+        e.submit_solution(V1, tid, TESTCID)
+    with pytest.raises(Revert, match="not enough delay"):
+        e.claim_solution(V1, tid)
+    e.increase_time(2001)
+    e.claim_solution(V1, tid)
+    assert events(e, "SolutionClaimed")[-1].args == {"addr": V1, "task": tid}
+    with pytest.raises(Revert, match="already claimed"):
+        e.claim_solution(V1, tid)
+
+
+def test_claim_with_fees_to_model_creator_and_solver(env):
+    """base.test.ts:911-987: model fee 3, task fee 4 -> model owner 3, solver 0.9 (fee minus
+    the 10 % solution fee), accrued treasury fees 0.1."""
+    e, tok = env
+    bootstrap_validator(e, tok)
+    model1 = A(42)
+    mid = e.register_model(USER1, model1, eth(3), TESTBUF)
+    tok.transfer(DEPLOYER, USER1, eth(4))
+    tid = e.submit_task(USER1, 0, USER1, mid, eth(4), TESTBUF)
+    solve(e, V1, tid)
+    e.increase_time(3600)
+    e.claim_solution(V1, tid)
+    assert tok.balance_of(USER1) == 0
+    assert tok.balance_of(model1) == eth(3)
+    assert tok.balance_of(V1) == eth(0.9)
+    assert e.accrued_fees == eth(0.1)
+
+
+# ----------------------------------------------------------------------------------- contestation
+@pytest.fixture(params=["not_reached", "reached"])
+def contest_env(env, request):
+    """deployBootstrapEngineSlashing{NotReached,Reached} (:133-145): engine pre-funded with
+    599000 (pseudo supply < 2000, slash = 0) or 597000 AIUS (slashing active)."""
+    e, tok = env
+    tok.mint(e.address, eth(599000 if request.param == "not_reached" else 597000))
+    return e, tok, request.param == "reached"
+
+
+def contest_setup(e, tok, validators, fee=0):
+    mid = model(e)
+    if fee:
+        tok.transfer(DEPLOYER, USER1, fee)
+    tid = task(e, mid, fee)
+    e.set_solution_mineable_rate(DEPLOYER, mid, eth(1))
+    for v in validators:
+        deposit(e, tok, v)
+    solve(e, V1, tid)
+    return tid
+
+
+def test_contest_guards(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2])
+    with pytest.raises(Revert):                                       # nonexistent task
+        e.submit_contestation(V2, ZERO32)
+    tid2 = e.submit_task(USER1, 0, USER1, e.tasks[tid].model, 0, TESTBUF)
+    with pytest.raises(Revert, match="solution does not exist"):
+        e.submit_contestation(V2, tid2)
+    if slashing:            # below MIN_SUPPLY_FOR_VALIDATOR_DEPOSITS the minimum stake is 0
+        with pytest.raises(Revert, match="min staked too low"):       # non validator
+            e.submit_contestation(USER2, tid)
+    e.set_paused(DEPLOYER, True)
+    with pytest.raises(Revert, match="paused"):
+        e.submit_contestation(V2, tid)
+
+
+def test_contest_blocks_claim_and_early_finish(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3])
+    e.submit_contestation(V2, tid)
+    e.increase_time(3600)
+    with pytest.raises(Revert, match="has contestation"):
+        e.claim_solution(V1, tid)
+    with pytest.raises(Revert, match="voting period not ended"):
+        e.contestation_vote_finish(V1, tid, 2)
+
+
+def test_cannot_finish_contestation_when_paused(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3])
+    e.submit_contestation(V2, tid)
+    e.vote_on_contestation(V3, tid, True)
+    e.increase_time(4000)
+    e.set_paused(DEPLOYER, True)
+    with pytest.raises(Revert, match="paused"):
+        e.contestation_vote_finish(V1, tid, 3)
+
+
+def test_successful_contestation_one_other_voter(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3])
+    e.submit_contestation(V2, tid)
+    e.vote_on_contestation(V3, tid, True)
+    stake = eth(2.10072) if slashing else eth(2.4)
+    assert [e.get_validator(v).staked for v in (V1, V2, V3)] == [stake] * 3
+    e.increase_time(4000)
+    e.contestation_vote_finish(V1, tid, 3)
+    assert events(e, "ContestationVoteFinish")[-1].args == {"id": tid, "start_idx": 0, "end_idx": 3}
+    assert e.get_contestation(tid).finish_start_index == 3
+    share = eth(0.14964) if slashing else 0
+    assert [tok.balance_of(v) for v in (V1, V2, V3)] == [0, share, share]
+    assert [e.get_validator(v).staked for v in (V1, V2, V3)] == [stake, eth(2.4), eth(2.4)]
+
+
+def test_contestor_cannot_vote_after_stake_since_window(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2])
+    e.submit_contestation(V2, tid)
+    e.increase_time(121)     # hardhat: +120 s, then the deposit's own block is >= 1 s later
+    deposit(e, tok, V3)
+    assert e.validator_can_vote(V3, tid) == 0x06
+    with pytest.raises(Revert, match="not allowed"):
+        e.vote_on_contestation(V3, tid, True)
+
+
+def test_successful_contestation_refunds_submitter(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3], fee=eth(1))
+    assert tok.balance_of(USER1) == 0
+    e.submit_contestation(V2, tid)
+    e.vote_on_contestation(V3, tid, True)
+    e.increase_time(4000)
+    e.contestation_vote_finish(V1, tid, 3)
+    assert tok.balance_of(USER1) == eth(1)
+
+
+def test_failed_contestation_no_other_voters(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3])
+    e.submit_contestation(V2, tid)
+    stake = eth(2.10072) if slashing else eth(2.4)
+    assert [e.get_validator(v).staked for v in (V1, V2)] == [stake, stake]
+    e.increase_time(4000)
+    e.contestation_vote_finish(V1, tid, 3)
+    assert [tok.balance_of(v) for v in (V1, V2)] == [eth(0.29928) if slashing else 0, 0]
+    assert [e.get_validator(v).staked for v in (V1, V2)] == [eth(2.4), stake]
+
+
+def test_failed_contestation_fee_to_original_solver(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3], fee=eth(1))
+    e.submit_contestation(V2, tid)
+    e.increase_time(4000)
+    e.contestation_vote_finish(V1, tid, 3)
+    # 0.9 solver share of the fee (+ the contester's slash, 0.29918 with the 1 AIUS fee in the engine)
+    assert tok.balance_of(V1) == (eth(1.19918) if slashing else eth(0.9))
+    assert e.accrued_fees == eth(0.1)
+
+
+def test_failed_contestation_two_voters(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3])
+    e.submit_contestation(V2, tid)
+    e.vote_on_contestation(V3, tid, False)
+    stake = eth(2.10072) if slashing else eth(2.4)
+    assert [e.get_validator(v).staked for v in (V1, V2, V3)] == [stake] * 3
+    e.increase_time(4000)
+    e.contestation_vote_finish(V1, tid, 3)
+    share = eth(0.14964) if slashing else 0
+    assert [tok.balance_of(v) for v in (V1, V2, V3)] == [share, 0, share]
+    assert [e.get_validator(v).staked for v in (V1, V2, V3)] == [eth(2.4), stake, eth(2.4)]
+
+
+def test_failed_contestation_three_voters(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3, V4])
+    e.submit_contestation(V2, tid)
+    e.vote_on_contestation(V3, tid, False)
+    e.vote_on_contestation(V4, tid, False)
+    stake = eth(2.10096) if slashing else eth(2.4)
+    assert [e.get_validator(v).staked for v in (V1, V2, V3, V4)] == [stake] * 4
+    e.increase_time(4000)
+    e.contestation_vote_finish(V1, tid, 3)
+    half, quarter = (eth(0.14952), eth(0.07476)) if slashing else (0, 0)
+    assert [tok.balance_of(v) for v in (V1, V2, V3, V4)] == [half, 0, quarter, quarter]
+    assert [e.get_validator(v).staked for v in (V1, V2)] == [eth(2.4), stake]
+
+
+def test_successful_contestation_two_other_voters(contest_env):
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3, V4])
+    e.submit_contestation(V2, tid)
+    e.vote_on_contestation(V3, tid, True)
+    e.vote_on_contestation(V4, tid, True)
+    e.increase_time(4000)
+    e.contestation_vote_finish(V1, tid, 3)
+    half, quarter = (eth(0.14952), eth(0.07476)) if slashing else (0, 0)
+    assert [tok.balance_of(v) for v in (V1, V2, V3, V4)] == [0, half, quarter, quarter]
+    assert e.get_validator(V1).staked == (eth(2.10096) if slashing else eth(2.4))
+
+
+def test_successful_contestation_two_other_voters_multiple_iterations(contest_env):
+    """contestationVoteFinish(taskid, 1) four times: one voter paid per call, index 0..4."""
+    e, tok, slashing = contest_env
+    tid = contest_setup(e, tok, [V1, V2, V3, V4])
+    e.submit_contestation(V2, tid)
+    e.vote_on_contestation(V3, tid, True)
+    e.vote_on_contestation(V4, tid, True)
+    e.increase_time(4000)
+    assert e.get_contestation(tid).finish_start_index == 0
+    half, quarter = (eth(0.14952), eth(0.07476)) if slashing else (0, 0)
+    expect = [[0, half, 0, 0], [0, half, quarter, 0], [0, half, quarter, quarter], [0, half, quarter, quarter]]
+    for i in range(4):
+        e.contestation_vote_finish(V1, tid, 1)
+        assert [tok.balance_of(v) for v in (V1, V2, V3, V4)] == expect[i]
+        assert e.get_contestation(tid).finish_start_index == i + 1

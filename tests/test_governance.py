@@ -1,0 +1,311 @@
+"""Governance scenarios of contract/test/governance.test.ts:27-444 (GovernorV1 + TimelockV1 +
+BaseTokenV1 votes) re-created on the Python twins, plus the OZ access-control / permit /
+cancel paths those contracts inherit."""
+import pytest
+
+from arbius_amd.chain import abi
+from arbius_amd.chain.mock_engine import E18, ZERO32, MockEngine, Revert
+from arbius_amd.chain.mock_governance import (ACTIVE, CANCELED, CANCELLER_ROLE, DEFEATED, EXECUTED, PENDING, PROPOSER_ROLE,
+                                              QUEUED, SUCCEEDED, TIMELOCK_ADMIN_ROLE, MockBaseToken,
+                                              deploy_governance)
+from arbius_amd.chain.secp256k1 import address_from_priv, sign
+from arbius_amd.ipfs.unixfs import onchain_cid
+
+TESTBUF = bytes.fromhex("746573740a")
+
+
+def A(n):
+    return "0x" + f"{n:040x}"
+
+
+DEPLOYER, USER1, USER2, LPREWARD = A(1), A(2), A(3), A(4)
+DESC = "Proposal #1: Give grant to team"
+ONE_DAY_BLOCKS, ONE_WEEK_BLOCKS = 0x19AF, 0xB3CB      # governance.test.ts:164,171
+
+
+@pytest.fixture
+def gov():
+    tok = MockBaseToken(l2_gateway=DEPLOYER, owner=DEPLOYER)
+    eng = MockEngine(tok, treasury=LPREWARD, owner=DEPLOYER)
+    token, tl, g, reg = deploy_governance(eng, DEPLOYER, extra_admin=USER1)
+    return eng, token, tl, g
+
+
+def _grant_proposal(token, tl):
+    return [token.address], [0], [abi.encode_call("transfer(address,uint256)", USER1, E18)]
+
+
+def _fund(token, tl, voters=(USER1,)):
+    for v in voters:
+        token.bridge_mint(DEPLOYER, v, E18)
+        token.delegate(v, v)
+    token.bridge_mint(DEPLOYER, tl.address, E18)
+
+
+def test_fixture_roles_and_delay(gov):
+    eng, token, tl, g = gov
+    assert tl.min_delay == 3 * 86400
+    assert not tl.has_role(PROPOSER_ROLE, DEPLOYER) and tl.has_role(PROPOSER_ROLE, USER1)
+    assert not tl.has_role(TIMELOCK_ADMIN_ROLE, DEPLOYER) and tl.has_role(TIMELOCK_ADMIN_ROLE, tl.address)
+    assert tl.has_role(PROPOSER_ROLE, g.address)
+    assert eng.owner == tl.address
+
+
+def test_successful_treasury_vote(gov):
+    eng, token, tl, g = gov
+    _fund(token, tl)
+    targets, values, calls = _grant_proposal(token, tl)
+    pid = g.propose(USER1, targets, values, calls, DESC)
+    dh = g.description_hash(DESC)
+    assert pid == g.hash_proposal(targets, values, calls, dh)
+    assert g.state(pid) == PENDING
+    eng.mine(ONE_DAY_BLOCKS)
+    assert g.state(pid) == ACTIVE
+    g.cast_vote(USER1, pid, 1)
+    eng.mine(ONE_WEEK_BLOCKS)
+    assert g.state(pid) == SUCCEEDED
+    g.queue(USER1, targets, values, calls, dh)
+    assert g.state(pid) == QUEUED
+    with pytest.raises(Revert, match="operation is not ready"):
+        g.execute(USER1, targets, values, calls, dh)
+    eng.increase_time(260000)
+    g.execute(USER1, targets, values, calls, dh)
+    assert g.state(pid) == EXECUTED
+    assert token.balance_of(tl.address) == 0
+    assert token.balance_of(USER1) == 2 * E18
+
+
+def test_successful_set_solution_mineable_rate(gov):
+    eng, token, tl, g = gov
+    _fund(token, tl)
+    mid = eng.register_model(USER1, USER1, 0, TESTBUF)
+    targets = [eng.address]
+    calls = [abi.encode_call("setSolutionMineableRate(bytes32,uint256)", mid, 1)]
+    desc = "Proposal #1: setSolutionMineableRate model_1"
+    pid = g.propose(USER1, targets, [0], calls, desc)
+    eng.mine(ONE_DAY_BLOCKS)
+    g.cast_vote(USER1, pid, 1)
+    eng.mine(ONE_WEEK_BLOCKS)
+    g.queue(USER1, targets, [0], calls, g.description_hash(desc))
+    eng.increase_time(260000)
+    g.execute(USER1, targets, [0], calls, g.description_hash(desc))
+    assert eng.models[mid].rate == 1
+
+
+def test_failed_treasury_vote(gov):
+    eng, token, tl, g = gov
+    _fund(token, tl, voters=(USER1, USER2))
+    targets, values, calls = _grant_proposal(token, tl)
+    pid = g.propose(USER1, targets, values, calls, DESC)
+    eng.mine(ONE_DAY_BLOCKS)
+    g.cast_vote(USER1, pid, 1)
+    g.cast_vote(USER2, pid, 0)
+    eng.mine(ONE_WEEK_BLOCKS)
+    assert g.state(pid) == DEFEATED
+    with pytest.raises(Revert, match="Governor: proposal not successful"):
+        g.queue(USER1, targets, values, calls, g.description_hash(DESC))
+
+
+def test_must_wait_one_day(gov):
+    eng, token, tl, g = gov
+    _fund(token, tl)
+    targets, values, calls = _grant_proposal(token, tl)
+    pid = g.propose(USER1, targets, values, calls, DESC)
+    with pytest.raises(Revert, match="Governor: vote not currently active"):
+        g.cast_vote(USER1, pid, 1)
+
+
+def test_must_wait_one_week(gov):
+    eng, token, tl, g = gov
+    _fund(token, tl)
+    targets, values, calls = _grant_proposal(token, tl)
+    pid = g.propose(USER1, targets, values, calls, DESC)
+    eng.mine(ONE_DAY_BLOCKS)
+    g.cast_vote(USER1, pid, 1)
+    with pytest.raises(Revert, match="Governor: proposal not successful"):
+        g.queue(USER1, targets, values, calls, g.description_hash(DESC))
+
+
+def test_threshold_quorum_and_double_vote(gov):
+    eng, token, tl, g = gov
+    token.bridge_mint(DEPLOYER, USER2, E18 // 2)
+    token.delegate(USER2, USER2)
+    targets, values, calls = _grant_proposal(token, tl)
+    with pytest.raises(Revert, match="below proposal threshold"):
+        g.propose(USER2, targets, values, calls, DESC)
+    _fund(token, tl)
+    # tokens minted AFTER the snapshot do not count; quorum is 4% of the snapshot supply
+    pid = g.propose(USER1, targets, values, calls, DESC)
+    eng.mine(ONE_DAY_BLOCKS)
+    token.bridge_mint(DEPLOYER, USER2, 100 * E18)
+    g.cast_vote(USER2, pid, 1)
+    assert g.proposal_votes(pid) == (0, E18 // 2, 0)
+    with pytest.raises(Revert, match="vote already cast"):
+        g.cast_vote(USER2, pid, 0)
+    with pytest.raises(Revert, match="invalid vote type"):
+        g.cast_vote(USER1, pid, 3)
+    assert g.quorum(g.proposal_snapshot(pid)) == (E18 // 2 + 2 * E18) * 4 // 100
+
+
+def test_cancel_pending_and_queued(gov):
+    eng, token, tl, g = gov
+    _fund(token, tl)
+    targets, values, calls = _grant_proposal(token, tl)
+    dh = g.description_hash(DESC)
+    pid = g.propose(USER1, targets, values, calls, DESC)
+    with pytest.raises(Revert, match="proposer above threshold"):
+        g.cancel(USER2, targets, values, calls, dh)
+    g.cancel(USER1, targets, values, calls, dh)
+    assert g.state(pid) == CANCELED
+    with pytest.raises(Revert, match="proposal not active"):
+        g.cancel(USER1, targets, values, calls, dh)
+    with pytest.raises(Revert, match="already exists"):
+        g.propose(USER1, targets, values, calls, DESC)
+    # a QUEUED proposal cannot be cancelled through the governor in the reference deployment:
+    # the fixture grants it PROPOSER and EXECUTOR but not CANCELLER (governance.test.ts:87-91),
+    # so the timelock's cancel reverts; with CANCELLER it drops the timelock operation too
+    desc2 = DESC + " (again)"
+    pid2 = g.propose(USER1, targets, values, calls, desc2)
+    eng.mine(ONE_DAY_BLOCKS)
+    g.cast_vote(USER1, pid2, 1)
+    eng.mine(ONE_WEEK_BLOCKS)
+    g.queue(USER1, targets, values, calls, g.description_hash(desc2))
+    qid = g.timelock_ids[pid2]
+    assert tl.is_operation_pending(qid)
+    with pytest.raises(Revert, match="is missing role"):
+        g.cancel(USER1, targets, values, calls, g.description_hash(desc2))
+    assert g.state(pid2) == QUEUED
+    tl._grant(CANCELLER_ROLE, g.address)
+    g.cancel(USER1, targets, values, calls, g.description_hash(desc2))
+    assert not tl.is_operation(qid) and g.state(pid2) == CANCELED
+
+
+def test_bookkeeping_ids_hashes_cids(gov):
+    eng, token, tl, g = gov
+    _fund(token, tl)
+    targets, values, calls = _grant_proposal(token, tl)
+    pid = g.propose(USER1, targets, values, calls, DESC)
+    assert g.proposals_created == [pid] and g.proposals_created_length() == 1
+    assert g.description_hashes[pid] == g.description_hash(DESC)
+    assert g.description_cids[pid] == "0x" + onchain_cid(DESC.encode()).hex()   # GovernorV1.sol:128
+
+
+def test_timelock_access_control(gov):
+    eng, token, tl, g = gov
+    upd = abi.encode_call("updateDelay(uint256)", 5)
+    with pytest.raises(Revert, match="is missing role"):
+        tl.schedule(DEPLOYER, tl.address, 0, upd, ZERO32, ZERO32, 3 * 86400)
+    with pytest.raises(Revert, match="insufficient delay"):
+        tl.schedule(USER1, tl.address, 0, upd, ZERO32, ZERO32, 10)
+    with pytest.raises(Revert, match="caller must be timelock"):
+        tl.update_delay(USER1, 5)
+    op = tl.schedule(USER1, tl.address, 0, upd, ZERO32, ZERO32, 3 * 86400)
+    with pytest.raises(Revert, match="already scheduled"):
+        tl.schedule(USER1, tl.address, 0, upd, ZERO32, ZERO32, 3 * 86400)
+    with pytest.raises(Revert, match="not ready"):
+        tl.execute(USER1, tl.address, 0, upd, ZERO32, ZERO32)
+    eng.increase_time(3 * 86400)
+    with pytest.raises(Revert, match="missing role"):
+        tl.execute(USER2, tl.address, 0, upd, ZERO32, ZERO32)
+    tl.execute(USER1, tl.address, 0, upd, ZERO32, ZERO32)
+    assert tl.is_operation_done(op) and tl.min_delay == 5
+    with pytest.raises(Revert, match="can only renounce roles for self"):
+        tl.renounce_role(USER2, PROPOSER_ROLE, USER1)
+    # an underlying revert surfaces as the timelock's revert string
+    bad = abi.encode_call("transfer(address,uint256)", USER2, 10 ** 30)
+    tl.schedule(USER1, token.address, 0, bad, ZERO32, ZERO32, 5)
+    eng.increase_time(5)
+    with pytest.raises(Revert, match="underlying transaction reverted"):
+        tl.execute(USER1, token.address, 0, bad, ZERO32, ZERO32)
+
+
+def test_votes_checkpoints_and_bridge():
+    eng = MockEngine(MockBaseToken(l2_gateway=DEPLOYER), owner=DEPLOYER)
+    token = eng.token
+    token.clock = eng
+    with pytest.raises(Revert, match="NOT_GATEWAY"):
+        token.bridge_mint(USER1, USER1, E18)
+    token.bridge_mint(DEPLOYER, USER1, 3 * E18)      # every entry point mines its own block
+    b0 = eng.block_number
+    assert token.get_votes(USER1) == 0              # undelegated balances carry no votes
+    token.delegate(USER1, USER2)
+    b1 = eng.block_number
+    token.transfer_call(USER1, USER2, E18)
+    assert b0 < b1 < eng.block_number
+    assert token.get_votes(USER2) == 2 * E18
+    assert token.get_past_votes(USER2, b0) == 0 and token.get_past_votes(USER2, b1) == 3 * E18
+    assert token.get_past_votes(USER2, eng.block_number) == 2 * E18     # eth_call sees the pending block
+    with pytest.raises(Revert, match="future lookup"):
+        token.get_past_votes(USER2, eng.block_number + 1)
+    token.bridge_burn(DEPLOYER, USER1, E18)
+    assert token.get_votes(USER2) == E18 and token.total_supply == 2 * E18
+
+
+def test_permit_eip2612():
+    eng = MockEngine(MockBaseToken(l2_gateway=DEPLOYER, chain_id=42170), owner=DEPLOYER)
+    token = eng.token
+    token.clock = eng
+    priv = 0xAC0974BEC39A17E36BA4A6B4D238FF944BACB478CBED5EFCAE784D7BF4F2FF80   # hardhat key #0
+    owner = address_from_priv(priv)
+    deadline = eng.timestamp + 3600
+    r, s, rec = sign(token.permit_digest(owner, USER2, 5 * E18, 0, deadline), priv)
+    token.permit(USER1, owner, USER2, 5 * E18, deadline, 27 + rec, r, s)
+    assert token.allowance(owner, USER2) == 5 * E18 and token.nonces[owner] == 1
+    with pytest.raises(Revert, match="invalid signature"):       # nonce consumed: replay fails
+        token.permit(USER1, owner, USER2, 5 * E18, deadline, 27 + rec, r, s)
+    eng.increase_time(7200)
+    with pytest.raises(Revert, match="expired deadline"):
+        token.permit(USER1, owner, USER2, 5 * E18, deadline, 27 + rec, r, s)
+
+
+def test_governance_over_jsonrpc_signed_txs():
+    """The CLI's governance path end to end: signed EIP-155 txs through the mock JSON-RPC node
+    (deploy_basic(governance=True) = 003-deploy-core-basic + the governance fixture):
+    delegate -> propose -> castVote -> Bravo queue(id) -> execute(id) of an Engine setter."""
+    import asyncio
+
+    from aiohttp.test_utils import TestServer
+
+    from arbius_amd.chain.mock_node import MockNode, deploy_basic
+    from arbius_amd.chain.rpc import RpcChainClient
+
+    key = "0x" + "33" * 32
+    me = address_from_priv(key)
+    node = MockNode()
+    info = deploy_basic(node, me, governance=True)
+    gov_addr, eng = info["governorAddress"], node.engine
+    node.engine.token.bridge_mint(me, me, 30_000 * E18)     # > 4 % quorum of the 597k engine supply
+
+    async def go():
+        server = TestServer(node.app())
+        await server.start_server()
+        try:
+            c = RpcChainClient(str(server.make_url("/")), key, eng.address, info["baseTokenAddress"],
+                               receipt_poll=0.001)
+            await c.send_sig(c.token_address, "delegate(address)", me)
+            assert (await c.call_sig(c.token_address, "getVotes(address)", ["uint256"], me))[0] == 30_000 * E18
+            call = abi.encode_call("setVersion(uint256)", 7)
+            desc = "Proposal #7: bump the engine version"
+            await c.send_sig(gov_addr, "propose(address[],uint256[],bytes[],string)", [eng.address], [0], [call], desc)
+            pid = node.contracts[gov_addr].proposals_created[-1]
+            state = lambda: c.call_sig(gov_addr, "state(uint256)", ["uint8"], pid)   # noqa: E731
+            assert (await state())[0] == PENDING
+            for _ in range(ONE_DAY_BLOCKS):
+                eng.mine(1)
+            await c.send_sig(gov_addr, "castVote(uint256,uint8)", pid, 1)
+            eng.mine(ONE_WEEK_BLOCKS)
+            assert (await state())[0] == SUCCEEDED
+            await c.send_sig(gov_addr, "queue(uint256)", pid)
+            assert (await state())[0] == QUEUED
+            await c.rpc("evm_increaseTime", [3 * 86400 + 1])
+            await c.rpc("evm_mine", [])
+            await c.send_sig(gov_addr, "execute(uint256)", pid)
+            assert (await state())[0] == EXECUTED
+            assert eng.version == 7
+            cid = await c.call_sig(gov_addr, "descriptionCids(uint256)", ["bytes"], pid)
+            assert cid[0] == "0x" + onchain_cid(desc.encode()).hex()
+            await c.close()
+        finally:
+            await server.close()
+
+    asyncio.run(go())
