@@ -111,24 +111,48 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   uint4 rw[WCH], rx[XCH];
   bool xv[XCH];
   int lc0 = 0;
-  auto load_tile = [&](int kt) {
-    const int k0 = kt * BK;
-    const int rs = k0 / p.Cin;
-    const int c0 = k0 - rs * p.Cin + cc * 8;
-    lc0 = c0;
-    const int r = rs / p.kw, s = rs - (rs / p.kw) * p.kw;
+  // Incremental K walk (tap-major, then 64-channel chunks inside the tap): the (r, s) tap, the
+  // per-row input offsets and the zero-padding masks change only when the walk crosses into the
+  // next tap (every Cin/64 k-tiles), so the per-k-tile address work is two adds per chunk
+  // instead of two integer divisions + a 64-bit multiply chain (MFMA:VALU was 1:13-15 on the
+  // 64x64 tiles of the UNet's small convs; profiles/pmc_r1_v10_sd15.md).
+  int woff[WCH];
 #pragma unroll
-    for (int i = 0; i < WCH; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      rw[i] = n < p.N ? ld16(p.w + (size_t)n * p.K + k0 + cc * 8) : make_uint4(0, 0, 0, 0);
-    }
+  for (int i = 0; i < WCH; ++i) {
+    const int n = n0 + (tid >> 3) + 32 * i;
+    woff[i] = n < p.N ? n * p.K + cc * 8 : -1;
+  }
+  int wk = kt0 * BK;                                  // K offset of the next tile to load
+  int wc = wk % p.Cin, wrs = wk / p.Cin;              // channel chunk, tap index
+  int wr = wrs / p.kw, ws = wrs - wr * p.kw;          // tap (r, s)
+  int xoff[XCH];                                      // element offset of (b, hi, wi, cc*8) or -1
+  auto set_tap = [&]() {
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
-      int hi = xho[i] + r, wi = xwo[i] + s;
+      int hi = xho[i] + wr, wi = xwo[i] + ws;
       const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
       if (p.upsample) { hi >>= 1; wi >>= 1; }
-      rx[i] = ok ? ld16(p.x + (((size_t)xb[i] * p.H + hi) * p.W + wi) * p.Cin + c0) : make_uint4(0, 0, 0, 0);
+      xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + cc * 8 : -1;
+    }
+  };
+  set_tap();
+  auto load_tile = [&]() {
+    lc0 = wc + cc * 8;
+#pragma unroll
+    for (int i = 0; i < WCH; ++i)
+      rw[i] = woff[i] >= 0 ? ld16(p.w + woff[i] + wk) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const bool ok = xoff[i] >= 0;
+      rx[i] = ok ? ld16(p.x + xoff[i] + wc) : make_uint4(0, 0, 0, 0);
       xv[i] = ok;
+    }
+    wk += BK;
+    wc += BK;
+    if (wc == p.Cin) {                                // next tap (uniform branch)
+      wc = 0;
+      if (++ws == p.kw) { ws = 0; ++wr; }
+      set_tap();
     }
   };
   auto norm_tile = [&]() {
@@ -170,14 +194,14 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   if (kt0 < kt1) {
-    load_tile(kt0);
+    load_tile();
     store_tile(0);
   }
   __syncthreads();
   for (int kt = kt0; kt < kt1; ++kt) {
     const int cur = (kt - kt0) & 1;
     const bool more = kt + 1 < kt1;
-    if (more) load_tile(kt + 1);
+    if (more) load_tile();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[TN], bfr[TM];
@@ -354,31 +378,49 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
   typedef __attribute__((address_space(1))) const void* gptr_t;
   typedef __attribute__((address_space(3))) void* lptr_t;
 
-  auto issue = [&](int kt, int stage) {
-    const int k0 = kt * BK;
-    const int rs = k0 / p.Cin;
-    const int cbase = k0 - rs * p.Cin;
-    const int r = rs / p.kw, s = rs - (rs / p.kw) * p.kw;
+  // incremental K walk, as in conv_igemm_kernel: tap-dependent row offsets recomputed only when
+  // the walk enters the next (r, s) tap
+  int woff[WCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) {
+    const int n = n0 + wrow[i];
+    woff[i] = n < p.N ? n * p.K + wcc[i] * 8 : -1;
+  }
+  int wk = kt0 * BK, wc = wk % p.Cin, wrs = wk / p.Cin;
+  int wr = wrs / p.kw, ws = wrs - wr * p.kw;
+  int xoff[XCH];
+  auto set_tap = [&]() {
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      int hi = xho[i] + wr, wi = xwo[i] + ws;
+      const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
+      if (p.upsample) { hi >>= 1; wi >>= 1; }
+      xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + xcc[i] * 8 : -1;
+    }
+  };
+  set_tap();
+  auto issue = [&](int stage) {
     bf16_t* sW = smem + stage * STAGE;
     bf16_t* sX = sW + BN * BK;
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
-      const int n = n0 + wrow[i];
-      const void* src = n < p.N ? (const void*)(p.w + (size_t)n * p.K + k0 + wcc[i] * 8)
-                                : (const void*)g_conv_zero_page;
+      const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
       // wave-uniform destination: first row of this wave's 8-row slab
       bf16_t* dst = sW + ((wave * 8) + 32 * i) * BK;
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
-      int hi = xho[i] + r, wi = xwo[i] + s;
-      const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
-      if (p.upsample) { hi >>= 1; wi >>= 1; }
-      const void* src = ok ? (const void*)(p.x + (((size_t)xb[i] * p.H + hi) * p.W + wi) * p.Cin + cbase + xcc[i] * 8)
-                           : (const void*)g_conv_zero_page;
+      const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
       bf16_t* dst = sX + ((wave * 8) + 32 * i) * BK;
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    }
+    wk += BK;
+    wc += BK;
+    if (wc == p.Cin) {
+      wc = 0;
+      if (++ws == p.kw) { ws = 0; ++wr; }
+      set_tap();
     }
   };
 
@@ -391,14 +433,14 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
   // prologue: NS-1 tiles in flight
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) issue(kt0 + s, s);
+    if (s < nk) issue(s);
 
   for (int i = 0; i < nk; ++i) {
     // tile i has landed once at most (NS-2) newer tiles are outstanding
     if (i + NS - 2 < nk) wait_vmcnt<(NS - 2) * LPT>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();  // every wave's DMA for tile i is visible
-    if (i + NS - 1 < nk) issue(kt0 + i + NS - 1, (i + NS - 1) % NS);  // that stage was read at i-1
+    if (i + NS - 1 < nk) issue((i + NS - 1) % NS);  // that stage was read at i-1
     const bf16_t* sW = smem + (i % NS) * STAGE;
     const bf16_t* sX = sW + BN * BK;
 #pragma unroll
