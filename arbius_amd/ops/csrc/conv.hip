@@ -48,6 +48,10 @@ struct ConvArgs {
   int nsplit, m_fastest;
 };
 
+// 64 zero bytes: the source of every masked 16-byte operand load (zero padding, rows past M,
+// channels past N) - loads stay unconditional, so hipcc can count vmcnt instead of draining.
+__device__ __attribute__((aligned(16))) uint4 g_conv_zero_page[4];
+
 // 1-D grid of tiles_total * nsplit blocks -> (split, n-tile, m-tile), XCD-aware: consecutive
 // logical ids share an XCD (L2).  When the weights outweigh the activations (small-M deep
 // levels: a 1280x11520 conv weight is 29 MB) the m-tiles of one weight panel run together
@@ -108,9 +112,6 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     xwo[i] = (rem % p.Wo) * p.stride - p.padw;
   }
 
-  uint4 rw[WCH], rx[XCH];
-  bool xv[XCH];
-  int lc0 = 0;
   // Incremental K walk (tap-major, then 64-channel chunks inside the tap): the (r, s) tap, the
   // per-row input offsets and the zero-padding masks change only when the walk crosses into the
   // next tap (every Cin/64 k-tiles), so the per-k-tile address work is two adds per chunk
@@ -136,6 +137,125 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     }
   };
   set_tap();
+
+  // Staging depth: small tiles (MFMA work per k-tile far below a load latency) keep two k-tiles
+  // of loads in flight; large tiles keep one (their VGPR budget is spent on accumulators).
+  constexpr bool DEEP = BN * BM <= 64 * 128;
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if constexpr (DEEP) {
+  // Two register sets (A, B) -> two LDS buffers: while the MFMAs consume LDS buffer j, the loads
+  // of the NEXT TWO k-tiles are in flight (one set landing, one just issued), and the LDS write
+  // waits only for the older set (counted vmcnt: every load is unconditional, masked rows read
+  // the zero page).  The old one-set ring exposed a full load latency per k-tile, which on the
+  // small UNet tiles is 10-20x the k-tile's MFMA time.
+  struct Stage {
+    uint4 w[WCH], x[XCH];
+    bool xv[XCH];
+    int lc;
+  };
+  Stage A, B;
+  // live = false: a dead prefetch past this block's last k-tile - reads the zero page, so the
+  // issue stays unconditional (no branch around the loads for hipcc's vmcnt counting to merge)
+  const bf16_t* zp = reinterpret_cast<const bf16_t*>(g_conv_zero_page);
+  auto load_regs = [&](Stage& S, bool live) {
+    S.lc = wc + cc * 8;
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) S.w[i] = ld16(live && woff[i] >= 0 ? p.w + woff[i] + wk : zp);
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      S.xv[i] = live && xoff[i] >= 0;
+      S.x[i] = ld16(S.xv[i] ? p.x + xoff[i] + wc : zp);
+    }
+    wk += BK;
+    wc += BK;
+    if (wc == p.Cin) {                                // next tap (uniform branch)
+      wc = 0;
+      if (++ws == p.kw) { ws = 0; ++wr; }
+      set_tap();
+    }
+  };
+  auto store_regs = [&](int buf, Stage& S) {
+    if constexpr (NORM) {
+      // GroupNorm(+SiLU) prologue; zero padding stays zero (only in-bounds chunks transformed)
+#pragma unroll
+      for (int i = 0; i < XCH; ++i) {
+        if (!S.xv[i]) continue;
+        const float4* t = reinterpret_cast<const float4*>(p.norm + ((size_t)xb[i] * p.Cin + S.lc) * 2);
+        const float4 t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
+        const float sc[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
+        const float sh[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
+        float f[8];
+        unpack8(S.x[i], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = fmaf(f[e], sc[e], sh[e]);
+          f[e] = p.norm_silu ? silu_f(v) : v;
+        }
+        S.x[i] = pack8(f);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      st16(&sW[buf][row * BK + ((cc ^ (row & 7)) << 3)], S.w[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      st16(&sX[buf][row * BK + ((cc ^ (row & 7)) << 3)], S.x[i]);
+    }
+  };
+
+  auto compute = [&](int cur) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TN], bfr[TM];
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int row = wn * (BN / WN) + a * 16 + l16;
+        af[a] = __builtin_bit_cast(bf16x8, ld16(&sW[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+      }
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        const int row = wm * (BM / WM) + b * 16 + l16;
+        bfr[b] = __builtin_bit_cast(bf16x8, ld16(&sX[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+      }
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+  };
+
+  // Loads and LDS writes are unconditional (dead ones move zeros into a buffer nobody reads), so
+  // every wait in the loop is a counted vmcnt of the older set only.
+  const int nk = kt1 - kt0;
+  load_regs(A, nk > 0);
+  load_regs(B, nk > 1);
+  store_regs(0, A);
+  __syncthreads();
+  for (int i = 0; i < nk; i += 2) {
+    // even step: LDS buffer 0 holds tile i; set A (stored) is free, set B holds tile i+1
+    load_regs(A, i + 2 < nk);
+    compute(0);
+    store_regs(1, B);
+    __syncthreads();
+    if (i + 1 >= nk) break;
+    // odd step: LDS buffer 1 holds tile i+1; set B is free, set A holds tile i+2
+    load_regs(B, i + 3 < nk);
+    compute(1);
+    store_regs(0, A);
+    __syncthreads();
+  }
+
+  } else {
+  uint4 rw[WCH], rx[XCH];
+  bool xv[XCH];
+  int lc0 = 0;
   auto load_tile = [&]() {
     lc0 = wc + cc * 8;
 #pragma unroll
@@ -187,11 +307,6 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     }
   };
 
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int a = 0; a < TN; ++a)
-#pragma unroll
-    for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   if (kt0 < kt1) {
     load_tile();
@@ -222,6 +337,8 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     }
     if (more) store_tile(cur ^ 1);
     __syncthreads();
+  }
+
   }
 
   // ---- epilogue: lane holds out[m][n .. n+3]
@@ -324,7 +441,6 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
 // barriers": counted vmcnt + raw s_barrier, never __syncthreads() while DMA is in flight).
 // The XOR swizzle moves to the per-lane SOURCE address (LDS image stays lane-linear, rule 21);
 // zero padding / masked rows read a zero page.
-__device__ __attribute__((aligned(16))) uint4 g_conv_zero_page[4];
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
