@@ -38,7 +38,7 @@ def _needs(obj: Path, src: Path) -> bool:
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
-    deps = [src] + list(CSRC.glob("*.h"))
+    deps = [src] + list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc"))
     return any(d.stat().st_mtime > t for d in deps)
 
 
