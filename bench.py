@@ -33,9 +33,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--model", default="anythingv3", choices=["anythingv3", "kandinsky2", "zeroscopev2xl", "damo"],
-                    help="anythingv3 = BASELINE headline config; kandinsky2 = config #3; zeroscopev2xl = #4")
-    ap.add_argument("--frames", type=int, default=24, help="video models: frames (config #4: 24)")
+    ap.add_argument("--model", default="anythingv3",
+                    choices=["anythingv3", "kandinsky2", "zeroscopev2xl", "damo", "robust_video_matting"],
+                    help="anythingv3 = BASELINE headline config; kandinsky2 = config #3; zeroscopev2xl = #4; "
+                         "robust_video_matting = #5 (1080p clip per task)")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="video models: frames (config #4: 24); matting: clip length (default 48 = 2 s at 24 fps)")
     ap.add_argument("--concurrent", type=int, default=2,
                     help="tasks solved concurrently per GPU (pipeline forks on private HIP streams)")
     ap.add_argument("--res", type=int, default=None, help="default 512 (anythingv3) / 768 (kandinsky2)")
@@ -49,8 +52,11 @@ def main():
     args = ap.parse_args()
     k2 = args.model == "kandinsky2"
     vid = args.model in ("zeroscopev2xl", "damo")
-    args.res = args.res or (768 if k2 else 576 if args.model == "zeroscopev2xl" else 256 if vid else 512)
-    args.height = 320 if args.model == "zeroscopev2xl" else args.res
+    rvm = args.model == "robust_video_matting"
+    args.frames = args.frames or (48 if rvm else 24)
+    args.res = args.res or (768 if k2 else 576 if args.model == "zeroscopev2xl" else 256 if vid else
+                            1920 if rvm else 512)
+    args.height = 320 if args.model == "zeroscopev2xl" else 1080 if rvm else args.res
     args.denoise_steps = args.denoise_steps or (100 if k2 else 50)
 
     from arbius_amd import ops
@@ -74,11 +80,32 @@ def main():
 
     wallet = "0x" + "11" * 20
     lat = []
-    C = max(1, args.concurrent)
+    C = max(1, args.concurrent) if hasattr(pipe, "fork") else 1
     forks = [pipe.fork() for _ in range(C)] if C > 1 else [pipe]
+
+    if rvm:   # BASELINE config #5: a synthetic 1080p clip (moving gradient + noise), green-screen output
+        import numpy as np
+        rng = np.random.default_rng(1234 + rank)
+        yy, xx = np.mgrid[0:args.height, 0:args.res]
+        base = ((xx[None] + 7 * np.arange(args.frames)[:, None, None]) % 256).astype(np.uint8)
+        clip = np.stack([base, (yy[None] % 256).astype(np.uint8).repeat(args.frames, 0),
+                         rng.integers(0, 256, base.shape, dtype=np.uint8)], axis=-1)
 
     def one_task(i, pipe=pipe):
         taskid = "0x" + keccak256(f"bench-task-{rank}-{i}".encode()).hex()
+        if rvm:
+            from arbius_amd.node.solver import solve_files
+            from arbius_amd.utils.mp4 import encode_mp4
+            t0 = time.perf_counter()
+            out = pipe(clip, "green-screen")
+            t1 = time.perf_counter()
+            tm = dict(pipe.timings)
+            tm.update({"infer_s": t1 - t0})
+            sol = solve_files([("out-1.mp4", encode_mp4(list(out), 24))], tm)
+            sol.timings["encode_cid_s"] = time.perf_counter() - t1
+            generate_commitment(wallet, taskid, sol.cid)
+            lat.append(time.perf_counter() - t0)
+            return sol
         if vid:  # BASELINE config #4: 576x320x24f text-to-video
             inp = {"prompt": f"a red cat walking on a castle wall, cinematic, task {i}", "num_frames": args.frames,
                    "width": args.res, "height": args.height, "num_inference_steps": args.denoise_steps,
@@ -157,23 +184,27 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if dev.type == "cuda" else "fp32",
-            "data": "synthetic prompts, random-init weights (%s architecture)" % (
-                "Kandinsky 2.1" if k2 else "UNet3D text-to-video" if vid else "SD1.5"),
+            "dtype": ("fp16" if rvm else "bf16") if dev.type == "cuda" else "fp32",
+            "data": ("synthetic 1080p clip, random-init weights (RVM MobileNetV3 architecture)" if rvm else
+                     "synthetic prompts, random-init weights (%s architecture)" % (
+                         "Kandinsky 2.1" if k2 else "UNet3D text-to-video" if vid else "SD1.5")),
             "config": {
-                "model": ("kandinsky2 (Kandinsky 2.1: prior + GLIDE UNet + MoVQ + XLM-R/CLIP text)" if k2 else
+                "model": ("robust_video_matting (MobileNetV3 + LR-ASPP + ConvGRU decoder + DGF), "
+                          f"{args.frames}-frame {args.res}x{args.height} clip" if rvm else
+                          "kandinsky2 (Kandinsky 2.1: prior + GLIDE UNet + MoVQ + XLM-R/CLIP text)" if k2 else
                           f"{args.model} (UNet3D + KL-VAE + OpenCLIP ViT-H text), {args.frames} frames" if vid else
                           "anythingv3 (SD1.5 UNet + KL-VAE + CLIP ViT-L/14 text)") + (" TINY" if args.tiny else ""),
                 "global_batch": n * C,
                 "concurrent_tasks_per_gpu": C,
                 "seq_len": (args.res // 8) * (args.height // 8),
-                "resolution": args.res if not vid else f"{args.res}x{args.height}",
-                "denoise_steps": args.denoise_steps,
-                "scheduler": "p_sampler" if k2 else "DPMSolverMultistep" if vid else args.scheduler,
-                "cfg_batch": 2,
+                "resolution": f"{args.res}x{args.height}" if (vid or rvm) else args.res,
+                "denoise_steps": None if rvm else args.denoise_steps,
+                "scheduler": None if rvm else "p_sampler" if k2 else "DPMSolverMultistep" if vid else args.scheduler,
+                "cfg_batch": 1 if rvm else 2,
                 "parallelism": f"task-dp{n}",
             },
             "p50_task_latency_ms": round(p50, 2),
+            **({"frames_per_second": round(n * C * args.frames * 1000.0 / ms_per_step, 1)} if (rvm or vid) else {}),
             "stage_s": {k: round(v, 4) for k, v in (last.timings.items() if last else [])},
             "weight_broadcast": {"bytes": bstats["bytes"], "seconds": round(bstats["seconds"], 4)},
             "init_s": round(t_init, 2),
