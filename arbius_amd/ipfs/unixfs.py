@@ -17,6 +17,8 @@ requires.  ``Tsize`` = total bytes of the child's DAG.
 """
 from __future__ import annotations
 
+import os
+
 import hashlib
 from dataclasses import dataclass
 from typing import Dict, List, Sequence, Tuple
@@ -114,8 +116,13 @@ class DagResult:
 
 
 def _leaf(chunk: bytes) -> Tuple[bytes, int, int]:
-    blk = pb_node([], unixfs_data(2, chunk, len(chunk)))
-    return blk, len(chunk), len(blk)
+    """pb_node([], unixfs_data(2, chunk, len(chunk))) assembled with ONE copy of the chunk:
+    0a <len(inner)> | 08 02 12 <n> chunk 18 <n>  (PBNode.Data = UnixFS{File, Data, filesize})."""
+    n = len(chunk)
+    vn = varint(n)
+    inner_len = 2 + 1 + len(vn) + n + 1 + len(vn)
+    blk = b"".join((b"\x0a", varint(inner_len), b"\x08\x02\x12", vn, chunk, b"\x18", vn))
+    return blk, n, len(blk)
 
 
 def add_file(content: bytes, chunk_size: int = CHUNK) -> DagResult:
@@ -128,10 +135,23 @@ def add_file(content: bytes, chunk_size: int = CHUNK) -> DagResult:
         return DagResult(blk, mh, len(blk), blocks, fsz)
 
     # nodes as (mh, filesize, tsize)
+    view = memoryview(content)
+
+    def leaf_at(off):
+        blk, fsz, _ = _leaf(view[off:off + chunk_size])
+        return multihash_sha256(blk), blk, fsz
+
+    offs = range(0, len(content), chunk_size)
+    if len(offs) >= 32:
+        # multi-MB video outputs: leaves are independent, and sha256 / the block copy release the
+        # GIL, so hash them on a thread pool (map keeps the leaf order -> the same DAG bytes)
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+            done = list(ex.map(leaf_at, offs))
+    else:
+        done = [leaf_at(o) for o in offs]
     leaves = []
-    for off in range(0, len(content), chunk_size):
-        blk, fsz, _ = _leaf(content[off:off + chunk_size])
-        mh = multihash_sha256(blk)
+    for mh, blk, fsz in done:
         blocks[mh] = blk
         leaves.append((mh, fsz, len(blk)))
 

@@ -36,6 +36,11 @@ torch.backends.cudnn.deterministic = True
 torch.backends.cudnn.benchmark = False
 
 
+def reference_ops() -> bool:
+    """True when every op runs its fp32 PyTorch reference (A/B runs, CPU)."""
+    return _FORCE_REF
+
+
 def set_reference_ops(flag: bool) -> None:
     global _FORCE_REF
     _FORCE_REF = bool(flag)
@@ -80,10 +85,11 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
         if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
             return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride, norm=table,
                                     norm_silu=nsilu)
-        if (x.shape[-1] <= 64 or w.shape[0] % 8) and (table is None or x.shape[-1] % 64 == 0):
-            # 3/4-channel conv_in / conv_out / SpatialNorm maps: zero-pad channels onto the MFMA
-            # kernel (a few wasted FLOPs on tiny layers) instead of a library fallback - MIOpen's
-            # deterministic mode would pick its naive direct kernel for these shapes.
+        if table is None or x.shape[-1] % 64 == 0:
+            # channel counts the kernel does not tile (3/4-channel conv_in / conv_out / SpatialNorm
+            # maps, MobileNet widths 16..960): zero-pad channels onto the MFMA kernel (some wasted
+            # FLOPs) instead of a library fallback - MIOpen's deterministic mode picks its naive
+            # direct kernel for these shapes (1.1 ms per RVM conv: profiles/rocprof_r1_v11_rvm.md).
             return _padded_conv(x, w, b, padding, upsample, residual, temb, stride, table, nsilu)
     if norm is not None:
         x = apply_norm_table(x, *norm)

@@ -33,6 +33,7 @@ _SIGS = {
     "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
     "arb_norm_table_apply": (c_int, [c_void_p] * 3 + [c_int, c_long, c_int, c_int, c_void_p]),
     "arb_conv2d_nhwc": (c_int, [c_void_p] * 8 + [c_int] * 12 + [c_void_p]),
+    "arb_conv2d_nhwc_f16": (c_int, [c_void_p] * 7 + [c_int] * 11 + [c_void_p]),
     "arb_group_norm_table": (c_int, [c_void_p] * 4 + [c_float] + [c_void_p] * 2 + [c_int] * 4 + [c_float, c_void_p]),
     "arb_conv2d_workspace": (c_size_t, [c_int] * 11),
     "arb_conv2d_plan": (c_int, [c_int] * 9 + [c_void_p]),
@@ -314,8 +315,17 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
                 norm_silu=False):
     """Implicit-GEMM conv (csrc/conv.hip).  x [B,H,W,Cin], w [Cout,k,k,Cin] -> [B,Ho,Wo,Cout].
     Fused epilogue: + bias[n] + temb[b, n] + residual[m, n]; optional GroupNorm(+SiLU)
-    prologue from a ``group_norm_table`` (the normalised x never hits HBM)."""
-    _bf16(x, w, b, residual, temb)
+    prologue from a ``group_norm_table`` (the normalised x never hits HBM).  fp16 tensors run the
+    fp16 twin of the kernel (mfma f16; no norm prologue)."""
+    f16 = x.dtype == torch.float16
+    if f16:
+        for t in (w, b, residual, temb):
+            if t is not None and t.dtype != torch.float16:
+                raise TypeError("conv2d fp16: every operand must be fp16")
+        if norm is not None:
+            raise ValueError("conv2d fp16: no norm prologue")
+    else:
+        _bf16(x, w, b, residual, temb)
     x = x.contiguous()
     w = w.contiguous()
     B, H, W, Cin = x.shape
@@ -344,6 +354,10 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     args = (B, H, W, Cin, Cout, 31 if temporal else kh, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
+    if f16:
+        _check(_fn("arb_conv2d_nhwc_f16")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), *args,
+                                          _stream()), "conv2d_f16")
+        return y
     _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), _p(norm), *args,
                                   int(bool(norm_silu)), _stream()), "conv2d")
     return y

@@ -48,6 +48,46 @@ struct ConvArgs {
   int nsplit, m_fastest;
 };
 
+// ---- element type: EL = 0 bf16 (the diffusion models), EL = 1 fp16 (robust video matting).
+// Storage is raw 16-bit either way; only the MFMA flavour and the f32 <-> 16-bit conversions
+// differ, so every tiling / schedule / reduction-order property holds for both.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <int EL>
+__device__ __forceinline__ float dec16(uint32_t bits) {
+  if constexpr (EL == 0) return __uint_as_float(bits << 16);
+  else return (float)__builtin_bit_cast(_Float16, (uint16_t)bits);
+}
+template <int EL>
+__device__ __forceinline__ uint32_t enc16(float v) {
+  if constexpr (EL == 0) return (uint32_t)f2bf(v);
+  else return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)v);
+}
+template <int EL>
+__device__ __forceinline__ f32x4 mma16(uint4 a, uint4 b, f32x4 c) {
+  if constexpr (EL == 0)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// lo/hi 16-bit halves of a packed pair -> f32
+template <int EL>
+__device__ __forceinline__ float lo16(uint32_t w) { return dec16<EL>(w & 0xffffu); }
+template <int EL>
+__device__ __forceinline__ float hi16(uint32_t w) { return dec16<EL>(w >> 16); }
+template <int EL>
+__device__ __forceinline__ void unpack8e(uint4 v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { f[2 * i] = lo16<EL>(w[i]); f[2 * i + 1] = hi16<EL>(w[i]); }
+}
+template <int EL>
+__device__ __forceinline__ uint4 pack8e(const float (&f)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = enc16<EL>(f[2 * i]) | (enc16<EL>(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // 64 zero bytes: the source of every masked 16-byte operand load (zero padding, rows past M,
 // channels past N) - loads stay unconditional, so hipcc can count vmcnt instead of draining.
 __device__ __attribute__((aligned(16))) uint4 g_conv_zero_page[4];
@@ -77,8 +117,9 @@ __device__ __forceinline__ void tile_coords(const ConvArgs& p, int BN, int BM, i
 // affine table (scale, shift) - the normalised activation is never written to HBM.  Zero
 // padding stays zero (the reference pads the NORMALISED tensor), so only in-bounds chunks
 // are transformed.
-template <int BN, int BM, int WN, int WM, int MINW, bool SPLIT, bool NORM>
+template <int BN, int BM, int WN, int WM, int MINW, bool SPLIT, bool NORM, int EL = 0>
 __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
+  static_assert(EL == 0 || !NORM, "norm prologue: bf16 only");
   constexpr int BK = 64;
   static_assert(WN * WM == 4, "4 waves");
   constexpr int TN = BN / WN / 16, TM = BM / WM / 16;  // 16x16 tiles per wave
@@ -213,21 +254,21 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TN], bfr[TM];
+      uint4 af[TN], bfr[TM];
 #pragma unroll
       for (int a = 0; a < TN; ++a) {
         const int row = wn * (BN / WN) + a * 16 + l16;
-        af[a] = __builtin_bit_cast(bf16x8, ld16(&sW[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+        af[a] = ld16(&sW[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
       }
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
         const int row = wm * (BM / WM) + b * 16 + l16;
-        bfr[b] = __builtin_bit_cast(bf16x8, ld16(&sX[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+        bfr[b] = ld16(&sX[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
       }
 #pragma unroll
       for (int a = 0; a < TN; ++a)
 #pragma unroll
-        for (int b = 0; b < TM; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < TM; ++b) acc[a][b] = mma16<EL>(af[a], bfr[b], acc[a][b]);
     }
   };
 
@@ -319,21 +360,21 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     if (more) load_tile();
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TN], bfr[TM];
+      uint4 af[TN], bfr[TM];
 #pragma unroll
       for (int a = 0; a < TN; ++a) {
         const int row = wn * (BN / WN) + a * 16 + l16;
-        af[a] = __builtin_bit_cast(bf16x8, ld16(&sW[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+        af[a] = ld16(&sW[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
       }
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
         const int row = wm * (BM / WM) + b * 16 + l16;
-        bfr[b] = __builtin_bit_cast(bf16x8, ld16(&sX[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+        bfr[b] = ld16(&sX[cur][row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
       }
 #pragma unroll
       for (int a = 0; a < TN; ++a)
 #pragma unroll
-        for (int b = 0; b < TM; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < TM; ++b) acc[a][b] = mma16<EL>(af[a], bfr[b], acc[a][b]);
     }
     if (more) store_tile(cur ^ 1);
     __syncthreads();
@@ -346,22 +387,22 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   auto emit = [&](int m, int n, float v0, float v1, float v2, float v3) {
     if (p.bias) {
       const uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
-      v0 += __uint_as_float(bv.x << 16); v1 += __uint_as_float(bv.x & 0xffff0000u);
-      v2 += __uint_as_float(bv.y << 16); v3 += __uint_as_float(bv.y & 0xffff0000u);
+      v0 += lo16<EL>(bv.x); v1 += hi16<EL>(bv.x);
+      v2 += lo16<EL>(bv.y); v3 += hi16<EL>(bv.y);
     }
     if (p.temb) {
       const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)(m / hw) * p.N + n);
-      v0 += __uint_as_float(tv.x << 16); v1 += __uint_as_float(tv.x & 0xffff0000u);
-      v2 += __uint_as_float(tv.y << 16); v3 += __uint_as_float(tv.y & 0xffff0000u);
+      v0 += lo16<EL>(tv.x); v1 += hi16<EL>(tv.x);
+      v2 += lo16<EL>(tv.y); v3 += hi16<EL>(tv.y);
     }
     if (p.res) {
       const uint2 rv = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.N + n);
-      v0 += __uint_as_float(rv.x << 16); v1 += __uint_as_float(rv.x & 0xffff0000u);
-      v2 += __uint_as_float(rv.y << 16); v3 += __uint_as_float(rv.y & 0xffff0000u);
+      v0 += lo16<EL>(rv.x); v1 += hi16<EL>(rv.x);
+      v2 += lo16<EL>(rv.y); v3 += hi16<EL>(rv.y);
     }
     uint2 o;
-    o.x = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
-    o.y = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
+    o.x = enc16<EL>(v0) | (enc16<EL>(v1) << 16);
+    o.y = enc16<EL>(v2) | (enc16<EL>(v3) << 16);
     *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
   };
   if constexpr (!SPLIT) {
@@ -449,6 +490,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
 __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
+  constexpr int EL = 0;   // LDS-DMA variant: bf16 only (fp16 convs use the register-staged kernel)
   constexpr int BK = 64;
   static_assert(WN * WM == 4, "4 waves");
   constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
@@ -561,21 +603,21 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
     const bf16_t* sX = sW + BN * BK;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TN], bfr[TM];
+      uint4 af[TN], bfr[TM];
 #pragma unroll
       for (int a = 0; a < TN; ++a) {
         const int row = wn * (BN / WN) + a * 16 + l16;
-        af[a] = __builtin_bit_cast(bf16x8, ld16(&sW[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+        af[a] = ld16(&sW[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
       }
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
         const int row = wm * (BM / WM) + b * 16 + l16;
-        bfr[b] = __builtin_bit_cast(bf16x8, ld16(&sX[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]));
+        bfr[b] = ld16(&sX[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
       }
 #pragma unroll
       for (int a = 0; a < TN; ++a)
 #pragma unroll
-        for (int b = 0; b < TM; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < TM; ++b) acc[a][b] = mma16<EL>(af[a], bfr[b], acc[a][b]);
     }
     // WAR on stage i%NS is covered by the next iteration's barrier: its refill is issued
     // only after every wave has arrived there, i.e. finished this tile's MFMAs (whose
@@ -599,28 +641,29 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
       }
       if (p.bias) {
         const uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
-        v0 += __uint_as_float(bv.x << 16); v1 += __uint_as_float(bv.x & 0xffff0000u);
-        v2 += __uint_as_float(bv.y << 16); v3 += __uint_as_float(bv.y & 0xffff0000u);
+        v0 += lo16<EL>(bv.x); v1 += hi16<EL>(bv.x);
+        v2 += lo16<EL>(bv.y); v3 += hi16<EL>(bv.y);
       }
       if (p.temb) {
         const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)bb * p.N + n);
-        v0 += __uint_as_float(tv.x << 16); v1 += __uint_as_float(tv.x & 0xffff0000u);
-        v2 += __uint_as_float(tv.y << 16); v3 += __uint_as_float(tv.y & 0xffff0000u);
+        v0 += lo16<EL>(tv.x); v1 += hi16<EL>(tv.x);
+        v2 += lo16<EL>(tv.y); v3 += hi16<EL>(tv.y);
       }
       if (p.res) {
         const uint2 rv = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.N + n);
-        v0 += __uint_as_float(rv.x << 16); v1 += __uint_as_float(rv.x & 0xffff0000u);
-        v2 += __uint_as_float(rv.y << 16); v3 += __uint_as_float(rv.y & 0xffff0000u);
+        v0 += lo16<EL>(rv.x); v1 += hi16<EL>(rv.x);
+        v2 += lo16<EL>(rv.y); v3 += hi16<EL>(rv.y);
       }
       uint2 o;
-      o.x = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
-      o.y = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
+      o.x = enc16<EL>(v0) | (enc16<EL>(v1) << 16);
+      o.y = enc16<EL>(v2) | (enc16<EL>(v3) << 16);
       *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
     }
   }
 }
 
 // Ordered split-K reduction + epilogue: out[m, n..n+7] from S fp32 slabs.
+template <int EL>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
   const long total = (long)p.M * (p.N / 8);
   const int hw = p.Ho * p.Wo;
@@ -640,21 +683,21 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
     }
     float t[8];
     if (p.bias) {
-      unpack8(ld16(p.bias + n), t);
+      unpack8e<EL>(ld16(p.bias + n), t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
     if (p.temb) {
-      unpack8(ld16(p.temb + (size_t)(m / hw) * p.N + n), t);
+      unpack8e<EL>(ld16(p.temb + (size_t)(m / hw) * p.N + n), t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
     if (p.res) {
-      unpack8(ld16(p.res + (size_t)m * p.N + n), t);
+      unpack8e<EL>(ld16(p.res + (size_t)m * p.N + n), t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
-    st16(p.out + (size_t)m * p.N + n, pack8(v));
+    st16(p.out + (size_t)m * p.N + n, pack8e<EL>(v));
   }
 }
 
@@ -823,7 +866,7 @@ static void launch_glds(const ConvArgs& p, dim3 grid, hipStream_t s) {
   conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT><<<grid, 256, lds, s>>>(p);
 }
 
-template <int BN, int BM, int WN, int WM, int MINW>
+template <int BN, int BM, int WN, int WM, int MINW, int EL = 0>
 static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStream_t s) {
   // stages of the LDS-DMA ring: as many as fit 160 KiB, at most 4
   constexpr int STAGE_BYTES = (BN + BM) * 64 * 2;
@@ -833,36 +876,47 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
   p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
   p.nsplit = pl.split > 1 ? pl.split : 1;
   p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;  // weight bytes vs unique activation bytes
+  if constexpr (EL != 0) {
+    glds = false;        // fp16: register-staged kernel only, no norm prologue
+    p.norm = nullptr;
+  }
+  auto reduce = [&]() {
+    long work = (long)p.M * (p.N / 8);
+    long blocks = (work + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<EL><<<(int)blocks, 256, 0, s>>>(p, pl.split);
+  };
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
     dim3 grid(p.tiles_total * pl.split);
-    if (glds && !p.norm) {
-      p.counters = nullptr;
-      launch_glds<BN, BM, WN, WM, NS, true>(p, grid, s);
-      long work = (long)p.M * (p.N / 8);
-      long blocks = (work + 255) / 256;
-      if (blocks > 2048) blocks = 2048;
-      splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
-    } else {
-      // register-staged kernel: in-launch reduction by each tile's last block
-      // In-launch reduction is opt-in (ARB_SPLITK_INLAUNCH=1): the agent-scope release/acquire
-      // pair writes back / invalidates the XCD's L2 per block, which measured 2-3x slower than
-      // the separate ordered reduce on SD1.5 shapes (profiles/rocprof_r1_v10_*).
-      p.counters = splitk_inlaunch() ? split_counters(s, p.tiles_total) : nullptr;
-      if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, true, true><<<grid, 256, 0, s>>>(p);
-      else conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false><<<grid, 256, 0, s>>>(p);
-      if (p.counters == nullptr) {     // no ticket region available: separate ordered reduce
-        long work = (long)p.M * (p.N / 8);
-        long blocks = (work + 255) / 256;
-        if (blocks > 2048) blocks = 2048;
-        splitk_reduce_kernel<<<(int)blocks, 256, 0, s>>>(p, pl.split);
+    if constexpr (EL == 0) {
+      if (glds && !p.norm) {
+        p.counters = nullptr;
+        launch_glds<BN, BM, WN, WM, NS, true>(p, grid, s);
+        reduce();
+        return;
       }
     }
+    // register-staged kernel.  In-launch reduction is opt-in (ARB_SPLITK_INLAUNCH=1): the
+    // agent-scope release/acquire pair writes back / invalidates the XCD's L2 per block, which
+    // measured 2-3x slower than the separate ordered reduce on SD1.5 shapes.
+    p.counters = splitk_inlaunch() ? split_counters(s, p.tiles_total) : nullptr;
+    if constexpr (EL == 0) {
+      if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, true, true><<<grid, 256, 0, s>>>(p);
+      else conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false><<<grid, 256, 0, s>>>(p);
+    } else {
+      conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false, EL><<<grid, 256, 0, s>>>(p);
+    }
+    if (p.counters == nullptr) reduce();   // separate ordered reduce
   } else {
     dim3 grid(p.tiles_total, 1);
-    if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, false, true><<<grid, 256, 0, s>>>(p);
-    else if (glds) launch_glds<BN, BM, WN, WM, NS, false>(p, grid, s);
-    else conv_igemm_kernel<BN, BM, WN, WM, MINW, false, false><<<grid, 256, 0, s>>>(p);
+    if constexpr (EL == 0) {
+      if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, false, true><<<grid, 256, 0, s>>>(p);
+      else if (glds) launch_glds<BN, BM, WN, WM, NS, false>(p, grid, s);
+      else conv_igemm_kernel<BN, BM, WN, WM, MINW, false, false><<<grid, 256, 0, s>>>(p);
+    } else {
+      conv_igemm_kernel<BN, BM, WN, WM, MINW, false, false, EL><<<grid, 256, 0, s>>>(p);
+    }
   }
 }
 
@@ -870,10 +924,10 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
 // cfg/split = -1: planned; >= 0: forced (autotuning).
 // norm: optional [B, Cin, 2] fp32 (scale, shift) GroupNorm table applied to x in the prologue
 // (+ SiLU when norm_silu) - see arb_group_norm_table.  Register-staged kernels only.
-ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* temb, const void* res,
-                            void* out, void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k,
-                            int pad, int upsample, int stride, int cfg, int split, int norm_silu,
-                            hipStream_t stream) {
+template <int EL>
+static int conv_run(const void* x, const void* w, const void* bias, const void* temb, const void* res, void* out,
+                    void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
+                    int stride, int cfg, int split, int norm_silu, hipStream_t stream) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
   ConvArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = (const bf16_t*)bias; a.temb = (const bf16_t*)temb;
@@ -884,18 +938,34 @@ ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, cons
   if (pl.split > 1 && ws == nullptr) return -3;
   const bool glds = pl.cfg < kNumCfgs;  // cfg >= kNumCfgs: register-staged variant (A/B)
   switch (pl.cfg % kNumCfgs) {
-    case 0: launch_conv<128, 128, 2, 2, 2>(a, pl, glds, stream); break;
-    case 1: launch_conv<64, 128, 2, 2, 2>(a, pl, glds, stream); break;
-    case 2: launch_conv<128, 64, 2, 2, 2>(a, pl, glds, stream); break;
-    case 3: launch_conv<64, 64, 2, 2, 2>(a, pl, glds, stream); break;
-    case 4: launch_conv<160, 64, 2, 2, 2>(a, pl, glds, stream); break;
-    case 5: launch_conv<160, 128, 2, 2, 1>(a, pl, glds, stream); break;
-    case 6: launch_conv<320, 32, 4, 1, 1>(a, pl, glds, stream); break;
-    case 7: launch_conv<256, 64, 4, 1, 1>(a, pl, glds, stream); break;
-    case 8: launch_conv<128, 256, 2, 2, 1>(a, pl, glds, stream); break;
-    default: launch_conv<64, 256, 1, 4, 1>(a, pl, glds, stream); break;
+    case 0: launch_conv<128, 128, 2, 2, 2, EL>(a, pl, glds, stream); break;
+    case 1: launch_conv<64, 128, 2, 2, 2, EL>(a, pl, glds, stream); break;
+    case 2: launch_conv<128, 64, 2, 2, 2, EL>(a, pl, glds, stream); break;
+    case 3: launch_conv<64, 64, 2, 2, 2, EL>(a, pl, glds, stream); break;
+    case 4: launch_conv<160, 64, 2, 2, 2, EL>(a, pl, glds, stream); break;
+    case 5: launch_conv<160, 128, 2, 2, 1, EL>(a, pl, glds, stream); break;
+    case 6: launch_conv<320, 32, 4, 1, 1, EL>(a, pl, glds, stream); break;
+    case 7: launch_conv<256, 64, 4, 1, 1, EL>(a, pl, glds, stream); break;
+    case 8: launch_conv<128, 256, 2, 2, 1, EL>(a, pl, glds, stream); break;
+    default: launch_conv<64, 256, 1, 4, 1, EL>(a, pl, glds, stream); break;
   }
   return (int)hipGetLastError();
+}
+
+ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, const void* temb, const void* res,
+                            void* out, void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k,
+                            int pad, int upsample, int stride, int cfg, int split, int norm_silu,
+                            hipStream_t stream) {
+  return conv_run<0>(x, w, bias, temb, res, out, ws, norm, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg, split,
+                     norm_silu, stream);
+}
+
+// fp16 twin (robust video matting): same plans and tiles on mfma_f32_16x16x32_f16, no norm prologue.
+ARB_API int arb_conv2d_nhwc_f16(const void* x, const void* w, const void* bias, const void* temb, const void* res,
+                                void* out, void* ws, int B, int H, int W, int Cin, int Cout, int k, int pad,
+                                int upsample, int stride, int cfg, int split, hipStream_t stream) {
+  return conv_run<1>(x, w, bias, temb, res, out, ws, nullptr, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg,
+                     split, 0, stream);
 }
 
 ARB_API int arb_conv2d_plan(int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample, int stride,

@@ -280,3 +280,21 @@ def test_norm_table_apply(cuda, B, H, W, C, silu):
     y = _lib.norm_table_apply(x, table, silu)
     r = ops.apply_norm_table(x.float(), table, silu)
     assert _rel(y, r) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride", [(12, 72, 128, 64, 128, 3, 1), (12, 36, 64, 80, 40, 1, 1),
+                                                     (4, 144, 256, 16, 24, 3, 2), (2, 18, 32, 960, 128, 1, 1),
+                                                     (1, 9, 16, 64, 64, 3, 1)])
+def test_conv2d_fp16(cuda, B, H, W, Cin, Cout, k, stride):
+    """fp16 twin of the implicit-GEMM kernel (robust video matting), incl. zero-padded channel
+    counts (ops.conv2d pads Cin to a multiple of 64) == fp32 reference conv."""
+    from arbius_amd import ops
+    torch.manual_seed(12)
+    x = torch.randn(B, H, W, Cin, device=cuda).half()
+    w = (torch.randn(Cout, k, k, Cin, device=cuda) / math.sqrt(k * k * Cin)).half()
+    b = torch.randn(Cout, device=cuda).half()
+    y = ops.conv2d(x, w, b, stride=stride, padding=k // 2)
+    r = ref.conv2d_nhwc(x.float(), w.float(), b.float(), stride, k // 2, False)
+    assert y.dtype == torch.float16 and tuple(y.shape) == tuple(r.shape)
+    assert _rel(y, r) < 5e-3
+    assert torch.equal(y, ops.conv2d(x, w, b, stride=stride, padding=k // 2))

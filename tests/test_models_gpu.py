@@ -130,3 +130,18 @@ def test_concurrent_streams_bitwise_equal_solo(cuda):
         for _ in range(3):
             conc = list(ex.map(lambda a: solve_image(a[0], a[1]).cid, zip(forks, inps)))
             assert conc == solo
+
+
+def test_rvm_hip_convs_match_library_path(cuda):
+    """The MFMA fp16 conv route of the matting network == the library (MIOpen) convs within
+    fp16 rounding: output frames differ by at most a couple of 8-bit levels on average."""
+    import numpy as np
+    pipe = build_pipeline("robust_video_matting", device=cuda)
+    frames = np.random.default_rng(1).integers(0, 256, (4, 360, 640, 3), dtype=np.uint8)
+    a = pipe(frames, "alpha-mask").astype(np.float32)
+    ops.set_reference_ops(True)
+    try:
+        b = pipe(frames, "alpha-mask").astype(np.float32)
+    finally:
+        ops.set_reference_ops(False)
+    assert np.abs(a - b).mean() < 2.0, np.abs(a - b).mean()
