@@ -163,6 +163,27 @@ def _clip_text_rules() -> List[Rule]:
     return R
 
 
+def _xlmr_rules() -> List[Rule]:
+    """M-CLIP XLM-Roberta-Large text tower (Kandinsky 2.1): HF ``XLMRobertaModel`` names under the
+    M-CLIP ``transformer.`` prefix, + ``LinearTransformation`` (1024 -> 768)."""
+    E, L = "transformer.embeddings", "transformer.encoder.layer.#"
+    R: List[Rule] = [("tok.weight", "copy", (f"{E}.word_embeddings.weight",)),
+                     ("pos.weight", "copy", (f"{E}.position_embeddings.weight",)),
+                     ("tok_type.weight", "copy", (f"{E}.token_type_embeddings.weight",)),
+                     ("ln.weight", "copy", (f"{E}.LayerNorm.weight",)), ("ln.bias", "copy", (f"{E}.LayerNorm.bias",)),
+                     ("proj.weight", "copy", ("LinearTransformation.weight",)),
+                     ("proj.bias", "copy", ("LinearTransformation.bias",))]
+    for p in ("weight", "bias"):
+        R.extend([(f"layers.#.qkv.{p}", "cat", (f"{L}.attention.self.query.{p}", f"{L}.attention.self.key.{p}",
+                                                 f"{L}.attention.self.value.{p}")),
+                  (f"layers.#.out.{p}", "copy", (f"{L}.attention.output.dense.{p}",)),
+                  (f"layers.#.ln1.{p}", "copy", (f"{L}.attention.output.LayerNorm.{p}",)),
+                  (f"layers.#.fc1.{p}", "copy", (f"{L}.intermediate.dense.{p}",)),
+                  (f"layers.#.fc2.{p}", "copy", (f"{L}.output.dense.{p}",)),
+                  (f"layers.#.ln2.{p}", "copy", (f"{L}.output.LayerNorm.{p}",))])
+    return R
+
+
 def normalize_clip_names(src: Dict[str, Tensor]) -> Dict[str, Tensor]:
     """transformers >= 5 drops the ``text_model.`` prefix of CLIPTextModel state dicts; the files of
     public SD checkpoints keep it.  Accept both."""
@@ -173,7 +194,7 @@ def normalize_clip_names(src: Dict[str, Tensor]) -> Dict[str, Tensor]:
 
 
 RULES: Dict[str, Callable[[], List[Rule]]] = {
-    "unet": _sd15_unet_rules, "vae": _vae_decoder_rules, "text": _clip_text_rules}
+    "unet": _sd15_unet_rules, "vae": _vae_decoder_rules, "text": _clip_text_rules, "mclip": _xlmr_rules}
 
 
 def _pattern(p: str) -> re.Pattern:

@@ -12,14 +12,16 @@ from arbius_amd.models.clip_text import CLIPTextConfig, CLIPTextEncoder
 from arbius_amd.models.registry import build_pipeline
 
 
-def test_clip_text_matches_transformers_clip():
+@pytest.mark.parametrize("act", ["quick_gelu", "gelu"])   # ViT-L/14 (SD1.5, Kandinsky prior) / ViT-H/14 (zeroscope)
+def test_clip_text_matches_transformers_clip(act):
     transformers = pytest.importorskip("transformers")
     torch.manual_seed(0)
     hf_cfg = transformers.CLIPTextConfig(vocab_size=1000, hidden_size=64, intermediate_size=128,
                                          num_hidden_layers=2, num_attention_heads=4, max_position_embeddings=77,
-                                         hidden_act="quick_gelu", bos_token_id=0, eos_token_id=2)
+                                         hidden_act=act, bos_token_id=0, eos_token_id=2)
     hf = transformers.CLIPTextModel(hf_cfg).eval()
-    ours = CLIPTextEncoder(CLIPTextConfig(vocab=1000, max_len=77, width=64, layers=2, heads=4, mlp=128)).eval()
+    ours = CLIPTextEncoder(CLIPTextConfig(vocab=1000, max_len=77, width=64, layers=2, heads=4, mlp=128,
+                                          quick_gelu=act == "quick_gelu")).eval()
     src = W.normalize_clip_names(dict(hf.state_dict()))
     W.load_state(ours, W.convert(W.RULES["text"](), dict(ours.named_parameters()), src))
     ids = torch.randint(1, 998, (2, 77))
@@ -64,3 +66,32 @@ def test_native_layout_round_trip_and_strictness(tmp_path):
 def test_missing_weights_dir_is_an_error(tmp_path):
     with pytest.raises(FileNotFoundError):
         build_pipeline("anythingv3", tiny=True, weights_dir=str(tmp_path))
+
+
+def test_mclip_xlmr_matches_transformers_xlm_roberta():
+    """Kandinsky's multilingual text tower (post-LN XLM-R, per-sequence K/V slicing instead of a
+    key mask) == transformers XLMRobertaModel with an attention mask, pads included."""
+    transformers = pytest.importorskip("transformers")
+    from arbius_amd.models.xlmr import MCLIPText, XLMRConfig
+    torch.manual_seed(0)
+    hf_cfg = transformers.XLMRobertaConfig(vocab_size=1000, hidden_size=32, num_hidden_layers=2,
+                                           num_attention_heads=2, intermediate_size=64, max_position_embeddings=100,
+                                           type_vocab_size=1, pad_token_id=1, layer_norm_eps=1e-5)
+    hf = transformers.XLMRobertaModel(hf_cfg, add_pooling_layer=False).eval()
+    ours = MCLIPText(XLMRConfig.tiny()).eval()
+    src = {"transformer." + k: v for k, v in hf.state_dict().items()}
+    src["LinearTransformation.weight"] = torch.randn(32, 32)
+    src["LinearTransformation.bias"] = torch.randn(32)
+    target = dict(ours.named_parameters())
+    W.load_state(ours, W.convert(W.RULES["mclip"](), target, src))
+    n = 9
+    ids = torch.full((1, 77), 1, dtype=torch.long)
+    ids[0, :n] = torch.randint(3, 999, (n,))
+    ids[0, 0], ids[0, n - 1] = 0, 2
+    mask = (ids != 1).long()
+    with torch.no_grad():
+        ref = hf(input_ids=ids, attention_mask=mask).last_hidden_state
+        got, pooled = ours(ids, n)
+    assert torch.allclose(got, ref, atol=3e-5, rtol=1e-4), (got - ref).abs().max()
+    exp_pool = ref[:, :n].mean(1) @ src["LinearTransformation.weight"].T + src["LinearTransformation.bias"]
+    assert torch.allclose(pooled, exp_pool, atol=3e-5, rtol=1e-4)
