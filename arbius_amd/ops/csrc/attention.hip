@@ -115,22 +115,52 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
 
   uint4 rk[KPT], rv[VPT];
   const uint32_t one_bits = 0x3F80u;  // bf16 1.0
-  auto load_kv = [&](int kv) {
+  // Per-thread staging geometry is fixed across key tiles: row / column of each 16-byte chunk,
+  // its in-range flag, and the row pointer (main K/V segment).  Full tiles of the main segment
+  // then cost one uniform offset add per chunk; partial / prefix-straddling tiles take the
+  // general path (bounds + prefix select per row).
+  int kr[KPT], kc[KPT], vr[VPT], vc[VPT];
+  bool kok[KPT], vok[VPT], vone[VPT];
+  const bf16_t* kp0[KPT];
+  const bf16_t* vp0[VPT];
 #pragma unroll
-    for (int i = 0; i < KPT; ++i) {
-      const int c = tid + 256 * i;
-      const int r = c / (KSTEPS * 4), col = (c % (KSTEPS * 4)) * 8;
-      rk[i] = (c < KCH && kv + r < a.Nk && col < D) ? ld16(krow(kv + r) + col) : make_uint4(0, 0, 0, 0);
+  for (int i = 0; i < KPT; ++i) {
+    const int c = tid + 256 * i;
+    kr[i] = c / (KSTEPS * 4);
+    kc[i] = (c % (KSTEPS * 4)) * 8;
+    kok[i] = c < KCH && kc[i] < D;
+    kp0[i] = kbase + (long)kr[i] * a.k_sn + kc[i];
+  }
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = tid + 256 * i;
+    vr[i] = c / (DT * 2);
+    vc[i] = (c % (DT * 2)) * 8;
+    vok[i] = c < VCH && vc[i] < D;
+    // column D is the first element of the first all-padding 8-chunk when D % 16 == 8
+    vone[i] = ONES && c < VCH && vc[i] == (D & ~7);
+    vp0[i] = vbase + (long)vr[i] * a.v_sn + vc[i];
+  }
+  auto load_kv = [&](int kv) {
+    if (kv >= a.Np && kv + KV_BLK <= a.Nk) {          // full tile of the main segment (uniform)
+      const long ko = (long)(kv - a.Np) * a.k_sn, vo = (long)(kv - a.Np) * a.v_sn;
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) rk[i] = kok[i] ? ld16(kp0[i] + ko) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        uint4 val = vok[i] ? ld16(vp0[i] + vo) : make_uint4(0, 0, 0, 0);
+        if (vone[i]) val.x = (val.x & 0xffff0000u) | one_bits;
+        rv[i] = val;
+      }
+      return;
     }
 #pragma unroll
+    for (int i = 0; i < KPT; ++i)
+      rk[i] = (kok[i] && kv + kr[i] < a.Nk) ? ld16(krow(kv + kr[i]) + kc[i]) : make_uint4(0, 0, 0, 0);
+#pragma unroll
     for (int i = 0; i < VPT; ++i) {
-      const int c = tid + 256 * i;
-      const int r = c / (DT * 2), col = (c % (DT * 2)) * 8;
-      uint4 val = (c < VCH && kv + r < a.Nk && col < D) ? ld16(vrow(kv + r) + col) : make_uint4(0, 0, 0, 0);
-      if (ONES && col == (D & ~7)) {
-        // column D is the first element of the first all-padding 8-chunk when D % 16 == 8
-        val.x = (val.x & 0xffff0000u) | one_bits;
-      }
+      uint4 val = (vok[i] && kv + vr[i] < a.Nk) ? ld16(vrow(kv + vr[i]) + vc[i]) : make_uint4(0, 0, 0, 0);
+      if (vone[i]) val.x = (val.x & 0xffff0000u) | one_bits;
       rv[i] = val;
     }
   };
