@@ -6,7 +6,7 @@ MODELS=${2:-sd15}
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python scripts/autotune_conv.py $O --models $MODELS --legacy-only --merge arbius_amd/ops/csrc/conv_plans.inc > $O/autotune.log 2>&1 || { tail -20 $O/autotune.log; exit 1; }
+timeout -k 10 900 python scripts/autotune_conv.py $O --models $MODELS ${AT_FLAGS---legacy-only} --merge arbius_amd/ops/csrc/conv_plans.inc > $O/autotune.log 2>&1 || { tail -20 $O/autotune.log; exit 1; }
 tail -3 $O/autotune.log
 cp $O/conv_plans.inc arbius_amd/ops/csrc/conv_plans.inc && python -m arbius_amd.ops.build > $O/build.log 2>&1 || { tail $O/build.log; exit 1; }
 for c in 1 2; do
