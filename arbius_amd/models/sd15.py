@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import time
 from dataclasses import dataclass, field
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
@@ -120,12 +120,15 @@ class SD15Pipeline(PipelineBase):
         return n.permute(0, 2, 3, 1).contiguous(), g  # NHWC
 
     def _unet_eval(self, x2, t, ctx):
-        if not self.use_graphs:
-            return self.unet(x2, torch.tensor([float(t)], device=self.device), ctx)
-        key = tuple(x2.shape)
-        if key not in self._graphs:
-            self._graphs[key] = _GraphedUNet(self.unet, x2.shape, ctx, self.dtype)
-        return self._graphs[key](x2, t, ctx)
+        # batch-invariant plans (ops.plan_batch): one CFG pair is the planning unit, so a
+        # lock-step group of k tasks (batch 2k) computes each task's bytes exactly as solo
+        with ops.plan_batch(2):
+            if not self.use_graphs:
+                return self.unet(x2, torch.tensor([float(t)], device=self.device), ctx)
+            key = tuple(x2.shape)
+            if key not in self._graphs:
+                self._graphs[key] = _GraphedUNet(self.unet, x2.shape, ctx, self.dtype)
+            return self._graphs[key](x2, t, ctx)
 
     @torch.no_grad()
     def __call__(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
@@ -154,6 +157,45 @@ class SD15Pipeline(PipelineBase):
             img = self.decode(x)
         self.timings = tm
         return img
+
+    @torch.no_grad()
+    def run_group(self, inps: List[dict]) -> List[np.ndarray]:
+        """Lock-step solve of k compatible tasks (same width / height / steps / scheduler): every
+        UNet evaluation runs the k CFG pairs as ONE batch-2k launch sequence (k x the rows per
+        GEMM / conv -> fuller tiles, 1/k of the launches per task), while text encoding, noise,
+        the sampler state and the VAE stay per task.  With batch-invariant plans each output
+        is bitwise the solo output (tests/test_models_gpu.py)."""
+        keys = {(int(i.get("width", 768)), int(i.get("height", 768)), int(i.get("num_inference_steps", 20)),
+                 i.get("scheduler", "DPMSolverMultistep")) for i in inps}
+        if len(keys) != 1:
+            raise ValueError(f"run_group needs identical width/height/steps/scheduler, got {sorted(keys)}")
+        width, height, steps, scheduler = keys.pop()
+        with self._stream_ctx():
+            sync = self._sync
+            tm: Dict[str, float] = {}
+            with span("text_s", tm, sync):
+                ctxs, xs, gens, scheds = [], [], [], []
+                for inp in inps:
+                    ctxs.append(self.encode_prompt(inp["prompt"], inp.get("negative_prompt", "")))
+                    x, gen = self.initial_noise(int(inp["seed"]), height // 8, width // 8,
+                                                self.cfg.unet.in_channels)
+                    sched = make_scheduler(scheduler, steps)
+                    xs.append((x * sched.init_noise_sigma).to(self.device))
+                    gens.append(gen)
+                    scheds.append(sched)
+                ctx = torch.cat(ctxs)
+                gs = [float(inp.get("guidance_scale", 12)) for inp in inps]
+            with span("denoise_s", tm, sync):
+                for i, t in enumerate(scheds[0].timesteps):
+                    xin = [s.scale_model_input(x, i).to(self.dtype) for s, x in zip(scheds, xs)]
+                    eps_all = self._unet_eval(torch.cat([v for x in xin for v in (x, x)]), t, ctx)
+                    for k, (s, g) in enumerate(zip(scheds, gs)):
+                        eps = ops.ref.cfg_combine(eps_all[2 * k:2 * k + 2], g)
+                        xs[k] = s.step(eps, i, xs[k], gens[k])
+            with span("vae_s", tm, sync):
+                imgs = [self.decode(x) for x in xs]
+            self.timings = tm
+            return imgs
 
     @torch.no_grad()
     def decode(self, latent):

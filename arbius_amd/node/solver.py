@@ -47,6 +47,34 @@ def solve_image(pipe, inp: dict, png_level: int = 6) -> Solution:
     return Solution([("out-1.png", png)], dag.cid_hex, dag, tm)
 
 
+def solve_images(pipe, inps: List[dict], png_level: int = 6) -> List[Solution]:
+    """k compatible SD-family tasks solved lock-step (``run_group``): same bytes as k solo solves."""
+    if len(inps) == 1 or not hasattr(pipe, "run_group"):
+        return [solve_image(pipe, i, png_level) for i in inps]
+    t0 = time.perf_counter()
+    imgs = pipe.run_group([dict(i, width=int(i.get("width", 768)), height=int(i.get("height", 768)),
+                                num_inference_steps=int(i.get("num_inference_steps", 20)),
+                                scheduler=i.get("scheduler", "DPMSolverMultistep")) for i in inps])
+    t1 = time.perf_counter()
+    out = []
+    for img in imgs:
+        png = encode_png(img, png_level)
+        dag = wrap_directory([("out-1.png", png)])
+        out.append(Solution([("out-1.png", png)], dag.cid_hex, dag, {}))
+    t2 = time.perf_counter()
+    tm = dict(getattr(pipe, "timings", {}))
+    tm.update({"infer_s": t1 - t0, "encode_cid_s": t2 - t1, "group": len(inps)})
+    for s in out:
+        s.timings = dict(tm)
+    return out
+
+
+def group_key(inp: dict):
+    """Tasks with equal keys can share lock-step launches (SD-family image templates)."""
+    return (int(inp.get("width", 768)), int(inp.get("height", 768)), int(inp.get("num_inference_steps", 20)),
+            inp.get("scheduler", "DPMSolverMultistep"))
+
+
 def solve_files(files, timings=None) -> Solution:
     dag = wrap_directory(list(files))
     return Solution(list(files), dag.cid_hex, dag, dict(timings or {}))

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 
 import torch
 import torch.nn.functional as F
@@ -46,6 +47,35 @@ def set_reference_ops(flag: bool) -> None:
     _FORCE_REF = bool(flag)
 
 
+# ------------------------------------------------------------------ batch-invariant planning
+# Consensus needs a task's bytes to be independent of which other tasks share its launches.
+# Inside ``plan_batch(unit)`` every conv / GEMM plan (tile config + split-K) is chosen for the
+# ``unit``-sample shape even when the tensor holds k*unit samples (lock-step task groups), and
+# plain linears run on the implicit-GEMM kernel too (a library GEMM picks its algorithm - and
+# so its k-reduction order - by M).  Per-element arithmetic then depends only on the unit
+# shape: a group of tasks reproduces every solo task's output bit for bit.  Thread-local, so
+# concurrent pipeline forks on other threads keep their own scope.
+_TL = threading.local()
+
+
+class plan_batch:
+    def __init__(self, unit: int):
+        self.unit = int(unit)
+
+    def __enter__(self):
+        self.prev = getattr(_TL, "pb", None)
+        _TL.pb = self.unit
+        return self
+
+    def __exit__(self, *exc):
+        _TL.pb = self.prev
+
+
+def _plan_div(batch: int) -> int:
+    pb = getattr(_TL, "pb", None)
+    return batch // pb if pb and batch > pb and batch % pb == 0 else 1
+
+
 def _hip(t: torch.Tensor) -> bool:
     return t.is_cuda and not _FORCE_REF
 
@@ -57,8 +87,8 @@ def linear(x, w, b=None, residual=None):
     GPU: with a residual (attention out-proj, FF down-proj, proj_out) the
     implicit-GEMM kernel fuses bias + residual into its epilogue; plain
     projections go to hipBLASLt (bias fused by the library)."""
-    if residual is not None and _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]):
-        return _lib.gemm(x, w, b, residual)
+    if _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]) and (residual is not None or getattr(_TL, "pb", None)):
+        return _lib.gemm(x, w, b, residual, plan_div=_plan_div(x.shape[0]))
     if residual is not None:
         x2 = x.reshape(-1, x.shape[-1])
         r2 = residual.reshape(-1, w.shape[0])
@@ -81,10 +111,13 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
     if _hip(x) and kern_ok:
         table, nsilu = norm if norm is not None else (None, False)
         if table is not None and not _NORM_PROLOGUE and x.shape[-1] % 8 == 0:
-            x, table, nsilu = _lib.norm_table_apply(x, table, nsilu), None, False
+            if "gnapply" in _EXP_SKIP:
+                table, nsilu = None, False
+            else:
+                x, table, nsilu = _lib.norm_table_apply(x, table, nsilu), None, False
         if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
             return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride, norm=table,
-                                    norm_silu=nsilu)
+                                    norm_silu=nsilu, plan_div=_plan_div(x.shape[0]))
         if table is None or x.shape[-1] % 64 == 0:
             # channel counts the kernel does not tile (3/4-channel conv_in / conv_out / SpatialNorm
             # maps, MobileNet widths 16..960): zero-pad channels onto the MFMA kernel (some wasted
@@ -140,21 +173,31 @@ def _padded_conv(x, w, b, padding, upsample, residual, temb, stride, table=None,
         x = F.pad(x, (0, wp.shape[-1] - cin))
     if wp.shape[0] != cout:
         y = _lib.conv2d_nhwc(x, wp, bp, padding, upsample, None, None, stride, norm=table,
-                             norm_silu=nsilu)[..., :cout]
+                             norm_silu=nsilu, plan_div=_plan_div(x.shape[0]))[..., :cout]
         if temb is not None:
             y = y + temb[:, None, None, :].to(y.dtype)
         if residual is not None:
             y = y + residual
         return y.contiguous()
-    return _lib.conv2d_nhwc(x, wp, bp, padding, upsample, residual, temb, stride, norm=table, norm_silu=nsilu)
+    return _lib.conv2d_nhwc(x, wp, bp, padding, upsample, residual, temb, stride, norm=table, norm_silu=nsilu,
+                            plan_div=_plan_div(x.shape[0]))
 
 
 # --------------------------------------------------------------------------- normalisation
+_EXP_SKIP = os.environ.get("ARBIUS_EXPERIMENT_SKIP", "")   # sensitivity experiments only (wrong outputs)
+_EXP_TABLES = {}
+
+
 def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
     """GroupNorm of x as a per-(batch, channel) affine table [B, C, 2] fp32 (scale, shift) for a
     consumer prologue (conv/GEMM); ``mod`` [B, 2C] folds the GLIDE scale-shift modulation
     (out = GN(x) * (mod[:, :C] + one_plus) + mod[:, C:])."""
     if _hip(x):
+        if "gnstats" in _EXP_SKIP:
+            key = (x.shape[0], x.shape[-1])
+            if key not in _EXP_TABLES:
+                _EXP_TABLES[key] = torch.ones(x.shape[0], x.shape[-1], 2, device=x.device)
+            return _EXP_TABLES[key]
         return _lib.group_norm_table(x, gamma, beta, groups, eps, mod, one_plus)
     return ref.group_norm_table(x, gamma, beta, groups, eps, mod, one_plus)
 

@@ -312,7 +312,7 @@ def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
 
 
 def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-1, split=-1, norm=None,
-                norm_silu=False):
+                norm_silu=False, plan_div=1):
     """Implicit-GEMM conv (csrc/conv.hip).  x [B,H,W,Cin], w [Cout,k,k,Cin] -> [B,Ho,Wo,Cout].
     Fused epilogue: + bias[n] + temb[b, n] + residual[m, n]; optional GroupNorm(+SiLU)
     prologue from a ``group_norm_table`` (the normalised x never hits HBM).  fp16 tensors run the
@@ -351,7 +351,10 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     if norm is not None:
         if norm.dtype != torch.float32 or tuple(norm.shape) != (B, Cin, 2) or not norm.is_contiguous():
             raise ValueError("conv2d norm table must be contiguous fp32 [B, Cin, 2]")
-    args = (B, H, W, Cin, Cout, 31 if temporal else kh, padding, int(bool(upsample)), stride, int(cfg), int(split))
+    kcode = 31 if temporal else kh
+    if plan_div > 1 and cfg < 0:     # batch-invariant: the plan of the B/plan_div-sample shape
+        cfg, split = conv_plan(B // plan_div, H, W, Cin, Cout, kcode, padding, upsample, stride)
+    args = (B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
     if f16:
@@ -363,8 +366,9 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     return y
 
 
-def gemm(x, w, b=None, residual=None, cfg=-1, split=-1):
-    """out = x @ w^T (+ b + residual) on the implicit-GEMM kernel. x [...,K], w [N,K]."""
+def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_div=1):
+    """out = x @ w^T (+ b + residual) on the implicit-GEMM kernel. x [...,K], w [N,K].
+    plan_div > 1: plan for M / plan_div rows (batch-invariant lock-step groups)."""
     _bf16(x, w, b, residual)
     K = x.shape[-1]
     N = w.shape[0]
@@ -372,6 +376,8 @@ def gemm(x, w, b=None, residual=None, cfg=-1, split=-1):
     M = x2.shape[0]
     if K % 64 or N % 8 or w.shape[1] != K:
         raise ValueError(f"gemm: unsupported K={K} N={N}")
+    if plan_div > 1 and cfg < 0:
+        cfg, split = conv_plan(1, 1, M // plan_div, K, N, 1, 0, 0, 1)
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))

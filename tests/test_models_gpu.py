@@ -145,3 +145,16 @@ def test_rvm_hip_convs_match_library_path(cuda):
     finally:
         ops.set_reference_ops(False)
     assert np.abs(a - b).mean() < 2.0, np.abs(a - b).mean()
+
+
+def test_lockstep_group_bitwise_equals_solo(cuda):
+    """Batch-invariant plans: k tasks solved lock-step in ONE batch-2k UNet launch sequence give
+    exactly the solo CIDs (consensus must not depend on which tasks shared a launch)."""
+    from arbius_amd.node.solver import solve_image, solve_images
+    pipe = build_pipeline("anythingv3", device=cuda)
+    inps = [{"prompt": f"castle {i}", "negative_prompt": "blurry", "width": 256, "height": 256,
+             "num_inference_steps": 4, "guidance_scale": 7.0 + i, "scheduler": "DPMSolverMultistep",
+             "seed": 40 + i} for i in range(3)]
+    solo = [solve_image(pipe, i).cid for i in inps]
+    assert [s.cid for s in solve_images(pipe, inps)] == solo
+    assert [s.cid for s in solve_images(pipe, inps[:2])] == solo[:2]

@@ -208,3 +208,21 @@ def test_boot_selftest_pins_per_hardware_cid(tmp_path):
                     mi355x={"selftest": True, "selftest_table": str(p)})
     with pytest.raises(SystemExit):
         asyncio.run(m2.boot())
+
+
+def test_lockstep_group_matches_solo_on_cpu_reference():
+    """run_group's bookkeeping (per-task noise, sampler state, guidance, VAE) on the CPU fp32
+    reference path: images equal the solo ones up to CPU GEMM batch rounding (<= 1 level)."""
+    import numpy as np
+    from arbius_amd.models.registry import build_pipeline
+    pipe = build_pipeline("anythingv3", tiny=True)
+    inps = [{"prompt": f"cat {i}", "negative_prompt": "", "width": 64, "height": 64, "num_inference_steps": 3,
+             "guidance_scale": 7.5 + i, "scheduler": "DPMSolverMultistep", "seed": 10 + i} for i in range(3)]
+    solo = [pipe(prompt=i["prompt"], negative_prompt="", width=64, height=64, num_inference_steps=3,
+                 guidance_scale=i["guidance_scale"], scheduler="DPMSolverMultistep", seed=i["seed"]) for i in inps]
+    grp = pipe.run_group(inps)
+    for a, b in zip(solo, grp):
+        assert np.abs(a.astype(int) - b.astype(int)).max() <= 1
+    import pytest
+    with pytest.raises(ValueError):
+        pipe.run_group([inps[0], dict(inps[1], num_inference_steps=4)])
