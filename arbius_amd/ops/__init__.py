@@ -71,9 +71,17 @@ class plan_batch:
         _TL.pb = self.prev
 
 
-def _plan_div(batch: int) -> int:
+# The canonical batch whose plans every batch-invariant launch uses (a multiple of the unit).
+# 2 = a solo task's own plans; 8 = plans tuned for lock-step groups of 4 (bench default),
+# which a solo task then also runs (same bits, slightly less fill on its own).
+PLAN_CANON = int(os.environ.get("ARBIUS_PLAN_CANON", "8"))
+
+
+def _canon_batch(batch: int):
     pb = getattr(_TL, "pb", None)
-    return batch // pb if pb and batch > pb and batch % pb == 0 else 1
+    if not pb or batch % pb:
+        return None
+    return max(PLAN_CANON, pb) // pb * pb
 
 
 def _hip(t: torch.Tensor) -> bool:
@@ -88,7 +96,7 @@ def linear(x, w, b=None, residual=None):
     implicit-GEMM kernel fuses bias + residual into its epilogue; plain
     projections go to hipBLASLt (bias fused by the library)."""
     if _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]) and (residual is not None or getattr(_TL, "pb", None)):
-        return _lib.gemm(x, w, b, residual, plan_div=_plan_div(x.shape[0]))
+        return _lib.gemm(x, w, b, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
     if residual is not None:
         x2 = x.reshape(-1, x.shape[-1])
         r2 = residual.reshape(-1, w.shape[0])
@@ -117,7 +125,7 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
                 x, table, nsilu = _lib.norm_table_apply(x, table, nsilu), None, False
         if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
             return _lib.conv2d_nhwc(x, w, b, padding, upsample, residual, temb, stride, norm=table,
-                                    norm_silu=nsilu, plan_div=_plan_div(x.shape[0]))
+                                    norm_silu=nsilu, plan_b=_canon_batch(x.shape[0]))
         if table is None or x.shape[-1] % 64 == 0:
             # channel counts the kernel does not tile (3/4-channel conv_in / conv_out / SpatialNorm
             # maps, MobileNet widths 16..960): zero-pad channels onto the MFMA kernel (some wasted
@@ -173,14 +181,14 @@ def _padded_conv(x, w, b, padding, upsample, residual, temb, stride, table=None,
         x = F.pad(x, (0, wp.shape[-1] - cin))
     if wp.shape[0] != cout:
         y = _lib.conv2d_nhwc(x, wp, bp, padding, upsample, None, None, stride, norm=table,
-                             norm_silu=nsilu, plan_div=_plan_div(x.shape[0]))[..., :cout]
+                             norm_silu=nsilu, plan_b=_canon_batch(x.shape[0]))[..., :cout]
         if temb is not None:
             y = y + temb[:, None, None, :].to(y.dtype)
         if residual is not None:
             y = y + residual
         return y.contiguous()
     return _lib.conv2d_nhwc(x, wp, bp, padding, upsample, residual, temb, stride, norm=table, norm_silu=nsilu,
-                            plan_div=_plan_div(x.shape[0]))
+                            plan_b=_canon_batch(x.shape[0]))
 
 
 # --------------------------------------------------------------------------- normalisation

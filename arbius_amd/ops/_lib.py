@@ -312,7 +312,7 @@ def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
 
 
 def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-1, split=-1, norm=None,
-                norm_silu=False, plan_div=1):
+                norm_silu=False, plan_b=None):
     """Implicit-GEMM conv (csrc/conv.hip).  x [B,H,W,Cin], w [Cout,k,k,Cin] -> [B,Ho,Wo,Cout].
     Fused epilogue: + bias[n] + temb[b, n] + residual[m, n]; optional GroupNorm(+SiLU)
     prologue from a ``group_norm_table`` (the normalised x never hits HBM).  fp16 tensors run the
@@ -352,8 +352,8 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
         if norm.dtype != torch.float32 or tuple(norm.shape) != (B, Cin, 2) or not norm.is_contiguous():
             raise ValueError("conv2d norm table must be contiguous fp32 [B, Cin, 2]")
     kcode = 31 if temporal else kh
-    if plan_div > 1 and cfg < 0:     # batch-invariant: the plan of the B/plan_div-sample shape
-        cfg, split = conv_plan(B // plan_div, H, W, Cin, Cout, kcode, padding, upsample, stride)
+    if plan_b and plan_b != B and cfg < 0:   # batch-invariant: the canonical batch's plan
+        cfg, split = conv_plan(plan_b, H, W, Cin, Cout, kcode, padding, upsample, stride)
     args = (B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
@@ -366,9 +366,9 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     return y
 
 
-def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_div=1):
+def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None):
     """out = x @ w^T (+ b + residual) on the implicit-GEMM kernel. x [...,K], w [N,K].
-    plan_div > 1: plan for M / plan_div rows (batch-invariant lock-step groups)."""
+    plan_batch = (batch, canonical batch): plan for M * canonical / batch rows (batch-invariant)."""
     _bf16(x, w, b, residual)
     K = x.shape[-1]
     N = w.shape[0]
@@ -376,8 +376,8 @@ def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_div=1):
     M = x2.shape[0]
     if K % 64 or N % 8 or w.shape[1] != K:
         raise ValueError(f"gemm: unsupported K={K} N={N}")
-    if plan_div > 1 and cfg < 0:
-        cfg, split = conv_plan(1, 1, M // plan_div, K, N, 1, 0, 0, 1)
+    if plan_batch and plan_batch[1] and plan_batch[1] != plan_batch[0] and cfg < 0:
+        cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))

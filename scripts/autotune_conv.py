@@ -25,14 +25,14 @@ NCFG = 20  # 0-9: LDS-DMA multi-stage, 10-19: register-staged
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
-def _run_meta(models, res):
+def _run_meta(models, res, batch=2):
     """Run the selected model families on the meta device (shapes only)."""
     with torch.device("meta"):
         if "sd15" in models:
             from arbius_amd.models.unet2d import UNet2DCondition, UNetConfig
             from arbius_amd.models.vae import VAEDecoder
-            UNet2DCondition(UNetConfig())(torch.zeros(2, res // 8, res // 8, 4), torch.tensor([500.0]),
-                                          torch.zeros(2, 77, 768))
+            UNet2DCondition(UNetConfig())(torch.zeros(batch, res // 8, res // 8, 4), torch.tensor([500.0]),
+                                          torch.zeros(batch, 77, 768))
             VAEDecoder()(torch.zeros(1, res // 8, res // 8, 4))
         if "kandinsky2" in models:
             from arbius_amd.models.glide_unet import GlideUNet
@@ -47,7 +47,7 @@ def _run_meta(models, res):
             VAEDecoder()(torch.zeros(8, 40, 72, 4))
 
 
-def collect_shapes(models=("sd15",), res=512):
+def collect_shapes(models=("sd15",), res=512, batch=2):
     convs, gemms = set(), set()
     orig_conv, orig_lin = ops.conv2d, ops.linear
 
@@ -58,13 +58,14 @@ def collect_shapes(models=("sd15",), res=512):
         return orig_conv(x, w, b, stride, padding, upsample, residual, temb, norm)
 
     def lin(x, w, b=None, residual=None):
-        if residual is not None and x.shape[-1] % 64 == 0:
+        # every linear: under batch-invariant planning plain projections run on this kernel too
+        if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
             gemms.add((x.numel() // x.shape[-1], x.shape[-1], w.shape[0]))
         return orig_lin(x, w, b, residual)
 
     ops.conv2d, ops.linear = conv, lin
     try:
-        _run_meta(models, res)
+        _run_meta(models, res, batch)
     finally:
         ops.conv2d, ops.linear = orig_conv, orig_lin
     return sorted(convs), sorted(gemms)
@@ -130,11 +131,12 @@ def main():
     ap.add_argument("--models", default="sd15", help="comma list: sd15,kandinsky2,video")
     ap.add_argument("--legacy-only", action="store_true", help="time only the register-staged cfgs (10-19)")
     ap.add_argument("--merge", default=None, help="existing conv_plans.inc to keep entries from")
+    ap.add_argument("--batch", type=int, default=2, help="SD UNet batch for shape collection (8 = groups of 4)")
     args = ap.parse_args()
     out_dir = args.out_dir
     os.makedirs(out_dir, exist_ok=True)
     dev = torch.device("cuda")
-    convs, gemms = collect_shapes(tuple(args.models.split(",")))
+    convs, gemms = collect_shapes(tuple(args.models.split(",")), batch=args.batch)
     results = []
     pinned = read_table(args.merge) if args.merge else {}
     print(f"{len(convs)} conv shapes, {len(gemms)} gemm shapes, {len(pinned)} pinned kept", flush=True)
