@@ -70,10 +70,11 @@ def build_pool(cfg, models):
     n = cfg.mi355x.gpus if cfg.mi355x.gpus is not None else (torch.cuda.device_count() if torch.cuda.is_available() else 0)
     if n > 1:
         from .parallel.workers import MultiGPUSolverPool
-        return MultiGPUSolverPool(n, names, "cuda", streams_per_gpu=cfg.mi355x.workers_per_gpu)
+        return MultiGPUSolverPool(n, names, "cuda", streams_per_gpu=cfg.mi355x.workers_per_gpu,
+                                  lockstep=cfg.mi355x.lockstep_group)
     from .node.pool import LocalSolverPool
     return LocalSolverPool("cuda:0" if n == 1 else "cpu", capacity=cfg.mi355x.workers_per_gpu,
-                           weights_dir=cfg.mi355x.weights_dir)
+                           lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir)
 
 
 async def _start(path: str):

@@ -92,6 +92,9 @@ class MI355XConfig(_Base):
     selftest: bool = True                 # boot CID self-test (index.ts:981-1001)
     selftest_table: Optional[str] = None  # override of config/selftest.json
     workers_per_gpu: int = 1              # concurrent task streams per GPU (pipeline forks)
+    lockstep_group: int = 4               # queued compatible SD tasks solved per stream in ONE batch
+                                          # (batch-invariant plans: same CIDs as solo; a lone task
+                                          # never waits for company)
 
 
 class MiningConfig(_Base):

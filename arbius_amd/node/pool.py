@@ -66,14 +66,21 @@ class LocalSolverPool:
     that many solves concurrently on pipeline forks (shared weights, private HIP stream
     and hipGraphs each) - concurrency never changes a solution's bytes."""
 
-    def __init__(self, device="cpu", pipeline_factory: Callable = None, capacity: int = 1, **factory_kw):
+    def __init__(self, device="cpu", pipeline_factory: Callable = None, capacity: int = 1, lockstep: int = 1,
+                 **factory_kw):
         from ..models.registry import build_pipeline
         self.device = device
-        self.capacity = max(1, int(capacity))
+        self.streams = max(1, int(capacity))
+        # lock-step groups only where launches are batch-invariant (the HIP kernels); the CPU
+        # reference path's library GEMMs are not, so grouping there would change CIDs
+        self.lockstep = max(1, int(lockstep)) if str(device).startswith("cuda") else 1
+        # concurrent solves the orchestrator may hand us: every stream takes lock-step groups
+        self.capacity = self.streams * self.lockstep
         self.factory = pipeline_factory or build_pipeline
         self.factory_kw = factory_kw
         self.pipes: Dict[str, object] = {}
         self._free: Dict[str, "queue.Queue"] = {}
+        self._pending: Dict[str, "queue.Queue"] = {}
         self._lock = threading.Lock()
 
     def _pipe(self, model):
@@ -82,8 +89,8 @@ class LocalSolverPool:
                 base = self.factory(model.name, device=self.device, **self.factory_kw)
                 self.pipes[model.name] = base
                 q = queue.Queue()
-                for _ in range(self.capacity):
-                    q.put(base if self.capacity == 1 or not hasattr(base, "fork") else base.fork())
+                for _ in range(self.streams):
+                    q.put(base if self.streams == 1 or not hasattr(base, "fork") else base.fork())
                 self._free[model.name] = q
             return self._free[model.name]
 
@@ -104,9 +111,41 @@ class LocalSolverPool:
         finally:
             free.put(pipe)
 
+    def _solve_waiting(self, model, pending: "queue.Queue"):
+        """A stream's turn: this request plus any queued compatible ones, solved lock-step."""
+        from .solver import solve_images, take_group
+        free = self._pipe(model)
+        pipe = free.get()
+        try:
+            try:
+                first = pending.get_nowait()
+            except queue.Empty:
+                return                      # an earlier turn already took this request in its group
+            batch = take_group(pending, first, self.lockstep, lambda r: r[0].kind, lambda r: r[1],
+                               lambda r: r[0].name)
+            try:
+                sols = (solve_images(pipe, [r[1] for r in batch]) if len(batch) > 1
+                        else [solve_task(batch[0][0], pipe, batch[0][1])])
+                for r, sol in zip(batch, sols):
+                    r[2].set_result(sol)
+            except BaseException as e:  # noqa: BLE001
+                for r in batch:
+                    if not r[2].done():
+                        r[2].set_exception(e)
+        finally:
+            free.put(pipe)
+
     async def solve(self, model, taskid, inp) -> Solution:
         loop = asyncio.get_running_loop()
-        return await loop.run_in_executor(None, self.solve_sync, model, taskid, inp)
+        if self.lockstep <= 1:
+            return await loop.run_in_executor(None, self.solve_sync, model, taskid, inp)
+        import concurrent.futures as cf
+        with self._lock:
+            pending = self._pending.setdefault(model.name, queue.Queue())
+        fut: cf.Future = cf.Future()
+        pending.put((model, inp, fut))
+        loop.run_in_executor(None, self._solve_waiting, model, pending)
+        return await asyncio.wrap_future(fut)
 
     async def close(self):
         self.pipes.clear()

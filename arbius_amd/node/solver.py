@@ -49,8 +49,8 @@ def solve_image(pipe, inp: dict, png_level: int = 6) -> Solution:
 
 def solve_images(pipe, inps: List[dict], png_level: int = 6) -> List[Solution]:
     """k compatible SD-family tasks solved lock-step (``run_group``): same bytes as k solo solves."""
-    if len(inps) == 1 or not hasattr(pipe, "run_group"):
-        return [solve_image(pipe, i, png_level) for i in inps]
+    if len(inps) == 1 or not hasattr(pipe, "run_group"):     # e.g. Kandinsky 2: one at a time
+        return [pipe.solve(i) if hasattr(pipe, "solve") else solve_image(pipe, i, png_level) for i in inps]
     t0 = time.perf_counter()
     imgs = pipe.run_group([dict(i, width=int(i.get("width", 768)), height=int(i.get("height", 768)),
                                 num_inference_steps=int(i.get("num_inference_steps", 20)),
@@ -73,6 +73,32 @@ def group_key(inp: dict):
     """Tasks with equal keys can share lock-step launches (SD-family image templates)."""
     return (int(inp.get("width", 768)), int(inp.get("height", 768)), int(inp.get("num_inference_steps", 20)),
             inp.get("scheduler", "DPMSolverMultistep"))
+
+
+def take_group(jobs, first, lockstep: int, kind_of, inp_of, model_of):
+    """Lock-step batching for a task-slot loop: after ``first`` came off the ``jobs`` queue, take
+    up to ``lockstep - 1`` more queued jobs that can share its launches (image tasks of the same
+    model with equal ``group_key``) without waiting; anything else goes back on the queue."""
+    batch = [first]
+    if lockstep <= 1 or kind_of(first) != "image":
+        return batch
+    import queue as _q
+    key = (model_of(first), group_key(inp_of(first)))
+    back = []
+    while len(batch) < lockstep:
+        try:
+            m = jobs.get_nowait()
+        except _q.Empty:
+            break
+        if m is not None and kind_of(m) == "image" and (model_of(m), group_key(inp_of(m))) == key:
+            batch.append(m)
+        else:
+            back.append(m)
+            if m is None:
+                break
+    for m in back:
+        jobs.put(m)
+    return batch
 
 
 def solve_files(files, timings=None) -> Solution:

@@ -43,7 +43,7 @@ def _free_port() -> int:
 
 
 def _worker_main(rank: int, world: int, port: int, device_type: str, models: List[str], tiny: bool,
-                 in_q, out_q, group: bool, weight_seed: int, streams: int = 1):
+                 in_q, out_q, group: bool, weight_seed: int, streams: int = 1, lockstep: int = 1):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import queue as _queue
     import threading
@@ -53,7 +53,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
 
     from ..models.registry import build_pipeline
     from ..node.models import Model
-    from ..node.solver import solve_task
+    from ..node.solver import solve_images, solve_task, take_group
     from . import dist as D
 
     try:
@@ -86,15 +86,22 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 msg = jobs.get()
                 if msg is None:
                     return
+                # lock-step group: queued compatible image tasks share one batch (same bytes as solo)
+                batch = take_group(jobs, msg, lockstep, lambda m: m[2], lambda m: m[5], lambda m: m[1])
                 jid, mname, kind, mid, taskid, inp = msg
                 try:
                     t0 = time.perf_counter()
-                    sol = solve_task(Model(mid, mname, {}, True, [], kind), slots[k][mname], inp)
-                    sol.dag = None  # blocks are recomputed by the pinner; keep the message small
-                    sol.timings["worker_s"] = time.perf_counter() - t0
-                    out_q.put(("ok", jid, rank, sol))
+                    if len(batch) == 1:
+                        sols = [solve_task(Model(mid, mname, {}, True, [], kind), slots[k][mname], inp)]
+                    else:
+                        sols = solve_images(slots[k][mname], [m[5] for m in batch])
+                    for m, sol in zip(batch, sols):
+                        sol.dag = None  # blocks are recomputed by the pinner; keep the message small
+                        sol.timings["worker_s"] = time.perf_counter() - t0
+                        out_q.put(("ok", m[0], rank, sol))
                 except Exception:  # noqa: BLE001
-                    out_q.put(("err", jid, rank, traceback.format_exc()))
+                    for m in batch:
+                        out_q.put(("err", m[0], rank, traceback.format_exc()))
 
         threads = [threading.Thread(target=slot_loop, args=(k,), daemon=True) for k in range(streams)]
         for t in threads:
@@ -119,7 +126,8 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
 
 class MultiGPUSolverPool:
     def __init__(self, n: int, models: List[str], device_type: str = "cuda", tiny: bool = False,
-                 weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1):
+                 weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1,
+                 lockstep: int = 1):
         self.n = n
         self.models = models
         self.device_type = device_type
@@ -130,6 +138,8 @@ class MultiGPUSolverPool:
         self.out_qs = [self.ctx.Queue() for _ in range(n)]
         self.procs: List[Optional[mp.Process]] = [None] * n
         self.streams = max(1, int(streams_per_gpu))
+        # tasks per lock-step group on one stream (HIP kernels only: batch-invariant launches)
+        self.lockstep = max(1, int(lockstep)) if device_type == "cuda" else 1
         self.busy: Dict[int, int] = {}           # job id -> rank
         self.idle: List[int] = []                # one entry per free task slot (rank repeated)
         self.futures: Dict[int, asyncio.Future] = {}
@@ -155,7 +165,7 @@ class MultiGPUSolverPool:
                     continue
                 if kind == "ready":
                     pending.discard(rank)
-                    self.idle.extend([rank] * self.streams)
+                    self.idle.extend([rank] * self.streams * self.lockstep)
                     self.broadcast_stats[rank] = payload
         self.idle.sort()
         self._pump_task = None
@@ -169,12 +179,13 @@ class MultiGPUSolverPool:
 
     @property
     def capacity(self) -> int:
-        return self.streams * sum(1 for p in self.procs if p is not None and p.is_alive())
+        return self.streams * self.lockstep * sum(1 for p in self.procs if p is not None and p.is_alive())
 
     def _spawn(self, rank, port, group):
         p = self.ctx.Process(target=_worker_main, daemon=True,
                              args=(rank, self.n, port, self.device_type, self.models, self.tiny,
-                                   self.in_qs[rank], self.out_qs[rank], group, self.weight_seed, self.streams))
+                                   self.in_qs[rank], self.out_qs[rank], group, self.weight_seed, self.streams,
+                                   self.lockstep))
         p.start()
         self.procs[rank] = p
 
@@ -186,7 +197,7 @@ class MultiGPUSolverPool:
         kind = msg[0]
         if kind == "ready":
             rank = msg[1]
-            self.idle = [r for r in self.idle if r != rank] + [rank] * self.streams
+            self.idle = [r for r in self.idle if r != rank] + [rank] * self.streams * self.lockstep
             return
         _, jid, rank, payload = msg
         if self.busy.pop(jid, None) is not None:

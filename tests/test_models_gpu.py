@@ -158,3 +158,24 @@ def test_lockstep_group_bitwise_equals_solo(cuda):
     solo = [solve_image(pipe, i).cid for i in inps]
     assert [s.cid for s in solve_images(pipe, inps)] == solo
     assert [s.cid for s in solve_images(pipe, inps[:2])] == solo[:2]
+
+
+def test_local_pool_lockstep_groups_match_solo(cuda):
+    """The node's single-GPU pool batches queued compatible tasks into lock-step groups; the
+    solutions are the solo ones."""
+    import asyncio
+    from arbius_amd.node.models import default_models
+    from arbius_amd.node.pool import LocalSolverPool
+    from arbius_amd.node.solver import solve_image
+    model = next(m for m in default_models().values() if m.name == "anythingv3")
+    pool = LocalSolverPool(cuda, capacity=1, lockstep=3)
+    inps = [{"prompt": f"tower {i}", "negative_prompt": "", "width": 256, "height": 256,
+             "num_inference_steps": 3, "guidance_scale": 7.5, "scheduler": "DDIM", "seed": 70 + i} for i in range(3)]
+
+    async def go():
+        return await asyncio.gather(*[pool.solve(model, f"t{i}", inp) for i, inp in enumerate(inps)])
+
+    sols = asyncio.run(go())
+    pipe = pool.pipes["anythingv3"]
+    assert [s.cid for s in sols] == [solve_image(pipe, inp).cid for inp in inps]
+    assert pool.capacity == 3
