@@ -167,7 +167,7 @@ def test_local_pool_lockstep_groups_match_solo(cuda):
     from arbius_amd.node.models import default_models
     from arbius_amd.node.pool import LocalSolverPool
     from arbius_amd.node.solver import solve_image
-    model = next(m for m in default_models().values() if m.name == "anythingv3")
+    model = next(m for m in default_models({"anythingv3": "0x" + "ab" * 32}).values() if m.name == "anythingv3")
     pool = LocalSolverPool(cuda, capacity=1, lockstep=3)
     inps = [{"prompt": f"tower {i}", "negative_prompt": "", "width": 256, "height": 256,
              "num_inference_steps": 3, "guidance_scale": 7.5, "scheduler": "DDIM", "seed": 70 + i} for i in range(3)]
