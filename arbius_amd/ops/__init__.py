@@ -159,19 +159,29 @@ _PAD_W = {}
 
 
 def _padded_weights(w, b):
-    key = (w.data_ptr(), w._version, None if b is None else b.data_ptr())
+    """Channel-padded copies of a conv's weight/bias, cached per live weight: the entry holds weak
+    references to the owning tensors (a view's base) and is reused only while they are alive and
+    unmodified - a freed tensor's address can come back as another weight of another dtype."""
+    import weakref
+
+    def owner(t):
+        return t if t._base is None else t._base
+
+    key = (w.data_ptr(), w._version, tuple(w.shape), tuple(w.stride()), w.dtype,
+           None if b is None else (b.data_ptr(), b._version))
     hit = _PAD_W.get(key)
-    if hit is None:
-        cout, kh, kw, cin = w.shape
-        ci, co = -(-cin // 64) * 64, -(-cout // 8) * 8
-        wp = torch.zeros(co, kh, kw, ci, dtype=w.dtype, device=w.device)
-        wp[:cout, :, :, :cin] = w
-        bp = None
-        if b is not None:
-            bp = torch.zeros(co, dtype=b.dtype, device=b.device)
-            bp[:cout] = b
-        hit = _PAD_W[key] = (wp, bp)
-    return hit
+    if hit is not None and hit[0]() is owner(w) and (b is None or hit[1]() is owner(b)):
+        return hit[2], hit[3]
+    cout, kh, kw, cin = w.shape
+    ci, co = -(-cin // 64) * 64, -(-cout // 8) * 8
+    wp = torch.zeros(co, kh, kw, ci, dtype=w.dtype, device=w.device)
+    wp[:cout, :, :, :cin] = w
+    bp = None
+    if b is not None:
+        bp = torch.zeros(co, dtype=b.dtype, device=b.device)
+        bp[:cout] = b
+    _PAD_W[key] = (weakref.ref(owner(w)), None if b is None else weakref.ref(owner(b)), wp, bp)
+    return wp, bp
 
 
 def _padded_conv(x, w, b, padding, upsample, residual, temb, stride, table=None, nsilu=False):
