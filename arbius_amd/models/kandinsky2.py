@@ -21,11 +21,13 @@ from __future__ import annotations
 
 import time
 from dataclasses import dataclass, field
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 import torch.nn as nn
 
+from .. import ops
 from ..utils.png import encode_png
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .glide_unet import GlideUNet, GlideUNetConfig
@@ -166,7 +168,8 @@ class Kandinsky2Pipeline(PipelineBase):
         for i, t in enumerate(sched.timesteps):
             xin = x.to(self.dtype)
             tbuf.fill_(float(t))
-            out = self._unet(torch.cat([xin, xin]), tbuf, text_full, text_pooled, img_embs)
+            with ops.plan_batch(2):      # batch-invariant plans: solo == lock-step group bytes
+                out = self._unet(torch.cat([xin, xin]), tbuf, text_full, text_pooled, img_embs)
             c, u = out[0:1].float(), out[1:2].float()
             eps = u[..., :zc] + g * (c[..., :zc] - u[..., :zc])
             x = sched.step(eps, i, x, gen, var=c[..., zc:])
@@ -177,6 +180,57 @@ class Kandinsky2Pipeline(PipelineBase):
         t3 = time.perf_counter()
         self.timings = {"text_prior_s": t1 - t0, "denoise_s": t2 - t1, "movq_s": t3 - t2}
         return img
+
+    @torch.no_grad()
+    def run_group(self, inps: List[dict]) -> List[np.ndarray]:
+        """Lock-step solve of k tasks of one resolution: text encoders, prior, noise, sampler and
+        MoVQ per task; every GLIDE UNet step runs the k (cond, uncond) pairs as one batch-2k
+        launch sequence under batch-invariant plans (bitwise the solo outputs)."""
+        sizes = {(int(i.get("width", 768)), int(i.get("height", 768))) for i in inps}
+        if len(sizes) != 1:
+            raise ValueError(f"run_group needs one resolution, got {sorted(sizes)}")
+        width, height = sizes.pop()
+        cfg = self.cfg
+        with self._stream_ctx():
+            sync = self._sync
+            t0 = time.perf_counter()
+            gens, xs, tf, tp, ie = [], [], [], [], []
+            h, w = height // 8, width // 8
+            zc = cfg.unet.in_channels
+            for inp in inps:
+                gen = torch.Generator(device="cpu").manual_seed(int(inp["seed"]))
+                hidden, pooled, lens = self.encode_clip(inp["prompt"])
+                img_emb = self.sample_prior(hidden, pooled, lens, gen, cfg.prior_steps, cfg.prior_cf_scale)
+                text_full, text_pooled = self.encode_xlmr(inp["prompt"])
+                tf.append(text_full)
+                tp.append(text_pooled)
+                ie.append(torch.cat([img_emb, self.buffers.zero_img_emb[None].to(self.dtype)]))
+                x = torch.randn((1, zc, h, w), generator=gen, dtype=torch.float32).permute(0, 2, 3, 1).contiguous()
+                xs.append(x.to(self.device))
+                gens.append(gen)
+            text_full, text_pooled, img_embs = torch.cat(tf), torch.cat(tp), torch.cat(ie)
+            sync()
+            t1 = time.perf_counter()
+            scheds = [GaussianDiffusion(cfg.num_steps, schedule="linear", predict="eps", learned_var=True,
+                                        clamp=cfg.latent_clamp) for _ in inps]
+            tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
+            g = cfg.guidance_scale
+            for i, t in enumerate(scheds[0].timesteps):
+                xin = [x.to(self.dtype) for x in xs]
+                tbuf.fill_(float(t))
+                with ops.plan_batch(2):
+                    out = self._unet(torch.cat([v for x in xin for v in (x, x)]), tbuf, text_full, text_pooled,
+                                     img_embs)
+                for k, s in enumerate(scheds):
+                    c, u = out[2 * k:2 * k + 1].float(), out[2 * k + 1:2 * k + 2].float()
+                    eps = u[..., :zc] + g * (c[..., :zc] - u[..., :zc])
+                    xs[k] = s.step(eps, i, xs[k], gens[k], var=c[..., zc:])
+            sync()
+            t2 = time.perf_counter()
+            imgs = [self.decode(x) for x in xs]
+            sync()
+            self.timings = {"text_prior_s": t1 - t0, "denoise_s": t2 - t1, "movq_s": time.perf_counter() - t2}
+            return imgs
 
     @torch.no_grad()
     def decode(self, latent):

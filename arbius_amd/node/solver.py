@@ -52,9 +52,7 @@ def solve_images(pipe, inps: List[dict], png_level: int = 6) -> List[Solution]:
     if len(inps) == 1 or not hasattr(pipe, "run_group"):     # e.g. Kandinsky 2: one at a time
         return [pipe.solve(i) if hasattr(pipe, "solve") else solve_image(pipe, i, png_level) for i in inps]
     t0 = time.perf_counter()
-    imgs = pipe.run_group([dict(i, width=int(i.get("width", 768)), height=int(i.get("height", 768)),
-                                num_inference_steps=int(i.get("num_inference_steps", 20)),
-                                scheduler=i.get("scheduler", "DPMSolverMultistep")) for i in inps])
+    imgs = pipe.run_group(list(inps))
     t1 = time.perf_counter()
     out = []
     for img in imgs:

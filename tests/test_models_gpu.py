@@ -179,3 +179,12 @@ def test_local_pool_lockstep_groups_match_solo(cuda):
     pipe = pool.pipes["anythingv3"]
     assert [s.cid for s in sols] == [solve_image(pipe, inp).cid for inp in inps]
     assert pool.capacity == 3
+
+
+def test_kandinsky2_lockstep_group_bitwise_equals_solo(cuda):
+    from arbius_amd.node.solver import solve_images
+    pipe = build_pipeline("kandinsky2", device=cuda)
+    pipe.cfg.num_steps = 3
+    inps = [{"prompt": f"arbius test cat {i}", "width": 256, "height": 256, "seed": 1337 + i} for i in range(2)]
+    solo = [pipe.solve(i).cid for i in inps]
+    assert [s.cid for s in solve_images(pipe, inps)] == solo
