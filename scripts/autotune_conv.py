@@ -37,8 +37,8 @@ def _run_meta(models, res, batch=2):
         if "kandinsky2" in models:
             from arbius_amd.models.glide_unet import GlideUNet
             from arbius_amd.models.movq import MoVQDecoder
-            GlideUNet()(torch.zeros(2, 96, 96, 4), torch.tensor([500.0]), torch.zeros(2, 77, 1024),
-                        torch.zeros(2, 768), torch.zeros(2, 768))
+            GlideUNet()(torch.zeros(batch, 96, 96, 4), torch.tensor([500.0]), torch.zeros(batch, 77, 1024),
+                        torch.zeros(batch, 768), torch.zeros(batch, 768))
             MoVQDecoder()(torch.zeros(1, 96, 96, 4))
         if "video" in models:   # BASELINE config #4: zeroscope 576x320x24f; VAE in chunks of 8 frames
             from arbius_amd.models.unet3d import UNet3DCondition
