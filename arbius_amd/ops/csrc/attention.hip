@@ -27,6 +27,8 @@
 //   * no atomics, fixed reduction order -> bitwise deterministic.
 #include "common.h"
 
+#include <cstdlib>
+
 #define KV_BLK 64
 
 struct AttnArgs {
@@ -50,16 +52,30 @@ struct AttnArgs {
   int Np;
 };
 
-template <int KSTEPS, int DT, int QT, bool ONES>
+// 16-byte sources of the LDS-DMA staging: zero padding, and V's ones column (row-sum trick)
+__device__ __attribute__((aligned(16))) uint4 g_attn_zero[1];
+__device__ __attribute__((aligned(16))) uint4 g_attn_ones[1] = {{0x3F80u, 0u, 0u, 0u}};
+
+// GLDS: K/V tiles arrive by LDS-DMA (global_load_lds, 16 B per lane straight into LDS, no VGPR
+// staging, no ds_write): K rows are 8 chunks (128 B, KSTEPS == 2 only) with the chunk XOR-swizzled
+// by (row & 7) on the SOURCE address (lane-linear LDS image, rule 21) and on the QK read; V rows
+// are VROW/8 chunks, already lane-linear; padding chunks read a zero page, V's row-sum column a
+// ones page.  One LDS array for everything (hipcc's vmcnt trap with two __shared__ objects).
+template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false>
 __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
-  constexpr int KROW = KSTEPS * 32 + 8;    // K tile row (elements): 16 B pad
+  static_assert(!GLDS || KSTEPS == 2, "LDS-DMA staging: 8-chunk K rows only");
+  constexpr int KROW = GLDS ? KSTEPS * 32 : KSTEPS * 32 + 8;   // K tile row (elements)
   constexpr int VROW = 16 * (DT | 1);      // V tile row: 16*(odd) -> tr-read conflict free
   constexpr int QBLK = 4 * QT * 16;        // queries per workgroup
   constexpr int KCH = KV_BLK * KSTEPS * 4;
   constexpr int VCH = KV_BLK * DT * 2;
   constexpr int KPT = (KCH + 255) / 256, VPT = (VCH + 255) / 256;
-  __shared__ __attribute__((aligned(16))) bf16_t sK[2][KV_BLK * KROW];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[2][KV_BLK * VROW];
+  // one array per pipeline stage: K rows then V rows.  Two distinct __shared__ objects give the
+  // LDS accesses disjoint alias scopes, so (GLDS, loop unrolled by 2 with static stage roles)
+  // hipcc need not drain the DMA into one stage before the ds_reads of the other.
+  constexpr int STAGE = KV_BLK * (KROW + VROW);
+  __shared__ __attribute__((aligned(16))) bf16_t sS0[STAGE];
+  __shared__ __attribute__((aligned(16))) bf16_t sS1[STAGE];
 
   const int nqb = (a.Nq + QBLK - 1) / QBLK;
   const int total = nqb * a.H * a.B;
@@ -168,27 +184,67 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < KPT; ++i) {
       const int c = tid + 256 * i;
-      if (c < KCH) st16(&sK[buf][(c / (KSTEPS * 4)) * KROW + (c % (KSTEPS * 4)) * 8], rk[i]);
+      if (c < KCH) st16(&(buf ? sS1 : sS0)[(c / (KSTEPS * 4)) * KROW + (c % (KSTEPS * 4)) * 8], rk[i]);
     }
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = tid + 256 * i;
-      if (c < VCH) st16(&sV[buf][(c / (DT * 2)) * VROW + (c % (DT * 2)) * 8], rv[i]);
+      if (c < VCH) st16(&(buf ? sS1 : sS0)[KV_BLK * KROW + (c / (DT * 2)) * VROW + (c % (DT * 2)) * 8], rv[i]);
     }
   };
-  if (kv_end > 0) {
-    load_kv(0);
-    store_kv(0);
+  // ---- LDS-DMA staging geometry (GLDS): per wave-instruction block b (64 chunks), lane l
+  constexpr int KBLK = KV_BLK * KSTEPS * 4 / 64;        // K blocks per tile (8)
+  constexpr int VCPR = VROW / 8;                         // V chunks per LDS row
+  constexpr int VBLK = KV_BLK * VCPR / 64;               // V blocks per tile
+  constexpr int KBW = (KBLK + 3) / 4, VBW = (VBLK + 3) / 4;   // blocks per wave
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  const bf16_t* gk[KBW];
+  const bf16_t* gv[VBW];
+  int gkr[KBW], gvr[VBW];
+  int gkm[KBW], gvm[VBW];           // 0: zero page, 1: data, 2: ones page (V row-sum column)
+  int gvb[VBW];
+  if constexpr (GLDS) {
+    static_assert(KBLK % 4 == 0, "K blocks split evenly over the 4 waves");
+#pragma unroll
+    for (int i = 0; i < KBW; ++i) {
+      const int blk = wave + 4 * i;
+      const int row = blk * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (row & 7);               // logical chunk at this position
+      gkr[i] = row;
+      gkm[i] = (blk < KBLK && lc * 8 < D) ? 1 : 0;
+      gk[i] = kbase + (long)row * a.k_sn + lc * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < VBW; ++i) {
+      // a wave short of V blocks re-issues its first one (same bytes to the same LDS slot), so
+      // every DMA is unconditional and the wait counts stay static
+      const int blk = (wave + 4 * i < VBLK) ? wave + 4 * i : wave;
+      gvb[i] = blk;
+      const int q = blk * 64 + lane;
+      const int row = q / VCPR, col = (q % VCPR) * 8;
+      gvr[i] = row;
+      gvm[i] = col < D ? 1 : (ONES && col == (D & ~7)) ? 2 : 0;
+      gv[i] = vbase + (long)row * a.v_sn + col;
+    }
   }
-  __syncthreads();
+  auto issue_kv = [&](int kv, bf16_t* dst) __attribute__((always_inline)) {
+    const long ko = (long)kv * a.k_sn, vo = (long)kv * a.v_sn;
+#pragma unroll
+    for (int i = 0; i < KBW; ++i) {
+      const void* src = (gkm[i] && kv + gkr[i] < a.Nk) ? (const void*)(gk[i] + ko) : (const void*)g_attn_zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (wave + 4 * i) * 512), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < VBW; ++i) {
+      const void* src = gvm[i] == 2 ? (const void*)g_attn_ones
+                        : (gvm[i] == 1 && kv + gvr[i] < a.Nk) ? (const void*)(gv[i] + vo) : (const void*)g_attn_zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + KV_BLK * KROW + gvb[i] * 512), 16, 0, 0);
+    }
+  };
 
-  int buf = 0;
-  for (int kv0 = 0; kv0 < kv_end; kv0 += KV_BLK, buf ^= 1) {
-    const bool more = kv0 + KV_BLK < kv_end;
-    if (more) load_kv(kv0 + KV_BLK);
+  auto compute = [&](int kv0, const bf16_t* cK, const bf16_t* cV) __attribute__((always_inline)) {
     const bool full = !a.causal && kv0 + KV_BLK <= a.Nk;
-    const bf16_t* cK = sK[buf];
-    const bf16_t* cV = sV[buf];
 
     // ---- S^T tiles: 4 key tiles x QT query tiles
     f32x4 st[QT][4];
@@ -198,7 +254,9 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       for (int qt = 0; qt < QT; ++qt) st[qt][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
-        const bf16x8 kf = __builtin_bit_cast(bf16x8, ld16(&cK[(16 * t + lq) * KROW + 32 * s + 8 * g]));
+        const int krw = 16 * t + lq;
+        const int kch = GLDS ? ((4 * s + g) ^ (krw & 7)) : (4 * s + g);
+        const bf16x8 kf = __builtin_bit_cast(bf16x8, ld16(&cK[krw * KROW + kch * 8]));
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
           st[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][s], st[qt][t], 0, 0, 0);
@@ -287,10 +345,43 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
           o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][ks], o[qt][dt], 0, 0, 0);
       }
     }
-    // the prefetched tile goes to the other buffer (last read one iteration ago, fenced by
-    // the previous barrier); this barrier publishes it and retires reads of `buf`.
-    if (more) store_kv(buf ^ 1);
+  };
+
+  if constexpr (GLDS) {
+    // stage roles are static (loop unrolled by 2): DMA into one stage while the other is read;
+    // a stage is refilled only after the barrier that retired its last reads
+    if (kv_end > 0) issue_kv(0, sS0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kv0 = 0; kv0 < kv_end; kv0 += 2 * KV_BLK) {
+      const int kv1 = kv0 + KV_BLK;
+      if (kv1 < kv_end) issue_kv(kv1, sS1);
+      compute(kv0, sS0, sS0 + KV_BLK * KROW);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kv1 >= kv_end) break;
+      if (kv1 + KV_BLK < kv_end) issue_kv(kv1 + KV_BLK, sS0);
+      compute(kv1, sS1, sS1 + KV_BLK * KROW);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    if (kv_end > 0) {
+      load_kv(0);
+      store_kv(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int kv0 = 0; kv0 < kv_end; kv0 += KV_BLK, buf ^= 1) {
+      const bool more = kv0 + KV_BLK < kv_end;
+      if (more) load_kv(kv0 + KV_BLK);
+      const bf16_t* cS = buf ? sS1 : sS0;
+      compute(kv0, cS, cS + KV_BLK * KROW);
+      // the prefetched tile goes to the other buffer (last read one iteration ago, fenced by
+      // the previous barrier); this barrier publishes it and retires reads of `buf`.
+      if (more) store_kv(buf ^ 1);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: denominator (MFMA ones-column or lane sums), normalise, store O[q][d]
@@ -327,11 +418,26 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+static bool attn_glds_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("ARB_ATTN_GLDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 template <int KSTEPS, int DT, int QT>
 static void launch_fa(const AttnArgs& a, hipStream_t s) {
   constexpr int QBLK = 4 * QT * 16;
   const int nqb = (a.Nq + QBLK - 1) / QBLK;
   dim3 grid(nqb * a.H * a.B);
+  if constexpr (KSTEPS == 2) {
+    if (a.Np == 0 && attn_glds_enabled()) {     // LDS-DMA staging (no prefix segment)
+      if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true><<<grid, 256, 0, s>>>(a);
+      else flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true><<<grid, 256, 0, s>>>(a);
+      return;
+    }
+  }
   if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true><<<grid, 256, 0, s>>>(a);
   else flash_attn_fwd_kernel<KSTEPS, DT, QT, false><<<grid, 256, 0, s>>>(a);
 }

@@ -79,6 +79,15 @@ def main():
                     "sdpa_us": round(t_sdpa, 1), "ours_tflops": round(fl / t_ours / 1e6, 1),
                     "sdpa_tflops": round(fl / t_sdpa / 1e6, 1)})
         print(json.dumps(out[-1]), flush=True)
+    # in-model layouts: strided views of a fused QKV activation, and sharper score distributions
+    for (B, N, H, D, amp) in [(2, 4096, 8, 40, 1.0), (2, 4096, 8, 40, 4.0), (8, 4096, 8, 40, 1.0)]:
+        qkv = (torch.randn(B, N, 3, H, D, device=dev) * amp).bfloat16()
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        t_ours = timeit(lambda: _lib.flash_attention(q, k, v, 1 / math.sqrt(D), False))
+        fl = 4.0 * B * H * N * N * D
+        out.append({"op": "attention_fused_qkv", "shape": [B, N, N, H, D], "amp": amp,
+                    "ours_us": round(t_ours, 1), "ours_tflops": round(fl / t_ours / 1e6, 1)})
+        print(json.dumps(out[-1]), flush=True)
     # ---- group norm
     for (B, HW, C) in [(2, 4096, 320), (2, 1024, 640), (2, 256, 1280), (2, 4096, 640), (2, 1024, 2560),
                        (1, 262144, 128), (1, 65536, 256)]:
