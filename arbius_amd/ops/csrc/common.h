@@ -25,8 +25,18 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
-__device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
-__device__ __forceinline__ void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+// 16-byte accesses as ONE <4 x i32> IR load/store: a HIP uint4 struct copy is lowered as two
+// <2 x i32> halves, and the second half's extra GEP can fall outside the LDS lowering's alias-
+// scope walk - the merged ds_read_b128 then carries no scope and hipcc drains every LDS-DMA
+// before it (s_waitcnt vmcnt(0)).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  const u32x4_t v = *reinterpret_cast<const u32x4_t*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  *reinterpret_cast<u32x4_t*>(p) = (u32x4_t){v.x, v.y, v.z, v.w};
+}
 
 __device__ __forceinline__ void unpack8(uint4 v, float (&f)[8]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};

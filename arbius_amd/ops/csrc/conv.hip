@@ -23,9 +23,11 @@
 //     kernel that applies the epilogue (no atomics -> bitwise reproducible).
 #include "common.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 struct ConvArgs {
   const bf16_t* x;      // [B, H, W, Cin]
@@ -113,6 +115,75 @@ __device__ __forceinline__ void tile_coords(const ConvArgs& p, int BN, int BM, i
   }
 }
 
+// Largest row block (a power-of-two fraction of BM, >= 16) whose fp32 staging fits LDSF floats.
+template <int BM, int OROW, int LDSF>
+constexpr int epi_rows() {
+  int r = BM;
+  while (r > 16 && r * OROW > LDSF) r /= 2;
+  return r;
+}
+
+// Non-split epilogue through LDS.  The MFMA layout leaves each lane 4 channels of ONE pixel, so
+// direct stores / residual loads touch 16 rows x 32 B per instruction.  Instead the fp32 tile
+// is staged in LDS (row = pixel, in row blocks that fit) and re-read as 8-channel chunks along
+// the rows: bias / temb / residual loads and the bf16 stores become contiguous 16-B accesses.
+// Arithmetic is unchanged (fp32 acc + bias + temb + residual, one rounding), so results are
+// bitwise those of the direct epilogue.  Call after the K loop; LDS is reused.
+template <int BN, int BM, int WN, int WM, int NT, int LDSF, int EL>
+__device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&acc)[BN / WN / 16][BM / WM / 16],
+                                             float* stage, int m0, int n0) {
+  constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
+  constexpr int OROW = BN + 4;           // floats per staged row (16-B pad: spreads the rows' banks)
+  constexpr int PR = epi_rows<BM, OROW, LDSF>();
+  static_assert(PR * OROW <= LDSF, "epilogue staging exceeds LDS");
+  static_assert(PR % (BM / WM) == 0 || (BM / WM) % PR == 0, "row blocks align with wave rows");
+  constexpr int CPR = BN / 8;            // 8-channel chunks per row
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WM, wm = wave % WM, g = lane >> 4, l16 = lane & 15;
+  const int hw = p.Ho * p.Wo;
+#pragma unroll 1
+  for (int r0 = 0; r0 < BM; r0 += PR) {
+    __syncthreads();                     // K loop / previous block's readers are done with LDS
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int rb = wm * (BM / WM) + b * 16;          // wave-uniform 16-row fragment block
+      if (rb < r0 || rb >= r0 + PR) continue;
+      const int rl = rb - r0 + l16;
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int col = wn * (BN / WN) + a * 16 + 4 * g;
+        *reinterpret_cast<f32x4*>(&stage[rl * OROW + col]) = acc[a][b];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < PR * CPR; c += NT) {
+      const int rl = c / CPR, ch = (c - rl * CPR) * 8;
+      const int m = m0 + r0 + rl, n = n0 + ch;
+      if (m >= p.M || n >= p.N) continue;
+      const f32x4 s0 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch]);
+      const f32x4 s1 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch + 4]);
+      float v[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      float t[8];
+      if (p.bias) {
+        unpack8e<EL>(ld16(p.bias + n), t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += t[e];
+      }
+      if (p.temb) {
+        unpack8e<EL>(ld16(p.temb + (size_t)(m / hw) * p.N + n), t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += t[e];
+      }
+      if (p.res) {
+        unpack8e<EL>(ld16(p.res + (size_t)m * p.N + n), t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += t[e];
+      }
+      st16(p.out + (size_t)m * p.N + n, pack8e<EL>(v));
+    }
+  }
+}
+
 // NORM: the A operand is GroupNorm(+SiLU)(x) computed on the fly from a per-(batch, channel)
 // affine table (scale, shift) - the normalised activation is never written to HBM.  Zero
 // padding stays zero (the reference pads the NORMALISED tensor), so only in-bounds chunks
@@ -125,8 +196,10 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   constexpr int TN = BN / WN / 16, TM = BM / WM / 16;  // 16x16 tiles per wave
   constexpr int WCH = BN * 8 / 256;           // 16-byte chunks per thread (W tile)
   constexpr int XCH = BM * 8 / 256;           // 16-byte chunks per thread (X tile)
-  __shared__ __attribute__((aligned(16))) bf16_t sW[2][BN * BK];
-  __shared__ __attribute__((aligned(16))) bf16_t sX[2][BM * BK];
+  // one LDS array (operand stages, then the epilogue's fp32 staging)
+  __shared__ __attribute__((aligned(16))) bf16_t smem_[2 * (BN + BM) * BK];
+  bf16_t (*const sW)[BN * BK] = reinterpret_cast<bf16_t (*)[BN * BK]>(smem_);
+  bf16_t (*const sX)[BM * BK] = reinterpret_cast<bf16_t (*)[BM * BK]>(smem_ + 2 * BN * BK);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
@@ -406,17 +479,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
   };
   if constexpr (!SPLIT) {
-#pragma unroll
-    for (int b = 0; b < TM; ++b) {
-      const int m = m0 + wm * (BM / WM) + b * 16 + l16;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int a = 0; a < TN; ++a) {
-        const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
-        if (n >= p.N) continue;
-        emit(m, n, acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
-      }
-    }
+    epilogue_lds<BN, BM, WN, WM, 256, (BN + BM) * BK, EL>(p, acc, reinterpret_cast<float*>(smem_), m0, n0);
     return;
   } else {
     // ---- split-K: fp32 slab, then IN-LAUNCH ordered reduction by the tile's last arriving
@@ -483,22 +546,61 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
 // The XOR swizzle moves to the per-lane SOURCE address (LDS image stays lane-linear, rule 21);
 // zero padding / masked rows read a zero page.
 
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+// LDS-DMA (16 B per lane, lane-linear at the wave-uniform LDS address) issued as inline asm:
+// hipcc's waitcnt pass does not track it, so it adds no conservative vmcnt drains before LDS
+// reads.  The kernel owns the RAW ordering: counted wait_vmcnt (builtin) + barrier.
+__device__ __forceinline__ void dma16(const void* src, const void* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lds);
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(a) : "memory");
 }
 
+// Ring stages as DISTINCT __shared__ objects, each addressed only through a compile-time stage
+// index (main loops unrolled by NS).  hipcc's waitcnt pass orders a ds_read after every
+// outstanding LDS-DMA unless alias scopes prove them disjoint; scopes exist per LDS variable and
+// survive only when a pointer derives from exactly one of them.  With one dynamic array (or a
+// runtime stage select) every K step began with s_waitcnt vmcnt(0), draining the whole ring.
+template <int S, typename T>
+__device__ __forceinline__ T* ring_stage(T* s0, T* s1, T* s2, T* s3) {
+  if constexpr (S == 0) return s0;
+  else if constexpr (S == 1) return s1;
+  else if constexpr (S == 2) return s2;
+  else return s3;
+}
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+// Counted vmcnt wait as the s_waitcnt BUILTIN (not inline asm): hipcc's waitcnt pass cannot see
+// an inline-asm wait, so it still counts the retired stage's DMA as outstanding and drains the
+// whole ring (vmcnt(0)) before the next ds_read of that stage.  gfx9 encoding: vmcnt[3:0] in
+// bits 3:0, vmcnt[5:4] in bits 15:14; expcnt (6:4) and lgkmcnt (11:8) left at their maxima.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+
+// NT = 64 * WN * WM threads: 4 waves (one per SIMD), or 8 waves for the 256-wide tiles (two per
+// SIMD: one wave's MFMA cluster runs while the other issues its LDS reads / DMA).
 template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
-__global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
+__global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) {
   constexpr int EL = 0;   // LDS-DMA variant: bf16 only (fp16 convs use the register-staged kernel)
   constexpr int BK = 64;
-  static_assert(WN * WM == 4, "4 waves");
+  constexpr int NT = 64 * WN * WM;
+  constexpr int RPI = NT / 8;        // tile rows covered by one DMA instruction of the workgroup
+  static_assert(WN * WM == 4 || WN * WM == 8, "4 or 8 waves");
+  static_assert((BN * 8) % NT == 0 && (BM * 8) % NT == 0, "whole DMA rounds per tile");
   constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
-  constexpr int WCH = BN * 8 / 256;  // glds per thread per tile (W)
-  constexpr int XCH = BM * 8 / 256;  // glds per thread per tile (X)
+  constexpr int WCH = BN * 8 / NT;   // glds per thread per tile (W)
+  constexpr int XCH = BM * 8 / NT;   // glds per thread per tile (X)
   constexpr int LPT = WCH + XCH;     // vmcnt units per tile per wave
   constexpr int STAGE = (BN + BM) * BK;  // bf16 elements per stage
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  __shared__ __attribute__((aligned(16))) bf16_t lds0[STAGE];
+  __shared__ __attribute__((aligned(16))) bf16_t lds1[STAGE];
+  __shared__ __attribute__((aligned(16))) bf16_t lds2[NS > 2 ? STAGE : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t lds3[NS > 3 ? STAGE : 8];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
@@ -515,14 +617,14 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
   int wrow[WCH], wcc[WCH];
 #pragma unroll
   for (int i = 0; i < WCH; ++i) {
-    wrow[i] = (tid >> 3) + 32 * i;
+    wrow[i] = (tid >> 3) + RPI * i;
     wcc[i] = pos ^ (wrow[i] & 7);
   }
   int xb[XCH], xho[XCH], xwo[XCH], xcc[XCH];
   bool xok[XCH];
 #pragma unroll
   for (int i = 0; i < XCH; ++i) {
-    const int row = (tid >> 3) + 32 * i;
+    const int row = (tid >> 3) + RPI * i;
     xcc[i] = pos ^ (row & 7);
     const int m = m0 + row;
     xok[i] = m < p.M;
@@ -557,20 +659,20 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
     }
   };
   set_tap();
-  auto issue = [&](int stage) {
-    bf16_t* sW = smem + stage * STAGE;
+  auto issue = [&](auto stage_c) {
+    bf16_t* sW = ring_stage<decltype(stage_c)::value>(lds0, lds1, lds2, lds3);
     bf16_t* sX = sW + BN * BK;
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
       // wave-uniform destination: first row of this wave's 8-row slab
-      bf16_t* dst = sW + ((wave * 8) + 32 * i) * BK;
+      bf16_t* dst = sW + ((wave * 8) + RPI * i) * BK;
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
       const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
-      bf16_t* dst = sX + ((wave * 8) + 32 * i) * BK;
+      bf16_t* dst = sX + ((wave * 8) + RPI * i) * BK;
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
     }
     wk += BK;
@@ -589,17 +691,18 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
     for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   // prologue: NS-1 tiles in flight
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) issue(s);
+  if (0 < nk) issue(IC<0>());
+  if (NS > 2 && 1 < nk) issue(IC<1>());
+  if (NS > 3 && 2 < nk) issue(IC<2>());
 
-  for (int i = 0; i < nk; ++i) {
+  auto step = [&](auto stage_c, int i) __attribute__((always_inline)) {
+    constexpr int S = decltype(stage_c)::value;
     // tile i has landed once at most (NS-2) newer tiles are outstanding
     if (i + NS - 2 < nk) wait_vmcnt<(NS - 2) * LPT>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();  // every wave's DMA for tile i is visible
-    if (i + NS - 1 < nk) issue((i + NS - 1) % NS);  // that stage was read at i-1
-    const bf16_t* sW = smem + (i % NS) * STAGE;
+    if (i + NS - 1 < nk) issue(IC<(S + NS - 1) % NS>());  // that stage was read at i-1
+    const bf16_t* sW = ring_stage<S>(lds0, lds1, lds2, lds3);
     const bf16_t* sX = sW + BN * BK;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -614,16 +717,35 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
         const int row = wm * (BM / WM) + b * 16 + l16;
         bfr[b] = ld16(&sX[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
       }
+      if constexpr (NT == 512) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < TN; ++a)
 #pragma unroll
         for (int b = 0; b < TM; ++b) acc[a][b] = mma16<EL>(af[a], bfr[b], acc[a][b]);
+      if constexpr (NT == 512) __builtin_amdgcn_s_setprio(0);
     }
     // WAR on stage i%NS is covered by the next iteration's barrier: its refill is issued
     // only after every wave has arrived there, i.e. finished this tile's MFMAs (whose
     // operands - these ds_reads - had to complete first).
+  };
+  for (int i = 0; i < nk; i += NS) {
+    step(IC<0>(), i);
+    if (i + 1 >= nk) break;
+    step(IC<1>(), i + 1);
+    if constexpr (NS > 2) {
+      if (i + 2 >= nk) break;
+      step(IC<2 % NS>(), i + 2);
+    }
+    if constexpr (NS > 3) {
+      if (i + 3 >= nk) break;
+      step(IC<3 % NS>(), i + 3);
+    }
   }
 
+  if constexpr (!SPLIT) {
+    epilogue_lds<BN, BM, WN, WM, NT, STAGE / 2, EL>(p, acc, reinterpret_cast<float*>(lds0), m0, n0);
+    return;
+  }
   const int hw = p.Ho * p.Wo;
 #pragma unroll
   for (int b = 0; b < TM; ++b) {
@@ -658,6 +780,229 @@ __global__ void __launch_bounds__(256, 1) conv_glds_kernel(ConvArgs p) {
       o.x = enc16<EL>(v0) | (enc16<EL>(v1) << 16);
       o.y = enc16<EL>(v2) | (enc16<EL>(v3) << 16);
       *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
+    }
+  }
+}
+
+// Persistent LDS-DMA variant for short-K GEMMs / 1x1 convs (K = 320..1280 on the UNet: the
+// transformer projections, GEGLU proj).  With 5-20 K-tiles per output tile, a one-tile-per-block
+// kernel spends most of its life in prologue latency and epilogue; here a grid of ~one block
+// per CU walks the flattened (tile, k-tile) sequence of its tiles through ONE NS-deep DMA ring,
+// so the next tile's operands are in flight while the current tile's epilogue runs.  The bias
+// rides the ring too (one DMA of BN channels with each tile's last k-tile: an ordinary global
+// load while LDS-DMA is in flight makes hipcc drain the ring).  Tile order: block b takes
+// logical tiles b, b + G, ... through the same bijective XCD remap as the other kernels (G is a
+// multiple of 8, so a block's tiles stay on its XCD).  No split-K, no norm prologue; temb /
+// residual (rare on short-K shapes) are read directly in the epilogue.
+template <int BN, int BM, int WN, int WM, int NS>
+__global__ void __launch_bounds__(64 * WN * WM, 1) conv_persist_kernel(ConvArgs p) {
+  constexpr int EL = 0;
+  constexpr int BK = 64;
+  constexpr int NT = 64 * WN * WM;
+  constexpr int RPI = NT / 8;
+  static_assert((BN * 8) % NT == 0 && (BM * 8) % NT == 0, "whole DMA rounds per tile");
+  static_assert(BN % 8 == 0 && BN / 8 <= 64, "bias DMA: one wave, 16 B per lane");
+  constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
+  constexpr int WCH = BN * 8 / NT, XCH = BM * 8 / NT;
+  constexpr int LPT = WCH + XCH;             // vmcnt units per k-tile per wave (bias DMA extra)
+  // W and X(+bias slot) of each stage are separate LDS objects: shallow address chains keep every
+  // ds_read's alias scope (a scope-less read waits for all LDS-DMA in flight)
+  constexpr int XST = BM * BK + BN;
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  __shared__ __attribute__((aligned(16))) bf16_t w0[BN * BK];
+  __shared__ __attribute__((aligned(16))) bf16_t w1[BN * BK];
+  __shared__ __attribute__((aligned(16))) bf16_t w2[NS > 2 ? BN * BK : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t w3[NS > 3 ? BN * BK : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t x0[XST];
+  __shared__ __attribute__((aligned(16))) bf16_t x1[XST];
+  __shared__ __attribute__((aligned(16))) bf16_t x2[NS > 2 ? XST : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t x3[NS > 3 ? XST : 8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WM, wm = wave % WM;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int nk = p.ktiles, total = p.tiles_total, G = gridDim.x;
+  const int mine = (total - (int)blockIdx.x + G - 1) / G;
+  const int J = mine * nk;
+  const int tiles_m = total / p.tiles_n;
+  auto origin = [&](int k, int& n0, int& m0) {
+    const int lin = xcd_remap((int)blockIdx.x + k * G, total);
+    if (p.m_fastest) {
+      m0 = (lin % tiles_m) * BM;
+      n0 = (lin / tiles_m) * BN;
+    } else {
+      n0 = (lin % p.tiles_n) * BN;
+      m0 = (lin / p.tiles_n) * BM;
+    }
+  };
+
+  const int pos = tid & 7;
+  int wrow[WCH], wcc[WCH], xcc[XCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) {
+    wrow[i] = (tid >> 3) + RPI * i;
+    wcc[i] = pos ^ (wrow[i] & 7);
+  }
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) xcc[i] = pos ^ (((tid >> 3) + RPI * i) & 7);
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+
+  // ---- issue side: geometry of the tile whose k-tiles are being fetched
+  int xb[XCH], xho[XCH], xwo[XCH], xoff[XCH], woff[WCH];
+  bool xok[XCH];
+  int wk = 0, wc = 0, wr = 0, ws = 0, ikt = 0, itile = 0, in0 = 0;
+  auto set_tap = [&]() {
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      int hi = xho[i] + wr, wi = xwo[i] + ws;
+      const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
+      if (p.upsample) { hi >>= 1; wi >>= 1; }
+      xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + xcc[i] * 8 : -1;
+    }
+  };
+  // The issued tile's row geometry is recomputed on EVERY issue (same values within a tile):
+  // a branch around it (only at a tile's first k-tile) made hipcc's waitcnt pass drain the ring
+  // before every k-tile's ds_reads.
+  auto tile_geometry = [&](int k) {
+    int n0, m0;
+    origin(k, n0, m0);
+    in0 = n0;
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int n = n0 + wrow[i];
+      woff[i] = n < p.N ? n * p.K + wcc[i] * 8 : -1;
+    }
+    const int hw = p.Ho * p.Wo;
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int m = m0 + (tid >> 3) + RPI * i;
+      xok[i] = m < p.M;
+      const int mm = xok[i] ? m : 0;
+      xb[i] = mm / hw;
+      const int rem = mm - xb[i] * hw;
+      xho[i] = (rem / p.Wo) * p.stride - p.pad;
+      xwo[i] = (rem % p.Wo) * p.stride - p.padw;
+    }
+  };
+  auto issue = [&](auto stage_c) {
+    tile_geometry(itile);
+    if (ikt == 0) { wk = 0; wc = 0; wr = 0; ws = 0; }
+    set_tap();
+    bf16_t* sW = ring_stage<decltype(stage_c)::value>(w0, w1, w2, w3);
+    bf16_t* sX = ring_stage<decltype(stage_c)::value>(x0, x1, x2, x3);
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
+      dma16(src, sW + ((wave * 8) + RPI * i) * BK);
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
+      dma16(src, sX + ((wave * 8) + RPI * i) * BK);
+    }
+    if (ikt == nk - 1 && wave == 0) {     // bias of this tile into the stage's bias slot
+      const int n = in0 + lane * 8;
+      const void* src = (p.bias && n < p.N) ? (const void*)(p.bias + n) : (const void*)g_conv_zero_page;
+      // lane l writes slot + 16 l: only the BN/8 lanes of the slot may be active (EXEC mask)
+      if (lane < BN / 8) dma16(src, sX + BM * BK);
+    }
+    wk += BK;
+    wc += BK;
+    if (wc == p.Cin) {
+      wc = 0;
+      if (++ws == p.kw) { ws = 0; ++wr; }
+      set_tap();
+    }
+    if (++ikt == nk) { ikt = 0; ++itile; }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (0 < J) issue(IC<0>());
+  if (NS > 2 && 1 < J) issue(IC<1>());
+  if (NS > 3 && 2 < J) issue(IC<2>());
+
+  int ckt = 0, ctile = 0;
+  const int hw = p.Ho * p.Wo;
+  auto step = [&](auto stage_c, int j) __attribute__((always_inline)) {
+    constexpr int S = decltype(stage_c)::value;
+    // stage j has landed once at most (NS-2)*LPT younger VM ops are outstanding (the bias DMA
+    // and epilogue stores only make this wait longer, never shorter)
+    if (j + NS - 2 < J) wait_vmcnt<(NS - 2) * LPT>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (j + NS - 1 < J) issue(IC<(S + NS - 1) % NS>());
+    const bf16_t* sW = ring_stage<S>(w0, w1, w2, w3);
+    const bf16_t* sX = ring_stage<S>(x0, x1, x2, x3);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      uint4 af[TN], bfr[TM];
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int row = wn * (BN / WN) + a * 16 + l16;
+        af[a] = ld16(&sW[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
+      }
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        const int row = wm * (BM / WM) + b * 16 + l16;
+        bfr[b] = ld16(&sX[row * BK + (((kk * 4 + g) ^ (row & 7)) << 3)]);
+      }
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = mma16<EL>(af[a], bfr[b], acc[a][b]);
+    }
+    if (++ckt < nk) return;
+    // ---- epilogue of the finished tile (the ring keeps fetching the next one meanwhile)
+    ckt = 0;
+    int n0, m0;
+    origin(ctile++, n0, m0);
+    const bf16_t* sB = sX + BM * BK;   // this stage's bias slot (issued with this k-tile)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int m = m0 + wm * (BM / WM) + b * 16 + l16;
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int nl = wn * (BN / WN) + a * 16 + 4 * g, n = n0 + nl;
+        float v0 = acc[a][b][0], v1 = acc[a][b][1], v2 = acc[a][b][2], v3 = acc[a][b][3];
+        acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if (m >= p.M || n >= p.N) continue;
+        const uint2 bv = *reinterpret_cast<const uint2*>(&sB[nl]);
+        v0 += lo16<EL>(bv.x); v1 += hi16<EL>(bv.x);
+        v2 += lo16<EL>(bv.y); v3 += hi16<EL>(bv.y);
+        if (p.temb) {
+          const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)(m / hw) * p.N + n);
+          v0 += lo16<EL>(tv.x); v1 += hi16<EL>(tv.x);
+          v2 += lo16<EL>(tv.y); v3 += hi16<EL>(tv.y);
+        }
+        if (p.res) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.N + n);
+          v0 += lo16<EL>(rv.x); v1 += hi16<EL>(rv.x);
+          v2 += lo16<EL>(rv.y); v3 += hi16<EL>(rv.y);
+        }
+        uint2 o;
+        o.x = enc16<EL>(v0) | (enc16<EL>(v1) << 16);
+        o.y = enc16<EL>(v2) | (enc16<EL>(v3) << 16);
+        *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
+      }
+    }
+  };
+  for (int j = 0; j < J; j += NS) {
+    step(IC<0>(), j);
+    if (j + 1 >= J) break;
+    step(IC<1>(), j + 1);
+    if constexpr (NS > 2) {
+      if (j + 2 >= J) break;
+      step(IC<2 % NS>(), j + 2);
+    }
+    if constexpr (NS > 3) {
+      if (j + 3 >= J) break;
+      step(IC<3 % NS>(), j + 3);
     }
   }
 }
@@ -725,13 +1070,40 @@ struct PinnedPlan {
 };
 #include "conv_plans.inc"
 
+// Optional run-time plan table (A/B of autotuned tables without a rebuild): ARB_CONV_PLANS names
+// a file in conv_plans.inc format ("{M, N, K, cfg, split},"); its entries take precedence.
+static const std::vector<PinnedPlan>& env_plans() {
+  static const std::vector<PinnedPlan> plans = [] {
+    std::vector<PinnedPlan> v;
+    const char* path = std::getenv("ARB_CONV_PLANS");
+    if (path == nullptr || path[0] == 0) return v;
+    FILE* f = std::fopen(path, "r");
+    if (f == nullptr) return v;
+    char line[256];
+    while (std::fgets(line, sizeof line, f)) {
+      PinnedPlan pp;
+      if (std::sscanf(line, " {%d, %d, %d, %d, %d}", &pp.M, &pp.N, &pp.K, &pp.cfg, &pp.split) == 5) v.push_back(pp);
+    }
+    std::fclose(f);
+    return v;
+  }();
+  return plans;
+}
+
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
-  if (want_cfg >= 0 && want_cfg < 2 * kNumCfgs) {
+  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 28))) {
+    if (want_cfg >= 24) return {want_cfg, 1, ktiles};   // persistent: no split-K
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
     const int per = (ktiles + split - 1) / split;
     return {want_cfg, (ktiles + per - 1) / per, per};
+  }
+  for (const PinnedPlan& pp : env_plans()) {
+    if (pp.M == M && pp.N == N && pp.K == K) {
+      const int per = (ktiles + pp.split - 1) / pp.split;
+      return {pp.cfg, pp.cfg >= 24 ? 1 : (ktiles + per - 1) / per, pp.cfg >= 24 ? ktiles : per};
+    }
   }
   for (const PinnedPlan& pp : kPinnedPlans) {
     if (pp.M == M && pp.N == N && pp.K == K) {
@@ -856,14 +1228,54 @@ ARB_API size_t arb_conv2d_workspace(int B, int H, int W, int Cin, int Cout, int 
 
 template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
 static void launch_glds(const ConvArgs& p, dim3 grid, hipStream_t s) {
-  constexpr size_t lds = (size_t)NS * (BN + BM) * 64 * sizeof(bf16_t);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
+  static_assert((size_t)NS * (BN + BM) * 64 * sizeof(bf16_t) <= 160 * 1024, "LDS");
+  conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT><<<grid, 64 * WN * WM, 0, s>>>(p);   // static LDS ring
+}
+
+// Persistent short-K tiles (cfg 24 + i): grid = min(tiles, 256 CUs).
+template <int BN, int BM, int WN, int WM, int NS>
+static void launch_persist(const ConvArgs& a, hipStream_t s) {
+  static_assert((size_t)NS * ((BN + BM) * 64 + BN) * sizeof(bf16_t) <= 160 * 1024, "LDS");   // static ring
+  ConvArgs p = a;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
+  p.nsplit = 1;
+  p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;
+  p.norm = nullptr;
+  p.counters = nullptr;
+  p.kt_per_split = p.ktiles;
+  int grid = p.tiles_total < 256 ? p.tiles_total : 256;
+  conv_persist_kernel<BN, BM, WN, WM, NS><<<grid, 64 * WN * WM, 0, s>>>(p);
+}
+
+// 8-wave LDS-DMA tiles (cfg 20 + i): two full K-tile stages, per-wave 128x64 / 160x64 outputs.
+struct BigCfg {
+  int bn, bm;
+};
+static const BigCfg kBigCfgs[] = {{256, 256}, {320, 128}, {256, 128}, {320, 192}};
+static_assert(sizeof(kBigCfgs) / sizeof(kBigCfgs[0]) == 4, "conv_plan accepts cfg 20..23");
+
+template <int BN, int BM, int WN, int WM>
+static void launch_big(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
+  constexpr int NS = 2;
+  static_assert(NS * (BN + BM) * 64 * 2 <= 160 * 1024, "LDS");
+  ConvArgs p = a;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
+  p.nsplit = pl.split > 1 ? pl.split : 1;
+  p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;
+  p.norm = nullptr;
+  p.counters = nullptr;
+  if (pl.split > 1) {
+    p.kt_per_split = pl.kt_per_split;
+    launch_glds<BN, BM, WN, WM, NS, true>(p, dim3(p.tiles_total * pl.split), s);
+    long work = (long)p.M * (p.N / 8);
+    long blocks = (work + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<0><<<(int)blocks, 256, 0, s>>>(p, pl.split);
+  } else {
+    launch_glds<BN, BM, WN, WM, NS, false>(p, dim3(p.tiles_total), s);
   }
-  conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT><<<grid, 256, lds, s>>>(p);
 }
 
 template <int BN, int BM, int WN, int WM, int MINW, int EL = 0>
@@ -936,6 +1348,26 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
   conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
   const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
   if (pl.split > 1 && ws == nullptr) return -3;
+  if (pl.cfg >= 24) {   // persistent short-K tiles (bf16, no norm prologue, no split)
+    if (EL != 0 || a.norm != nullptr) return -4;
+    switch (pl.cfg - 24) {
+      case 0: launch_persist<128, 128, 2, 2, 4>(a, stream); break;
+      case 1: launch_persist<256, 128, 4, 2, 3>(a, stream); break;
+      case 2: launch_persist<160, 128, 2, 2, 4>(a, stream); break;
+      default: launch_persist<128, 64, 2, 2, 4>(a, stream); break;
+    }
+    return (int)hipGetLastError();
+  }
+  if (pl.cfg >= 20) {   // 8-wave LDS-DMA tiles (bf16, no norm prologue)
+    if (EL != 0 || a.norm != nullptr) return -4;
+    switch (pl.cfg - 20) {
+      case 0: launch_big<256, 256, 2, 4>(a, pl, stream); break;
+      case 1: launch_big<320, 128, 4, 2>(a, pl, stream); break;
+      case 2: launch_big<256, 128, 4, 2>(a, pl, stream); break;
+      default: launch_big<320, 192, 2, 4>(a, pl, stream); break;
+    }
+    return (int)hipGetLastError();
+  }
   const bool glds = pl.cfg < kNumCfgs;  // cfg >= kNumCfgs: register-staged variant (A/B)
   switch (pl.cfg % kNumCfgs) {
     case 0: launch_conv<128, 128, 2, 2, 2, EL>(a, pl, glds, stream); break;

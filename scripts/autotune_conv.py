@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from arbius_amd import ops  # noqa: E402
 from arbius_amd.ops import _lib  # noqa: E402
 
-NCFG = 20  # 0-9: LDS-DMA multi-stage, 10-19: register-staged
+NCFG = 20  # 0-9: LDS-DMA multi-stage, 10-19: register-staged, 20-23: 8-wave LDS-DMA (KBIG)
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
@@ -84,19 +84,32 @@ def read_table(path):
     return out
 
 
-def candidates(M, N, K, legacy_only):
+def candidates(M, N, K, mode):
     """(cfg, split) pairs worth timing: split-K only when the grid is short of 2 waves."""
-    cfgs = range(10, NCFG) if legacy_only else range(NCFG)
+    big = list(range(20, 20 + len(KBIG))) + list(range(24, 24 + len(KPERSIST)))
+    cfgs = {"legacy": range(10, NCFG), "big": big, "glds": list(range(10)) + big}.get(mode, list(range(NCFG)) + big)
     for cfg in cfgs:
-        bn, bm = KCFG[cfg % 10]
+        bn, bm = KPERSIST[cfg - 24] if cfg >= 24 else KBIG[cfg - 20] if cfg >= 20 else KCFG[cfg % 10]
+        if cfg >= 20 and bn > N + N // 2:
+            continue
+        if cfg >= 24:      # persistent short-K kernel: no split-K
+            if K <= 2560:
+                yield cfg, 1
+            continue
         tiles = -(-N // bn) * -(-M // bm)
         for sp in SPLITS:
-            if sp > 1 and (sp > (K // 64) // 2 or tiles >= 512):
+            if sp > 1 and (sp > (K // 64) // 2 or tiles >= (256 if cfg >= 20 else 512)):
                 continue
             yield cfg, sp
 
 
 KCFG = [(128, 128), (64, 128), (128, 64), (64, 64), (160, 64), (160, 128), (320, 32), (256, 64), (128, 256), (64, 256)]
+KBIG = [(256, 256), (320, 128), (256, 128), (320, 192)]
+KPERSIST = [(128, 128), (256, 128), (160, 128), (128, 64)]
+
+
+def _agrees(y, ref):
+    return ((y.float() - ref.float()).norm() / ref.float().norm().clamp_min(1e-6)).item() < 1e-2
 
 
 def graph_time(fn, reps=10, rounds=5):
@@ -130,6 +143,9 @@ def main():
     ap.add_argument("out_dir", nargs="?", default="gpurun_out")
     ap.add_argument("--models", default="sd15", help="comma list: sd15,kandinsky2,video")
     ap.add_argument("--legacy-only", action="store_true", help="time only the register-staged cfgs (10-19)")
+    ap.add_argument("--mode", default="all", help="all | glds (LDS-DMA cfgs vs the current plan) | big | legacy")
+    ap.add_argument("--big-only", action="store_true",
+                    help="time only the 8-wave cfgs (20-23) against the current plan; re-pin where they win")
     ap.add_argument("--merge", default=None, help="existing conv_plans.inc to keep entries from")
     ap.add_argument("--batch", type=int, default=2, help="SD UNet batch for shape collection (8 = groups of 4)")
     args = ap.parse_args()
@@ -137,6 +153,7 @@ def main():
     os.makedirs(out_dir, exist_ok=True)
     dev = torch.device("cuda")
     convs, gemms = collect_shapes(tuple(args.models.split(",")), batch=args.batch)
+    mode = "big" if args.big_only else "legacy" if args.legacy_only else args.mode
     results = []
     pinned = read_table(args.merge) if args.merge else {}
     print(f"{len(convs)} conv shapes, {len(gemms)} gemm shapes, {len(pinned)} pinned kept", flush=True)
@@ -149,33 +166,42 @@ def main():
         Ho, Wo = (Hl + 2 * pad - kh) // st + 1, (Wl + 2 * padw - kw) // st + 1
         M, K = B * Ho * Wo, kh * kw * C
         auto = _lib.conv_plan(B, H, W, C, Co, 31 if kw != kh else kh, pad, up, st)
-        best = None
-        for cfg, sp in candidates(M, Co, K, args.legacy_only):
+        y_ref = _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st)
+        t_auto = graph_time(lambda: _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st))
+        best = (t_auto, auto[0], auto[1]) if mode in ("big", "glds") else None
+        for cfg, sp in candidates(M, Co, K, mode):
             if True:
                 try:
+                    if not _agrees(_lib.conv2d_nhwc(x, w, b, pad, up, None, None, st, cfg, sp), y_ref):
+                        print("MISMATCH conv", (B, H, W, C, Co, kh, pad, up, st), cfg, sp, flush=True)
+                        continue
                     t = graph_time(lambda: _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st, cfg, sp))
                 except Exception as e:  # noqa: BLE001
                     print("skip", cfg, sp, e, flush=True)
                     continue
                 if best is None or t < best[0]:
                     best = (t, cfg, sp)
-        t_auto = graph_time(lambda: _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st))
         fl = 2.0 * M * Co * K
         rec = {"kind": "conv", "shape": [B, H, W, C, Co, kh, kw, pad, up, st], "MNK": [M, Co, K], "best_us": round(best[0], 2),
                "best_cfg": best[1], "best_split": best[2], "best_tflops": round(fl / best[0] / 1e6, 1),
                "auto_cfg": auto, "auto_us": round(t_auto, 2)}
         results.append(rec)
-        pinned[(M, Co, K)] = (best[1], best[2])
+        if best[1] >= 0:
+            pinned[(M, Co, K)] = (best[1], best[2])
         print(json.dumps(rec), flush=True)
     for (M, K, N) in gemms:
         x = torch.randn(M, K, device=dev).bfloat16()
         w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
         b = torch.randn(N, device=dev).bfloat16()
         r = torch.randn(M, N, device=dev).bfloat16()
-        best = None
-        for cfg, sp in candidates(M, N, K, args.legacy_only):
+        y_ref = _lib.gemm(x, w, b, r)
+        best = (graph_time(lambda: _lib.gemm(x, w, b, r)), *pinned.get((M, N, K), (-1, 1))) if mode in ("big", "glds") else None
+        for cfg, sp in candidates(M, N, K, mode):
             if True:
                 try:
+                    if not _agrees(_lib.gemm(x, w, b, r, cfg, sp), y_ref):
+                        print("MISMATCH gemm", (M, N, K), cfg, sp, flush=True)
+                        continue
                     t = graph_time(lambda: _lib.gemm(x, w, b, r, cfg, sp))
                 except Exception as e:  # noqa: BLE001
                     continue
@@ -186,7 +212,7 @@ def main():
         rec = {"kind": "gemm_res", "MNK": [M, N, K], "best_us": round(best[0], 2), "best_cfg": best[1],
                "best_split": best[2], "best_tflops": round(fl / best[0] / 1e6, 1), "hipblaslt_addmm_add_us": round(t_blas, 2)}
         results.append(rec)
-        if (M, N, K) not in {tuple(r["MNK"]) for r in results if r["kind"] == "conv"}:
+        if best[1] >= 0 and (M, N, K) not in {tuple(r["MNK"]) for r in results if r["kind"] == "conv"}:
             pinned[(M, N, K)] = (best[1], best[2])
         print(json.dumps(rec), flush=True)
     json.dump(results, open(os.path.join(out_dir, "autotune_conv.json"), "w"), indent=1)

@@ -122,7 +122,7 @@ def test_gemm(cuda, M, K, N):
     assert _rel(y, x.float() @ w.float().t() + b.float() + r.float()) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(20)))
+@pytest.mark.parametrize("cfg", list(range(20)) + [20, 21, 22, 23, 24, 25, 26, 27])
 @pytest.mark.parametrize("split", [1, 3])
 def test_conv2d_all_tile_configs(cuda, cfg, split):
     """Every tile config of both kernel variants (LDS-DMA ring / register staged) and split-K."""
@@ -135,6 +135,41 @@ def test_conv2d_all_tile_configs(cuda, cfg, split):
     y = _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg, split)
     ref_y = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, 1, False) + r.float()
     assert _rel(y, ref_y) < 1e-2, (cfg, split, _rel(y, ref_y))
+
+
+@pytest.mark.parametrize("cfg", [24, 25, 26, 27])
+@pytest.mark.parametrize("res", [False, True])
+def test_gemm_persistent_many_tiles(cuda, cfg, res):
+    """Persistent short-K kernel: > 256 tiles, so blocks walk several tiles through one DMA ring
+    (bias rides the ring; residual read in the epilogue).  Bitwise equal to the one-tile kernels."""
+    torch.manual_seed(6)
+    M, K, N = 8200, 320, 648
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    r = torch.randn(M, N, device=cuda).bfloat16() if res else None
+    y = _lib.gemm(x, w, b, r, cfg, 1)
+    ref_y = x.float() @ w.float().t() + b.float() + (r.float() if res else 0)
+    assert _rel(y, ref_y) < 1e-2
+    assert torch.equal(y, _lib.gemm(x, w, b, r, 15, 1))
+
+
+@pytest.mark.parametrize("cfg", [20, 21, 22, 23])
+@pytest.mark.parametrize("Cout,k", [(320, 3), (640, 1), (1280, 3)])
+def test_conv2d_big_tiles_match_register_staged(cuda, cfg, Cout, k):
+    """8-wave LDS-DMA tiles (partial M and N edge tiles) against the 4-wave register-staged
+    kernel: same per-element K order (32-wide MFMA steps in K-tile order), so bitwise equal."""
+    torch.manual_seed(5)
+    B, H, W, Cin = 2, 37, 29, 320
+    x = torch.randn(B, H, W, Cin, device=cuda).bfloat16()
+    w = (torch.randn(Cout, k, k, Cin, device=cuda) / math.sqrt(k * k * Cin)).bfloat16()
+    b = torch.randn(Cout, device=cuda).bfloat16()
+    pad = k // 2
+    y = _lib.conv2d_nhwc(x, w, b, pad, False, None, None, 1, cfg, 1)
+    ref_y = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, pad, False)
+    assert _rel(y, ref_y) < 1e-2
+    y_reg = _lib.conv2d_nhwc(x, w, b, pad, False, None, None, 1, 15, 1)
+    assert torch.equal(y, y_reg)
 
 
 @pytest.mark.parametrize("B,H,W,C,G,mh,mw,one_plus,silu", [
