@@ -92,7 +92,8 @@ class FeedForward(nn.Module):
         self.out = Linear(mult * dim, dim)
 
     def forward(self, x, residual):
-        return self.out(ops.geglu(self.proj(x)), residual=residual)
+        # GEGLU fused into the projection GEMM's epilogue on the GPU (ops.linear_geglu)
+        return self.out(ops.linear_geglu(x, self.proj.weight, self.proj.bias), residual=residual)
 
 
 class BasicTransformerBlock(nn.Module):

@@ -17,6 +17,7 @@ from __future__ import annotations
 import math
 import os
 import threading
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -105,6 +106,29 @@ def linear(x, w, b=None, residual=None):
             y = y.add_(b)
         return y.reshape(*x.shape[:-1], w.shape[0])
     return F.linear(x, w, b)
+
+
+_GEGLU_FUSED = os.environ.get("ARBIUS_GEGLU_FUSED", "1") != "0"   # A/B switch (same numerics)
+_GEGLU_W = {}   # id(weight) -> (weakref(weight), weakref(bias), interleaved w, interleaved b)
+
+
+def linear_geglu(x, w, b=None):
+    """GEGLU feed-forward projection: value * gelu(gate) of (x @ w^T + b) split in halves.
+
+    GPU: one implicit-GEMM launch with the GEGLU in its epilogue (the [M, 2F] pre-activation
+    never reaches HBM; no separate geglu pass).  The projection rows are interleaved once into
+    [value 8 | gate 8] blocks so every output tile holds matching value / gate channels."""
+    if (_GEGLU_FUSED and _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]) and w.shape[0] % 16 == 0
+            and x.dtype == torch.bfloat16):
+        ent = _GEGLU_W.get(id(w))
+        stamp = (w.data_ptr(), w._version, None if b is None else (b.data_ptr(), b._version))
+        if ent is None or ent[0]() is not w or (b is not None and ent[1]() is not b) or ent[4] != stamp:
+            wi = _lib.interleave_geglu(w.detach())
+            bi = _lib.interleave_geglu(b.detach()) if b is not None else None
+            ent = (weakref.ref(w), weakref.ref(b) if b is not None else (lambda: None), wi, bi, stamp)
+            _GEGLU_W[id(w)] = ent
+        return _lib.gemm_geglu(x, ent[2], ent[3], plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
+    return geglu(linear(x, w, b))
 
 
 def _gemm_ok(K, N):

@@ -38,6 +38,7 @@ _SIGS = {
     "arb_conv2d_workspace": (c_size_t, [c_int] * 11),
     "arb_conv2d_plan": (c_int, [c_int] * 9 + [c_void_p]),
     "arb_gemm_bias_res": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p]),
+    "arb_gemm_geglu": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p]),
     "arb_temporal_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_void_p]),
     "arb_convgru_gates": (c_int, [c_int] + [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_void_p]),
 }
@@ -385,3 +386,31 @@ def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None):
     _check(_fn("arb_gemm_bias_res")(_p(x2), _p(w.contiguous()), _p(b), _p(r2), _p(y), _p(ws), M, N, K, int(cfg),
                                     int(split), _stream()), "gemm")
     return y.reshape(*x.shape[:-1], N)
+
+
+def gemm_geglu(x, w_il, b_il=None, cfg=-1, split=-1, plan_batch=None):
+    """value * gelu(gate) of x @ w^T + b in the GEMM epilogue.  ``w_il`` / ``b_il``: the projection's
+    rows interleaved in blocks of 16 as [value 8 | gate 8] (``interleave_geglu``); out [..., N/2].
+    Bitwise equal to ``geglu(gemm(x, w, b))`` (both halves rounded to bf16 before the product)."""
+    _bf16(x, w_il, b_il)
+    K = x.shape[-1]
+    N = w_il.shape[0]
+    x2 = x.reshape(-1, K).contiguous()
+    M = x2.shape[0]
+    if K % 64 or N % 16 or w_il.shape[1] != K:
+        raise ValueError(f"gemm_geglu: unsupported K={K} N={N}")
+    if plan_batch and plan_batch[1] and plan_batch[1] != plan_batch[0] and cfg < 0:
+        cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
+    y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+    ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
+    _check(_fn("arb_gemm_geglu")(_p(x2), _p(w_il.contiguous()), _p(b_il), _p(y), _p(ws), M, N, K, int(cfg),
+                                 int(split), _stream()), "gemm_geglu")
+    return y.reshape(*x.shape[:-1], N // 2)
+
+
+def interleave_geglu(t):
+    """[value F | gate F] rows (dim 0) -> blocks of 16 rows [value 8 | gate 8] (F % 8 == 0)."""
+    F_ = t.shape[0] // 2
+    v, g = t[:F_].reshape(F_ // 8, 8, *t.shape[1:]), t[F_:].reshape(F_ // 8, 8, *t.shape[1:])
+    return torch.stack([v, g], dim=1).reshape(t.shape).contiguous()

@@ -48,6 +48,7 @@ struct ConvArgs {
   int ktiles, kt_per_split;
   int tiles_n, tiles_total;
   int nsplit, m_fastest;
+  int geglu = 0;        // GEGLU epilogue: W rows interleaved [value 8 | gate 8] per 16; out [M, N/2]
 };
 
 // ---- element type: EL = 0 bf16 (the diffusion models), EL = 1 fp16 (robust video matting).
@@ -156,6 +157,36 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&ac
       }
     }
     __syncthreads();
+    if (p.geglu) {
+      // value chunk ch, gate chunk ch + 8 -> 8 outputs at column n / 2; both halves rounded to
+      // bf16 first (the unfused GEMM -> geglu path's numerics, bitwise)
+      constexpr int PPR = BN / 16;
+      const int NO = p.N >> 1;
+      for (int c = tid; c < PR * PPR; c += NT) {
+        const int rl = c / PPR, ch = (c - rl * PPR) * 16;
+        const int m = m0 + r0 + rl, n = n0 + ch;
+        if (m >= p.M || n >= p.N) continue;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch]);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch + 4]);
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch + 8]);
+        const f32x4 g1 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch + 12]);
+        float va[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        float vg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        if (p.bias) {
+          float t[8];
+          unpack8e<EL>(ld16(p.bias + n), t);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) va[e] += t[e];
+          unpack8e<EL>(ld16(p.bias + n + 8), t);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) vg[e] += t[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) va[e] = dec16<EL>(enc16<EL>(va[e])) * gelu_f(dec16<EL>(enc16<EL>(vg[e])));
+        st16(p.out + (size_t)m * NO + (n >> 1), pack8e<EL>(va));
+      }
+      continue;
+    }
     for (int c = tid; c < PR * CPR; c += NT) {
       const int rl = c / CPR, ch = (c - rl * CPR) * 8;
       const int m = m0 + r0 + rl, n = n0 + ch;
@@ -1010,6 +1041,40 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_persist_kernel(ConvArgs 
 // Ordered split-K reduction + epilogue: out[m, n..n+7] from S fp32 slabs.
 template <int EL>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
+  if (p.geglu) {   // 16 channels (value 8 | gate 8) -> 8 GEGLU outputs, same rounding as epilogue_lds
+    const long tot = (long)p.M * (p.N / 16);
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < tot; i += (long)gridDim.x * 256) {
+      const int m = (int)(i / (p.N / 16));
+      const int n = (int)(i - (long)m * (p.N / 16)) * 16;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 a = reinterpret_cast<const float4*>(p.ws + (size_t)m * p.N + n)[q];
+        v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+      }
+      for (int s = 1; s < S; ++s) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 a = reinterpret_cast<const float4*>(p.ws + ((size_t)s * p.M + m) * p.N + n)[q];
+          v[4 * q] += a.x; v[4 * q + 1] += a.y; v[4 * q + 2] += a.z; v[4 * q + 3] += a.w;
+        }
+      }
+      if (p.bias) {
+        float t[8];
+        unpack8e<EL>(ld16(p.bias + n), t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += t[e];
+        unpack8e<EL>(ld16(p.bias + n + 8), t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[8 + e] += t[e];
+      }
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = dec16<EL>(enc16<EL>(v[e])) * gelu_f(dec16<EL>(enc16<EL>(v[8 + e])));
+      st16(p.out + (size_t)m * (p.N >> 1) + (n >> 1), pack8e<EL>(o));
+    }
+    return;
+  }
   const long total = (long)p.M * (p.N / 8);
   const int hw = p.Ho * p.Wo;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -1312,7 +1377,7 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
     // register-staged kernel.  In-launch reduction is opt-in (ARB_SPLITK_INLAUNCH=1): the
     // agent-scope release/acquire pair writes back / invalidates the XCD's L2 per block, which
     // measured 2-3x slower than the separate ordered reduce on SD1.5 shapes.
-    p.counters = splitk_inlaunch() ? split_counters(s, p.tiles_total) : nullptr;
+    p.counters = (splitk_inlaunch() && !p.geglu) ? split_counters(s, p.tiles_total) : nullptr;
     if constexpr (EL == 0) {
       if (p.norm) conv_igemm_kernel<BN, BM, WN, WM, MINW, true, true><<<grid, 256, 0, s>>>(p);
       else conv_igemm_kernel<BN, BM, WN, WM, MINW, true, false><<<grid, 256, 0, s>>>(p);
@@ -1339,14 +1404,19 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
 template <int EL>
 static int conv_run(const void* x, const void* w, const void* bias, const void* temb, const void* res, void* out,
                     void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
-                    int stride, int cfg, int split, int norm_silu, hipStream_t stream) {
+                    int stride, int cfg, int split, int norm_silu, hipStream_t stream, int geglu = 0) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
   ConvArgs a;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = (const bf16_t*)bias; a.temb = (const bf16_t*)temb;
   a.res = (const bf16_t*)res; a.out = (bf16_t*)out; a.ws = (float*)ws;
   a.norm = (const float*)norm; a.norm_silu = norm_silu;
   conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
-  const ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
+  a.geglu = geglu;
+  ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
+  if (geglu) {
+    if (Cout % 16 != 0 || temb != nullptr || res != nullptr || norm != nullptr) return -1;
+    if (pl.cfg >= 24) pl = {kNumCfgs + 5, 1, a.ktiles};   // persistent kernel has no GEGLU epilogue
+  }
   if (pl.split > 1 && ws == nullptr) return -3;
   if (pl.cfg >= 24) {   // persistent short-K tiles (bf16, no norm prologue, no split)
     if (EL != 0 || a.norm != nullptr) return -4;
@@ -1408,6 +1478,14 @@ ARB_API int arb_conv2d_plan(int B, int H, int W, int Cin, int Cout, int k, int p
   cfg_split[0] = pl.cfg;
   cfg_split[1] = pl.split;
   return 0;
+}
+
+// GEGLU projection: out[M, N/2] = value * gelu(gate) of x W^T + b, with W / b rows interleaved in
+// blocks of 16 as [value 8 | gate 8] (see ops.linear_geglu); N % 16 == 0, K % 64 == 0.
+ARB_API int arb_gemm_geglu(const void* x, const void* w, const void* bias, void* out, void* ws, int M, int N, int K,
+                           int cfg, int split, hipStream_t stream) {
+  return conv_run<0>(x, w, bias, nullptr, nullptr, out, ws, nullptr, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, 0, stream,
+                     1);
 }
 
 // Plain GEMM with fused epilogue: out[M,N] = x[M,K] W[N,K]^T (+bias +residual); K % 64 == 0.

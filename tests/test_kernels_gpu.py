@@ -154,6 +154,24 @@ def test_gemm_persistent_many_tiles(cuda, cfg, res):
     assert torch.equal(y, _lib.gemm(x, w, b, r, 15, 1))
 
 
+@pytest.mark.parametrize("M,K,N,cfg,split", [
+    (8200, 320, 2560, -1, -1), (8200, 320, 2560, 15, 1), (8200, 320, 2560, 25, 1), (8200, 320, 2560, 21, 1),
+    (8200, 320, 2560, 0, 1), (512, 1280, 10240, 13, 3), (512, 1280, 10240, 22, 2), (300, 640, 5120, 3, 1)])
+def test_gemm_geglu_bitwise_equals_unfused(cuda, M, K, N, cfg, split):
+    """GEGLU in the GEMM epilogue (interleaved value/gate rows) == geglu(gemm(x, w, b)) bitwise,
+    for register / LDS-DMA / 8-wave tiles, split-K (reduce kernel) and the persistent remap."""
+    torch.manual_seed(7)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    want = _lib.geglu(_lib.gemm(x, w, b, None, cfg, split))
+    got = _lib.gemm_geglu(x, _lib.interleave_geglu(w), _lib.interleave_geglu(b), cfg, split)
+    assert got.shape == (M, N // 2)
+    assert torch.equal(got, want)
+    r = ref.geglu(x.float() @ w.float().t() + b.float())
+    assert _rel(got, r) < 2e-2
+
+
 @pytest.mark.parametrize("cfg", [20, 21, 22, 23])
 @pytest.mark.parametrize("Cout,k", [(320, 3), (640, 1), (1280, 3)])
 def test_conv2d_big_tiles_match_register_staged(cuda, cfg, Cout, k):
