@@ -466,19 +466,35 @@ ARB_API int arb_flash_attention(const void* q, const void* k, const void* v, voi
   a.scale_log2 = scale * 1.4426950408889634f;
   a.causal = causal;
   const int ks = (D + 31) / 32, dt = (D + 15) / 16;
-  // Small query counts: 1 q-tile per wave keeps more workgroups in flight.
-  const bool small = (long)B * H * Nq < 256L * 128;
+  // Small query counts: 1 q-tile per wave keeps more workgroups in flight.  Large ones (>= 1024
+  // workgroups even at 4 q-tiles per wave, e.g. the batched SD level-0 self-attention): 4 q-tiles
+  // per wave halve the K/V fragment LDS reads per query (LDS bandwidth is the shared limit).
+  const long rows = (long)B * H * Nq;
+  const bool small = rows < 256L * 128;
+  static const int qt_env = [] {
+    const char* e = std::getenv("ARB_ATTN_QT");
+    return e ? std::atoi(e) : 0;
+  }();
+  const bool wide = Np == 0 && (qt_env == 4 || (qt_env == 0 && rows >= 256L * 1024));
 #define FA_CASE(KS, DTT)                                  \
   if (ks == KS && dt == DTT) {                            \
     if (small) launch_fa<KS, DTT, 1>(a, stream);          \
     else launch_fa<KS, DTT, 2>(a, stream);                \
     return (int)hipGetLastError();                        \
   }
+#define FA_CASE4(KS, DTT)                                 \
+  if (ks == KS && dt == DTT) {                            \
+    if (small) launch_fa<KS, DTT, 1>(a, stream);          \
+    else if (wide) launch_fa<KS, DTT, 4>(a, stream);      \
+    else launch_fa<KS, DTT, 2>(a, stream);                \
+    return (int)hipGetLastError();                        \
+  }
   FA_CASE(1, 1) FA_CASE(1, 2)
-  FA_CASE(2, 3) FA_CASE(2, 4)
+  FA_CASE4(2, 3) FA_CASE4(2, 4)
   FA_CASE(3, 5) FA_CASE(3, 6)
   FA_CASE(4, 7) FA_CASE(4, 8)
   FA_CASE(5, 9) FA_CASE(5, 10)
 #undef FA_CASE
+#undef FA_CASE4
   return -2;
 }

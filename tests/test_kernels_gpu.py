@@ -45,7 +45,8 @@ def test_layer_norm(cuda, M, C):
     (2, 64, 64, 8, 160, False), (2, 4096, 77, 8, 40, False), (2, 1024, 77, 8, 80, False),
     (2, 77, 77, 12, 64, True), (3, 100, 37, 4, 64, False), (5, 24, 24, 5, 64, False),
     (1, 300, 300, 2, 128, True), (2, 200, 130, 3, 32, False), (1, 129, 65, 1, 96, False),
-    (1, 200, 100, 3, 72, False), (2, 150, 150, 2, 24, True), (1, 64, 64, 1, 8, False)])
+    (1, 200, 100, 3, 72, False), (2, 150, 150, 2, 24, True), (1, 64, 64, 1, 8, False),
+    (8, 4096, 4096, 8, 40, False), (4, 8192, 300, 8, 64, False)])   # last two: 4 q-tiles per wave
 def test_flash_attention(cuda, B, Nq, Nk, H, D, causal):
     torch.manual_seed(1)
     # fused-QKV-like strided views
