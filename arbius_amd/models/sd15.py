@@ -13,6 +13,8 @@ graph launch, so the step is bound by the kernels, not by Python.
 """
 from __future__ import annotations
 
+import os
+
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -27,7 +29,7 @@ from .graphs import CAPTURE_LOCK, PipelineBase
 from .layers import init_weights
 from .schedulers import make_scheduler
 from .tokenizer import CLIPTokenizer
-from .unet2d import UNet2DCondition, UNetConfig
+from .unet2d import CrossAttention, UNet2DCondition, UNetConfig, cross_kv_mode
 from .vae import VAEConfig, VAEDecoder
 
 
@@ -43,7 +45,12 @@ class SD15Config:
 
 
 class _GraphedUNet:
-    """Static-shape hipGraph wrapper around one UNet forward."""
+    """Static-shape hipGraph wrapper around one UNet forward.
+
+    Two graphs: ``kv_graph`` projects the text context through every cross-attention to_kv
+    (replayed once per new context, i.e. once per task / lock-step group), ``graph`` is the
+    per-step UNet that reads those K/V buffers instead of re-projecting the constant context
+    at every denoising step (unet2d.cross_kv_mode)."""
 
     def __init__(self, unet, x_shape, ctx, dtype):
         dev = ctx.device
@@ -51,28 +58,49 @@ class _GraphedUNet:
         self.x = torch.zeros(x_shape, dtype=dtype, device=dev)
         self.t = torch.zeros(1, dtype=torch.float32, device=dev)
         self.ctx = ctx.clone()
+        self.kv = {}
+        self._ctx_obj = None
         CAPTURE_LOCK.acquire()
         try:
             self._capture(unet, dev)
         finally:
             CAPTURE_LOCK.release()
 
+    HOIST = os.environ.get("ARBIUS_CROSS_KV_HOIST", "1") != "0"   # A/B switch (same numerics)
+
+    def _project_kv(self, unet):
+        if not self.HOIST:
+            return
+        for m in unet.modules():
+            if isinstance(m, CrossAttention):
+                self.kv[id(m)] = m.context_kv(self.ctx)
+
     def _capture(self, unet, dev):
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):  # warm-up: allocator + kernel-library load outside capture
-                self.out = unet(self.x, self.t, self.ctx)
+                self._project_kv(unet)
+                with cross_kv_mode("consume" if self.HOIST else None, self.kv):
+                    self.out = unet(self.x, self.t, self.ctx)
         torch.cuda.current_stream(dev).wait_stream(s)
+        self.kv_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.kv_graph, capture_error_mode="thread_local"):
+            self._project_kv(unet)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.out = unet(self.x, self.t, self.ctx)
+            with cross_kv_mode("consume" if self.HOIST else None, self.kv):
+                self.out = unet(self.x, self.t, self.ctx)
 
     def __call__(self, x, t, ctx):
         self.x.copy_(x)
         self.t.fill_(float(t))
-        if ctx.data_ptr() != self.ctx.data_ptr():
+        if ctx is not self._ctx_obj:
+            # a new context object = a new task / group (the reference is held, so identity
+            # cannot be recycled by the allocator while it is cached)
             self.ctx.copy_(ctx)
+            self.kv_graph.replay()
+            self._ctx_obj = ctx
         self.graph.replay()
         return self.out
 

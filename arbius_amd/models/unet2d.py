@@ -18,6 +18,7 @@ has none, inference lives in an external container):
 """
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
@@ -66,6 +67,28 @@ class SelfAttention(nn.Module):
         return self.to_out(o.reshape(B, N, C), residual=residual)
 
 
+# Cross-attention K/V hoisting: the text context is constant over a task's denoising steps, so
+# the graphed UNet computes every cross-attention K/V projection once per context (a separate
+# small hipGraph, "produce") and the per-step graph reads them ("consume").  Thread-local: the
+# modules are shared by the pipeline forks, each fork owns its K/V buffers.
+_KV = threading.local()
+
+
+class cross_kv_mode:
+    """``with cross_kv_mode("produce" | "consume", table): ...`` - see ``_KV`` above."""
+
+    def __init__(self, mode, table):
+        self.mode, self.table = mode, table
+
+    def __enter__(self):
+        self.prev = (getattr(_KV, "mode", None), getattr(_KV, "table", None))
+        _KV.mode, _KV.table = self.mode, self.table
+        return self
+
+    def __exit__(self, *exc):
+        _KV.mode, _KV.table = self.prev
+
+
 class CrossAttention(nn.Module):
     def __init__(self, dim, ctx_dim, heads):
         super().__init__()
@@ -74,11 +97,21 @@ class CrossAttention(nn.Module):
         self.to_kv = Linear(ctx_dim, 2 * dim, bias=False)
         self.to_out = Linear(dim, dim)
 
+    def context_kv(self, ctx):
+        return self.to_kv(ctx)
+
     def forward(self, x, ctx, residual):
         B, N, C = x.shape
         H = self.heads
         q = self.to_q(x).view(B, N, H, C // H)
-        kv = self.to_kv(ctx).view(B, ctx.shape[1], 2, H, C // H)
+        mode = getattr(_KV, "mode", None)
+        if mode == "consume":
+            kv = _KV.table[id(self)]
+        else:
+            kv = self.to_kv(ctx)
+            if mode == "produce":
+                _KV.table[id(self)] = kv
+        kv = kv.view(B, ctx.shape[1], 2, H, C // H)
         o = ops.attention(q, kv[:, :, 0], kv[:, :, 1])
         return self.to_out(o.reshape(B, N, C), residual=residual)
 
