@@ -14,7 +14,8 @@ from pathlib import Path
 import torch
 
 _HERE = Path(__file__).resolve().parent
-_LIB_PATH = _HERE / "libarbius_kernels.so"
+# ARBIUS_KERNEL_LIB: an alternative in-tree build (A/B runs of a kernel change)
+_LIB_PATH = _HERE / os.environ.get("ARBIUS_KERNEL_LIB", "libarbius_kernels.so")
 _lib = None
 _SYMBOLS = {}
 
