@@ -71,7 +71,8 @@ def build_pool(cfg, models):
     if n > 1:
         from .parallel.workers import MultiGPUSolverPool
         return MultiGPUSolverPool(n, names, "cuda", streams_per_gpu=cfg.mi355x.workers_per_gpu,
-                                  lockstep=cfg.mi355x.lockstep_group)
+                                  lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir,
+                                  hang_timeout=cfg.mi355x.hang_timeout_s)
     from .node.pool import LocalSolverPool
     return LocalSolverPool("cuda:0" if n == 1 else "cpu", capacity=cfg.mi355x.workers_per_gpu,
                            lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir)
@@ -112,7 +113,8 @@ async def _start(path: str):
         chain = _chain(cfg)
     log.debug("Loaded wallet (%s)", chain.address)
     ids = dict(getattr(cfg.mi355x, "model_ids", {}) or {})
-    models = {k: v for k, v in default_models(ids).items() if v.name in set(cfg.mi355x.models)}
+    models = {k: v for k, v in default_models(ids, int(cfg.mi355x.min_model_filter_fee)).items()
+              if v.name in set(cfg.mi355x.models)}
     pool = build_pool(cfg, models)
     miner = Miner(cfg, db, chain, make_pinner(cfg), pool, models)
     runner = await start_rpc(db, cfg.rpc.host, cfg.rpc.port, miner)

@@ -78,14 +78,17 @@ class IPFSConfig(_Base):
 class MI355XConfig(_Base):
     """Extension block (ignored by the reference miner)."""
     gpus: Optional[int] = None            # default: all visible
-    dtype: Literal["bf16", "fp16"] = "bf16"
     models: List[str] = Field(default_factory=lambda: ["kandinsky2"])  # enabled model names
     model_ids: Dict[str, str] = Field(default_factory=dict)  # template name -> on-chain model id
-    weights_dir: Optional[str] = None     # safetensors; None = random-init (benchmark only)
-    reference_hydration_quirks: bool = False  # mirror models.ts:185-194 quirks Q2/Q3
+    weights_dir: Optional[str] = None     # safetensors (+ tokenizer files); None = random-init (benchmark only)
+    hang_timeout_s: float = 300.0         # kill a GPU worker whose busy slot has not progressed this long
+    # models.ts:185-194 quirks Q2/Q3 (decimal must be integral, max never enforced).  ON by default:
+    # validity decides contestations, so this node must judge inputs as the deployed miners do
+    reference_hydration_quirks: bool = True
     job_lease_seconds: float = 900.0
     poll_interval_ms: int = 100           # index.ts:1081
-    min_model_filter_fee: str = "0"
+    log_window_blocks: int = 2000         # eth_getLogs back-fill window (halved on provider errors)
+    min_model_filter_fee: str = "0"      # MiningFilter.minfee of every enabled model (wei)
     verify_fraction: float = 0.0          # re-solve this fraction of others' solutions (Q10)
     chain_id: Optional[int] = None
     mock_chain: bool = False              # in-process MockEngine (testing / plumbing config)

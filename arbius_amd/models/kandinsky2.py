@@ -29,6 +29,7 @@ import torch.nn as nn
 
 from .. import ops
 from ..utils.png import encode_png
+from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .glide_unet import GlideUNet, GlideUNetConfig
 from .graphs import GraphCache, PipelineBase
@@ -131,6 +132,7 @@ class Kandinsky2Pipeline(PipelineBase):
         sched = GaussianDiffusion(steps, schedule="cosine", predict="x0", learned_var=False)
         x = torch.randn((1, d), generator=gen, dtype=torch.float32).to(self.device)
         for i, t in enumerate(sched.timesteps):
+            beat()
             xin = x.to(self.dtype)
             c = self.prior(xin, t, hidden[0:1], pooled[0:1], lens[0]).float()
             u = self.prior(xin, t, hidden[1:2], pooled[1:2], lens[1]).float()
@@ -166,6 +168,7 @@ class Kandinsky2Pipeline(PipelineBase):
         sched = GaussianDiffusion(steps, schedule="linear", predict="eps", learned_var=True, clamp=cfg.latent_clamp)
         tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
         for i, t in enumerate(sched.timesteps):
+            beat()
             xin = x.to(self.dtype)
             tbuf.fill_(float(t))
             with ops.plan_batch(2):      # batch-invariant plans: solo == lock-step group bytes
@@ -216,6 +219,7 @@ class Kandinsky2Pipeline(PipelineBase):
             tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
             g = cfg.guidance_scale
             for i, t in enumerate(scheds[0].timesteps):
+                beat()
                 xin = [x.to(self.dtype) for x in xs]
                 tbuf.fill_(float(t))
                 with ops.plan_batch(2):

@@ -16,6 +16,11 @@ def _load(pipe, name: str, weights_dir: Optional[str]):
 
 def build_pipeline(name: str, device="cpu", tiny: bool = False, weights_dir: Optional[str] = None,
                    weight_seed: int = 0, **kw):
+    """``tokenizer_dir`` defaults to ``weights_dir``: tokenizer files are auto-discovered there
+    (models/tokenizer.py ``TOKENIZER_SUBDIRS``), so real weights always run with their real
+    tokenizers."""
+    if kw.get("tokenizer_dir") is None and weights_dir:
+        kw["tokenizer_dir"] = weights_dir
     if name == "anythingv3":
         from .sd15 import SD15Config, SD15Pipeline
         cfg = SD15Config.tiny() if tiny else SD15Config()

@@ -29,6 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..utils.progress import beat
 
 CL = torch.channels_last
 GREEN = (120 / 255, 255 / 255, 155 / 255)     # RVM's green-screen background
@@ -335,6 +336,7 @@ class RVMPipeline:
         out = []
         green = torch.tensor(GREEN, dtype=self.dtype, device=self.device).view(1, 3, 1, 1)
         for i in range(0, T, self.cfg.chunk):
+            beat()
             chunk = torch.from_numpy(np.ascontiguousarray(frames[i:i + self.cfg.chunk])).to(self.device)
             src = (chunk.permute(0, 3, 1, 2).to(self.dtype) / 255.0)[None]     # [1, t, 3, H, W]
             fgr, pha, rec = self.net(src, rec, ratio)

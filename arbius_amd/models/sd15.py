@@ -24,6 +24,7 @@ import torch
 
 from .. import ops
 from ..utils.trace import span
+from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .graphs import CAPTURE_LOCK, PipelineBase
 from .layers import init_weights
@@ -177,6 +178,7 @@ class SD15Pipeline(PipelineBase):
             x = (x * sched.init_noise_sigma).to(self.device)
         with span("denoise_s", tm, sync):
             for i, t in enumerate(sched.timesteps):
+                beat()
                 xin = sched.scale_model_input(x, i).to(self.dtype)
                 eps2 = self._unet_eval(torch.cat([xin, xin]), t, ctx)
                 eps = ops.ref.cfg_combine(eps2, guidance_scale)
@@ -215,6 +217,7 @@ class SD15Pipeline(PipelineBase):
                 gs = [float(inp.get("guidance_scale", 12)) for inp in inps]
             with span("denoise_s", tm, sync):
                 for i, t in enumerate(scheds[0].timesteps):
+                    beat()
                     xin = [s.scale_model_input(x, i).to(self.dtype) for s, x in zip(scheds, xs)]
                     eps_all = self._unet_eval(torch.cat([v for x in xin for v in (x, x)]), t, ctx)
                     for k, (s, g) in enumerate(zip(scheds, gs)):

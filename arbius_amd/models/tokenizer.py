@@ -17,14 +17,36 @@ BOS, EOS, VOCAB, MAX_LEN = 49406, 49407, 49408, 77
 _WORD = re.compile(r"[a-z]+|[0-9]|[^\sa-z0-9]+")
 
 
+# where checkpoint directories keep their tokenizer files: the root, the diffusers ``tokenizer/``
+# folder, or a per-tower folder of a multi-encoder pipeline (Kandinsky 2: CLIP + XLM-R)
+TOKENIZER_SUBDIRS = ("", "tokenizer", "clip_tokenizer", "tokenizer_clip", "text_encoder")
+
+
+def find_file(root: Optional[str], name: str, subdirs=TOKENIZER_SUBDIRS) -> Optional[Path]:
+    """First ``root/<subdir>/name`` that exists (tokenizer auto-discovery from a weights dir)."""
+    if not root:
+        return None
+    for sub in subdirs:
+        f = Path(root) / sub / name
+        if f.is_file():
+            return f
+    return None
+
+
 class CLIPTokenizer:
+    """``vocab_dir``: a directory holding ``vocab.json`` + ``merges.txt`` directly or in one of
+    ``TOKENIZER_SUBDIRS`` (so a pipeline can be handed its weights dir)."""
+
     def __init__(self, vocab_dir: Optional[str] = None, max_len: int = MAX_LEN, vocab: int = VOCAB):
         self.max_len = max_len
         self.vocab = vocab
         self._bpe = None
-        if vocab_dir and (Path(vocab_dir) / "vocab.json").exists():
+        self.source = "hashed-words"
+        vj = find_file(vocab_dir, "vocab.json")
+        if vj is not None and (vj.parent / "merges.txt").is_file():
             from transformers import CLIPTokenizer as HFTok  # offline, local files only
-            self._bpe = HFTok(str(Path(vocab_dir) / "vocab.json"), str(Path(vocab_dir) / "merges.txt"))
+            self._bpe = HFTok(str(vj), str(vj.parent / "merges.txt"))
+            self.source = str(vj.parent)
 
     def _hash_ids(self, text: str) -> List[int]:
         ids = []

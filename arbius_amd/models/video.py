@@ -21,6 +21,7 @@ from typing import Dict, Optional
 import torch
 
 from ..utils.mp4 import encode_mp4
+from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .graphs import GraphCache, PipelineBase
 from .layers import init_weights
@@ -127,6 +128,7 @@ class VideoPipeline(PipelineBase):
         sync()
         t1 = time.perf_counter()
         for i, t in enumerate(sched.timesteps):
+            beat()
             xin = sched.scale_model_input(x, i).to(self.dtype)
             tbuf.fill_(float(t))
             out = unet(torch.cat([xin, xin]), tbuf, ctx)
@@ -145,6 +147,7 @@ class VideoPipeline(PipelineBase):
         z = (latent / self.cfg.vae.scaling_factor).to(self.dtype)
         out = []
         for i in range(0, z.shape[0], self.cfg.vae_chunk):
+            beat()
             img = self.vae(z[i:i + self.cfg.vae_chunk]).float()
             out.append(((img / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8).cpu())
         return torch.cat(out).numpy()                             # [F, H, W, 3]

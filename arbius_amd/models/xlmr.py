@@ -57,9 +57,14 @@ class XLMRTokenizer:
     def __init__(self, vocab: int, max_len: int = 77, model_dir: Optional[str] = None):
         self.vocab, self.max_len = vocab, max_len
         self._sp = None
-        if model_dir and (Path(model_dir) / "sentencepiece.bpe.model").exists():
+        self.source = "hashed-words"
+        from .tokenizer import find_file
+        f = find_file(model_dir, "sentencepiece.bpe.model",
+                      ("", "xlmr_tokenizer", "tokenizer_xlmr", "mclip_tokenizer", "tokenizer", "text_encoder"))
+        if f is not None:
             import sentencepiece as spm
-            self._sp = spm.SentencePieceProcessor(model_file=str(Path(model_dir) / "sentencepiece.bpe.model"))
+            self._sp = spm.SentencePieceProcessor(model_file=str(f))
+            self.source = str(f.parent)
 
     def __call__(self, text: str) -> Tuple[List[int], int]:
         if self._sp is not None:

@@ -30,7 +30,7 @@ from ..ipfs.pin import Pinner
 from ..ipfs.unixfs import cid_hex_to_str
 from ..store.db import DB
 from ..utils.protocol import expretry, generate_commitment, taskid2seed
-from .models import Model, check_model_filter, get_model_by_id, hydrate_input
+from .models import Model, check_model_filter, get_model_by_id, hydrate_input, hydration_modes_agree
 from .solver import EVIL_CID
 
 log = logging.getLogger("arbius.miner")
@@ -74,11 +74,13 @@ class Miner:
         self.sleep = sleep or asyncio.sleep
         self.retry_sleep = retry_sleep or asyncio.sleep
         self.metrics = Metrics()
-        self.quirks = bool(getattr(cfg.mi355x, "reference_hydration_quirks", False))
+        self.quirks = bool(getattr(cfg.mi355x, "reference_hydration_quirks", True))
         self.lease_s = float(getattr(cfg.mi355x, "job_lease_seconds", 900.0))
         self.poll_s = float(getattr(cfg.mi355x, "poll_interval_ms", 100)) / 1000.0
+        self.log_window = max(1, int(getattr(cfg.mi355x, "log_window_blocks", 2000)))
         self._bg: set = set()
         self._running_solves: Dict[int, asyncio.Task] = {}
+        self._inflight: set = set()          # job ids leased and running in this process
         self.stopped = False
 
     # ------------------------------------------------------------------ helpers
@@ -127,6 +129,12 @@ class Miner:
         except Exception:  # noqa: BLE001
             log.warning("Task (%s) request was unable to be parsed", taskid)
             self.db.store_invalid_task(taskid)
+            return None
+        if not hydration_modes_agree(pre, template):
+            # spec-correct and reference hydration disagree: whatever we decide, part of the
+            # network decides otherwise -> stay out (no solve, no invalid mark, no contest)
+            log.warning("Task (%s) input validity is ambiguous (spec vs reference hydration): skipped", taskid)
+            self.metrics.inc("tasks_ambiguous_input")
             return None
         inp, err, msg = hydrate_input(pre, template, self.quirks)
         if err:
@@ -177,22 +185,35 @@ class Miner:
             await self.version_check()
 
     async def poll_events(self):
+        """Back-fill ``eth_getLogs`` from the persisted cursor in bounded windows (providers cap the
+        block range / result size of one call; after downtime on Nova the gap is large).  The
+        cursor is persisted after every window; a failing window is halved until it passes."""
         latest = await self.chain.block_number()
         cur = self.db.get_cursor()
-        start = latest if cur is None else cur + 1  # first boot: only new events (reference .on semantics)
-        if cur is None:
+        if cur is None:      # first boot: only new events (reference .on semantics)
             self.db.set_cursor(latest)
             return 0
-        if start > latest:
-            return 0
-        evs = await self.chain.get_events(start, latest)
-        for ev in evs:
+        start = cur + 1
+        n = 0
+        while start <= latest:
+            end = min(latest, start + self.log_window - 1)
             try:
-                await self.on_event(ev)
+                evs = await self.chain.get_events(start, end)
             except Exception as e:  # noqa: BLE001
-                log.error("event handler %s failed: %r", ev.name, e)
-        self.db.set_cursor(latest)
-        return len(evs)
+                if self.log_window <= 1:
+                    raise
+                self.log_window = max(1, self.log_window // 2)
+                log.warning("eth_getLogs %d..%d failed (%r): window -> %d blocks", start, end, e, self.log_window)
+                continue
+            for ev in evs:
+                try:
+                    await self.on_event(ev)
+                except Exception as e:  # noqa: BLE001
+                    log.error("event handler %s failed: %r", ev.name, e)
+            self.db.set_cursor(end)
+            n += len(evs)
+            start = end + 1
+        return n
 
     # ------------------------------------------------------------------ processors (index.ts:379-750)
     async def process_pin_task_input(self, taskid, input_str):
@@ -480,7 +501,15 @@ class Miner:
             return self.process_contestation_vote_finish(data["taskid"])
         raise SystemExit(f"method ({method}) has no implementation")  # index.ts:914-916
 
+    async def _renew(self, jobid):
+        """Lease heartbeat: a job that outlives ``job_lease_seconds`` (a long solve) must not be
+        leased and run a second time."""
+        while True:
+            await asyncio.sleep(max(0.05, self.lease_s / 3.0))
+            self.db.renew_lease(jobid, self.lease_s)
+
     async def _run_job(self, job):
+        hb = asyncio.ensure_future(self._renew(job["id"]))
         try:
             await self._dispatch(job["method"], json.loads(job["data"]))
             self.metrics.inc(f"jobs_ok_{job['method']}")
@@ -491,16 +520,21 @@ class Miner:
             self.db.store_failed_job(job)
             self.metrics.inc(f"jobs_failed_{job['method']}")
         finally:
+            hb.cancel()
             self.db.delete_job(job["id"])
+            self._inflight.discard(job["id"])
 
     async def process_jobs(self) -> int:
         """One scheduler pass: concurrent jobs fire-and-forget, solves fill the GPU
         pool, other blocking jobs run in priority order."""
-        jobs = self.db.runnable_jobs(self.now())
+        # jobs already running in this process are skipped even if their lease lapsed (they renew
+        # it, but a stalled event loop could still let one expire)
+        jobs = [j for j in self.db.runnable_jobs(self.now()) if j["id"] not in self._inflight]
         n = 0
         for job in jobs:
             if job["concurrent"]:
                 if self.db.lease_job(job["id"], "node", self.lease_s):
+                    self._inflight.add(job["id"])
                     self._spawn(self._run_job(job))
                     n += 1
         for job in jobs:
@@ -510,12 +544,14 @@ class Miner:
                 if len(self._running_solves) >= max(1, getattr(self.pool, "capacity", 1)):
                     continue
                 if self.db.lease_job(job["id"], "gpu", self.lease_s):
+                    self._inflight.add(job["id"])
                     t = self._spawn(self._run_job(job))
                     self._running_solves[job["id"]] = t
                     t.add_done_callback(lambda _t, jid=job["id"]: self._running_solves.pop(jid, None))
                     n += 1
                 continue
             if self.db.lease_job(job["id"], "node", self.lease_s):
+                self._inflight.add(job["id"])
                 await self._run_job(job)
                 n += 1
         return n

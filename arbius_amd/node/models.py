@@ -7,7 +7,9 @@ reference defects made opt-in:
 * Q2 (``models.ts:185-189``): ``decimal`` rejected non-integral numbers;
 * Q3 (``models.ts:194``): the ``max`` bound was never enforced.
 
-Default is spec-correct; ``quirks=True`` reproduces the reference exactly.
+``hydrate_input``'s own default is spec-correct; the node runs with ``quirks=True`` (config
+``reference_hydration_quirks``, default on) so it judges inputs exactly as deployed miners do, and
+never contests or solves a task on which the two modes disagree (``hydration_modes_agree``).
 """
 from __future__ import annotations
 
@@ -63,9 +65,10 @@ class Model:
     kind: str = "image"   # image | video | matting
 
 
-def default_models(ids: Optional[Dict[str, str]] = None) -> Dict[str, Model]:
+def default_models(ids: Optional[Dict[str, str]] = None, minfee: int = 0) -> Dict[str, Model]:
     """Known templates.  Only kandinsky2 has a mainnet id (miner/src/config.json:7-16);
-    others get ids from config / registration (``ids`` name -> id)."""
+    others get ids from config / registration (``ids`` name -> id).  ``minfee``: the
+    ``MiningFilter.minfee`` of every model (index.ts:846-851 hard-codes 0)."""
     ids = dict(ids or {})
     ids.setdefault("kandinsky2", KANDINSKY2_ID)
     kinds = {"anythingv3": "image", "kandinsky2": "image", "zeroscopev2xl": "video", "damo": "video",
@@ -75,7 +78,8 @@ def default_models(ids: Optional[Dict[str, str]] = None) -> Dict[str, Model]:
         mid = ids.get(name)
         if mid is None:
             continue
-        out[mid.lower()] = Model(mid.lower(), name, load_template(name), True, [MiningFilter()], kind)
+        out[mid.lower()] = Model(mid.lower(), name, load_template(name), True, [MiningFilter(minfee=int(minfee))],
+                                 kind)
     return out
 
 
@@ -153,3 +157,12 @@ def hydrate_input(pre: Any, template: dict, quirks: bool = False) -> Tuple[Optio
         else:
             inp[var] = row.get("default")
     return inp, False, ""
+
+
+def hydration_modes_agree(pre: Any, template: dict) -> bool:
+    """True when spec-correct and reference-quirk hydration reach the same verdict (valid or not).
+    A task on which they disagree is neither solved nor marked invalid: contesting it, or voting on
+    its contestation, could put this node on the slashed minority side."""
+    _, e1, _ = hydrate_input(pre, template, False)
+    _, e2, _ = hydrate_input(pre, template, True)
+    return e1 == e2

@@ -46,6 +46,16 @@ def is_dist():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def backend_name() -> str:
+    """'nccl' (= RCCL on ROCm), 'gloo', or 'none' at world size 1."""
+    return str(dist.get_backend()) if is_dist() else "none"
+
+
+def shutdown():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def barrier(dev=None):
     if is_dist():
         if dev is not None and dev.type == "cuda":

@@ -12,7 +12,13 @@
 * a worker that dies (HIP fault, OOM, kill) is detected by the watchdog, its in-flight
   task fails over to the caller's retry (another worker), and the worker is respawned
   standalone (deterministic init / safetensors load instead of the broken group) -
-  elastic N -> N-1 -> N.
+  elastic N -> N-1 -> N;
+* a worker that HANGS (a HIP kernel that never finishes blocks its host thread) is found by
+  heartbeats: every busy task slot stamps a shared-memory clock at each denoising step
+  (``utils.progress.beat``); a slot silent for ``hang_timeout`` seconds gets its process killed,
+  and the death path above takes over;
+* with ``weights_dir`` rank 0 reads the safetensors and broadcasts them; a respawned worker
+  reads the same files (byte-identical weights, so the same CIDs as its peers).
 * every worker has its OWN request and result queue: a process killed in the middle of
   a queue operation can leave that queue's lock held or a truncated message in its
   pipe, so both queues are replaced on respawn and no other worker's traffic shares them.
@@ -43,7 +49,8 @@ def _free_port() -> int:
 
 
 def _worker_main(rank: int, world: int, port: int, device_type: str, models: List[str], tiny: bool,
-                 in_q, out_q, group: bool, weight_seed: int, streams: int = 1, lockstep: int = 1):
+                 in_q, out_q, group: bool, weight_seed: int, streams: int = 1, lockstep: int = 1,
+                 weights_dir: Optional[str] = None, beats=None):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import queue as _queue
     import threading
@@ -69,19 +76,27 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
             dist.init_process_group(backend, rank=rank, world_size=world, **kw)
         pipes = {}
         bstats = {"bytes": 0, "seconds": 0.0}
+        from ..utils import progress
+        if beats is not None:
+            progress.set_hook(progress.shared_stamp_hook(beats, rank * streams))
+        src = (not group) or world == 1 or rank == 0     # this process materialises the weights
         for name in models:
             pipe = build_pipeline(name, device=dev, tiny=tiny, weight_seed=weight_seed,
-                                  init=(not group) or rank == 0)
+                                  init=src and not weights_dir, weights_dir=weights_dir if src else None,
+                                  tokenizer_dir=weights_dir)
             if group and world > 1:
                 st = D.broadcast_modules(pipe.modules().values())
                 bstats["bytes"] += st["bytes"]
                 bstats["seconds"] += st["seconds"]
+                if hasattr(pipe, "_reset_graphs"):
+                    pipe._reset_graphs()
             pipes[name] = pipe
         # `streams` task slots: slot k solves on its own pipeline forks (private HIP stream + graphs)
         slots = [{n: (p if streams == 1 else p.fork()) for n, p in pipes.items()} for _ in range(streams)]
         jobs: "_queue.Queue" = _queue.Queue()
 
         def slot_loop(k):
+            progress.set_slot(k)
             while True:
                 msg = jobs.get()
                 if msg is None:
@@ -89,7 +104,11 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 # lock-step group: queued compatible image tasks share one batch (same bytes as solo)
                 batch = take_group(jobs, msg, lockstep, lambda m: m[2], lambda m: m[5], lambda m: m[1])
                 jid, mname, kind, mid, taskid, inp = msg
+                progress.beat()                     # busy from now on (0 = idle)
                 try:
+                    if inp.get("__fault__") == "hang" and os.environ.get("ARBIUS_FAULT_INJECTION") == "1":
+                        while True:                 # test hook: a hung kernel - no beats, no result
+                            time.sleep(1.0)
                     t0 = time.perf_counter()
                     if len(batch) == 1:
                         sols = [solve_task(Model(mid, mname, {}, True, [], kind), slots[k][mname], inp)]
@@ -102,6 +121,9 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 except Exception:  # noqa: BLE001
                     for m in batch:
                         out_q.put(("err", m[0], rank, traceback.format_exc()))
+                finally:
+                    if beats is not None:
+                        beats[rank * streams + k] = 0.0
 
         threads = [threading.Thread(target=slot_loop, args=(k,), daemon=True) for k in range(streams)]
         for t in threads:
@@ -127,17 +149,23 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
 class MultiGPUSolverPool:
     def __init__(self, n: int, models: List[str], device_type: str = "cuda", tiny: bool = False,
                  weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1,
-                 lockstep: int = 1):
+                 lockstep: int = 1, weights_dir: Optional[str] = None, hang_timeout: float = 300.0):
         self.n = n
         self.models = models
         self.device_type = device_type
         self.tiny = tiny
         self.weight_seed = weight_seed
+        self.weights_dir = weights_dir
+        self.hang_timeout = float(hang_timeout)
         self.ctx = mp.get_context("spawn")
+        self.hangs = 0
         self.in_qs = [self.ctx.Queue() for _ in range(n)]
         self.out_qs = [self.ctx.Queue() for _ in range(n)]
         self.procs: List[Optional[mp.Process]] = [None] * n
         self.streams = max(1, int(streams_per_gpu))
+        # per task slot: time of its last progress beat, 0.0 while idle (shared memory, no lock:
+        # one writer per slot, the watchdog only reads)
+        self.beats = self.ctx.Array("d", n * self.streams, lock=False)
         # tasks per lock-step group on one stream (HIP kernels only: batch-invariant launches)
         self.lockstep = max(1, int(lockstep)) if device_type == "cuda" else 1
         self.busy: Dict[int, int] = {}           # job id -> rank
@@ -175,17 +203,21 @@ class MultiGPUSolverPool:
         return hardware_id("cuda:0" if self.device_type == "cuda" else "cpu")
 
     def weights_id(self) -> str:
-        return f"random-init-seed{self.weight_seed}" + ("-tiny" if self.tiny else "")
+        base = (f"safetensors:{os.path.basename(os.path.normpath(self.weights_dir))}" if self.weights_dir
+                else f"random-init-seed{self.weight_seed}")
+        return base + ("-tiny" if self.tiny else "")
 
     @property
     def capacity(self) -> int:
         return self.streams * self.lockstep * sum(1 for p in self.procs if p is not None and p.is_alive())
 
     def _spawn(self, rank, port, group):
+        for k in range(self.streams):
+            self.beats[rank * self.streams + k] = 0.0
         p = self.ctx.Process(target=_worker_main, daemon=True,
                              args=(rank, self.n, port, self.device_type, self.models, self.tiny,
                                    self.in_qs[rank], self.out_qs[rank], group, self.weight_seed, self.streams,
-                                   self.lockstep))
+                                   self.lockstep, self.weights_dir, self.beats))
         p.start()
         self.procs[rank] = p
 
@@ -228,7 +260,24 @@ class MultiGPUSolverPool:
                 self._watchdog()
                 await asyncio.sleep(0.005)
 
+    def hung_ranks(self, now: Optional[float] = None) -> List[int]:
+        """Workers with a busy task slot that has not beaten for ``hang_timeout`` seconds."""
+        now = time.time() if now is None else now
+        out = []
+        for r in range(self.n):
+            stamps = [self.beats[r * self.streams + k] for k in range(self.streams)]
+            if any(t > 0.0 and now - t > self.hang_timeout for t in stamps):
+                out.append(r)
+        return out
+
     def _watchdog(self):
+        for r in self.hung_ranks():
+            p = self.procs[r]
+            if p is not None and p.is_alive():
+                log.error("GPU worker %d hung (no progress beat for %.0f s): killing it", r, self.hang_timeout)
+                self.hangs += 1
+                p.kill()
+                p.join(30)
         for r, p in enumerate(self.procs):
             if p is not None and not p.is_alive():
                 log.error("GPU worker %d died (exit %s): failing its tasks over, respawning", r, p.exitcode)

@@ -2,33 +2,36 @@
 """Headline benchmark: tasks solved / hour (whole node) + p50 task latency,
 anythingv3 (SD1.5 architecture) 512x512, 50 denoising steps (BASELINE.json).
 
-One "step" = every rank solves ONE complete task end to end: CLIP text encode,
+One "step" = every rank solves its task slots end to end: CLIP text encode,
 50 CFG (batch 2) UNet evaluations + sampler, VAE decode, deterministic PNG
 encode, wrapped-directory CIDv0 and the solution commitment.  Synthetic
-prompts, random-init weights of the real architecture (no checkpoints offline).
+prompts, random-init weights of the real architecture (no checkpoints offline;
+``--weights-dir`` loads real safetensors on rank 0 instead).
 
-N GPUs = N independent task workers (task-level data parallel, weak scaling);
-rank 0 initialises the weights and RCCL-broadcasts them over xGMI (outside the
-timed region, reported separately).
+N GPUs = N independent task workers, one process per GPU (task-level data
+parallel, weak scaling).  Rank 0 materialises the weights (random init or
+safetensors) and RCCL-broadcasts them over xGMI to every other rank (outside the
+timed region, reported as ``weight_broadcast``).  There are no per-step
+collectives; the timed region is bracketed by a barrier + device sync on both
+sides and ms/step is the MAX over ranks.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  python bench.py [--gpus N] [--steps K] [--warmup W]      # N > 1: spawns N rank processes
+  torchrun --nproc-per-node N bench.py --gpus N ...         # one rank per process (driver path)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import statistics
 import sys
 import time
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -48,11 +51,12 @@ def main():
     ap.add_argument("--denoise-steps", type=int, default=None, help="default 50 / 100")
     ap.add_argument("--scheduler", default="DPMSolverMultistep")
     ap.add_argument("--guidance", type=float, default=12.0)
+    ap.add_argument("--weights-dir", default=None, help="safetensors dir (rank 0 loads, RCCL-broadcast)")
     ap.add_argument("--reference-ops", action="store_true", help="A/B: PyTorch ops instead of HIP kernels")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--tiny", action="store_true", help="tiny config (CPU plumbing check only)")
-    ap.add_argument("--device", default=None)
-    args = ap.parse_args()
+    ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu (gloo ranks)")
+    args = ap.parse_args(argv)
     k2 = args.model == "kandinsky2"
     vid = args.model in ("zeroscopev2xl", "damo")
     rvm = args.model == "robust_video_matting"
@@ -61,24 +65,50 @@ def main():
                             1920 if rvm else 512)
     args.height = 320 if args.model == "zeroscopev2xl" else 1080 if rvm else args.res
     args.denoise_steps = args.denoise_steps or (100 if k2 else 50)
+    return args
+
+
+def _device_type(args) -> str:
+    """cuda / cpu WITHOUT initialising HIP (device_count does not; is_available may)."""
+    if args.device:
+        return "cuda" if args.device.startswith("cuda") else "cpu"
+    import torch
+    return "cuda" if torch.cuda.device_count() > 0 else "cpu"
+
+
+def run(args):
+    import torch
 
     from arbius_amd import ops
     from arbius_amd.models.registry import build_pipeline
     from arbius_amd.node.solver import solve_image
     from arbius_amd.parallel import dist as D
-    from arbius_amd.utils.protocol import generate_commitment, taskid2seed
     from arbius_amd.utils.keccak import keccak256
+    from arbius_amd.utils.protocol import generate_commitment, taskid2seed
 
+    k2 = args.model == "kandinsky2"
+    vid = args.model in ("zeroscopev2xl", "damo")
+    rvm = args.model == "robust_video_matting"
     if args.reference_ops:
         ops.set_reference_ops(True)
-    dev_type = "cuda" if (args.device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda") else "cpu"
-    rank, local, world, dev = D.init(device_type=dev_type)
+    rank, local, world, dev = D.init(device_type=_device_type(args))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the process group has {world} ranks")
+    if world > 1:
+        # N ranks share the host: keep each rank's CPU-side work (tokenizer, noise, PNG) off the
+        # other ranks' cores
+        torch.set_num_threads(max(1, min(torch.get_num_threads(), 4)))
     n = world
 
     t_init = time.perf_counter()
-    pipe = build_pipeline(args.model, device=dev, tiny=args.tiny, init=(rank == 0),
+    src = rank == 0
+    pipe = build_pipeline(args.model, device=dev, tiny=args.tiny, init=src and not args.weights_dir,
+                          weights_dir=args.weights_dir if src else None,
+                          tokenizer_dir=args.weights_dir,
                           use_graphs=(dev.type == "cuda" and not args.no_graphs))
     bstats = D.broadcast_modules(pipe.modules().values())
+    if hasattr(pipe, "_reset_graphs"):
+        pipe._reset_graphs()
     t_init = time.perf_counter() - t_init
 
     wallet = "0x" + "11" * 20
@@ -94,90 +124,55 @@ def main():
         clip = np.stack([base, (yy[None] % 256).astype(np.uint8).repeat(args.frames, 0),
                          rng.integers(0, 256, base.shape, dtype=np.uint8)], axis=-1)
 
+    def tid_of(i, j=None):
+        return "0x" + keccak256((f"bench-task-{rank}-{i}" + ("" if j is None else f"-{j}")).encode()).hex()
+
     def one_task(i, pipe=pipe):
-        taskid = "0x" + keccak256(f"bench-task-{rank}-{i}".encode()).hex()
+        """Solve this slot's task(s) of step i; every solution gets its own task id's commitment."""
+        t0 = time.perf_counter()
         if rvm:
             from arbius_amd.node.solver import solve_files
             from arbius_amd.utils.mp4 import encode_mp4
-            t0 = time.perf_counter()
             out = pipe(clip, "green-screen")
             t1 = time.perf_counter()
             tm = dict(pipe.timings)
             tm.update({"infer_s": t1 - t0})
             sol = solve_files([("out-1.mp4", encode_mp4(list(out), 24))], tm)
             sol.timings["encode_cid_s"] = time.perf_counter() - t1
-            generate_commitment(wallet, taskid, sol.cid)
-            lat.append(time.perf_counter() - t0)
-            return sol
-        if vid:  # BASELINE config #4: 576x320x24f text-to-video
+            done = [(tid_of(i), sol)]
+        elif vid:  # BASELINE config #4: 576x320x24f text-to-video
             inp = {"prompt": f"a red cat walking on a castle wall, cinematic, task {i}", "num_frames": args.frames,
                    "width": args.res, "height": args.height, "num_inference_steps": args.denoise_steps,
-                   "seed": taskid2seed(taskid), "fps": 24}
-            t0 = time.perf_counter()
-            sol = pipe.solve(inp)
-            generate_commitment(wallet, taskid, sol.cid)
-            lat.append(time.perf_counter() - t0)
-            return sol
-        if k2 and args.group > 1:
+                   "seed": taskid2seed(tid_of(i)), "fps": 24}
+            done = [(tid_of(i), pipe.solve(inp))]
+        elif k2:   # templates/kandinsky2.json inputs; hidden defaults 100 steps, guidance 4, prior 5 steps
             from arbius_amd.node.solver import solve_images
             pipe.cfg.num_steps = args.denoise_steps
-            inps = []
-            for j in range(args.group):
-                tid = "0x" + keccak256(f"bench-task-{rank}-{i}-{j}".encode()).hex()
-                inps.append({"prompt": f"a red cat sitting on a castle wall, oil painting, task {i}.{j}",
-                             "width": args.res, "height": args.res, "seed": taskid2seed(tid)})
-            t0 = time.perf_counter()
-            sols = solve_images(pipe, inps)
-            for sol in sols:
-                generate_commitment(wallet, taskid, sol.cid)
-            lat.extend([time.perf_counter() - t0] * len(sols))
-            return sols[-1]
-        if k2:   # templates/kandinsky2.json inputs; hidden defaults 100 steps, guidance 4, prior 5 steps
-            pipe.cfg.num_steps = args.denoise_steps
-            inp = {"prompt": f"a red cat sitting on a castle wall, oil painting, task {i}",
-                   "width": args.res, "height": args.res, "seed": taskid2seed(taskid)}
-            t0 = time.perf_counter()
-            sol = pipe.solve(inp)
-            generate_commitment(wallet, taskid, sol.cid)
-            lat.append(time.perf_counter() - t0)
-            return sol
-        if args.group > 1:
+            tids = [tid_of(i, j) for j in range(max(1, args.group))]
+            inps = [{"prompt": f"a red cat sitting on a castle wall, oil painting, task {i}.{j}",
+                     "width": args.res, "height": args.res, "seed": taskid2seed(t)} for j, t in enumerate(tids)]
+            done = list(zip(tids, solve_images(pipe, inps) if len(inps) > 1 else [pipe.solve(inps[0])]))
+        else:
             from arbius_amd.node.solver import solve_images
-            inps = []
-            for j in range(args.group):
-                tid = "0x" + keccak256(f"bench-task-{rank}-{i}-{j}".encode()).hex()
-                inps.append({"prompt": f"a detailed anime illustration of a castle on a hill, task {i}.{j}",
-                             "negative_prompt": "lowres, bad anatomy, bad hands, text, error",
-                             "width": args.res, "height": args.res, "num_inference_steps": args.denoise_steps,
-                             "guidance_scale": args.guidance, "scheduler": args.scheduler,
-                             "seed": taskid2seed(tid)})
-            t0 = time.perf_counter()
-            sols = solve_images(pipe, inps)
-            for j, sol in enumerate(sols):
-                generate_commitment(wallet, taskid, sol.cid)
-            dt = time.perf_counter() - t0
-            lat.extend([dt] * len(sols))
-            return sols[-1]
-        inp = {
-            "prompt": f"a detailed anime illustration of a castle on a hill, task {i}",
-            "negative_prompt": "lowres, bad anatomy, bad hands, text, error",
-            "width": args.res, "height": args.res,
-            "num_inference_steps": args.denoise_steps,
-            "guidance_scale": args.guidance,
-            "scheduler": args.scheduler,
-            "seed": taskid2seed(taskid),
-        }
-        t0 = time.perf_counter()
-        sol = solve_image(pipe, inp)
-        generate_commitment(wallet, taskid, sol.cid)
-        lat.append(time.perf_counter() - t0)
-        return sol
+            tids = [tid_of(i, j) for j in range(max(1, args.group))]
+            inps = [{"prompt": f"a detailed anime illustration of a castle on a hill, task {i}.{j}",
+                     "negative_prompt": "lowres, bad anatomy, bad hands, text, error",
+                     "width": args.res, "height": args.res, "num_inference_steps": args.denoise_steps,
+                     "guidance_scale": args.guidance, "scheduler": args.scheduler,
+                     "seed": taskid2seed(t)} for j, t in enumerate(tids)]
+            sols = solve_images(pipe, inps) if len(inps) > 1 else [solve_image(pipe, inps[0])]
+            done = list(zip(tids, sols))
+        for tid, sol in done:
+            generate_commitment(wallet, tid, sol.cid)
+        dt = time.perf_counter() - t0
+        lat.extend([dt] * len(done))
+        return done[-1][1]
 
     from concurrent.futures import ThreadPoolExecutor
     ex = ThreadPoolExecutor(C) if C > 1 else None
 
     def one_step(i):
-        """One bench step = C tasks, concurrently on C pipeline forks (C = 1: one task)."""
+        """One bench step = C task slots, concurrently on C pipeline forks (C = 1: one slot)."""
         if ex is None:
             return one_task(i)
         futs = [ex.submit(one_task, i * C + j, forks[j]) for j in range(C)]
@@ -200,14 +195,17 @@ def main():
     sync()
     D.barrier(dev)
     elapsed = time.perf_counter() - t0
-    ms_per_step = D.max_over_ranks(elapsed * 1000.0 / args.steps, dev)
+    my_ms = elapsed * 1000.0 / args.steps
+    ms_per_step = D.max_over_ranks(my_ms, dev)
     all_lat = D.all_gather_floats(lat, dev)
+    per_rank = D.all_gather_floats([my_ms, float(len(lat)), float(bstats["bytes"])], dev)
     flat = sorted(x for r in all_lat for x in r)
     p50 = statistics.median(flat) * 1000.0 if flat else float("nan")
 
     if rank == 0:
-        G = args.group if not (vid or rvm) else 1
-        tasks_per_hour = n * C * G * 3600.0 * 1000.0 / ms_per_step
+        G = max(1, args.group) if not (vid or rvm) else 1
+        per_gpu_tasks = C * G
+        tasks_per_hour = n * per_gpu_tasks * 3600.0 * 1000.0 / ms_per_step
         out = {
             "metric": "tasks_solved_per_hour",
             "value": round(tasks_per_hour, 2),
@@ -220,17 +218,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": ("fp16" if rvm else "bf16") if dev.type == "cuda" else "fp32",
-            "data": ("synthetic 1080p clip, random-init weights (RVM MobileNetV3 architecture)" if rvm else
-                     "synthetic prompts, random-init weights (%s architecture)" % (
-                         "Kandinsky 2.1" if k2 else "UNet3D text-to-video" if vid else "SD1.5")),
+            "data": ("synthetic 1080p clip, " if rvm else "synthetic prompts, ") + (
+                f"safetensors weights ({os.path.basename(os.path.normpath(args.weights_dir))})"
+                if args.weights_dir else "random-init weights") + " (%s architecture)" % (
+                "RVM MobileNetV3" if rvm else "Kandinsky 2.1" if k2 else "UNet3D text-to-video" if vid else "SD1.5"),
             "config": {
                 "model": ("robust_video_matting (MobileNetV3 + LR-ASPP + ConvGRU decoder + DGF), "
                           f"{args.frames}-frame {args.res}x{args.height} clip" if rvm else
                           "kandinsky2 (Kandinsky 2.1: prior + GLIDE UNet + MoVQ + XLM-R/CLIP text)" if k2 else
                           f"{args.model} (UNet3D + KL-VAE + OpenCLIP ViT-H text), {args.frames} frames" if vid else
                           "anythingv3 (SD1.5 UNet + KL-VAE + CLIP ViT-L/14 text)") + (" TINY" if args.tiny else ""),
-                "global_batch": n * C * G,
-                "concurrent_tasks_per_gpu": C * G,
+                "global_batch": n * per_gpu_tasks,
+                "concurrent_tasks_per_gpu": per_gpu_tasks,
                 "streams_per_gpu": C,
                 "lockstep_group": G,
                 "seq_len": (args.res // 8) * (args.height // 8),
@@ -238,20 +237,76 @@ def main():
                 "denoise_steps": None if rvm else args.denoise_steps,
                 "scheduler": None if rvm else "p_sampler" if k2 else "DPMSolverMultistep" if vid else args.scheduler,
                 "cfg_batch": 1 if rvm else 2,
-                "parallelism": f"task-dp{n}",
+                "parallelism": f"dp{n}",
+                "parallelism_detail": f"task-level data parallel: {n} independent worker process(es), "
+                                      "one per GPU, weights broadcast from rank 0, no per-step collectives",
             },
             "p50_task_latency_ms": round(p50, 2),
+            "per_rank": [{"rank": r, "ms_per_step": round(v[0], 2), "tasks": int(v[1]),
+                          "tasks_per_hour": round(per_gpu_tasks * 3600.0 * 1000.0 / v[0], 2),
+                          "weight_broadcast_bytes": int(v[2])} for r, v in enumerate(per_rank)],
             **({"frames_per_second": round(n * C * args.frames * 1000.0 / ms_per_step, 1)} if (rvm or vid) else {}),
             "stage_s": {k: round(v, 4) for k, v in (last.timings.items() if last else [])},
-            "weight_broadcast": {"bytes": bstats["bytes"], "seconds": round(bstats["seconds"], 4)},
+            "weight_broadcast": {"bytes": int(max(v[2] for v in per_rank)), "seconds": round(bstats["seconds"], 4),
+                                 "backend": D.backend_name()},
             "init_s": round(t_init, 2),
             "native_kernels_loaded": ops.native_loaded(),
             "reference_ops": bool(args.reference_ops),
         }
         print(json.dumps(out), flush=True)
-    if D.is_dist():
-        import torch.distributed as tdist
-        tdist.destroy_process_group()
+    if ex is not None:
+        ex.shutdown()
+    D.shutdown()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank: int, world: int, port: int, argv):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    run(parse_args(argv))
+
+
+def spawn(argv, world: int) -> int:
+    """``python bench.py --gpus N`` without torchrun: N fresh rank processes (spawn context - the
+    parent never touches the GPU).  A rank that fails takes the others down (they would wait in
+    the next collective forever); the exit code is the first failure's."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, argv), daemon=False) for r in range(world)]
+    for p in procs:
+        p.start()
+    rc = 0
+    while any(p.is_alive() for p in procs):
+        for p in procs:
+            p.join(0.2)
+            if p.exitcode not in (None, 0) and rc == 0:
+                rc = p.exitcode if p.exitcode > 0 else 1
+                for q in procs:
+                    if q.is_alive():
+                        q.terminate()
+    for p in procs:
+        p.join()
+        if p.exitcode not in (0, None) and rc == 0:
+            rc = p.exitcode if p.exitcode > 0 else 1
+    return rc
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if launched == 0 and args.gpus > 1:
+        sys.exit(spawn(argv, args.gpus))
+    run(args)
 
 
 if __name__ == "__main__":

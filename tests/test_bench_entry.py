@@ -1,0 +1,54 @@
+"""bench.py contract on CPU (gloo ranks): ``--gpus N`` without torchrun spawns N rank processes,
+rank 0 broadcasts the weights, every rank solves its tasks, one JSON line with whole-node numbers;
+a ``--gpus`` that disagrees with the launcher's world size fails loudly."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--device", "cpu", "--tiny", "--steps", "1", "--warmup", "0", "--denoise-steps", "2", "--res", "64",
+        "--concurrent", "1", "--group", "2"]
+
+
+def _run(args, env=None, timeout=600):
+    e = dict(os.environ, **(env or {}))
+    e.pop("WORLD_SIZE", None) if env is None else None
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=ROOT)
+
+
+def _json(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(900)
+def test_bench_spawns_gpus_ranks_and_broadcasts():
+    r = _run(["--gpus", "2", *TINY])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["global_batch"] == 4                 # 2 ranks x 1 stream x group 2
+    assert [p["rank"] for p in d["per_rank"]] == [0, 1]
+    assert all(p["tasks"] == 2 for p in d["per_rank"])      # every rank solved its tasks
+    assert d["weight_broadcast"]["bytes"] > 0 and d["weight_broadcast"]["backend"] == "gloo"
+    assert d["value"] == pytest.approx(2 * 2 * 3600e3 / d["ms_per_step"], rel=1e-3)
+
+
+@pytest.mark.timeout(600)
+def test_bench_single_rank_unchanged():
+    r = _run(["--gpus", "1", *TINY])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r.stdout)
+    assert d["n_gpus"] == 1 and d["weight_broadcast"]["bytes"] == 0 and len(d["per_rank"]) == 1
+
+
+@pytest.mark.timeout(600)
+def test_bench_gpus_must_match_launcher_world():
+    env = {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29599"}
+    r = _run(["--gpus", "2", *TINY], env=env)
+    assert r.returncode != 0 and "--gpus 2" in (r.stderr + r.stdout)

@@ -71,7 +71,10 @@ def test_e2e_fake_gpu():
     assert cid_hex_to_str(e.solutions[tid].cid) in m.pinner.pins
     # pinTaskInput pinned the raw input
     assert len(m.pinner.pins) == 2
-    assert m.db.get_solution(tid) is None or True
+    # our own SolutionSubmitted event is recorded like any other (index.ts:236-266)
+    asyncio.run(m.poll_events())
+    row = m.db.get_solution(tid)
+    assert row is not None and row["validator"].lower() == MINER.lower() and row["cid"] == e.solutions[tid].cid
     assert m.metrics.counters.get("claims") == 1
 
 
