@@ -93,6 +93,9 @@ async def _start(path: str):
         print(f"unable to parse {path}: {e}", file=sys.stderr)
         sys.exit(1)
     init_logging(cfg.log_path)
+    from .numerics import NUMERICS_VERSION, check_mining_env
+    check_mining_env()                 # A/B knobs would produce non-consensus CIDs
+    log.info("numerics version %s", NUMERICS_VERSION)
     if cfg.evilmode:
         for _ in range(20):
             log.warning("YOU HAVE EVIL MODE ENABLED, YOU WILL BE SLASHED")

@@ -1,0 +1,126 @@
+"""Consensus numerics: the version of this node's output bytes, the golden CIDs that pin it on
+gfx950, and the env knobs that would change it.
+
+A solution is valid only if every honest miner produces the same bytes, and
+CIDs are hardware-specific (``docs/src/pages/register-model.mdx:78-80``): the reference pins one
+A100 CID in its boot self-test (``miner/src/index.ts:981-1001``).  This node pins a set of
+golden tasks per (hardware, weights) in ``tests/golden_cids.json``; every kernel, plan, sampler
+or encoder change that flips one output bit fails ``tests/test_golden_gpu.py`` until
+``NUMERICS_VERSION`` is bumped and the goldens are re-pinned (``scripts/pin_goldens.py``).  Two
+nodes on the same NUMERICS_VERSION produce the same CIDs; nodes on different versions would
+contest each other and must not mine the same model registration.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Dict, List, Tuple
+
+# bump on ANY change of output bytes (kernels, conv plans, sampler arithmetic, PNG/MP4 encoders)
+NUMERICS_VERSION = "r2.0-baseline"
+
+# Environment knobs that select a different kernel library, plan table, tiling or reference ops.
+# They exist for A/B measurement only; ``start`` refuses to mine with any of them set.
+NUMERICS_ENV_KNOBS = (
+    "ARBIUS_PLAN_CANON", "ARB_CONV_PLANS", "ARB_GN_GROUP", "ARBIUS_NORM_PROLOGUE", "ARBIUS_KERNEL_LIB",
+    "ARBIUS_EXPERIMENT_SKIP", "ARBIUS_REFERENCE_OPS", "ARB_ATTN_GLDS", "ARB_ATTN_QT", "ARB_LN_ROWS",
+    "ARB_SPLITK_INLAUNCH", "ARBIUS_GEGLU_FUSED", "ARBIUS_CROSS_KV_HOIST", "ARBIUS_FAULT_INJECTION",
+    "ARBIUS_SAMPLER_REF",
+)
+
+
+def numerics_env_overrides(env=None) -> Dict[str, str]:
+    env = os.environ if env is None else env
+    return {k: env[k] for k in NUMERICS_ENV_KNOBS if env.get(k, "") != ""}
+
+
+def check_mining_env(env=None) -> None:
+    """Refuse to mine with a numerics-changing knob set: it would produce non-consensus CIDs."""
+    bad = numerics_env_overrides(env)
+    if bad:
+        raise SystemExit("refusing to mine: numerics-changing environment knobs are set "
+                         f"({', '.join(f'{k}={v}' for k, v in sorted(bad.items()))}); their outputs differ from "
+                         f"every other node on NUMERICS_VERSION {NUMERICS_VERSION}. Unset them.")
+
+
+# ---------------------------------------------------------------------------------------------
+# golden tasks (run on one GPU by tests/test_golden_gpu.py and scripts/pin_goldens.py)
+def _sd_inp(prompt, seed, res, steps, sched, g, neg="blurry, lowres"):
+    return {"prompt": prompt, "negative_prompt": neg, "width": res, "height": res, "num_inference_steps": steps,
+            "guidance_scale": g, "scheduler": sched, "seed": seed}
+
+
+SD_SOLO = _sd_inp("arbius test cat", 1337, 512, 4, "DPMSolverMultistep", 12.0)
+SD_GROUP = [_sd_inp(f"a detailed anime illustration of a castle, golden {i}", 2000 + i, 512, 4,
+                    "DPMSolverMultistep", 7.0 + i) for i in range(8)]
+SD_SCHEDULERS = ("DDIM", "K_EULER", "K_EULER_ANCESTRAL", "DPMSolverMultistep", "PNDM", "KLMS")
+
+
+def golden_cases(device) -> List[Tuple[str, Callable[[], object]]]:
+    """(name, fn) pairs; fn() -> a CID hex string or a list of them.  Pipelines are built lazily
+    and shared between cases of one family."""
+    from .models.registry import build_pipeline
+    from .node.solver import solve_image, solve_images
+
+    cache: Dict[str, object] = {}
+
+    def pipe(name):
+        if name not in cache:
+            cache[name] = build_pipeline(name, device=device)
+        return cache[name]
+
+    def sd_solo():
+        return solve_image(pipe("anythingv3"), SD_SOLO).cid
+
+    def sd_group_streams():
+        """8 tasks as 2 concurrent streams x lock-step groups of 4 (the bench configuration):
+        every CID must equal its solo CID."""
+        from concurrent.futures import ThreadPoolExecutor
+        base = pipe("anythingv3")
+        forks = [base.fork(), base.fork()]
+        with ThreadPoolExecutor(2) as ex:
+            futs = [ex.submit(solve_images, forks[j], SD_GROUP[4 * j:4 * j + 4]) for j in range(2)]
+            grouped = [s.cid for f in futs for s in f.result()]
+        solo = [solve_image(base, i).cid for i in SD_GROUP]
+        if grouped != solo:
+            raise AssertionError(f"lock-step/stream CIDs differ from solo: {grouped} vs {solo}")
+        return grouped
+
+    def sd_sched(s):
+        return lambda: solve_image(pipe("anythingv3"), _sd_inp("arbius test cat", 42, 256, 3, s, 7.0)).cid
+
+    def k2():
+        p = pipe("kandinsky2")
+        old = (p.cfg.num_steps, p.cfg.prior_steps)
+        p.cfg.num_steps, p.cfg.prior_steps = 2, 2
+        try:
+            return p.solve({"prompt": "arbius test cat", "width": 768, "height": 768, "seed": 1337}).cid
+        finally:
+            p.cfg.num_steps, p.cfg.prior_steps = old
+
+    def video(name):
+        def f():
+            if name == "damo":      # templates/damo.json inputs only (no negative prompt / size / guidance)
+                inp = {"prompt": "a red cat walking on a castle wall", "num_frames": 8, "num_inference_steps": 2,
+                       "fps": 8, "seed": 1337}
+            else:
+                inp = {"prompt": "a red cat walking on a castle wall", "negative_prompt": "blurry", "num_frames": 8,
+                       "width": 256, "height": 256, "num_inference_steps": 2, "guidance_scale": 9.0, "fps": 8,
+                       "seed": 1337}
+            return pipe(name).solve(inp).cid
+        return f
+
+    def rvm():
+        import numpy as np
+
+        from .node.solver import solve_files
+        from .utils.mp4 import encode_mp4
+        rng = np.random.default_rng(1337)
+        clip = rng.integers(0, 256, (8, 180, 320, 3), dtype=np.uint8)
+        out = pipe("robust_video_matting")(clip, "green-screen")
+        return solve_files([("out-1.mp4", encode_mp4(list(out), 24))]).cid
+
+    cases = [("sd15_512_dpm4_solo", sd_solo), ("sd15_512_dpm4_2streams_group4", sd_group_streams)]
+    cases += [(f"sd15_256_{s}_3", sd_sched(s)) for s in SD_SCHEDULERS]
+    cases += [("kandinsky2_768_2+2", k2), ("zeroscopev2xl_256x256x8_2", video("zeroscopev2xl")),
+              ("damo_256x256x8_2", video("damo")), ("rvm_320x180x8", rvm)]
+    return cases

@@ -1,0 +1,37 @@
+"""Consensus guard rails that need no GPU: the numerics-changing env knobs are refused by
+``start`` and the golden-CID table is versioned."""
+import json
+import os
+
+import pytest
+
+from arbius_amd import numerics
+
+
+def test_mining_refuses_numerics_knobs():
+    numerics.check_mining_env({"PATH": "/bin", "ARBIUS_PLAN_CANON": ""})     # empty = unset
+    for k in ("ARBIUS_PLAN_CANON", "ARB_CONV_PLANS", "ARB_GN_GROUP", "ARBIUS_NORM_PROLOGUE",
+              "ARBIUS_KERNEL_LIB", "ARBIUS_EXPERIMENT_SKIP", "ARBIUS_REFERENCE_OPS"):
+        with pytest.raises(SystemExit, match=k):
+            numerics.check_mining_env({k: "1"})
+
+
+def test_start_refuses_knobs_before_touching_chain(tmp_path, monkeypatch):
+    from arbius_amd import cli
+    cfg = tmp_path / "MiningConfig.json"
+    cfg.write_text(json.dumps({"db_path": str(tmp_path / "db.sqlite"), "mi355x": {"mock_chain": True}}))
+    monkeypatch.setenv("ARB_CONV_PLANS", "/tmp/other_plans.txt")
+    with pytest.raises(SystemExit, match="ARB_CONV_PLANS"):
+        cli.main(["start", str(cfg)])
+
+
+def test_golden_table_is_versioned():
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden_cids.json")))
+    assert {"numerics_version", "key", "cases"} <= set(g)
+
+
+def test_selftest_table_pinned_for_this_numerics_version():
+    from arbius_amd.node import miner
+    t = json.load(open(os.path.join(os.path.dirname(miner.__file__), "..", "config", "selftest.json")))
+    assert t["numerics_version"] == numerics.NUMERICS_VERSION
+    assert t["kandinsky2"]["expected"]["gfx950/random-init-seed0"].startswith("0x1220")
