@@ -1,5 +1,9 @@
-"""The subset of the EngineV1 / BaseToken ABI the node uses:
-function signatures, return tuples and event layouts (indexed/non-indexed)."""
+"""The EngineV1 ABI (all 77 functions and 31 events of
+``miner/src/artifacts/contracts/EngineV1.sol/EngineV1.json``; events declared at
+``contract/contracts/EngineV1.sol:141-206`` plus OpenZeppelin's ``Initialized`` /
+``OwnershipTransferred``) and the BaseToken ERC20 calls the node makes:
+function signatures, return tuples and event layouts (indexed/non-indexed).
+``tests/test_engine_abi.py`` checks every selector, return list and topic against the artifact."""
 from __future__ import annotations
 
 from typing import Dict, List, Tuple
@@ -49,6 +53,25 @@ FUNCS: Dict[str, Tuple[str, List[str]]] = {
     "owner": ("owner()", ["address"]),
     "treasury": ("treasury()", ["address"]),
     "pauser": ("pauser()", ["address"]),
+    # remaining public getters / pure helpers / init (EngineV1.sol:70-137, 387-543)
+    "baseToken": ("baseToken()", ["address"]),
+    "prevhash": ("prevhash()", ["bytes32"]),
+    "startBlockTime": ("startBlockTime()", ["uint64"]),
+    "commitments": ("commitments(bytes32)", ["uint256"]),
+    "contestationVoteYeas": ("contestationVoteYeas(bytes32,uint256)", ["address"]),
+    "contestationVoteNays": ("contestationVoteNays(bytes32,uint256)", ["address"]),
+    "contestationVotedIndex": ("contestationVotedIndex(bytes32)", ["uint256"]),
+    "pendingValidatorWithdrawRequests": ("pendingValidatorWithdrawRequests(address,uint256)", ["uint256", "uint256"]),
+    "pendingValidatorWithdrawRequestsCount": ("pendingValidatorWithdrawRequestsCount(address)", ["uint256"]),
+    "validatorWithdrawPendingAmount": ("validatorWithdrawPendingAmount(address)", ["uint256"]),
+    "getSlashAmount": ("getSlashAmount()", ["uint256"]),
+    "diffMul": ("diffMul(uint256,uint256)", ["uint256"]),
+    "reward": ("reward(uint256,uint256)", ["uint256"]),
+    "targetTs": ("targetTs(uint256)", ["uint256"]),
+    "hashModel": ("hashModel((uint256,address,uint256,bytes),address)", ["bytes32"]),
+    "hashTask": ("hashTask((bytes32,uint256,address,uint64,uint8,bytes),address,bytes32)", ["bytes32"]),
+    "initialize": ("initialize(address,address)", []),
+    "renounceOwnership": ("renounceOwnership()", []),
     # ERC20 (base token)
     "balanceOf": ("balanceOf(address)", ["uint256"]),
     "allowance": ("allowance(address,address)", ["uint256"]),
@@ -85,7 +108,29 @@ EVENTS: Dict[str, Tuple[str, List[Tuple[str, str, bool]]]] = {
     "ModelRegistered": ("ModelRegistered(bytes32)", [("id", "bytes32", True)]),
     "ValidatorDeposit": ("ValidatorDeposit(address,address,uint256)",
                          [("addr", "address", True), ("validator", "address", True), ("amount", "uint256", False)]),
+    "ValidatorWithdrawInitiated": ("ValidatorWithdrawInitiated(address,uint256,uint256,uint256)",
+                                   [("addr", "address", True), ("count", "uint256", True),
+                                    ("unlockTime", "uint256", False), ("amount", "uint256", False)]),
+    "ValidatorWithdrawCancelled": ("ValidatorWithdrawCancelled(address,uint256)",
+                                   [("addr", "address", True), ("count", "uint256", True)]),
+    "ValidatorWithdraw": ("ValidatorWithdraw(address,address,uint256,uint256)",
+                          [("addr", "address", True), ("to", "address", True), ("count", "uint256", True),
+                           ("amount", "uint256", False)]),
+    "SignalSupport": ("SignalSupport(address,bytes32,bool)",
+                      [("addr", "address", True), ("model", "bytes32", True), ("supported", "bool", False)]),
+    "TreasuryTransferred": ("TreasuryTransferred(address)", [("to", "address", True)]),
+    "PauserTransferred": ("PauserTransferred(address)", [("to", "address", True)]),
+    "PausedChanged": ("PausedChanged(bool)", [("paused", "bool", True)]),
+    "SolutionMineableRateChange": ("SolutionMineableRateChange(bytes32,uint256)",
+                                   [("id", "bytes32", True), ("rate", "uint256", False)]),
+    "Initialized": ("Initialized(uint8)", [("version", "uint8", False)]),
+    "OwnershipTransferred": ("OwnershipTransferred(address,address)",
+                             [("previousOwner", "address", True), ("newOwner", "address", True)]),
 }
+# the 10 parameter setters emit <Param>Changed(uint256 indexed amount) (EngineV1.sol:193-206)
+for _p in ENGINE_PARAMS:
+    _e = _p[0].upper() + _p[1:] + "Changed"
+    EVENTS[_e] = (_e + "(uint256)", [("amount", "uint256", True)])
 
 TOPIC_TO_EVENT = {abi.topic(sig): name for name, (sig, _) in EVENTS.items()}
 

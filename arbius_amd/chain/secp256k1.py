@@ -1,7 +1,13 @@
 """secp256k1 ECDSA for Ethereum transactions: deterministic RFC 6979 nonces,
 low-s normalisation, recovery id, public-key recovery (ecrecover) and address
-derivation.  Pure Python integer arithmetic in Jacobian coordinates (no Ethereum
-library exists in this image).
+derivation (no Ethereum library exists in this image).
+
+``sign`` / ``pubkey`` / ``recover`` run the native C++ implementation
+(``native/src/secp256k1.cpp``: complete projective formulas, fixed-window
+constant-time scalar multiplication - the private key never steers a branch) when
+the extension is built.  The pure-Python Jacobian double-and-add below is the
+variable-time reference the native code is tested against (tests/test_native.py);
+it signs only when the extension is missing (CPU checkout before build()).
 """
 from __future__ import annotations
 
@@ -76,7 +82,23 @@ def _affine(p):
     return ((p[0] * zi * zi) % P, (p[1] * zi * zi * zi) % P)
 
 
+def _native():
+    try:
+        from .. import native
+    except Exception:  # noqa: BLE001
+        return None
+    return native if getattr(native, "loaded", False) and hasattr(native, "secp256k1_sign") else None
+
+
 def pubkey(priv: int) -> Tuple[int, int]:
+    nat = _native()
+    if nat is not None:
+        raw = nat.secp256k1_pubkey(int(priv).to_bytes(32, "big"))
+        return int.from_bytes(raw[:32], "big"), int.from_bytes(raw[32:], "big")
+    return py_pubkey(priv)
+
+
+def py_pubkey(priv: int) -> Tuple[int, int]:
     return _affine(_jmul(G, priv))
 
 
@@ -117,6 +139,15 @@ def _rfc6979_k(priv: int, h: bytes) -> int:
 
 def sign(msg_hash: bytes, priv) -> Tuple[int, int, int]:
     """-> (r, s, recovery_id) with low-s (EIP-2)."""
+    nat = _native()
+    if nat is not None:
+        r, s, rec = nat.secp256k1_sign(bytes(msg_hash), _priv_int(priv).to_bytes(32, "big"))
+        return int.from_bytes(r, "big"), int.from_bytes(s, "big"), rec
+    return py_sign(msg_hash, priv)
+
+
+def py_sign(msg_hash: bytes, priv) -> Tuple[int, int, int]:
+    """Variable-time reference of ``sign`` (tests, no-extension fallback)."""
     d = _priv_int(priv)
     z = int.from_bytes(msg_hash, "big")
     k = _rfc6979_k(d, msg_hash)
@@ -132,6 +163,14 @@ def sign(msg_hash: bytes, priv) -> Tuple[int, int, int]:
 
 def recover(msg_hash: bytes, r: int, s: int, rec: int) -> Optional[Tuple[int, int]]:
     """ecrecover: public key from a signature."""
+    nat = _native()
+    if nat is not None:
+        raw = nat.secp256k1_recover(bytes(msg_hash), int(r).to_bytes(32, "big"), int(s).to_bytes(32, "big"), rec)
+        return None if raw is None else (int.from_bytes(raw[:32], "big"), int.from_bytes(raw[32:], "big"))
+    return py_recover(msg_hash, r, s, rec)
+
+
+def py_recover(msg_hash: bytes, r: int, s: int, rec: int) -> Optional[Tuple[int, int]]:
     x = r + (N if rec & 2 else 0)
     alpha = (x * x * x + 7) % P
     beta = pow(alpha, (P + 1) // 4, P)

@@ -36,7 +36,7 @@ from .graphs import GraphCache, PipelineBase
 from .layers import Linear, init_weights
 from .movq import MoVQConfig, MoVQDecoder
 from .prior import PriorConfig, PriorTransformer
-from .schedulers import GaussianDiffusion
+from .schedulers import GaussianDiffusion, GroupSampler, TaskSampler
 from .tokenizer import CLIPTokenizer
 from .xlmr import MCLIPText, XLMRConfig, XLMRTokenizer
 
@@ -130,14 +130,38 @@ class Kandinsky2Pipeline(PipelineBase):
     def sample_prior(self, hidden, pooled, lens, gen, steps: int, cf_scale: float):
         d = self.cfg.prior.clip_dim
         sched = GaussianDiffusion(steps, schedule="cosine", predict="x0", learned_var=False)
-        x = torch.randn((1, d), generator=gen, dtype=torch.float32).to(self.device)
+        x = torch.randn((1, d), generator=gen, dtype=torch.float32)
+        ts = TaskSampler(sched, x.view(d // 4, 4), gen, self.device)
+        xin = torch.empty((d // 4, 4), dtype=self.dtype, device=self.device)
+
+        def rows(k, out):     # out = (cond, uncond) prior outputs [1, d]
+            return (None if out is None else out[1].reshape(-1, 4), None if out is None else out[0].reshape(-1, 4),
+                    xin, None)
+
+        samp = GroupSampler([ts], [float(cf_scale)], xin, rows)
+        samp.write_input(0)
         for i, t in enumerate(sched.timesteps):
             beat()
-            xin = x.to(self.dtype)
-            c = self.prior(xin, t, hidden[0:1], pooled[0:1], lens[0]).float()
-            u = self.prior(xin, t, hidden[1:2], pooled[1:2], lens[1]).float()
-            x = sched.step(u + cf_scale * (c - u), i, x, gen)
+            xv = xin.view(1, d)
+            c = self.prior(xv, t, hidden[0:1], pooled[0:1], lens[0]).contiguous()
+            u = self.prior(xv, t, hidden[1:2], pooled[1:2], lens[1]).contiguous()
+            samp.step(i, (c, u))
+        x = ts.x.view(1, d)
         return (x * self.prior.clip_std.float() + self.prior.clip_mean.float()).to(self.dtype)
+
+    def _group_sampler(self, tasks, h, w):
+        """k decoder tasks on one batch-2k GLIDE UNet input: rows 2k / 2k+1 = (cond, uncond); the
+        cond row's channels 4..7 are the learned variance of p_sample."""
+        zc = self.cfg.unet.in_channels
+        xin = torch.empty((2 * len(tasks), h, w, zc), dtype=self.dtype, device=self.device)
+
+        def rows(k, out):
+            return (None if out is None else out[2 * k + 1], None if out is None else out[2 * k],
+                    xin[2 * k], xin[2 * k + 1])
+
+        samp = GroupSampler(tasks, [float(self.cfg.guidance_scale)] * len(tasks), xin, rows)
+        samp.write_input(0)
+        return samp
 
     @torch.no_grad()
     def __call__(self, prompt: str, width: int = 768, height: int = 768, seed: int = 0,
@@ -164,21 +188,20 @@ class Kandinsky2Pipeline(PipelineBase):
         h, w = height // 8, width // 8
         zc = cfg.unet.in_channels
         x = torch.randn((1, zc, h, w), generator=gen, dtype=torch.float32).permute(0, 2, 3, 1).contiguous()
-        x = x.to(self.device)
         sched = GaussianDiffusion(steps, schedule="linear", predict="eps", learned_var=True, clamp=cfg.latent_clamp)
+        ts = TaskSampler(sched, x, gen, self.device)
+        samp = self._group_sampler([ts], h, w)
+        samp.g = [float(g)]
         tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
         for i, t in enumerate(sched.timesteps):
             beat()
-            xin = x.to(self.dtype)
             tbuf.fill_(float(t))
             with ops.plan_batch(2):      # batch-invariant plans: solo == lock-step group bytes
-                out = self._unet(torch.cat([xin, xin]), tbuf, text_full, text_pooled, img_embs)
-            c, u = out[0:1].float(), out[1:2].float()
-            eps = u[..., :zc] + g * (c[..., :zc] - u[..., :zc])
-            x = sched.step(eps, i, x, gen, var=c[..., zc:])
+                out = self._unet(samp.xin, tbuf, text_full, text_pooled, img_embs)
+            samp.step(i, out)            # ONE fused CFG + p_sample launch (learned variance, clamp)
         sync()
         t2 = time.perf_counter()
-        img = self.decode(x)
+        img = self.decode(ts.x)
         sync()
         t3 = time.perf_counter()
         self.timings = {"text_prior_s": t1 - t0, "denoise_s": t2 - t1, "movq_s": t3 - t2}
@@ -209,29 +232,24 @@ class Kandinsky2Pipeline(PipelineBase):
                 tp.append(text_pooled)
                 ie.append(torch.cat([img_emb, self.buffers.zero_img_emb[None].to(self.dtype)]))
                 x = torch.randn((1, zc, h, w), generator=gen, dtype=torch.float32).permute(0, 2, 3, 1).contiguous()
-                xs.append(x.to(self.device))
+                sched = GaussianDiffusion(cfg.num_steps, schedule="linear", predict="eps", learned_var=True,
+                                          clamp=cfg.latent_clamp)
+                xs.append(TaskSampler(sched, x, gen, self.device))    # draws this task's noise now
                 gens.append(gen)
             text_full, text_pooled, img_embs = torch.cat(tf), torch.cat(tp), torch.cat(ie)
             sync()
             t1 = time.perf_counter()
-            scheds = [GaussianDiffusion(cfg.num_steps, schedule="linear", predict="eps", learned_var=True,
-                                        clamp=cfg.latent_clamp) for _ in inps]
+            samp = self._group_sampler(xs, h, w)
             tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
-            g = cfg.guidance_scale
-            for i, t in enumerate(scheds[0].timesteps):
+            for i, t in enumerate(xs[0].sched.timesteps):
                 beat()
-                xin = [x.to(self.dtype) for x in xs]
                 tbuf.fill_(float(t))
                 with ops.plan_batch(2):
-                    out = self._unet(torch.cat([v for x in xin for v in (x, x)]), tbuf, text_full, text_pooled,
-                                     img_embs)
-                for k, s in enumerate(scheds):
-                    c, u = out[2 * k:2 * k + 1].float(), out[2 * k + 1:2 * k + 2].float()
-                    eps = u[..., :zc] + g * (c[..., :zc] - u[..., :zc])
-                    xs[k] = s.step(eps, i, xs[k], gens[k], var=c[..., zc:])
+                    out = self._unet(samp.xin, tbuf, text_full, text_pooled, img_embs)
+                samp.step(i, out)
             sync()
             t2 = time.perf_counter()
-            imgs = [self.decode(x) for x in xs]
+            imgs = [self.decode(ts.x) for ts in xs]
             sync()
             self.timings = {"text_prior_s": t1 - t0, "denoise_s": t2 - t1, "movq_s": time.perf_counter() - t2}
             return imgs

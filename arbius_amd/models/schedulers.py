@@ -3,17 +3,27 @@
 K_EULER_ANCESTRAL, PNDM, KLMS) plus the plain DDPM ancestral ``p_sampler``
 used by Kandinsky2 (``docs/src/pages/register-model.mdx:140-168``).
 
-All samplers share the SD noise schedule (scaled-linear betas 0.00085->0.012,
-1000 train steps) and run in fp32 on the latent's device; the per-step work is
-a few elementwise ops on a [1,4,64,64] latent, negligible next to the UNet.
-Formulas follow the published algorithms (DDIM, Karras-Euler, DPM-Solver++(2M),
-PLMS, k-LMS); byte-parity with the external Cog containers is "parity unpinned"
-(the reference ships no container outputs to compare against).
+Every sampler is expressed as ONE generic per-element update whose coefficients the host
+computes per step (``StepPlan``)::
+
+    e   = u + g (c - u)                                  classifier-free guidance
+    E   = he0 e + he1 H[-1] + he2 H[-2] + he3 H[-3]      multistep history (PNDM, k-LMS)
+    x0  = clamp(px X + pe E)                              eps- / x0-prediction
+    out = ox Xsrc + oe E + ox0 x0 + od (x0 - P) + std N   (std learned: Kandinsky p_sample)
+
+On a GPU the whole update of a lock-step group - CFG, sampler, the history / x0 stores and the
+next step's bf16 UNet input - is ONE launch of ``ops/csrc/sampler.hip``; on CPU the same formula
+runs in fp32 torch (``ops.ref.sampler_step``).  Ancestral noise is drawn from each task's CPU
+generator up front, in exactly the order the step-by-step algorithm draws it, and copied to the
+device once (no per-step host sync).  Formulas follow the published algorithms (DDIM,
+Karras-Euler, DPM-Solver++(2M), PLMS, k-LMS, improved-DDPM p_sample); byte-parity with the
+external Cog containers is "parity unpinned" (the reference ships no container outputs).
 """
 from __future__ import annotations
 
 import math
-from typing import List, Optional
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -34,10 +44,33 @@ def sd_alphas_cumprod(n_train=1000, beta_start=0.00085, beta_end=0.012, schedule
     return np.cumprod(1.0 - betas)
 
 
+@dataclass
+class StepPlan:
+    """Coefficients of one sampler step (see module docstring).  ``hist`` are offsets into the
+    eps history (1 = the previous stored eps); ``store_hist`` appends this step's e."""
+    he: Tuple[float, float, float, float] = (1.0, 0.0, 0.0, 0.0)
+    hist: Tuple[int, int, int] = (1, 2, 3)
+    store_hist: bool = False
+    px: float = 0.0
+    pe: float = 0.0
+    clamp: Optional[float] = None
+    ox: float = 0.0
+    oe: float = 0.0
+    ox0: float = 0.0
+    od: float = 0.0
+    std: float = 0.0
+    learned: Optional[Tuple[float, float]] = None     # (log beta, posterior log var) of p_sample
+    noise: bool = False
+    store_x0: bool = False
+    read_p: bool = False
+    use_cur: bool = False
+    store_cur: bool = False
+    in_scale: float = 1.0                             # scale_model_input of THIS step
+
+
 class Scheduler:
     name = "base"
     init_noise_sigma = 1.0
-    needs_noise = False
 
     def __init__(self, steps: int, n_train: int = 1000, alphas_cumprod=None):
         self.steps = steps
@@ -45,10 +78,19 @@ class Scheduler:
         self.ac = sd_alphas_cumprod(n_train) if alphas_cumprod is None else np.asarray(alphas_cumprod)
         self.timesteps: List[float] = []
 
-    def scale_model_input(self, x, i):
-        return x
+    def in_scale(self, i) -> float:
+        return 1.0
 
-    def step(self, eps, i, x, generator: Optional[torch.Generator] = None):
+    def plans(self) -> List[StepPlan]:
+        """All steps' plans, in order (schedulers with multistep state advance it here)."""
+        out = []
+        for i in range(len(self.timesteps)):
+            p = self._plan(i)
+            p.in_scale = self.in_scale(i)
+            out.append(p)
+        return out
+
+    def _plan(self, i) -> StepPlan:
         raise NotImplementedError
 
     def _leading(self, offset=1):
@@ -64,25 +106,16 @@ class DDIM(Scheduler):
         self.eta = eta
         self.timesteps = self._leading(1)
         self.ratio = self.n_train // steps
-        self.needs_noise = eta > 0
 
-    def step(self, eps, i, x, generator=None):
+    def _plan(self, i):
         t = self.timesteps[i]
         tp = t - self.ratio
         a_t = float(self.ac[t])
         a_p = float(self.ac[tp]) if tp >= 0 else float(self.ac[0])
-        x0 = (x - math.sqrt(1 - a_t) * eps) / math.sqrt(a_t)
         var = (1 - a_p) / (1 - a_t) * (1 - a_t / a_p)
         std = self.eta * math.sqrt(max(var, 0.0))
-        out = math.sqrt(a_p) * x0 + math.sqrt(max(1 - a_p - std * std, 0.0)) * eps
-        if std > 0:
-            out = out + std * _randn_like(x, generator)
-        return out
-
-
-def _randn_like(x, generator):
-    n = torch.randn(x.shape, generator=generator, dtype=torch.float32, device="cpu")
-    return n.to(x.device)
+        return StepPlan(px=1.0 / math.sqrt(a_t), pe=-math.sqrt(1 - a_t) / math.sqrt(a_t), ox0=math.sqrt(a_p),
+                        oe=math.sqrt(max(1 - a_p - std * std, 0.0)), std=std, noise=std > 0)
 
 
 class _Sigma(Scheduler):
@@ -97,30 +130,26 @@ class _Sigma(Scheduler):
         self.timesteps = [float(v) for v in ts]
         self.init_noise_sigma = float(math.sqrt(self.sigmas.max() ** 2 + 1))
 
-    def scale_model_input(self, x, i):
-        return x / math.sqrt(self.sigmas[i] ** 2 + 1)
+    def in_scale(self, i):
+        return 1.0 / math.sqrt(self.sigmas[i] ** 2 + 1)
 
 
 class EulerDiscrete(_Sigma):
     name = "K_EULER"
 
-    def step(self, eps, i, x, generator=None):
+    def _plan(self, i):
         s, sn = self.sigmas[i], self.sigmas[i + 1]
-        return x + eps * (sn - s)
+        return StepPlan(ox=1.0, oe=float(sn - s))
 
 
 class EulerAncestral(_Sigma):
     name = "K_EULER_ANCESTRAL"
-    needs_noise = True
 
-    def step(self, eps, i, x, generator=None):
+    def _plan(self, i):
         s, sn = self.sigmas[i], self.sigmas[i + 1]
         up = math.sqrt(max(sn ** 2 * (s ** 2 - sn ** 2) / s ** 2, 0.0))
         down = math.sqrt(max(sn ** 2 - up ** 2, 0.0))
-        x = x + eps * (down - s)
-        if up > 0:
-            x = x + _randn_like(x, generator) * up
-        return x
+        return StepPlan(ox=1.0, oe=float(down - s), std=up, noise=up > 0)
 
 
 class LMSDiscrete(_Sigma):
@@ -129,7 +158,6 @@ class LMSDiscrete(_Sigma):
     def __init__(self, steps, order=4, **kw):
         super().__init__(steps, **kw)
         self.order = order
-        self.derivs = []
         # 16-point Gauss-Legendre on each interval (deterministic, no scipy)
         self._gl_x, self._gl_w = np.polynomial.legendre.leggauss(16)
 
@@ -148,16 +176,11 @@ class LMSDiscrete(_Sigma):
 
         return float(0.5 * (b - a) * np.sum(self._gl_w * basis(xs)))
 
-    def step(self, eps, i, x, generator=None):
-        self.derivs.append(eps)  # d = (x - x0)/sigma = eps for eps-prediction
-        if len(self.derivs) > self.order:
-            self.derivs.pop(0)
+    def _plan(self, i):
+        # d = (x - x0) / sigma = eps for eps-prediction; the last `order` d's, newest first
         order = min(i + 1, self.order)
-        coeffs = [self._coef(order, i, k) for k in range(order)]
-        out = x
-        for c, d in zip(coeffs, reversed(self.derivs)):
-            out = out + c * d
-        return out
+        c = [self._coef(order, i, k) for k in range(order)] + [0.0] * (4 - order)
+        return StepPlan(he=tuple(c), store_hist=True, ox=1.0, oe=1.0)
 
 
 class DPMSolverMultistep(Scheduler):
@@ -168,8 +191,6 @@ class DPMSolverMultistep(Scheduler):
         super().__init__(steps, **kw)
         ts = np.linspace(0, self.n_train - 1, steps + 1).round()[::-1][:-1].astype(np.int64)
         self.timesteps = [int(v) for v in ts]
-        self.prev_x0 = None
-        self.prev_lambda = None
 
     def _coefs(self, t):
         if t < 0:
@@ -178,26 +199,26 @@ class DPMSolverMultistep(Scheduler):
         alpha, sigma = math.sqrt(a), math.sqrt(1 - a)
         return alpha, sigma, math.log(alpha) - math.log(sigma)
 
-    def step(self, eps, i, x, generator=None):
-        t = self.timesteps[i]
-        s = self.timesteps[i + 1] if i + 1 < len(self.timesteps) else -1
-        a_t, s_t, l_t = self._coefs(t)
-        a_s, s_s, l_s = self._coefs(s)
-        x0 = (x - s_t * eps) / a_t
-        last = i == len(self.timesteps) - 1
-        lower_final = last and len(self.timesteps) < 15 or s < 0
-        if s < 0:
-            out = x0
-        else:
-            h = l_s - l_t
-            em1 = math.expm1(-h)  # e^{-h} - 1
-            out = (s_s / s_t) * x - a_s * em1 * x0
-            if self.prev_x0 is not None and not lower_final:
-                h0 = l_t - self.prev_lambda
-                r0 = h0 / h
-                d1 = (x0 - self.prev_x0) / r0
-                out = out - 0.5 * a_s * em1 * d1
-        self.prev_x0, self.prev_lambda = x0, l_t
+    def plans(self):
+        out, prev_lambda = [], None
+        n = len(self.timesteps)
+        for i, t in enumerate(self.timesteps):
+            s = self.timesteps[i + 1] if i + 1 < n else -1
+            a_t, s_t, l_t = self._coefs(t)
+            a_s, s_s, l_s = self._coefs(s)
+            p = StepPlan(px=1.0 / a_t, pe=-s_t / a_t, store_x0=True)
+            lower_final = (i == n - 1) and n < 15 or s < 0
+            if s < 0:
+                p.ox0 = 1.0
+            else:
+                h = l_s - l_t
+                em1 = math.expm1(-h)                       # e^{-h} - 1
+                p.ox, p.ox0 = s_s / s_t, -a_s * em1
+                if prev_lambda is not None and not lower_final:
+                    r0 = (l_t - prev_lambda) / h
+                    p.od, p.read_p = -0.5 * a_s * em1 / r0, True
+            prev_lambda = l_t
+            out.append(p)
         return out
 
 
@@ -212,42 +233,37 @@ class PNDM(Scheduler):
         plms = np.concatenate([ts[:-1], ts[-2:-1], ts[-1:]])[::-1]
         self.timesteps = [int(v) for v in plms]
         self.ratio = self.n_train // steps
-        self.ets = []
-        self.cur_sample = None
-        self.counter = 0
 
-    def _prev(self, x, t, tp, e):
+    def _prev_coefs(self, t, tp):
         a_t = float(self.ac[t])
         a_p = float(self.ac[tp]) if tp >= 0 else float(self.ac[0])
         b_t, b_p = 1 - a_t, 1 - a_p
-        coeff = (a_p / a_t) ** 0.5
         den = a_t * b_p ** 0.5 + (a_t * b_t * a_p) ** 0.5
-        return coeff * x - (a_p - a_t) * e / den
+        return (a_p / a_t) ** 0.5, -(a_p - a_t) / den
 
-    def step(self, eps, i, x, generator=None):
-        t = self.timesteps[i]
-        tp = t - self.ratio
-        if self.counter != 1:
-            self.ets = self.ets[-3:]
-            self.ets.append(eps)
-        else:
-            tp = t
-            t = t + self.ratio
-        if len(self.ets) == 1 and self.counter == 0:
-            e = eps
-            self.cur_sample = x
-        elif len(self.ets) == 1 and self.counter == 1:
-            e = (eps + self.ets[-1]) / 2
-            x = self.cur_sample
-            self.cur_sample = None
-        elif len(self.ets) == 2:
-            e = (3 * self.ets[-1] - self.ets[-2]) / 2
-        elif len(self.ets) == 3:
-            e = (23 * self.ets[-1] - 16 * self.ets[-2] + 5 * self.ets[-3]) / 12
-        else:
-            e = (55 * self.ets[-1] - 59 * self.ets[-2] + 37 * self.ets[-3] - 9 * self.ets[-4]) / 24
-        self.counter += 1
-        return self._prev(x, t, tp, e)
+    def plans(self):
+        out, n_ets = [], 0
+        for counter, t in enumerate(self.timesteps):
+            tp = t - self.ratio
+            p = StepPlan()
+            if counter != 1:
+                n_ets = min(n_ets + 1, 4)
+                p.store_hist = True
+            else:
+                tp, t = t, t + self.ratio
+            if n_ets == 1 and counter == 0:
+                p.he, p.store_cur = (1.0, 0.0, 0.0, 0.0), True
+            elif n_ets == 1 and counter == 1:
+                p.he, p.use_cur = (0.5, 0.5, 0.0, 0.0), True          # (eps + ets[-1]) / 2 on the stored x
+            elif n_ets == 2:
+                p.he = (1.5, -0.5, 0.0, 0.0)
+            elif n_ets == 3:
+                p.he = (23 / 12, -16 / 12, 5 / 12, 0.0)
+            else:
+                p.he = (55 / 24, -59 / 24, 37 / 24, -9 / 24)
+            p.ox, p.oe = self._prev_coefs(t, tp)
+            out.append(p)
+        return out
 
 
 def space_timesteps(n_train: int, steps: int) -> List[int]:
@@ -268,10 +284,8 @@ class GaussianDiffusion(Scheduler):
       interpolation between log(beta_t) and the clipped posterior log-variance
       (improved-DDPM); otherwise the fixed-small posterior variance;
     * ``clamp``: pred_x0 clamp (Kandinsky decodes with clamp(-2, 2)).
-    The respaced chain recomputes betas from the kept alphas_cumprod.
-    ``step(out, i, x, generator, var=v)`` - ``v`` in [-1, 1] is the var head."""
+    The respaced chain recomputes betas from the kept alphas_cumprod."""
     name = "p_sampler"
-    needs_noise = True
 
     def __init__(self, steps, n_train=1000, schedule="linear", beta_start=0.0001, beta_end=0.02,
                  predict="eps", learned_var=True, clamp=None):
@@ -288,30 +302,21 @@ class GaussianDiffusion(Scheduler):
         self.timesteps = [int(v) for v in use[::-1]]
         self.predict, self.learned_var, self.clamp = predict, learned_var, clamp
 
-    def pred_x0(self, out, j, x):
-        a = float(self.ac[j])
-        if self.predict == "x0":
-            x0 = out
-        else:
-            x0 = math.sqrt(1.0 / a) * x - math.sqrt(1.0 / a - 1.0) * out
-        if self.clamp is not None:
-            x0 = x0.clamp(-self.clamp, self.clamp)
-        return x0
-
-    def step(self, out, i, x, generator=None, var=None):
+    def _plan(self, i):
         j = len(self.use) - 1 - i              # respaced index, counting down
         a, ap, b = float(self.ac[j]), float(self.ac_prev[j]), float(self.betas[j])
-        x0 = self.pred_x0(out.float(), j, x.float())
-        mean = (b * math.sqrt(ap) / (1 - a)) * x0 + ((1 - ap) * math.sqrt(1 - b) / (1 - a)) * x.float()
-        if j == 0:
-            return mean
-        if self.learned_var and var is not None:
-            frac = (var.float() + 1.0) * 0.5
-            logv = frac * math.log(b) + (1.0 - frac) * float(self.post_logvar[j])
-            std = torch.exp(0.5 * logv)
+        p = StepPlan(clamp=self.clamp, ox0=b * math.sqrt(ap) / (1 - a), ox=(1 - ap) * math.sqrt(1 - b) / (1 - a))
+        if self.predict == "x0":
+            p.px, p.pe = 0.0, 1.0
         else:
-            std = math.exp(0.5 * float(self.post_logvar[j]))
-        return mean + std * _randn_like(x, generator)
+            p.px, p.pe = math.sqrt(1.0 / a), -math.sqrt(1.0 / a - 1.0)
+        if j > 0:
+            p.noise = True
+            if self.learned_var:
+                p.learned = (math.log(b), float(self.post_logvar[j]))
+            else:
+                p.std = math.exp(0.5 * float(self.post_logvar[j]))
+        return p
 
 
 SCHEDULERS = {
@@ -330,3 +335,95 @@ def make_scheduler(name: str, steps: int) -> Scheduler:
         return SCHEDULERS[name](steps)
     except KeyError:
         raise ValueError(f"unknown scheduler {name!r}; choices {sorted(SCHEDULERS)}") from None
+
+
+# ---------------------------------------------------------------------------------------------
+class TaskSampler:
+    """One task's sampler state on the device: fp32 latent X, previous x0 P, PNDM's stored
+    sample, a 4-slot eps history ring, and the task's whole ancestral-noise sequence (drawn now
+    from its CPU generator in step order, copied once with a non-blocking H2D from pinned memory)."""
+
+    def __init__(self, sched: Scheduler, x: torch.Tensor, gen: Optional[torch.Generator], device,
+                 plans: Optional[List[StepPlan]] = None):
+        self.sched = sched
+        self.plans = plans if plans is not None else sched.plans()
+        dev = torch.device(device)
+        self.x = x.detach().to(device=dev, dtype=torch.float32, copy=True).contiguous()   # never alias the caller
+        shape = self.x.shape
+        need = lambda f: any(f(p) for p in self.plans)             # noqa: E731
+        self.p = torch.zeros(shape, dtype=torch.float32, device=dev) if need(lambda p: p.store_x0 or p.read_p) \
+            else None
+        self.cur = torch.zeros(shape, dtype=torch.float32, device=dev) if need(lambda p: p.store_cur) else None
+        self.hist = torch.zeros((4,) + tuple(shape), dtype=torch.float32, device=dev) if need(
+            lambda p: p.store_hist) else None
+        self.n_hist = 0
+        self.noise_idx = []
+        k = 0
+        for p in self.plans:
+            self.noise_idx.append(k if p.noise else -1)
+            k += int(p.noise)
+        self.noise = None
+        if k:
+            if gen is None:
+                raise ValueError("an ancestral sampler needs the task's generator")
+            draws = torch.stack([torch.randn(tuple(shape), generator=gen, dtype=torch.float32) for _ in range(k)])
+            if dev.type == "cuda":
+                draws = draws.pin_memory()
+            self.noise = draws.to(dev, non_blocking=True)
+
+    def hist_slot(self, back: int) -> Optional[torch.Tensor]:
+        """The eps stored ``back`` appends ago (1 = most recent), or None."""
+        if self.hist is None or back > self.n_hist or back > 4:
+            return None
+        return self.hist[(self.n_hist - back) % 4]
+
+    def task_args(self, i: int, u, c, g: float, xin0=None, xin1=None, next_scale: float = 1.0) -> dict:
+        p = self.plans[i]
+        h = [self.hist_slot(b) if coef != 0.0 else None for b, coef in zip(p.hist, p.he[1:])]
+        return {"u": u, "c": c, "x": self.x, "xsrc": self.cur if p.use_cur else self.x, "p": self.p,
+                "cur": self.cur, "hs": self.hist[self.n_hist % 4] if p.store_hist else None,
+                "h1": h[0], "h2": h[1], "h3": h[2],
+                "noise": self.noise[self.noise_idx[i]] if p.noise else None, "xin0": xin0, "xin1": xin1,
+                "g": g, "he": p.he, "px": p.px, "pe": p.pe, "clamp": p.clamp, "ox": p.ox, "oe": p.oe,
+                "ox0": p.ox0, "od": p.od, "std": p.std, "learned": p.learned, "in_scale": next_scale,
+                "store_x0": p.store_x0, "store_cur": p.store_cur, "read_p": p.read_p}
+
+    def advance(self, i: int):
+        if self.plans[i].store_hist:
+            self.n_hist += 1
+
+
+class GroupSampler:
+    """The k tasks of one lock-step group (k = 1 for a solo task): ``step(i, out)`` runs the fused
+    CFG + sampler update of every task from the UNet output ``out`` and writes the next step's
+    UNet input into ``xin`` (one HIP launch on a GPU).
+
+    ``rows(k)`` -> (uncond view, cond view, xin view 0, xin view 1) of task k."""
+
+    def __init__(self, tasks: List[TaskSampler], guidance: List[float], xin: torch.Tensor, rows):
+        self.tasks, self.g, self.xin, self.rows = tasks, guidance, xin, rows
+        self.n = len(tasks[0].plans)
+
+    def write_input(self, i: int = 0):
+        """xin <- bf16(X * in_scale(i)) for every task (once, before the first UNet call)."""
+        for k, t in enumerate(self.tasks):
+            _, _, d0, d1 = self.rows(k, None)
+            v = (t.x * t.plans[i].in_scale).to(self.xin.dtype)
+            d0.copy_(v.reshape(d0.shape))
+            if d1 is not None:
+                d1.copy_(v.reshape(d1.shape))
+
+    def step(self, i: int, out: torch.Tensor):
+        from .. import ops
+        last = i == self.n - 1
+        args = []
+        for k, t in enumerate(self.tasks):
+            u, c, d0, d1 = self.rows(k, out)
+            nscale = 1.0 if last else t.plans[i + 1].in_scale
+            args.append(t.task_args(i, u, c, self.g[k], None if last else d0, None if last else d1, nscale))
+        ops.sampler_step(args)
+        for t in self.tasks:
+            t.advance(i)
+
+    def latent(self, k: int) -> torch.Tensor:
+        return self.tasks[k].x

@@ -28,7 +28,7 @@ from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .graphs import CAPTURE_LOCK, PipelineBase
 from .layers import init_weights
-from .schedulers import make_scheduler
+from .schedulers import GroupSampler, TaskSampler, make_scheduler
 from .tokenizer import CLIPTokenizer
 from .unet2d import CrossAttention, UNet2DCondition, UNetConfig, cross_kv_mode
 from .vae import VAEConfig, VAEDecoder
@@ -94,7 +94,8 @@ class _GraphedUNet:
                 self.out = unet(self.x, self.t, self.ctx)
 
     def __call__(self, x, t, ctx):
-        self.x.copy_(x)
+        if x.data_ptr() != self.x.data_ptr():       # the sampler writes the static buffer itself
+            self.x.copy_(x)
         self.t.fill_(float(t))
         if ctx is not self._ctx_obj:
             # a new context object = a new task / group (the reference is held, so identity
@@ -154,10 +155,13 @@ class SD15Pipeline(PipelineBase):
         with ops.plan_batch(2):
             if not self.use_graphs:
                 return self.unet(x2, torch.tensor([float(t)], device=self.device), ctx)
-            key = tuple(x2.shape)
-            if key not in self._graphs:
-                self._graphs[key] = _GraphedUNet(self.unet, x2.shape, ctx, self.dtype)
-            return self._graphs[key](x2, t, ctx)
+            return self._graph(tuple(x2.shape), ctx)(x2, t, ctx)
+
+    def _graph(self, shape, ctx):
+        with ops.plan_batch(2):
+            if shape not in self._graphs:
+                self._graphs[shape] = _GraphedUNet(self.unet, shape, ctx, self.dtype)
+            return self._graphs[shape]
 
     @torch.no_grad()
     def __call__(self, prompt: str, negative_prompt: str = "", width: int = 512, height: int = 512,
@@ -175,18 +179,31 @@ class SD15Pipeline(PipelineBase):
             h, w = height // 8, width // 8
             x, gen = self.initial_noise(seed, h, w, self.cfg.unet.in_channels)
             sched = make_scheduler(scheduler, num_inference_steps)
-            x = (x * sched.init_noise_sigma).to(self.device)
+            samp = self._group_sampler([TaskSampler(sched, x * sched.init_noise_sigma, gen, self.device)],
+                                       [guidance_scale], h, w, ctx)
         with span("denoise_s", tm, sync):
             for i, t in enumerate(sched.timesteps):
                 beat()
-                xin = sched.scale_model_input(x, i).to(self.dtype)
-                eps2 = self._unet_eval(torch.cat([xin, xin]), t, ctx)
-                eps = ops.ref.cfg_combine(eps2, guidance_scale)
-                x = sched.step(eps, i, x, gen)
+                samp.step(i, self._unet_eval(samp.xin, t, ctx))   # UNet, then ONE fused CFG+sampler launch
         with span("vae_s", tm, sync):
-            img = self.decode(x)
+            img = self.decode(samp.latent(0))
         self.timings = tm
         return img
+
+    def _group_sampler(self, tasks, guidance, h, w, ctx):
+        """Sampler for k tasks sharing one batch-2k UNet input: rows 2k / 2k+1 = (uncond, cond).
+        With hipGraphs the sampler writes the next input straight into the graph's static buffer."""
+        shape = (2 * len(tasks), h, w, self.cfg.unet.in_channels)
+        xin = self._graph(shape, ctx).x if self.use_graphs else torch.empty(shape, dtype=self.dtype,
+                                                                              device=self.device)
+
+        def rows(k, out):
+            return (None if out is None else out[2 * k], None if out is None else out[2 * k + 1],
+                    xin[2 * k], xin[2 * k + 1])
+
+        samp = GroupSampler(tasks, [float(g) for g in guidance], xin, rows)
+        samp.write_input(0)
+        return samp
 
     @torch.no_grad()
     def run_group(self, inps: List[dict]) -> List[np.ndarray]:
@@ -204,27 +221,22 @@ class SD15Pipeline(PipelineBase):
             sync = self._sync
             tm: Dict[str, float] = {}
             with span("text_s", tm, sync):
-                ctxs, xs, gens, scheds = [], [], [], []
+                ctxs, tasks = [], []
                 for inp in inps:
                     ctxs.append(self.encode_prompt(inp["prompt"], inp.get("negative_prompt", "")))
                     x, gen = self.initial_noise(int(inp["seed"]), height // 8, width // 8,
                                                 self.cfg.unet.in_channels)
                     sched = make_scheduler(scheduler, steps)
-                    xs.append((x * sched.init_noise_sigma).to(self.device))
-                    gens.append(gen)
-                    scheds.append(sched)
+                    tasks.append(TaskSampler(sched, x * sched.init_noise_sigma, gen, self.device))
                 ctx = torch.cat(ctxs)
-                gs = [float(inp.get("guidance_scale", 12)) for inp in inps]
+                samp = self._group_sampler(tasks, [float(inp.get("guidance_scale", 12)) for inp in inps],
+                                           height // 8, width // 8, ctx)
             with span("denoise_s", tm, sync):
-                for i, t in enumerate(scheds[0].timesteps):
+                for i, t in enumerate(tasks[0].sched.timesteps):
                     beat()
-                    xin = [s.scale_model_input(x, i).to(self.dtype) for s, x in zip(scheds, xs)]
-                    eps_all = self._unet_eval(torch.cat([v for x in xin for v in (x, x)]), t, ctx)
-                    for k, (s, g) in enumerate(zip(scheds, gs)):
-                        eps = ops.ref.cfg_combine(eps_all[2 * k:2 * k + 2], g)
-                        xs[k] = s.step(eps, i, xs[k], gens[k])
+                    samp.step(i, self._unet_eval(samp.xin, t, ctx))
             with span("vae_s", tm, sync):
-                imgs = [self.decode(x) for x in xs]
+                imgs = [self.decode(samp.latent(k)) for k in range(len(tasks))]
             self.timings = tm
             return imgs
 

@@ -25,7 +25,7 @@ from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .graphs import GraphCache, PipelineBase
 from .layers import init_weights
-from .schedulers import make_scheduler
+from .schedulers import GroupSampler, TaskSampler, make_scheduler
 from .tokenizer import CLIPTokenizer
 from .unet3d import UNet3DCondition, UNet3DConfig
 from .vae import VAEConfig, VAEDecoder
@@ -122,21 +122,25 @@ class VideoPipeline(PipelineBase):
         x = torch.randn((1, zc, F, H // 8, W // 8), generator=gen, dtype=torch.float32)
         x = x[0].permute(1, 2, 3, 0).contiguous()                 # [F, h, w, 4] frame-major NHWC
         sched = make_scheduler(cfg.scheduler, steps)
-        x = (x * sched.init_noise_sigma).to(self.device)
+        ts = TaskSampler(sched, x * sched.init_noise_sigma, gen, self.device)
+        xin = torch.empty((2 * F,) + tuple(x.shape[1:]), dtype=self.dtype, device=self.device)
+
+        def rows(k, out):       # frames of the uncond pass, then the cond pass
+            return (None if out is None else out[:F], None if out is None else out[F:], xin[:F], xin[F:])
+
+        samp = GroupSampler([ts], [g], xin, rows)
+        samp.write_input(0)
         tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
         unet = self._unet(F)
         sync()
         t1 = time.perf_counter()
         for i, t in enumerate(sched.timesteps):
             beat()
-            xin = sched.scale_model_input(x, i).to(self.dtype)
             tbuf.fill_(float(t))
-            out = unet(torch.cat([xin, xin]), tbuf, ctx)
-            u, c = out[:F].float(), out[F:].float()
-            x = sched.step(u + g * (c - u), i, x, gen)
+            samp.step(i, unet(xin, tbuf, ctx))      # UNet3D, then ONE fused CFG + sampler launch
         sync()
         t2 = time.perf_counter()
-        frames = self.decode(x)
+        frames = self.decode(ts.x)
         sync()
         t3 = time.perf_counter()
         self.timings = {"text_s": t1 - t0, "denoise_s": t2 - t1, "vae_s": t3 - t2}

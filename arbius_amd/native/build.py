@@ -11,6 +11,8 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 SRC = HERE / "src" / "native.cpp"
+SOURCES = [SRC, HERE / "src" / "secp256k1.cpp"]
+HEADERS = [HERE / "src" / "secp256k1.h"]
 
 
 def target() -> Path:
@@ -19,11 +21,12 @@ def target() -> Path:
 
 def build(force: bool = False) -> Path:
     out = target()
-    if out.exists() and not force and out.stat().st_mtime >= SRC.stat().st_mtime:
+    if out.exists() and not force and all(out.stat().st_mtime >= f.stat().st_mtime for f in SOURCES + HEADERS):
         return out
     import pybind11
     cmd = ["g++", "-O3", "-shared", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-pthread",
-           "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], str(SRC), "-lz", "-o", str(out)]
+           "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], *map(str, SOURCES), "-lz", "-o",
+           str(out)]
     subprocess.run(cmd, check=True)
     return out
 

@@ -5,6 +5,8 @@
 //  * png_encode         - deterministic PNG (filter 0 rows + zlib at a fixed level):
 //                         byte-identical to utils/png.py (same zlib, same params),
 //                         without the Python-side row copy;
+//  * secp256k1_*        - ECDSA signing (RFC 6979, constant-time in the key), public key,
+//                         ecrecover (secp256k1.cpp);
 //  * pcm_slice_body     - the H.264 I_PCM macroblock payload of one picture for
 //                         utils/mp4.py: RGB -> BT.601 YCbCr 4:2:0 (integer) and the
 //                         macroblock raster, multi-threaded over macroblock rows
@@ -15,6 +17,8 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <zlib.h>
+
+#include "secp256k1.h"
 
 #include <algorithm>
 #include <cstdint>
@@ -204,7 +208,54 @@ static py::bytes pcm_slice_body(py::array_t<uint8_t, py::array::c_style | py::ar
   return py::bytes(out);
 }
 
+static py::bytes as_bytes32(const py::bytes& b, const char* what) {
+  std::string s = b;
+  if (s.size() != 32) throw std::invalid_argument(std::string(what) + " must be 32 bytes");
+  return b;
+}
+
+static py::tuple py_secp_sign(const py::bytes& hash, const py::bytes& priv) {
+  std::string h = as_bytes32(hash, "hash"), k = as_bytes32(priv, "private key");
+  uint8_t r[32], s[32];
+  int rec;
+  {
+    py::gil_scoped_release nogil;
+    rec = secp256k1_sign((const uint8_t*)h.data(), (const uint8_t*)k.data(), r, s);
+  }
+  std::fill(k.begin(), k.end(), 0);
+  if (rec < 0) throw std::invalid_argument("invalid secp256k1 private key");
+  return py::make_tuple(py::bytes((const char*)r, 32), py::bytes((const char*)s, 32), rec);
+}
+
+static py::bytes py_secp_pubkey(const py::bytes& priv) {
+  std::string k = as_bytes32(priv, "private key");
+  uint8_t out[64];
+  const int rc = secp256k1_pubkey((const uint8_t*)k.data(), out);
+  std::fill(k.begin(), k.end(), 0);
+  if (rc) throw std::invalid_argument("invalid secp256k1 private key");
+  return py::bytes((const char*)out, 64);
+}
+
+static py::object py_secp_recover(const py::bytes& hash, const py::bytes& r, const py::bytes& s, int rec) {
+  std::string h = as_bytes32(hash, "hash"), rr = as_bytes32(r, "r"), ss = as_bytes32(s, "s");
+  uint8_t out[64];
+  if (secp256k1_recover((const uint8_t*)h.data(), (const uint8_t*)rr.data(), (const uint8_t*)ss.data(), rec, out))
+    return py::none();
+  return py::bytes((const char*)out, 64);
+}
+
+static py::bytes py_sha256(const py::bytes& data) {
+  std::string d = data;
+  uint8_t out[32];
+  sha256_digest((const uint8_t*)d.data(), d.size(), out);
+  return py::bytes((const char*)out, 32);
+}
+
 PYBIND11_MODULE(_native, m) {
+  m.def("secp256k1_sign", &py_secp_sign, "ECDSA sign (RFC 6979, low-s) -> (r, s, recid)");
+  m.def("secp256k1_pubkey", &py_secp_pubkey, "uncompressed public key X||Y");
+  m.def("secp256k1_recover", &py_secp_recover, "ecrecover -> X||Y or None");
+  m.def("sha256", &py_sha256, "SHA-256 (the RFC 6979 HMAC's hash; checked against hashlib)");
   m.doc() = "arbius_amd native CPU runtime (keccak256, PNG, H.264 I_PCM payload)";
   m.def("keccak256", &keccak256, "Ethereum keccak-256");
   m.def("png_encode", &png_encode, py::arg("img"), py::arg("level") = 6, "deterministic filter-0 PNG");

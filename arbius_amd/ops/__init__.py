@@ -334,6 +334,14 @@ def silu(x):
     return ref.silu(x)
 
 
+# --------------------------------------------------------------------------- sampler
+def sampler_step(tasks):
+    """Fused CFG + diffusion-sampler update of a lock-step group (models/schedulers.py)."""
+    if _hip(tasks[0]["x"]):
+        return _lib.sampler_step(tasks)
+    return ref.sampler_step(tasks)
+
+
 def native_loaded() -> bool:
     """True when the HIP kernel library is loaded in this process."""
     return _lib.loaded()

@@ -42,6 +42,7 @@ _SIGS = {
     "arb_gemm_geglu": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p]),
     "arb_temporal_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_void_p]),
     "arb_convgru_gates": (c_int, [c_int] + [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_void_p]),
+    "arb_sampler_step": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
 }
 
 
@@ -415,3 +416,55 @@ def interleave_geglu(t):
     F_ = t.shape[0] // 2
     v, g = t[:F_].reshape(F_ // 8, 8, *t.shape[1:]), t[F_:].reshape(F_ // 8, 8, *t.shape[1:])
     return torch.stack([v, g], dim=1).reshape(t.shape).contiguous()
+
+
+# --------------------------------------------------------------------------- fused CFG + sampler step
+class _SampTask(ctypes.Structure):
+    """Mirror of ``SampTask`` in csrc/sampler.hip (13 pointers, 16 floats, flags)."""
+    _fields_ = ([(n, c_void_p) for n in ("u", "c", "x", "xsrc", "p", "cur", "hs", "h1", "h2", "h3", "noise",
+                                         "xin0", "xin1")]
+                + [(n, c_float) for n in ("g", "he0", "he1", "he2", "he3", "px", "pe", "clampv", "ox", "oe",
+                                          "ox0", "od", "stdv", "logb", "plv", "in_scale")]
+                + [("flags", c_int), ("_pad", c_int)])
+
+
+def sampler_step(tasks):
+    """One launch of the fused CFG + sampler update for up to 8 tasks (dicts from
+    ``models.schedulers.TaskSampler.task_args``).  Shapes / dtypes / contiguity are checked here."""
+    if not 1 <= len(tasks) <= 8:
+        raise ValueError("sampler_step: 1..8 tasks per launch")
+    x0 = tasks[0]["x"]
+    n_pix = x0.numel() // 4
+    cout = tasks[0]["u"].shape[-1]
+    arr = (_SampTask * len(tasks))()
+    for k, a in enumerate(tasks):
+        x = a["x"]
+        if x.dtype != torch.float32 or not x.is_contiguous() or x.numel() != n_pix * 4 or x.shape[-1] != 4:
+            raise ValueError("sampler_step: x must be contiguous fp32 [..., 4] of the group's size")
+        for key in ("u", "c"):
+            t = a[key]
+            if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.numel() != n_pix * cout or t.shape[-1] != cout:
+                raise ValueError(f"sampler_step: {key} must be contiguous bf16 [..., {cout}] matching x")
+        for key in ("xsrc", "p", "cur", "hs", "h1", "h2", "h3", "noise"):
+            t = a.get(key)
+            if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n_pix * 4):
+                raise ValueError(f"sampler_step: {key} must be contiguous fp32 like x")
+        for key in ("xin0", "xin1"):
+            t = a.get(key)
+            if t is not None and (t.dtype != torch.bfloat16 or not t.is_contiguous() or t.numel() != n_pix * 4):
+                raise ValueError(f"sampler_step: {key} must be contiguous bf16 like x")
+        r = arr[k]
+        for key in ("u", "c", "x", "xsrc", "p", "cur", "hs", "h1", "h2", "h3", "noise", "xin0", "xin1"):
+            t = a.get(key)
+            setattr(r, key, t.data_ptr() if t is not None else None)
+        he = a["he"]
+        r.g, r.he0, r.he1, r.he2, r.he3 = a["g"], he[0], he[1], he[2], he[3]
+        r.px, r.pe, r.clampv = a["px"], a["pe"], a["clamp"] or 0.0
+        r.ox, r.oe, r.ox0, r.od, r.stdv = a["ox"], a["oe"], a["ox0"], a["od"], a["std"]
+        lb, plv = a["learned"] if a["learned"] is not None else (0.0, 0.0)
+        r.logb, r.plv, r.in_scale = lb, plv, a["in_scale"]
+        if a["learned"] is not None and cout != 8:
+            raise ValueError("sampler_step: learned variance needs the var channels (cout 8)")
+        r.flags = (int(bool(a["store_x0"])) | int(bool(a["store_cur"])) << 1 | int(a["learned"] is not None) << 2
+                   | int(a["clamp"] is not None) << 3 | int(bool(a["read_p"])) << 4)
+    _check(_fn("arb_sampler_step")(ctypes.cast(arr, c_void_p), len(tasks), n_pix, cout, _stream()), "sampler_step")

@@ -133,3 +133,41 @@ def convgru_gates1(ih, h, cat_buf, cx):
 def convgru_gates2(c, h, z):
     zf = z.float()
     return ((1 - zf) * h.float() + zf * torch.tanh(c.float())).to(h.dtype)
+
+
+def sampler_step(tasks):
+    """fp32 torch form of csrc/sampler.hip (same formula, same order of terms; CPU / A-B path)."""
+    for a in tasks:
+        x = a["x"]
+        u, c = a["u"].float(), a["c"].float()
+        uu, cc = u[..., :4].reshape(x.shape), c[..., :4].reshape(x.shape)
+        e = uu + a["g"] * (cc - uu)
+        he = a["he"]
+        E = he[0] * e
+        for coef, key in zip(he[1:], ("h1", "h2", "h3")):
+            if a.get(key) is not None:
+                E = E + coef * a[key]
+        x0 = a["px"] * x + a["pe"] * E
+        if a["clamp"] is not None:
+            x0 = x0.clamp(-a["clamp"], a["clamp"])
+        out = a["ox"] * a["xsrc"] + a["oe"] * E + a["ox0"] * x0
+        if a["read_p"]:
+            out = out + a["od"] * (x0 - a["p"])
+        if a.get("noise") is not None:
+            if a["learned"] is not None:
+                lb, plv = a["learned"]
+                f = (c[..., 4:].reshape(x.shape) + 1.0) * 0.5
+                std = torch.exp(0.5 * (f * lb + (1.0 - f) * plv))
+            else:
+                std = a["std"]
+            out = out + std * a["noise"]
+        if a.get("hs") is not None:
+            a["hs"].copy_(e)
+        if a["store_x0"]:
+            a["p"].copy_(x0)
+        if a["store_cur"]:
+            a["cur"].copy_(x)
+        x.copy_(out)
+        for key in ("xin0", "xin1"):
+            if a.get(key) is not None:
+                a[key].copy_((out * a["in_scale"]).reshape(a[key].shape).to(a[key].dtype))

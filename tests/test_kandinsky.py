@@ -13,7 +13,7 @@ from arbius_amd import ops
 from arbius_amd.models.kandinsky2 import Kandinsky2Config, Kandinsky2Pipeline
 from arbius_amd.models.layers import init_weights
 from arbius_amd.models.prior import PriorConfig, PriorTransformer
-from arbius_amd.models.schedulers import GaussianDiffusion, space_timesteps
+from arbius_amd.models.schedulers import GaussianDiffusion, TaskSampler, space_timesteps
 from arbius_amd.models.xlmr import MCLIPText, XLMRConfig
 from arbius_amd.node.pool import LocalSolverPool
 
@@ -31,11 +31,15 @@ def test_gaussian_diffusion_last_step_is_mean_and_var_range():
     x = torch.randn(1, 4, 4, 4)
     eps = torch.randn_like(x)
     g = torch.Generator().manual_seed(0)
-    last = sched.step(eps, 9, x, g, var=torch.zeros_like(x))
+    ts = TaskSampler(sched, x, g, "cpu")
+    assert ts.noise.shape[0] == 9                         # no draw at the final (j == 0) step
+    out = torch.cat([eps, torch.zeros_like(eps)], -1)      # eps + learned-variance channels
+    from arbius_amd import ops
+    ops.ref.sampler_step([ts.task_args(9, out, out, 1.0)])
     a = float(sched.ac[0])
     x0 = (x - math.sqrt(1 - a) * eps) / math.sqrt(a)
     # j == 0: ac_prev = 1 -> posterior mean is exactly x0, no noise
-    assert torch.allclose(last, x0, atol=1e-5)
+    assert torch.allclose(ts.x, x0, atol=1e-5)
     # var = +1 -> log beta ; var = -1 -> clipped posterior log variance
     j = 5
     b = float(sched.betas[j])

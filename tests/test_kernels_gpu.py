@@ -4,6 +4,7 @@ import math
 import pytest
 import torch
 
+from arbius_amd import ops
 from arbius_amd.ops import _lib, ref
 
 pytestmark = pytest.mark.gpu
@@ -352,3 +353,47 @@ def test_conv2d_fp16(cuda, B, H, W, Cin, Cout, k, stride):
     assert y.dtype == torch.float16 and tuple(y.shape) == tuple(r.shape)
     assert _rel(y, r) < 5e-3
     assert torch.equal(y, ops.conv2d(x, w, b, stride=stride, padding=k // 2))
+
+
+@pytest.mark.parametrize("name", ["DDIM", "K_EULER", "K_EULER_ANCESTRAL", "DPMSolverMultistep", "PNDM", "KLMS",
+                                  "p_sampler"])
+def test_fused_sampler_hip_vs_fp32_reference(cuda, name):
+    """csrc/sampler.hip (one launch per step for a lock-step group of 3) vs ops.ref.sampler_step
+    (fp32 torch): final latents and every step's bf16 UNet input; bitwise run-to-run."""
+    from arbius_amd.models import schedulers as S
+
+    def run(ref_ops):
+        g = torch.Generator().manual_seed(11)
+        cout = 8 if name == "p_sampler" else 4
+        tasks = []
+        for k in range(3):
+            sched = (S.GaussianDiffusion(6, clamp=2.0) if name == "p_sampler" else S.make_scheduler(name, 7))
+            x = torch.randn(1, 16, 24, 4, generator=g) * sched.init_noise_sigma
+            tasks.append(S.TaskSampler(sched, x, torch.Generator().manual_seed(100 + k), cuda))
+        xin = torch.empty(6, 16, 24, 4, dtype=torch.bfloat16, device=cuda)
+
+        def rows(k, out):
+            return (None if out is None else out[2 * k], None if out is None else out[2 * k + 1],
+                    xin[2 * k], xin[2 * k + 1])
+
+        samp = S.GroupSampler(tasks, [7.5, 3.0, 12.0], xin, rows)
+        ops.set_reference_ops(ref_ops)
+        try:
+            samp.write_input(0)
+            ins = []
+            for i in range(len(tasks[0].plans)):
+                out = (torch.randn(6, 16, 24, cout, generator=g) * 0.5).to(cuda, torch.bfloat16)
+                samp.step(i, out)
+                ins.append(xin.float().clone())
+        finally:
+            ops.set_reference_ops(False)
+        return [t.x.clone() for t in tasks], ins
+
+    a, ai = run(False)
+    b, bi = run(True)
+    a2, _ = run(False)
+    for x, y, z in zip(a, b, a2):
+        assert torch.equal(x, z), "fused sampler must be bitwise deterministic"
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-4 * max(1.0, y.abs().max().item())), (x - y).abs().max()
+    for x, y in zip(ai[:-1], bi[:-1]):
+        assert (x - y).abs().max() <= 0.02 * max(1.0, y.abs().max().item())   # one bf16 ulp at most

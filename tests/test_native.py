@@ -32,3 +32,28 @@ def test_pcm_body_matches_python(hw):
     a = native.pcm_slice_body(f)
     assert a == pcm_slice_body_py(f)
     assert a == native.pcm_slice_body(f, threads=3)      # thread count never changes bytes
+
+
+def test_native_secp256k1_matches_python_reference():
+    """C++ ECDSA (constant-time ladder) == the Python reference: pubkeys, RFC 6979 signatures
+    (r, s, recid) and ecrecover, on random keys / digests and edge scalars."""
+    import os as _os
+    import random
+
+    from arbius_amd import native
+    from arbius_amd.chain import secp256k1 as S
+    if not (native.loaded and hasattr(native, "secp256k1_sign")):
+        import pytest
+        pytest.skip("native extension not built")
+    rng = random.Random(7)
+    keys = [1, 2, 3, S.N - 1, S.N - 2, 0xac0974bec39a17e36ba4a6b4d238ff944bacb478cbed5efcae784d7bf4f2ff80]
+    keys += [rng.randrange(1, S.N) for _ in range(40)]
+    for d in keys:
+        assert S.pubkey(d) == S.py_pubkey(d)
+        for h in (bytes(32), b"\xff" * 32, _os.urandom(32), rng.randbytes(32)):
+            got = S.sign(h, d)
+            assert got == S.py_sign(h, d)
+            assert S.recover(h, *got) == S.py_recover(h, *got) == S.py_pubkey(d)
+    # hardhat account 0 (miner/test/utils.test.ts:18)
+    assert S.address_from_priv(keys[5]).lower() == "0xf39fd6e51aad88f6f4ce6ab8827279cfffb92266"
+    assert native.secp256k1_recover(b"\x01" * 32, bytes(32), b"\x01" * 32, 0) is None   # r = 0
