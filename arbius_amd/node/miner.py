@@ -141,6 +141,17 @@ class Miner:
             log.warning("Task (%s) hydration error %s", taskid, msg)
             self.db.store_invalid_task(taskid)
             return None
+        for row in template.get("input", []):
+            if row.get("type") == "file" and inp.get(row["variable"]):
+                from ..utils.video_io import VideoSourceError, check_source
+                try:
+                    await asyncio.get_running_loop().run_in_executor(None, check_source, inp[row["variable"]])
+                except VideoSourceError as e:
+                    # untrusted source this node will not read (local file, private address, plain
+                    # http): skip - not invalid, other miners may legitimately read it
+                    log.warning("Task (%s) input %s refused: %s", taskid, row["variable"], e)
+                    self.metrics.inc("tasks_refused_source")
+                    return None
         inp["seed"] = taskid2seed(taskid)
         self.db.store_task_input(taskid, cid, inp)
         self.queue("pinTaskInput", 10, 0, True, {"taskid": taskid, "input": pre_str})

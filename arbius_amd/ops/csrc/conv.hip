@@ -1155,10 +1155,14 @@ static const std::vector<PinnedPlan>& env_plans() {
   return plans;
 }
 
+// cfg ids: 0..9 LDS-DMA 4-wave, 10..19 register-staged 4-wave, 20..23 8-wave LDS-DMA 2-stage,
+// 24..27 persistent short-K, 28..31 8-wave LDS-DMA 3-stage ring (two K-tiles in flight)
+static inline bool is_persist(int cfg) { return cfg >= 24 && cfg < 28; }
+
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
-  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 28))) {
-    if (want_cfg >= 24) return {want_cfg, 1, ktiles};   // persistent: no split-K
+  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 32))) {
+    if (is_persist(want_cfg)) return {want_cfg, 1, ktiles};   // persistent: no split-K
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
     const int per = (ktiles + split - 1) / split;
@@ -1167,7 +1171,7 @@ static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split
   for (const PinnedPlan& pp : env_plans()) {
     if (pp.M == M && pp.N == N && pp.K == K) {
       const int per = (ktiles + pp.split - 1) / pp.split;
-      return {pp.cfg, pp.cfg >= 24 ? 1 : (ktiles + per - 1) / per, pp.cfg >= 24 ? ktiles : per};
+      return {pp.cfg, is_persist(pp.cfg) ? 1 : (ktiles + per - 1) / per, is_persist(pp.cfg) ? ktiles : per};
     }
   }
   for (const PinnedPlan& pp : kPinnedPlans) {
@@ -1320,9 +1324,8 @@ struct BigCfg {
 static const BigCfg kBigCfgs[] = {{256, 256}, {320, 128}, {256, 128}, {320, 192}};
 static_assert(sizeof(kBigCfgs) / sizeof(kBigCfgs[0]) == 4, "conv_plan accepts cfg 20..23");
 
-template <int BN, int BM, int WN, int WM>
+template <int BN, int BM, int WN, int WM, int NS = 2>
 static void launch_big(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
-  constexpr int NS = 2;
   static_assert(NS * (BN + BM) * 64 * 2 <= 160 * 1024, "LDS");
   ConvArgs p = a;
   p.tiles_n = (p.N + BN - 1) / BN;
@@ -1415,9 +1418,19 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
   ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
   if (geglu) {
     if (Cout % 16 != 0 || temb != nullptr || res != nullptr || norm != nullptr) return -1;
-    if (pl.cfg >= 24) pl = {kNumCfgs + 5, 1, a.ktiles};   // persistent kernel has no GEGLU epilogue
+    if (is_persist(pl.cfg)) pl = {kNumCfgs + 5, 1, a.ktiles};   // persistent kernel has no GEGLU epilogue
   }
   if (pl.split > 1 && ws == nullptr) return -3;
+  if (pl.cfg >= 28) {   // 8-wave 3-stage LDS-DMA ring (bf16, no norm prologue)
+    if (EL != 0 || a.norm != nullptr) return -4;
+    switch (pl.cfg - 28) {
+      case 0: launch_big<128, 256, 2, 4, 3>(a, pl, stream); break;
+      case 1: launch_big<256, 128, 4, 2, 3>(a, pl, stream); break;
+      case 2: launch_big<192, 192, 2, 4, 3>(a, pl, stream); break;
+      default: launch_big<320, 64, 4, 2, 3>(a, pl, stream); break;
+    }
+    return (int)hipGetLastError();
+  }
   if (pl.cfg >= 24) {   // persistent short-K tiles (bf16, no norm prologue, no split)
     if (EL != 0 || a.norm != nullptr) return -4;
     switch (pl.cfg - 24) {

@@ -178,12 +178,18 @@ def run(args):
         futs = [ex.submit(one_task, i * C + j, forks[j]) for j in range(C)]
         return [f.result() for f in futs][-1]
 
+    def progress(msg):      # stderr heartbeat: long steps (video models) must not look hung
+        print(f"[bench rank {rank}] {msg} ({time.perf_counter() - t_start:.1f} s)", file=sys.stderr, flush=True)
+
+    t_start = time.perf_counter()
     for i in range(args.warmup):
         if ex is None:
             one_task(-1 - i)
         else:               # capture every fork's graphs once, one after the other
             for j in range(C):
                 one_task(-1 - i * C - j, forks[j])
+                progress(f"warmup {i} slot {j} done")
+        progress(f"warmup {i} done")
     lat.clear()
     sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
     D.barrier(dev)
@@ -192,6 +198,7 @@ def run(args):
     last = None
     for i in range(args.steps):
         last = one_step(i)
+        progress(f"step {i} done")
     sync()
     D.barrier(dev)
     elapsed = time.perf_counter() - t0

@@ -86,13 +86,16 @@ def read_table(path):
 
 def candidates(M, N, K, mode):
     """(cfg, split) pairs worth timing: split-K only when the grid is short of 2 waves."""
-    big = list(range(20, 20 + len(KBIG))) + list(range(24, 24 + len(KPERSIST)))
-    cfgs = {"legacy": range(10, NCFG), "big": big, "glds": list(range(10)) + big}.get(mode, list(range(NCFG)) + big)
+    deep = list(range(28, 28 + len(KDEEP)))
+    big = list(range(20, 20 + len(KBIG))) + list(range(24, 24 + len(KPERSIST))) + deep
+    cfgs = {"legacy": range(10, NCFG), "big": big, "glds": list(range(10)) + big, "deep": deep}.get(
+        mode, list(range(NCFG)) + big)
     for cfg in cfgs:
-        bn, bm = KPERSIST[cfg - 24] if cfg >= 24 else KBIG[cfg - 20] if cfg >= 20 else KCFG[cfg % 10]
+        bn, bm = (KDEEP[cfg - 28] if cfg >= 28 else KPERSIST[cfg - 24] if cfg >= 24 else KBIG[cfg - 20]
+                  if cfg >= 20 else KCFG[cfg % 10])
         if cfg >= 20 and bn > N + N // 2:
             continue
-        if cfg >= 24:      # persistent short-K kernel: no split-K
+        if 24 <= cfg < 28:      # persistent short-K kernel: no split-K
             if K <= 2560:
                 yield cfg, 1
             continue
@@ -106,6 +109,7 @@ def candidates(M, N, K, mode):
 KCFG = [(128, 128), (64, 128), (128, 64), (64, 64), (160, 64), (160, 128), (320, 32), (256, 64), (128, 256), (64, 256)]
 KBIG = [(256, 256), (320, 128), (256, 128), (320, 192)]
 KPERSIST = [(128, 128), (256, 128), (160, 128), (128, 64)]
+KDEEP = [(128, 256), (256, 128), (192, 192), (320, 64)]     # 8-wave, 3-stage ring
 
 
 def _agrees(y, ref):
@@ -188,7 +192,7 @@ def main():
         auto = _lib.conv_plan(B, H, W, C, Co, 31 if kw != kh else kh, pad, up, st)
         y_ref = _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st)
         t_auto = graph_time(lambda: _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st))
-        best = (t_auto, auto[0], auto[1]) if mode in ("big", "glds") else None
+        best = (t_auto, auto[0], auto[1]) if mode in ("big", "glds", "deep") else None
         for cfg, sp in candidates(M, Co, K, mode):
             if True:
                 try:
@@ -219,7 +223,7 @@ def main():
         b = torch.randn(N, device=dev).bfloat16()
         r = torch.randn(M, N, device=dev).bfloat16() if has_res else None
         y_ref = _lib.gemm(x, w, b, r)
-        best = (graph_time(lambda: _lib.gemm(x, w, b, r)), *pinned.get((M, N, K), (-1, 1))) if mode in ("big", "glds") else None
+        best = (graph_time(lambda: _lib.gemm(x, w, b, r)), *pinned.get((M, N, K), (-1, 1))) if mode in ("big", "glds", "deep") else None
         for cfg, sp in candidates(M, N, K, mode):
             if True:
                 try:

@@ -105,7 +105,7 @@ def test_hung_worker_is_killed_and_failed_over(monkeypatch):
     monkeypatch.setenv("ARBIUS_FAULT_INJECTION", "1")       # inherited by the spawned workers
 
     async def go():
-        pool = MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, hang_timeout=3.0)
+        pool = MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, hang_timeout=20.0)
         try:
             ok = await asyncio.wait_for(pool.solve(SD, "t0", INP), 300)
             with pytest.raises(RuntimeError):

@@ -1,5 +1,6 @@
 """Robust video matting (BASELINE config #5) on CPU: recurrence semantics,
 time-batched chunks == frame-by-frame, output types, MP4 input/output, node run."""
+import pytest
 import asyncio
 import json
 
@@ -41,25 +42,68 @@ def test_chunking_does_not_change_output():
 
 def test_output_types_and_mp4_io(tmp_path):
     frames = np.random.default_rng(2).integers(0, 256, (3, 64, 96, 3), dtype=np.uint8)
-    p = tmp_path / "in.mp4"
-    p.write_bytes(encode_mp4(list(frames), 10))
-    dec, fps = load_video(str(p))
+    import base64
+    src = "data:video/mp4;base64," + base64.b64encode(encode_mp4(list(frames), 10)).decode()
+    dec, fps = load_video(src)
     assert dec.shape == frames.shape and fps == 10
     pipe = RVMPipeline(RVMConfig.tiny())
     alpha = pipe(dec, "alpha-mask")
     assert (alpha[..., 0] == alpha[..., 1]).all()
-    sol = pipe.solve({"input_video": str(p), "output_type": "green-screen"})
-    sol2 = pipe.solve({"input_video": str(p), "output_type": "green-screen"})
+    sol = pipe.solve({"input_video": src, "output_type": "green-screen"})
+    sol2 = pipe.solve({"input_video": src, "output_type": "green-screen"})
     assert sol.files[0][0] == "out-1.mp4" and sol.cid == sol2.cid
 
 
 def test_rvm_through_node(tmp_path):
     frames = np.random.default_rng(3).integers(0, 256, (2, 48, 64, 3), dtype=np.uint8)
-    p = tmp_path / "v.mp4"
-    p.write_bytes(encode_mp4(list(frames), 5))
+    import base64
+    src = "data:video/mp4;base64," + base64.b64encode(encode_mp4(list(frames), 5)).decode()
     e, tok, mid = make_world("robust_video_matting")
     pool = LocalSolverPool("cpu", tiny=True)
     m = make_miner(e, mid, pool, model="robust_video_matting")
-    tid = asyncio.run(_full_cycle(e, mid, m, {"input_video": str(p), "output_type": "alpha-mask"}))
+    tid = asyncio.run(_full_cycle(e, mid, m, {"input_video": src, "output_type": "alpha-mask"}))
     row = json.loads(m.db.get_task_input(tid, e.tasks[tid].cid)["data"])
     assert pool.solve_sync(m.models[mid.lower()], tid, row).cid == e.solutions[tid].cid
+
+
+@pytest.mark.parametrize("ref", ["/etc/passwd", "file:///etc/passwd", "http://example.com/a.mp4",
+                                 "https://127.0.0.1/a.mp4", "https://localhost:8335/api/jobs/get",
+                                 "https://169.254.169.254/latest/meta-data", "https://10.1.2.3/v.mp4",
+                                 "https://[::1]/v.mp4", "https://user:pw@example.com/v.mp4", "ipfs://not-a-cid", ""])
+def test_untrusted_video_sources_refused(ref):
+    from arbius_amd.utils.video_io import VideoSourceError, check_source, fetch
+    with pytest.raises(VideoSourceError):
+        check_source(ref)
+    with pytest.raises(VideoSourceError):
+        fetch(ref)
+
+
+def test_allowed_video_sources_classified():
+    from arbius_amd.utils.video_io import check_source
+    assert check_source("ipfs://QmYwAPJzv5CZsnA625s3Xf2nemtYgPpHdWEz79ojWnPbdG") == "ipfs"
+    assert check_source("QmYwAPJzv5CZsnA625s3Xf2nemtYgPpHdWEz79ojWnPbdG") == "ipfs"
+    assert check_source("data:video/mp4;base64,AAAA") == "data"
+
+
+def test_miner_skips_task_with_refused_video_source():
+    """An on-chain input_video pointing at a local file / private host is neither solved nor
+    marked invalid (no contest on a source-policy decision)."""
+    import asyncio
+    from arbius_amd.node.pool import FakeSolverPool
+    from test_node_e2e import make_miner, make_world, submit
+    e, tok, mid = make_world("robust_video_matting")
+    pool = FakeSolverPool()
+    m = make_miner(e, mid, pool, model="robust_video_matting")
+
+    async def go():
+        await m.boot()
+        await m.poll_events()
+        await m.drain()
+        tid = submit(e, mid, {"input_video": "https://169.254.169.254/latest/meta-data"})
+        await m.poll_events()
+        await m.drain()
+        return tid
+
+    tid = asyncio.run(go())
+    assert pool.calls == [] and m.db.get_invalid_task(tid) is None
+    assert m.metrics.counters.get("tasks_refused_source") == 1
