@@ -81,7 +81,18 @@ FUNCS: Dict[str, Tuple[str, List[str]]] = {
 
 
 # the 10 uint256 parameter setters / getters (EngineV1.sol:313-383)
-ENGINE_PARAMS = ['validatorMinimumPercentage', 'slashAmountPercentage', 'solutionFeePercentage', 'retractionFeePercentage', 'treasuryRewardPercentage', 'minClaimSolutionTime', 'minRetractionWaitTime', 'minContestationVotePeriodTime', 'maxContestationValidatorStakeSince', 'exitValidatorMinUnlockTime']
+ENGINE_PARAMS = [
+    'validatorMinimumPercentage',
+    'slashAmountPercentage',
+    'solutionFeePercentage',
+    'retractionFeePercentage',
+    'treasuryRewardPercentage',
+    'minClaimSolutionTime',
+    'minRetractionWaitTime',
+    'minContestationVotePeriodTime',
+    'maxContestationValidatorStakeSince',
+    'exitValidatorMinUnlockTime',
+]
 for _p in ENGINE_PARAMS:
     FUNCS["set" + _p[0].upper() + _p[1:]] = ("set" + _p[0].upper() + _p[1:] + "(uint256)", [])
     FUNCS[_p] = (_p + "()", ["uint256"])

@@ -11,7 +11,7 @@ Amounts are integers in wei (18 decimals).  Addresses are lowercase 0x-hex.
 from __future__ import annotations
 
 import itertools
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 from ..utils.keccak import keccak256
@@ -455,7 +455,8 @@ class MockEngine:
         self._emit("TaskSubmitted", tx, id=tid, model=model, fee=int(fee), sender=_addr(sender))
         self.tasks[tid] = task
         self.prevhash = tid
-        self._tx_inputs[tx] = ("submitTask", (int(version), _addr(owner), model, int(fee), bytes(input_)), _addr(sender))
+        args = (int(version), _addr(owner), model, int(fee), bytes(input_))
+        self._tx_inputs[tx] = ("submitTask", args, _addr(sender))
         return tid
 
     @property

@@ -20,7 +20,7 @@ from . import abi
 import re
 
 from .engine_abi import ENGINE_PARAMS, FUNCS, encode_log
-from .mock_engine import MockEngine, MockToken, Revert
+from .mock_engine import MockEngine, Revert
 from .tx import decode_raw_tx
 
 TOKEN_ADDRESS = "0xe3dbc4f88eaa632ddf9708732e2832eeaa6688ab"
@@ -322,7 +322,7 @@ def main(argv=None):
     node = MockNode()
     if a.deploy:
         import json
-        print(json.dumps(deploy_basic(node, a.deploy, governance=a.governance), indent=2), flush=True)
+        print(json.dumps(deploy_basic(node, a.deploy, governance=a.governance), indent=2), flush=True)  # noqa: T201
     web.run_app(node.app(), host=a.host, port=a.port)
 
 

@@ -14,7 +14,7 @@ from typing import List, Optional
 
 from . import abi, secp256k1
 from .client import ChainClient, ChainEvent, TxError
-from .engine_abi import EVENTS, FUNCS, TOPIC_TO_EVENT, decode_log
+from .engine_abi import FUNCS, TOPIC_TO_EVENT, decode_log
 from .tx import Tx
 
 log = logging.getLogger("arbius.chain")

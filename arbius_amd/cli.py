@@ -67,7 +67,7 @@ def build_pool(cfg, models):
         return ReplicateSolverPool(cfg.ml.replicate.api_token)
     import torch
     names = sorted({m.name for m in models.values()})
-    n = cfg.mi355x.gpus if cfg.mi355x.gpus is not None else (torch.cuda.device_count() if torch.cuda.is_available() else 0)
+    n = cfg.mi355x.gpus if cfg.mi355x.gpus is not None else torch.cuda.device_count()
     if n > 1:
         from .parallel.workers import MultiGPUSolverPool
         return MultiGPUSolverPool(n, names, "cuda", streams_per_gpu=cfg.mi355x.workers_per_gpu,
@@ -231,7 +231,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser(prog="arbius_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
     p = sub.add_parser("start"); p.add_argument("config")
-    p = sub.add_parser("mock-node"); p.add_argument("--host", default="127.0.0.1"); p.add_argument("--port", type=int, default=8545)
+    p = sub.add_parser("mock-node")
+    p.add_argument("--host", default="127.0.0.1")
+    p.add_argument("--port", type=int, default=8545)
     sub.add_parser("gen-wallet")
     p = sub.add_parser("cid"); p.add_argument("file"); p.add_argument("--wrap", default=None)
     p = sub.add_parser("decode-calldata"); p.add_argument("data")

@@ -21,7 +21,7 @@ import os
 
 import hashlib
 from dataclasses import dataclass
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, Sequence, Tuple
 
 CHUNK = 262144
 MAX_LINKS = 174

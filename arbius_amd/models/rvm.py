@@ -18,10 +18,9 @@ place by the gate kernel.  BatchNorm is folded into conv biases (inference).
 """
 from __future__ import annotations
 
-import math
 import time
-from dataclasses import dataclass, field
-from typing import List, Optional, Tuple
+from dataclasses import dataclass
+from typing import List, Tuple
 
 import numpy as np
 import torch

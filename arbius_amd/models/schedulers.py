@@ -22,7 +22,7 @@ external Cog containers is "parity unpinned" (the reference ships no container o
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
 import numpy as np

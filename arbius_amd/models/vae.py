@@ -11,7 +11,6 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Tuple
 
-import torch
 import torch.nn as nn
 
 from .. import ops

@@ -279,7 +279,8 @@ def load_native(pipe, weights_dir: str):
         target = dict(mod.named_parameters())
         if set(state) != set(target):
             raise KeyError(f"{name}.safetensors: names differ from the engine module "
-                           f"(missing {sorted(set(target) - set(state))[:3]}, extra {sorted(set(state) - set(target))[:3]})")
+                           f"(missing {sorted(set(target) - set(state))[:3]}, "
+                           f"extra {sorted(set(state) - set(target))[:3]})")
         for k, v in state.items():
             if tuple(v.shape) != tuple(target[k].shape):
                 raise ValueError(f"{name}.{k}: shape {tuple(v.shape)} != {tuple(target[k].shape)}")
@@ -358,7 +359,7 @@ def main(argv: Optional[List[str]] = None):
     from .registry import build_pipeline
     pipe = build_pipeline(a.model, device="cpu", init=False, weights_dir=a.src)
     save_native(pipe, a.dst)
-    print(f"wrote {sorted(pipe.modules())} to {a.dst}")
+    print(f"wrote {sorted(pipe.modules())} to {a.dst}")  # noqa: T201 (CLI output)
 
 
 if __name__ == "__main__":

@@ -16,7 +16,6 @@ from __future__ import annotations
 import hashlib
 import re
 from dataclasses import dataclass
-from pathlib import Path
 from typing import List, Optional, Tuple
 
 import torch

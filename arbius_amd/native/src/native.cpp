@@ -38,7 +38,8 @@ static const uint64_t RC[24] = {
     0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
     0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
     0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
-static const int ROTC[25] = {0, 36, 3, 41, 18, 1, 44, 10, 45, 2, 62, 6, 43, 15, 61, 28, 55, 25, 21, 56, 27, 20, 39, 8, 14};  // [x*5+y]
+static const int ROTC[25] = {0, 36, 3, 41, 18, 1, 44, 10, 45, 2, 62, 6, 43,   // [x*5+y]
+                             15, 61, 28, 55, 25, 21, 56, 27, 20, 39, 8, 14};
 
 static inline uint64_t rol(uint64_t x, int n) { return n ? (x << n) | (x >> (64 - n)) : x; }
 

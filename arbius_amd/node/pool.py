@@ -13,7 +13,7 @@ import asyncio
 import hashlib
 import queue
 import threading
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict
 
 import numpy as np
 

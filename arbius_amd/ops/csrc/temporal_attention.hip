@@ -90,7 +90,8 @@ __global__ void __launch_bounds__(256) temporal_attn_kernel(TAArgs a) {
     for (int kt = 0; kt < NKT; ++kt) {
       sc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][ks], qf[ks], sc[kt], 0, 0, 0);
+      for (int ks = 0; ks < KS; ++ks)
+        sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][ks], qf[ks], sc[kt], 0, 0, 0);
     }
     // sc[kt][r] = S^T[key = kt*16 + 4g + r][query = qt*16 + r16]
     float mx = -INFINITY;
@@ -163,7 +164,10 @@ ARB_API int arb_temporal_attention(const void* q, const void* k, const void* v, 
   if (blocks > 0x7fffffffL) return -2;
   const int kt32 = (F + 31) / 32;
 #define TA_CASE(KT, DDV) \
-  if (kt32 == KT && D == DDV) { temporal_attn_kernel<KT, DDV><<<(unsigned)blocks, 256, 0, stream>>>(a); return (int)hipGetLastError(); }
+  if (kt32 == KT && D == DDV) {                                                  \
+    temporal_attn_kernel<KT, DDV><<<(unsigned)blocks, 256, 0, stream>>>(a);      \
+    return (int)hipGetLastError();                                                \
+  }
   TA_CASE(1, 64) TA_CASE(2, 64) TA_CASE(3, 64)
   TA_CASE(1, 32) TA_CASE(2, 32) TA_CASE(3, 32)
   TA_CASE(1, 128) TA_CASE(2, 128) TA_CASE(3, 128)

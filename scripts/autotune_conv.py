@@ -206,7 +206,8 @@ def main():
                 if best is None or t < best[0]:
                     best = (t, cfg, sp)
         fl = 2.0 * M * Co * K
-        rec = {"kind": "conv", "shape": [B, H, W, C, Co, kh, kw, pad, up, st], "MNK": [M, Co, K], "best_us": round(best[0], 2),
+        rec = {"kind": "conv", "shape": [B, H, W, C, Co, kh, kw, pad, up, st], "MNK": [M, Co, K],
+               "best_us": round(best[0], 2),
                "best_cfg": best[1], "best_split": best[2], "best_tflops": round(fl / best[0] / 1e6, 1),
                "auto_cfg": auto, "auto_us": round(t_auto, 2)}
         results.append(rec)
@@ -223,7 +224,9 @@ def main():
         b = torch.randn(N, device=dev).bfloat16()
         r = torch.randn(M, N, device=dev).bfloat16() if has_res else None
         y_ref = _lib.gemm(x, w, b, r)
-        best = (graph_time(lambda: _lib.gemm(x, w, b, r)), *pinned.get((M, N, K), (-1, 1))) if mode in ("big", "glds", "deep") else None
+        best = None
+        if mode in ("big", "glds", "deep"):
+            best = (graph_time(lambda: _lib.gemm(x, w, b, r)), *pinned.get((M, N, K), (-1, 1)))
         for cfg, sp in candidates(M, N, K, mode):
             if True:
                 try:
@@ -238,8 +241,10 @@ def main():
         t_blas = graph_time(lambda: torch.addmm(r, x, w.t()).add_(b)) if has_res else graph_time(
             lambda: torch.nn.functional.linear(x, w, b))
         fl = 2.0 * M * N * K
-        rec = {"kind": "gemm_res" if has_res else "gemm", "MNK": [M, N, K], "best_us": round(best[0], 2), "best_cfg": best[1],
-               "best_split": best[2], "best_tflops": round(fl / best[0] / 1e6, 1), "hipblaslt_addmm_add_us": round(t_blas, 2)}
+        rec = {"kind": "gemm_res" if has_res else "gemm", "MNK": [M, N, K], "best_us": round(best[0], 2),
+               "best_cfg": best[1],
+               "best_split": best[2], "best_tflops": round(fl / best[0] / 1e6, 1),
+               "hipblaslt_addmm_add_us": round(t_blas, 2)}
         results.append(rec)
         if best[1] >= 0 and (M, N, K) not in {tuple(r["MNK"]) for r in results if r["kind"] == "conv"}:
             pinned[(M, N, K)] = (best[1], best[2])

@@ -5,8 +5,8 @@ import pytest
 
 from arbius_amd.chain import abi
 from arbius_amd.chain.mock_engine import E18, ZERO32, MockEngine, Revert
-from arbius_amd.chain.mock_governance import (ACTIVE, CANCELED, CANCELLER_ROLE, DEFEATED, EXECUTED, PENDING, PROPOSER_ROLE,
-                                              QUEUED, SUCCEEDED, TIMELOCK_ADMIN_ROLE, MockBaseToken,
+from arbius_amd.chain.mock_governance import (ACTIVE, CANCELED, CANCELLER_ROLE, DEFEATED, EXECUTED, PENDING,
+                                              PROPOSER_ROLE, QUEUED, SUCCEEDED, TIMELOCK_ADMIN_ROLE, MockBaseToken,
                                               deploy_governance)
 from arbius_amd.chain.secp256k1 import address_from_priv, sign
 from arbius_amd.ipfs.unixfs import onchain_cid

@@ -6,7 +6,6 @@ import json
 import math
 
 import numpy as np
-import pytest
 import torch
 
 from arbius_amd import ops

@@ -2,7 +2,6 @@
 windowed event back-fill, ambiguous-input handling, lease heartbeats, GPU-worker hang
 detection, and weights_dir plumbing through the one-process-per-device pool."""
 import asyncio
-import os
 
 import pytest
 

@@ -35,3 +35,12 @@ def test_selftest_table_pinned_for_this_numerics_version():
     t = json.load(open(os.path.join(os.path.dirname(miner.__file__), "..", "config", "selftest.json")))
     assert t["numerics_version"] == numerics.NUMERICS_VERSION
     assert t["kandinsky2"]["expected"]["gfx950/random-init-seed0"].startswith("0x1220")
+
+
+def test_repository_lint_clean():
+    """scripts/lint.py (the CI lint step): syntax, unused imports, whitespace, line length."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "lint.py")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:]

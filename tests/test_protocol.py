@@ -80,7 +80,8 @@ def test_seed():
 
 
 @pytest.mark.parametrize("sig,topic", [
-    ("TaskSubmitted(bytes32,bytes32,uint256,address)", "0xc3d3e0544c80e3bb83f62659259ae1574f72a91515ab3cae3dd75cf77e1b0aea"),
+    ("TaskSubmitted(bytes32,bytes32,uint256,address)",
+     "0xc3d3e0544c80e3bb83f62659259ae1574f72a91515ab3cae3dd75cf77e1b0aea"),
 ])
 def test_event_topics(sig, topic):
     assert abi.topic(sig) == topic

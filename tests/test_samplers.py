@@ -3,12 +3,10 @@ ops/csrc/sampler.hip) reproduces every textbook sampler step by step: DDIM (eta 
 Euler, Euler-ancestral, DPM-Solver++(2M), PNDM/PLMS, k-LMS and p_sample (eps / x0 prediction,
 learned variance, clamp), including the order in which ancestral noise is drawn from the task's
 generator and classifier-free guidance on separate uncond / cond rows."""
-import math
 
 import pytest
 import torch
 
-from arbius_amd import ops
 from arbius_amd.models import schedulers as S
 from oracles import step_samplers as O
 

@@ -58,7 +58,8 @@ def test_two_task_streams_per_worker():
         pool = MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, streams_per_gpu=2)
         try:
             assert pool.capacity == 2
-            a, b = await asyncio.gather(pool.solve(MODEL, "a", dict(INP, seed=1)), pool.solve(MODEL, "b", dict(INP, seed=2)))
+            a, b = await asyncio.gather(pool.solve(MODEL, "a", dict(INP, seed=1)),
+                                        pool.solve(MODEL, "b", dict(INP, seed=2)))
             assert [a.cid, b.cid] == ref
         finally:
             await pool.close()
