@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .layers import Conv2d, GroupNorm, Linear, timestep_embedding
+from .layers import Conv2d, GroupNorm, LayerNorm, Linear, timestep_embedding
 
 
 @dataclass
@@ -122,6 +122,7 @@ class GlideUNet(nn.Module):
         self.img_tokens = Linear(cfg.image_embed_dim, cfg.image_tokens * cfg.encoder_channels)
         self.text_proj = Linear(cfg.text_dim, cfg.encoder_channels)
         self.text_pool = Linear(cfg.pooled_dim, ed)
+        self.text_norm = LayerNorm(ed)                  # diffusers add_embedding.text_norm (ln_model_n)
         self.conv_in = Conv2d(cfg.in_channels, mc, 3)
         self.down = nn.ModuleList()
         chans = [mc]
@@ -172,7 +173,8 @@ class GlideUNet(nn.Module):
             t = t.expand(B)
         emb = timestep_embedding(t, self.cfg.model_channels).to(x.dtype)
         emb = self.time2(ops.silu(self.time1(emb)))
-        emb = emb + self.img_emb(image_embed) + self.text_pool(text_pooled)
+        # time + (image_proj(image) + LN(text_proj(pooled text)))  (diffusers TextImageTimeEmbedding)
+        emb = emb + (self.img_emb(image_embed) + self.text_norm(self.text_pool(text_pooled)))
         emb_act = ops.silu(emb)
         itok = self.img_tokens(image_embed).view(B, self.cfg.image_tokens, self.cfg.encoder_channels)
         ctx = torch.cat([itok, self.text_proj(text_tokens)], dim=1)

@@ -18,8 +18,9 @@ _WORD = re.compile(r"[a-z]+|[0-9]|[^\sa-z0-9]+")
 
 
 # where checkpoint directories keep their tokenizer files: the root, the diffusers ``tokenizer/``
-# folder, or a per-tower folder of a multi-encoder pipeline (Kandinsky 2: CLIP + XLM-R)
-TOKENIZER_SUBDIRS = ("", "tokenizer", "clip_tokenizer", "tokenizer_clip", "text_encoder")
+# folder, or a per-tower folder of a multi-encoder pipeline (Kandinsky 2: XLM-R in tokenizer/,
+# CLIP in the prior checkout's prior/tokenizer/)
+TOKENIZER_SUBDIRS = ("", "tokenizer", "clip_tokenizer", "tokenizer_clip", "prior/tokenizer", "text_encoder")
 
 
 def find_file(root: Optional[str], name: str, subdirs=TOKENIZER_SUBDIRS) -> Optional[Path]:

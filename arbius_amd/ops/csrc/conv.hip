@@ -1422,6 +1422,9 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
     if (Cout % 16 != 0 || temb != nullptr || res != nullptr || norm != nullptr) return -1;
     if (is_persist(pl.cfg)) pl = {kNumCfgs + 5, 1, a.ktiles};   // persistent kernel has no GEGLU epilogue
   }
+  // The 8-wave / persistent families have no GroupNorm prologue: a normed call on a shape pinned to
+  // one of them runs the register-staged 128x128 tile at the pinned split (same grid coverage).
+  if (norm != nullptr && pl.cfg >= 20) pl = conv_plan(a.M, a.N, a.ktiles, kNumCfgs, is_persist(pl.cfg) ? 1 : pl.split);
   if (pl.split > 1 && ws == nullptr) return -3;
   if (pl.cfg >= 28) {   // 8-wave 3-stage LDS-DMA ring (bf16, no norm prologue)
     if (EL != 0 || a.norm != nullptr) return -4;

@@ -104,7 +104,8 @@ def test_hung_worker_is_killed_and_failed_over(monkeypatch):
     monkeypatch.setenv("ARBIUS_FAULT_INJECTION", "1")       # inherited by the spawned workers
 
     async def go():
-        pool = MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, hang_timeout=20.0)
+        # 45 s: a CPU-contended tiny solve (pytest -n) must not look like a hang
+        pool = MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, hang_timeout=45.0)
         try:
             ok = await asyncio.wait_for(pool.solve(SD, "t0", INP), 300)
             with pytest.raises(RuntimeError):

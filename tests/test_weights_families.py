@@ -1,0 +1,174 @@
+"""Public-checkpoint layouts of every template family (arbius_amd/models/weights.py ``LAYOUTS``):
+Kandinsky 2.1 (diffusers kandinsky-community decoder + prior), the UNet3D text-to-video models
+(zeroscope / damo, diffusers), and Robust Video Matting (upstream rvm_mobilenetv3 state dict,
+BatchNorm folded at load).  diffusers / torchvision are not installed here, so each mapping is
+pinned by an export -> load round trip through the public names (exact tensors), the BatchNorm
+fold and the zero-image embedding by direct numerical checks against torch / transformers.
+Output-byte parity with the reference's containers stays "parity unpinned"."""
+import os
+
+import pytest
+import torch
+
+from arbius_amd.models import weights as W
+from arbius_amd.models.registry import build_pipeline
+
+
+def _params(pipe):
+    return {f"{m}.{k}": v.detach().clone() for m, mod in pipe.modules().items() for k, v in mod.named_parameters()}
+
+
+def _round_trip(model, tmp_path, **kw):
+    a = build_pipeline(model, tiny=True, weight_seed=0, **kw)
+    W.write_public(a, model, str(tmp_path))
+    b = build_pipeline(model, tiny=True, weight_seed=11, weights_dir=str(tmp_path), **kw)
+    pa, pb = _params(a), _params(b)
+    assert pa.keys() == pb.keys()
+    diff = [k for k in pa if not torch.equal(pa[k], pb[k])]
+    assert not diff, diff[:5]
+    return a, b
+
+
+def test_kandinsky2_public_layout_round_trip(tmp_path):
+    _round_trip("kandinsky2", tmp_path)
+    unet = W.read_safetensors(os.path.join(tmp_path, "unet/diffusion_pytorch_model.safetensors"))
+    for k in ("add_embedding.text_norm.weight", "encoder_hid_proj.image_embeds.weight",
+              "down_blocks.1.attentions.0.add_k_proj.weight", "down_blocks.0.downsamplers.0.conv1.weight",
+              "up_blocks.0.upsamplers.0.conv2.weight", "mid_block.attentions.0.group_norm.weight"):
+        assert k in unet, k
+    movq = W.read_safetensors(os.path.join(tmp_path, "movq/diffusion_pytorch_model.safetensors"))
+    assert movq["decoder.up_blocks.0.attentions.0.spatial_norm.conv_y.weight"].dim() == 4     # OIHW on disk
+    assert "decoder.conv_norm_out.norm_layer.weight" in movq and "post_quant_conv.weight" in movq
+    prior = W.read_safetensors(os.path.join(tmp_path, "prior/prior/diffusion_pytorch_model.safetensors"))
+    assert prior["prd_embedding"].dim() == 3 and prior["positional_embedding"].dim() == 3
+    assert "transformer_blocks.0.norm3.weight" in prior and "proj_to_clip_embeddings.weight" in prior
+    clip = W.read_safetensors(os.path.join(tmp_path, "prior/text_encoder/model.safetensors"))
+    assert "text_projection.weight" in clip and "text_model.final_layer_norm.weight" in clip
+    mclip = W.read_safetensors(os.path.join(tmp_path, "text_encoder/model.safetensors"))
+    assert "LinearTransformation.weight" in mclip
+
+
+def test_kandinsky2_missing_module_is_an_error(tmp_path):
+    a = build_pipeline("kandinsky2", tiny=True, weight_seed=0)
+    W.write_public(a, "kandinsky2", str(tmp_path))
+    os.remove(os.path.join(tmp_path, "movq/diffusion_pytorch_model.safetensors"))
+    with pytest.raises(FileNotFoundError, match="movq"):
+        build_pipeline("kandinsky2", tiny=True, weights_dir=str(tmp_path))
+
+
+def test_kandinsky2_zero_image_embedding_from_clip_vision(tmp_path):
+    """No native buffers file: the decoder's unconditional image embedding is the CLIP vision
+    tower's embedding of an all-zero image (diffusers get_zero_embed), computed at load."""
+    transformers = pytest.importorskip("transformers")
+    a = build_pipeline("kandinsky2", tiny=True, weight_seed=0)
+    W.write_public(a, "kandinsky2", str(tmp_path))
+    os.remove(os.path.join(tmp_path, "buffers.safetensors"))
+    d = a.cfg.prior.clip_dim
+    torch.manual_seed(0)
+    vcfg = transformers.CLIPVisionConfig(hidden_size=32, intermediate_size=64, num_hidden_layers=2,
+                                         num_attention_heads=2, image_size=32, patch_size=8, projection_dim=d)
+    vis = transformers.CLIPVisionModelWithProjection(vcfg).eval()
+    vis.save_pretrained(os.path.join(tmp_path, "prior", "image_encoder"), safe_serialization=True)
+    with torch.no_grad():
+        ref = vis(pixel_values=torch.zeros(1, 3, 32, 32)).image_embeds[0]
+    b = build_pipeline("kandinsky2", tiny=True, weight_seed=3, weights_dir=str(tmp_path))
+    assert torch.allclose(b.buffers.zero_img_emb.float(), ref, atol=1e-6)
+
+
+def test_glide_unet_text_norm_is_applied():
+    """add_embedding.text_norm (LayerNorm) sits between the pooled-text projection and the time
+    embedding sum: scaling its weight changes the UNet output."""
+    a = build_pipeline("kandinsky2", tiny=True, weight_seed=0)
+    u = a.unet
+    c = u.cfg
+    x = torch.randn(1, 8, 8, c.in_channels)
+    args = (torch.tensor([10.0]), torch.randn(1, 77, c.text_dim), torch.randn(1, c.pooled_dim),
+            torch.randn(1, c.image_embed_dim))
+    with torch.no_grad():
+        y0 = u(x, *args)
+        u.text_norm.weight.mul_(3.0)
+        y1 = u(x, *args)
+    assert not torch.allclose(y0, y1)
+
+
+@pytest.mark.parametrize("model", ["zeroscopev2xl", "damo"])
+def test_video_unet3d_public_layout_round_trip(model, tmp_path):
+    _round_trip(model, tmp_path)
+    unet = W.read_safetensors(os.path.join(tmp_path, "unet/diffusion_pytorch_model.safetensors"))
+    for k in ("transformer_in.transformer_blocks.0.attn2.to_q.weight", "down_blocks.0.temp_convs.0.conv4.3.weight",
+              "down_blocks.0.temp_attentions.0.proj_in.weight", "mid_block.temp_convs.1.conv1.0.weight",
+              "up_blocks.1.attentions.0.transformer_blocks.0.attn2.to_k.weight"):
+        assert k in unet, k
+    assert unet["down_blocks.0.temp_convs.0.conv1.2.weight"].shape[2:] == (3, 1, 1)      # Conv3d (3,1,1)
+
+
+def test_penultimate_text_tower_accepts_23_layer_export(tmp_path):
+    """zeroscope's diffusers text_encoder keeps 23 of OpenCLIP ViT-H's 24 layers (the last one is
+    never run with the penultimate-layer readout): the engine's unused last layer stays optional."""
+    from arbius_amd.models.clip_text import CLIPTextConfig, CLIPTextEncoder
+    from arbius_amd.models.layers import init_weights
+    cfg = CLIPTextConfig(vocab=1000, width=32, layers=3, heads=2, mlp=64, skip_last=1)
+    enc = init_weights(CLIPTextEncoder(cfg), 0).eval()
+    state = {}
+    for tname, t in enc.named_parameters():
+        for dst, kind, srcs in W._clip_text_rules():
+            m = W._pattern(dst).match(tname)
+            if m:
+                W._from_target(kind, t.detach(), [W._fill(s, m.groups()) for s in srcs], state)
+                break
+    state = {k: v for k, v in state.items() if ".layers.2." not in k}      # the 23-of-24 style export
+    enc2 = CLIPTextEncoder(cfg).eval()
+    src = W._CLIP
+    W.load_state(enc2, W.convert(src.rules(enc2), dict(enc2.named_parameters()), src.rename(state),
+                                 src.optional(enc2)))
+    ids = torch.randint(1, 998, (1, 77))
+    ids[0, 5] = 999
+    with torch.no_grad():
+        assert torch.equal(enc(ids)[0], enc2(ids)[0])
+
+
+def test_rvm_batchnorm_fold_matches_conv_bn():
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(8, 16, 3, padding=1, bias=False).double()
+    bn = torch.nn.BatchNorm2d(16, eps=1e-3).double().eval()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_()
+        bn.running_mean.normal_()
+        bn.running_var.uniform_(0.2, 2.0)
+    w = W._to_target("bnw@0.001", [conv.weight, bn.weight, bn.running_var], conv.weight)
+    b = W._to_target("bnb@0.001", [bn.weight, bn.bias, bn.running_mean, bn.running_var], bn.bias)
+    x = torch.randn(2, 8, 9, 9, dtype=torch.float64)
+    with torch.no_grad():
+        ref = bn(conv(x))
+        got = torch.nn.functional.conv2d(x, w, b, padding=1)
+    assert torch.allclose(got, ref, atol=1e-10)
+
+
+def test_rvm_public_layout_round_trip_safetensors_and_pth(tmp_path):
+    a = build_pipeline("robust_video_matting", tiny=True, weight_seed=0)
+    files = W.export_public(a, "robust_video_matting")
+    (rel, state), = files.items()
+    for k in ("backbone.features.0.1.running_var", "backbone.features.1.block.0.0.weight",
+              "backbone.features.4.block.2.fc1.weight", "aspp.aspp2.1.weight", "decoder.decode4.gru.ih.0.weight",
+              "decoder.decode3.gru.ih.0.bias", "decoder.decode0.conv.3.weight", "project_mat.conv.weight",
+              "refiner.conv.6.bias"):
+        assert k in state, k
+    for fmt in ("safetensors", "pth"):
+        d = tmp_path / fmt
+        d.mkdir()
+        if fmt == "pth":
+            torch.save(state, d / "rvm_mobilenetv3.pth")      # the upstream release format (tensor dict)
+        else:
+            W.write_safetensors(state, str(d / "rvm_mobilenetv3.safetensors"))
+        b = build_pipeline("robust_video_matting", tiny=True, weight_seed=9, weights_dir=str(d))
+        pa, pb = _params(a), _params(b)
+        bad = [k for k in pa if not torch.allclose(pa[k], pb[k], rtol=1e-6, atol=0)]
+        assert not bad, bad[:5]
+
+
+def test_read_checkpoint_refuses_non_tensor_pickles(tmp_path):
+    p = tmp_path / "x.pth"
+    torch.save({"a": torch.zeros(2), "meta": {"lr": 0.1}}, p)
+    with pytest.raises(ValueError):
+        W.read_checkpoint(str(p))
