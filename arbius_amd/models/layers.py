@@ -82,9 +82,10 @@ class GroupNorm(nn.Module):
                               self.silu if silu is None else silu)
 
     def table(self, x, mod=None, one_plus=0.0, silu=None):
-        """(affine table, silu) for a consumer's fused GroupNorm prologue."""
-        return (ops.group_norm_table(x, self.weight, self.bias, self.groups, self.eps, mod, one_plus),
-                self.silu if silu is None else silu)
+        """This GroupNorm of ``x`` for a consumer (``ops.NormSpec``): a fused operand prologue from
+        the (lazily computed) affine table, or one stats + table-apply pass in front of it."""
+        return ops.NormSpec(x, self.weight, self.bias, self.groups, self.eps, mod, one_plus,
+                            self.silu if silu is None else silu)
 
 
 class LayerNorm(nn.Module):

@@ -86,7 +86,10 @@ class ConvAct(nn.Module):
         self.act = act
 
     def forward(self, x):
-        x = _conv(self.conv, x)
+        c = self.conv
+        if c.groups > 1 and c.groups == c.in_channels == c.out_channels:     # depthwise: fused HIP pass
+            return ops.depthwise_conv(x, c.weight, c.bias, c.stride[0], c.dilation[0], self.act)
+        x = _conv(c, x)
         if self.act == "relu":
             return F.relu(x)
         if self.act == "hs":
@@ -249,13 +252,15 @@ class RecurrentDecoder(nn.Module):
 class DeepGuidedFilter(nn.Module):
     def __init__(self, hid=16):
         super().__init__()
-        self.register_buffer("box", torch.full((4, 1, 3, 3), 1.0 / 9.0))
         self.c1 = ConvAct(4 * 2 + hid, hid, 1, act="relu", bias=True)
         self.c2 = ConvAct(hid, hid, 1, act="relu", bias=True)
         self.c3 = nn.Conv2d(hid, 4, 1)
 
     def _boxf(self, x):
-        return F.conv2d(x, self.box.to(x.dtype), padding=1, groups=4)
+        # 3x3 mean with zero padding (RVM's box filter: a ones/9 depthwise conv) as a count-including
+        # average pool: a native NHWC kernel instead of MIOpen's naive path for this 4-channel
+        # depthwise conv (80 us per call at 512x288, profiles/rocprof_r2_rvm.md)
+        return F.avg_pool2d(x, 3, stride=1, padding=1, count_include_pad=True)
 
     def forward(self, fine_src, base_src, base_fgr, base_pha, base_hid):
         fine_x = torch.cat([fine_src, fine_src.mean(1, keepdim=True)], dim=1)

@@ -137,7 +137,10 @@ class VideoPipeline(PipelineBase):
         for i, t in enumerate(sched.timesteps):
             beat()
             tbuf.fill_(float(t))
-            samp.step(i, unet(xin, tbuf, ctx))      # UNet3D, then ONE fused CFG + sampler launch
+            # UNet3D, then ONE fused CFG + sampler launch.  No plan_batch scope here: the video
+            # linears (M = 2F x HW rows) stay on hipBLASLt, measured faster than the implicit-GEMM
+            # kernel's cost-model plans at these shapes (zeroscope 928 vs 693 tasks/h).
+            samp.step(i, unet(xin, tbuf, ctx))
         sync()
         t2 = time.perf_counter()
         frames = self.decode(ts.x)

@@ -40,11 +40,14 @@ MINER_VERSION = 0
 
 
 class Metrics:
-    """Counters / latency samples exported on the RPC server's /metrics route."""
+    """Counters / latency samples exported on the RPC server's /metrics route: a bounded window
+    of samples per latency (p50 / p99 gauges) and a cumulative Prometheus histogram."""
+    BUCKETS = (0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0, 10.0, 30.0, 60.0, 120.0, 300.0, 900.0)
 
     def __init__(self):
         self.counters: Dict[str, int] = {}
         self.latencies: Dict[str, list] = {}
+        self.hist: Dict[str, list] = {}        # name -> [bucket counts..., +Inf count, sum]
 
     def inc(self, name, n=1):
         self.counters[name] = self.counters.get(name, 0) + n
@@ -54,6 +57,24 @@ class Metrics:
         v.append(seconds)
         if len(v) > keep:          # bounded window for the p50/p99 export
             del v[: len(v) - keep]
+        h = self.hist.setdefault(name, [0] * (len(self.BUCKETS) + 1) + [0.0])
+        for i, b in enumerate(self.BUCKETS):
+            if seconds <= b:
+                h[i] += 1
+        h[len(self.BUCKETS)] += 1
+        h[-1] += seconds
+
+    def prometheus_histograms(self):
+        lines = []
+        for k in sorted(self.hist):
+            h = self.hist[k]
+            lines.append(f"# TYPE arbius_{k}_seconds histogram")
+            for i, b in enumerate(self.BUCKETS):
+                lines.append(f'arbius_{k}_seconds_bucket{{le="{b:g}"}} {h[i]}')
+            lines.append(f'arbius_{k}_seconds_bucket{{le="+Inf"}} {h[len(self.BUCKETS)]}')
+            lines.append(f"arbius_{k}_seconds_sum {h[-1]:.6f}")
+            lines.append(f"arbius_{k}_seconds_count {h[len(self.BUCKETS)]}")
+        return lines
 
     def p50(self, name):
         v = sorted(self.latencies.get(name, []))

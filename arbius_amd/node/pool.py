@@ -136,6 +136,19 @@ class LocalSolverPool:
             free.put(pipe)
 
     async def solve(self, model, taskid, inp) -> Solution:
+        import time
+        t0 = time.time()
+        sol = await self._solve(model, taskid, inp)
+        st = self.__dict__.setdefault("_gpu", {"task_s": 0.0, "tasks": 0})
+        st["task_s"] += time.time() - t0
+        st["tasks"] += 1
+        return sol
+
+    def gpu_stats(self):
+        """Solved-task count and summed solve seconds of this process's one device (``/metrics``)."""
+        return {0: dict(self.__dict__.get("_gpu", {"task_s": 0.0, "tasks": 0}))}
+
+    async def _solve(self, model, taskid, inp) -> Solution:
         loop = asyncio.get_running_loop()
         if self.lockstep <= 1:
             return await loop.run_in_executor(None, self.solve_sync, model, taskid, inp)

@@ -113,12 +113,22 @@ def make_app(db, miner=None) -> web.Application:
                     lines.append(f"arbius_{k}_p50 {vals[len(vals) // 2]:.6f}")
                     lines.append(f"arbius_{k}_p99 {vals[min(len(vals) - 1, int(len(vals) * 0.99))]:.6f}")
                     lines.append(f"arbius_{k}_count {len(vals)}")
+            lines.extend(miner.metrics.prometheus_histograms())
         lines.append(f"arbius_jobs_queued {len(db.get_jobs())}")
         if miner is not None:
             pool = getattr(miner, "pool", None)
             lines.append(f"arbius_gpu_workers {int(getattr(pool, 'capacity', 0) or 0)}")
             lines.append(f"arbius_gpu_workers_busy {len(getattr(pool, 'busy', {}) or {})}")
             lines.append(f"arbius_gpu_worker_restarts {int(getattr(pool, 'restarts', 0) or 0)}")
+            per_gpu = getattr(pool, "gpu_stats", None)
+            if callable(per_gpu):
+                stats = per_gpu()
+                lines.append("# TYPE arbius_gpu_task_seconds_total counter")     # summed solve durations
+                lines += [f'arbius_gpu_task_seconds_total{{gpu="{g}"}} {v["task_s"]:.3f}' for g, v in stats.items()]
+                lines.append("# TYPE arbius_gpu_tasks_total counter")
+                lines += [f'arbius_gpu_tasks_total{{gpu="{g}"}} {v["tasks"]}' for g, v in stats.items()]
+        from ..utils.gpu_metrics import gpu_gauges
+        lines.extend(gpu_gauges())
         return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
 
     async def health(_req):

@@ -131,6 +131,30 @@ def linear_geglu(x, w, b=None):
     return geglu(linear(x, w, b))
 
 
+class NormSpec:
+    """A GroupNorm(+scale-shift modulation)(+SiLU) of ``x`` to be applied to a consumer's operand.
+    Iterating the spec yields ``(table, silu)`` with the affine table computed lazily, so a consumer
+    that never needs it (CPU reference paths) never launches the stats kernels.  A fused
+    table-and-apply pass that rebuilt each image's table per block measured slower than
+    stats + table + table-apply (e.g. 39.8 vs 26.6 us at [8, 4096, 320]: the per-block rebuild
+    serialises one partials round trip per group), so the consumer applies the table."""
+    __slots__ = ("x", "gamma", "beta", "groups", "eps", "mod", "one_plus", "silu", "_table")
+
+    def __init__(self, x, gamma, beta, groups, eps, mod=None, one_plus=0.0, silu=False):
+        self.x, self.gamma, self.beta, self.groups, self.eps = x, gamma, beta, groups, eps
+        self.mod, self.one_plus, self.silu, self._table = mod, one_plus, silu, None
+
+    def table(self):
+        if self._table is None:
+            self._table = group_norm_table(self.x, self.gamma, self.beta, self.groups, self.eps, self.mod,
+                                           self.one_plus)
+        return self._table
+
+    def __iter__(self):
+        yield self.table()
+        yield self.silu
+
+
 def _gemm_ok(K, N):
     return K % 64 == 0 and N % 8 == 0
 
@@ -223,6 +247,30 @@ def _padded_conv(x, w, b, padding, upsample, residual, temb, stride, table=None,
         return y.contiguous()
     return _lib.conv2d_nhwc(x, wp, bp, padding, upsample, residual, temb, stride, norm=table, norm_silu=nsilu,
                             plan_b=_canon_batch(x.shape[0]))
+
+
+_DW_W = {}
+
+
+def depthwise_conv(x, weight, bias, stride=1, dilation=1, act=None):
+    """Depthwise k x k conv (+ bias + ReLU / hardswish), NCHW (channels_last on the GPU).
+    GPU fp16: one HIP pass (csrc/depthwise.hip) with the weight transposed once to [k*k, C];
+    otherwise the PyTorch reference."""
+    C, _, k, _ = weight.shape
+    if (_hip(x) and x.dtype == torch.float16 and k in (3, 5) and C % 8 == 0 and stride in (1, 2)
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        stamp = (weight.data_ptr(), weight._version)
+        ent = _DW_W.get(id(weight))
+        if ent is None or ent[0]() is not weight or ent[1] != stamp:
+            ent = (weakref.ref(weight), stamp, weight.detach().reshape(C, k * k).t().contiguous())
+            _DW_W[id(weight)] = ent
+        return _lib.dwconv_f16(x, ent[2], bias, k, stride, dilation, act)
+    y = F.conv2d(x, weight, bias, stride=stride, padding=dilation * (k // 2), dilation=dilation, groups=C)
+    if act == "relu":
+        return F.relu(y)
+    if act == "hs":
+        return F.hardswish(y)
+    return y
 
 
 # --------------------------------------------------------------------------- normalisation

@@ -43,6 +43,7 @@ _SIGS = {
     "arb_temporal_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_void_p]),
     "arb_convgru_gates": (c_int, [c_int] + [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_void_p]),
     "arb_sampler_step": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "arb_dwconv_f16": (c_int, [c_void_p] * 4 + [c_int] * 8 + [c_void_p]),
 }
 
 
@@ -228,6 +229,27 @@ def _cl_fp16(*ts):
     for t in ts:
         if t.dtype != torch.float16 or not t.is_contiguous(memory_format=torch.channels_last):
             raise TypeError("convgru kernels take fp16 channels_last NCHW tensors")
+
+
+_DW_ACT = {None: 0, "relu": 1, "hs": 2}
+
+
+def dwconv_f16(x, wt, bias, k, stride, dil, act=None):
+    """Depthwise k x k conv + bias + activation (csrc/depthwise.hip).  x: fp16 channels_last NCHW
+    [B, C, H, W] (NHWC memory); wt [k*k, C] fp16 (taps-major); padding dil * (k // 2).  Returns a
+    channels_last NCHW tensor."""
+    if x.dtype != torch.float16 or wt.dtype != torch.float16 or (bias is not None and bias.dtype != torch.float16):
+        raise TypeError("dwconv_f16: fp16 tensors only")
+    B, C, H, W = x.shape
+    if not x.is_contiguous(memory_format=torch.channels_last) or C % 8 or tuple(wt.shape) != (k * k, C):
+        raise ValueError(f"dwconv_f16: unsupported x {tuple(x.shape)} / wt {tuple(wt.shape)}")
+    pad = dil * (k // 2)
+    Ho = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    y = torch.empty(B, Ho, Wo, C, dtype=x.dtype, device=x.device)
+    _check(_fn("arb_dwconv_f16")(_p(x), _p(wt.contiguous()), _p(bias), _p(y), B, H, W, C, k, stride, dil,
+                                 _DW_ACT[act], _stream()), "dwconv_f16")
+    return y.permute(0, 3, 1, 2)
 
 
 def convgru_gates1(ih, h, cat_buf, cx):

@@ -3,9 +3,10 @@
 // The normalisation of every ResBlock / Transformer2D input of the SD1.5 UNet
 // and VAE.  Three short, wide kernels (each fills the chip;
 // hipGraph replay keeps the launch gaps at ~1 us):
-//   1. gn_stats    grid (chunks, B): every thread keeps RPT rows x 8 channels in
-//      registers (all loads in flight at once), computes EXACT per-channel
-//      (n, mean, M2) by two passes over registers, and the block combines them
+//   1. gn_stats    grid (chunks, B): each block walks ~64 KB of rows in slabs; per slab every
+//      thread keeps RPT rows x 8 channels in registers (next slab's loads in flight), computes
+//      EXACT per-channel (n, mean, M2) by two passes over registers and Chan-combines the slabs;
+//      the block then combines them once
 //      per group with the exact parallel-variance algebra
 //      (N = sum n, mu = sum n*mean / N, M2 = sum [M2_c + n_c (mean_c - mu)^2]).
 //   2. gn_finalize grid (G, B): one group per block, 256 threads combine the
@@ -37,9 +38,24 @@ __device__ __forceinline__ Stat chan_combine(Stat a, Stat b) {
   return r;
 }
 
+// Stats partition, a function of (HW, C) only - so the reduction order never depends on the
+// batch (lock-step groups stay bitwise equal to solo tasks).  Large images (>= 1M elements per
+// image): slabs of 8 rows per thread (16 x 16-B loads in flight with the next slab's), up to
+// ~64 KB of rows per block and at least 16 blocks per image.  Small images: one 4-row slab per
+// block (as many blocks as possible: these calls are latency-bound).
+__host__ __device__ inline int gn_srpt(int HW, int C) { return (long)HW * C >= (1L << 20) ? 8 : 4; }
+__host__ __device__ inline int gn_iters(int HW, int C) {
+  const int NV = C >> 3, k = NV >= 256 ? 1 : 256 / NV, srpt = gn_srpt(HW, C);
+  if (srpt == 4) return 1;
+  int it = (32768 / C) / (k * srpt);
+  const int cap = HW / (k * srpt * 16);
+  if (it > cap) it = cap;
+  return it < 1 ? 1 : (it > 16 ? 16 : it);
+}
+
 // Thread geometry: NV = C/8 channel vectors.  NV < 256: k = 256/NV row lanes, thread
 // (v = t % NV, rl = t / NV).  NV >= 256: one row lane, thread owns vectors t, t+256 (VPT).
-template <int VPT>
+template <int VPT, int GN_SRPT>
 __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict__ x, Stat* __restrict__ part,
                                                        int HW, int C, int G) {
   const int chunk = blockIdx.x, b = blockIdx.y, chunks = gridDim.x;
@@ -47,52 +63,85 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
   const int k = NV >= 256 ? 1 : 256 / NV;
   const int t = threadIdx.x;
   const int v = NV >= 256 ? t : t % NV, rl = NV >= 256 ? 0 : t / NV;
-  const int rows = k * GN_RPT;
-  const int r0 = chunk * rows;
+  const int r0 = chunk * k * GN_SRPT * gn_iters(HW, C);
   __shared__ float sh_n[256];
   __shared__ float sh_mean[256 * 8 * VPT];
   __shared__ float sh_m2[256 * 8 * VPT];
 
-  float f[VPT][GN_RPT][8];
-  float n = 0.f;
   const bf16_t* base = x + ((size_t)b * HW) * C;
+  // The block walks ITER slabs of k*GN_SRPT rows (ITER from (HW, C) only: batch-invariant).  Per
+  // slab each thread takes the EXACT (mean, M2) of its GN_SRPT rows per channel (two passes over
+  // registers) and Chan-combines it into a running per-channel Stat; the next slab's loads are in
+  // flight meanwhile.  The per-group LDS combine below then runs once per block, not per slab.
+  const int iters = gn_iters(HW, C);
+  Stat acc[VPT][8];
 #pragma unroll
-  for (int i = 0; i < GN_RPT; ++i) {
-    const int r = r0 + rl + i * k;
-    const bool ok = rl < k && r < HW;
-    n += ok ? 1.f : 0.f;
+  for (int j = 0; j < VPT; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[j][e] = Stat{0.f, 0.f, 0.f, 0.f};
+  uint4 raw[2][VPT][GN_SRPT];
+  auto load = [&](uint4 (&dst)[VPT][GN_SRPT], int it) {
+#pragma unroll
+    for (int i = 0; i < GN_SRPT; ++i) {
+      const int r = r0 + it * k * GN_SRPT + rl + i * k;
+      const bool ok = rl < k && it < iters && r < HW;
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int vv = v + 256 * j;
+        dst[j][i] = (ok && vv < NV) ? ld16(base + (size_t)r * C + vv * 8) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  float nt = 0.f;
+  auto process = [&](const uint4 (&src)[VPT][GN_SRPT], int it) {
+    float n = 0.f;
+#pragma unroll
+    for (int i = 0; i < GN_SRPT; ++i) {
+      const int r = r0 + it * k * GN_SRPT + rl + i * k;
+      n += (rl < k && it < iters && r < HW) ? 1.f : 0.f;
+    }
+    if (n == 0.f) return;
+    nt += n;
+    const float inv_n = 1.f / n;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
-      const int vv = v + 256 * j;
-      if (ok && vv < NV) {
-        unpack8(ld16(base + (size_t)r * C + vv * 8), f[j][i]);
-      } else {
+      float f[GN_SRPT][8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[j][i][e] = 0.f;
+      for (int i = 0; i < GN_SRPT; ++i) unpack8(src[j][i], f[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < GN_SRPT; ++i) s += f[i][e];
+        const float mean = s * inv_n;
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < GN_SRPT; ++i) {
+          const int r = r0 + it * k * GN_SRPT + rl + i * k;
+          const float d = f[i][e] - mean;
+          m2 += (rl < k && r < HW) ? d * d : 0.f;
+        }
+        acc[j][e] = chan_combine(acc[j][e], Stat{n, mean, m2, 0.f});
       }
     }
+  };
+  // two register sets: slab it+1 is loading while slab it is reduced
+  load(raw[0], 0);
+  for (int it = 0; it < iters; it += 2) {
+    load(raw[1], it + 1);
+    process(raw[0], it);
+    if (it + 1 >= iters) break;
+    load(raw[0], it + 2);
+    process(raw[1], it + 1);
   }
-  sh_n[t] = n;
-  const float inv_n = n > 0.f ? 1.f / n : 0.f;
+  sh_n[t] = nt;
 #pragma unroll
-  for (int j = 0; j < VPT; ++j) {
+  for (int j = 0; j < VPT; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < GN_RPT; ++i) s += f[j][i][e];
-      const float mean = s * inv_n;
-      float m2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < GN_RPT; ++i) {
-        const int r = r0 + rl + i * k;
-        const float d = f[j][i][e] - mean;
-        m2 += (rl < k && r < HW) ? d * d : 0.f;
-      }
-      sh_mean[(t * VPT + j) * 8 + e] = mean;
-      sh_m2[(t * VPT + j) * 8 + e] = m2;
+      sh_mean[(t * VPT + j) * 8 + e] = acc[j][e].mean;
+      sh_m2[(t * VPT + j) * 8 + e] = acc[j][e].m2;
     }
-  }
   __syncthreads();
   // Per-group combine, parallel: L = 256/G lanes per group (consecutive lanes of one wave),
   // each takes every L-th (channel, row-lane) item; the L partials are merged by a fixed
@@ -236,9 +285,30 @@ static int gn_chunks(int HW, int C) {
   return (HW + rows - 1) / rows;
 }
 
+// stats blocks per image: gn_iters slabs of k * gn_srpt rows each
+static int gn_stat_chunks(int HW, int C) {
+  const int NV = C / 8;
+  const int k = NV >= 256 ? 1 : 256 / NV;
+  const int rows = k * gn_srpt(HW, C) * gn_iters(HW, C);
+  return (HW + rows - 1) / rows;
+}
+
+static void launch_gn_stats(const void* x, Stat* part, int B, int HW, int C, int G, hipStream_t stream) {
+  dim3 grid(gn_stat_chunks(HW, C), B);
+  const bool wide = C / 8 > 256, big = gn_srpt(HW, C) == 8;
+  const bf16_t* xb = (const bf16_t*)x;
+  if (wide) {
+    if (big) gn_stats_kernel<2, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G);
+    else gn_stats_kernel<2, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G);
+  } else {
+    if (big) gn_stats_kernel<1, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G);
+    else gn_stats_kernel<1, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G);
+  }
+}
+
 ARB_API size_t arb_group_norm_workspace(int B, int HW, int C, int G) {
   // partial stats + final (mean, rstd); 256-byte aligned split
-  const size_t part = (size_t)B * gn_chunks(HW, C) * G * sizeof(Stat);
+  const size_t part = (size_t)B * gn_stat_chunks(HW, C) * G * sizeof(Stat);
   return ((part + 255) / 256) * 256 + (size_t)B * G * sizeof(float2);
 }
 
@@ -345,20 +415,17 @@ static int gn_run(const void* x, void* y, const void* gamma, const void* beta, v
                   int C, int G, float eps, int silu, const void* mod, int H, int W, int mh, int mw, float one_plus,
                   hipStream_t stream) {
   if (C % 8 != 0 || C / 8 > 512 || C % G != 0 || G > 256) return -1;
-  const int chunks = gn_chunks(HW, C);
+  const int chunks = gn_chunks(HW, C), schunks = gn_stat_chunks(HW, C);
   Stat* part = (Stat*)workspace;
-  const size_t part_bytes = ((size_t)B * chunks * G * sizeof(Stat) + 255) / 256 * 256;
+  const size_t part_bytes = ((size_t)B * schunks * G * sizeof(Stat) + 255) / 256 * 256;
   float2* stats = (float2*)((char*)workspace + part_bytes);
   dim3 g1(chunks, B);
   const bool wide = C / 8 > 256;
   if (gn_group_path(HW, C, G)) {
     launch_gn_group(x, nullptr, stats, nullptr, nullptr, nullptr, 0.f, B, HW, C, G, eps, stream);
   } else {
-    if (wide)
-      gn_stats_kernel<2><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
-    else
-      gn_stats_kernel<1><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
-    gn_finalize_kernel<<<dim3(G, B), 256, 0, stream>>>(part, stats, chunks, G, eps);
+    launch_gn_stats(x, part, B, HW, C, G, stream);
+    gn_finalize_kernel<<<dim3(G, B), 256, 0, stream>>>(part, stats, schunks, G, eps);
   }
 #define GN_APPLY(VPT, MOD)                                                                                    \
   gn_apply_kernel<VPT, MOD><<<g1, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, stats, (const bf16_t*)gamma, \
@@ -432,13 +499,9 @@ ARB_API int arb_group_norm_table(const void* x, const void* gamma, const void* b
     launch_gn_group(x, (float2*)table, nullptr, gamma, beta, mod, one_plus, B, HW, C, G, eps, stream);
     return (int)hipGetLastError();
   }
-  const int chunks = gn_chunks(HW, C);
+  const int chunks = gn_stat_chunks(HW, C);
   Stat* part = (Stat*)workspace;
-  dim3 g1(chunks, B);
-  if (C / 8 > 256)
-    gn_stats_kernel<2><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
-  else
-    gn_stats_kernel<1><<<g1, 256, 0, stream>>>((const bf16_t*)x, part, HW, C, G);
+  launch_gn_stats(x, part, B, HW, C, G, stream);
   gn_table_kernel<<<dim3(G, B), 256, 0, stream>>>(part, (float2*)table, (const bf16_t*)gamma, (const bf16_t*)beta,
                                                   (const bf16_t*)mod, one_plus, chunks, C, G, eps);
   return (int)hipGetLastError();

@@ -169,6 +169,8 @@ class MultiGPUSolverPool:
         # tasks per lock-step group on one stream (HIP kernels only: batch-invariant launches)
         self.lockstep = max(1, int(lockstep)) if device_type == "cuda" else 1
         self.busy: Dict[int, int] = {}           # job id -> rank
+        self._started: Dict[int, float] = {}     # job id -> dispatch time
+        self._gpu: Dict[int, dict] = {}          # rank -> {"task_s", "tasks"} (/metrics)
         self.idle: List[int] = []                # one entry per free task slot (rank repeated)
         self.futures: Dict[int, asyncio.Future] = {}
         self._ids = itertools.count(1)
@@ -234,6 +236,11 @@ class MultiGPUSolverPool:
         _, jid, rank, payload = msg
         if self.busy.pop(jid, None) is not None:
             self.idle.append(rank)
+        t0 = self._started.pop(jid, None)
+        if t0 is not None and kind == "ok":
+            st = self._gpu.setdefault(rank, {"task_s": 0.0, "tasks": 0})
+            st["task_s"] += time.time() - t0
+            st["tasks"] += 1
         fut = self.futures.pop(jid, None)
         if fut is None or fut.done():
             return
@@ -307,9 +314,14 @@ class MultiGPUSolverPool:
         fut = asyncio.get_running_loop().create_future()
         self.futures[jid] = fut
         self.busy[jid] = rank
+        self._started[jid] = time.time()
         self.in_qs[rank].put((jid, model.name, model.kind, model.id, taskid, dict(inp)))
         self._ensure_pump()
         return await fut
+
+    def gpu_stats(self):
+        """Per-GPU solved-task count and summed solve seconds (``/metrics``)."""
+        return {r: dict(self._gpu.get(r, {"task_s": 0.0, "tasks": 0})) for r in range(self.n)}
 
     def kill_worker(self, rank: int):
         """Fault injection (tests): hard-kill one worker process."""

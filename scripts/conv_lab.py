@@ -112,6 +112,55 @@ def libs_ab():
                           "bitwise_equal": same}), flush=True)
 
 
+GN_SHAPES = [(8, 4096, 320), (8, 4096, 640), (8, 4096, 960), (8, 1024, 640), (8, 1024, 1280), (8, 1024, 1920),
+             (8, 256, 1280), (8, 256, 2560), (8, 64, 1280), (2, 4096, 320)]
+
+
+def gn_ab():
+    """GroupNorm-table (stats + table) per library build, interleaved; GB/s of the one read of x."""
+    import ctypes
+    dev = torch.device("cuda")
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "arbius_amd", "ops")
+    names = os.environ.get("LAB_LIBS", "libarbius_kernels_base.so,libarbius_kernels.so").split(",")
+    fns = {}
+    for n in names:
+        L = ctypes.CDLL(os.path.join(here, n))
+        f = L.arb_group_norm_table
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_float] + [ctypes.c_void_p] * 2 + [ctypes.c_int] * 4 + \
+            [ctypes.c_float, ctypes.c_void_p]
+        ws = L.arb_group_norm_workspace
+        ws.restype, ws.argtypes = ctypes.c_size_t, [ctypes.c_int] * 4
+        fns[n] = (f, ws)
+    P = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
+    for (B, HW, C) in GN_SHAPES:
+        x = (torch.randn(B, HW, C, device=dev) * 2 + 0.5).bfloat16()
+        g = (torch.rand(C, device=dev) + 0.5).bfloat16()
+        bt = torch.randn(C, device=dev).bfloat16()
+        calls, tabs = {}, {}
+        for n, (f, wsf) in fns.items():
+            ws = torch.empty(max(16, int(wsf(B, HW, C, 32))), dtype=torch.uint8, device=dev)
+            tab = torch.empty(B, C, 2, device=dev)
+
+            def call(f=f, ws=ws, tab=tab):
+                rc = f(P(x), P(g), P(bt), P(None), 0.0, P(ws), P(tab), B, HW, C, 32, 1e-5,
+                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                assert rc == 0, rc
+            calls[n] = call
+            call()
+            torch.cuda.synchronize()
+            tabs[n] = tab.clone()
+        ref = tabs[names[0]]
+        err = max(float((t - ref).abs().max() / ref.abs().max()) for t in tabs.values())
+        res = {n: [] for n in names}
+        for _ in range(3):
+            for n in names:
+                res[n].append(graph_time(calls[n]))
+        med = {n: round(sorted(v)[1], 1) for n, v in res.items()}
+        gbs = {n: round(B * HW * C * 2 / t / 1e3, 0) for n, t in med.items()}
+        print(json.dumps({"gn": [B, HW, C], "us": med, "GBps": gbs, "max_rel_diff": err}), flush=True)
+
+
 def pmc():
     dev = torch.device("cuda")
     shape = SHAPES[sys.argv[2]]
@@ -124,4 +173,4 @@ def pmc():
 
 
 if __name__ == "__main__":
-    {"sweep": sweep, "pmc": pmc, "ab": libs_ab}[sys.argv[1]]()
+    {"sweep": sweep, "pmc": pmc, "ab": libs_ab, "gn": gn_ab}[sys.argv[1]]()

@@ -253,6 +253,25 @@ def test_convgru_gates(cuda, N, C, H, W):
     assert _rel(hn, ref.convgru_gates2(c, h, z)) < 2e-3
 
 
+@pytest.mark.parametrize("B,C,H,W,k,stride,dil,act", [
+    (2, 72, 64, 64, 3, 2, 1, "relu"), (3, 120, 32, 30, 5, 1, 1, None), (2, 960, 16, 16, 5, 1, 2, "hs"),
+    (1, 200, 17, 13, 3, 1, 1, "hs"), (4, 16, 135, 240, 3, 1, 1, "relu"), (2, 672, 33, 31, 5, 2, 1, "hs")])
+def test_depthwise_conv_f16(cuda, B, C, H, W, k, stride, dil, act):
+    """RVM MobileNetV3 depthwise conv + bias + act (csrc/depthwise.hip) vs fp32 torch, bitwise re-run."""
+    import torch.nn.functional as F
+    torch.manual_seed(8)
+    cl = torch.channels_last
+    x = torch.randn(B, C, H, W, device=cuda).half().contiguous(memory_format=cl)
+    w = (torch.randn(C, 1, k, k, device=cuda) / k).half()
+    b = torch.randn(C, device=cuda).half()
+    y = ops.depthwise_conv(x, w, b, stride, dil, act)
+    r = F.conv2d(x.float(), w.float(), b.float(), stride=stride, padding=dil * (k // 2), dilation=dil, groups=C)
+    r = F.relu(r) if act == "relu" else (F.hardswish(r) if act == "hs" else r)
+    assert y.shape == r.shape and y.is_contiguous(memory_format=cl)
+    assert _rel(y, r) < 2e-3
+    assert torch.equal(y, ops.depthwise_conv(x, w, b, stride, dil, act))
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k", [(2, 64, 64, 4, 320, 3), (2, 64, 64, 320, 4, 3), (1, 96, 96, 4, 1024, 1),
                                               (1, 128, 128, 128, 3, 3), (1, 96, 96, 4, 512, 3)])
 def test_small_channel_conv_padded_onto_mfma(cuda, B, H, W, Cin, Cout, k):

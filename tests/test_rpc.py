@@ -45,3 +45,38 @@ def test_rpc_routes():
             await client.close()
 
     _run(go())
+
+
+def test_metrics_histograms_and_per_gpu_counters():
+    """/metrics: cumulative Prometheus latency histograms and per-GPU solved-task counters."""
+    from arbius_amd.node.miner import Metrics
+
+    class _Pool:
+        capacity, busy, restarts = 2, {}, 0
+
+        def gpu_stats(self):
+            return {0: {"task_s": 3.5, "tasks": 2}, 1: {"task_s": 1.25, "tasks": 1}}
+
+    class _Miner:
+        metrics = Metrics()
+        pool = _Pool()
+
+    for s in (0.3, 0.7, 12.0):
+        _Miner.metrics.observe("solve", s)
+
+    async def go():
+        client = TestClient(TestServer(make_app(DB(":memory:"), _Miner())))
+        await client.start_server()
+        try:
+            text = await (await client.get("/metrics")).text()
+        finally:
+            await client.close()
+        return text
+
+    text = _run(go())
+    assert "# TYPE arbius_solve_seconds histogram" in text
+    assert 'arbius_solve_seconds_bucket{le="0.5"} 1' in text
+    assert 'arbius_solve_seconds_bucket{le="1"} 2' in text
+    assert 'arbius_solve_seconds_bucket{le="+Inf"} 3' in text
+    assert "arbius_solve_seconds_count 3" in text and "arbius_solve_seconds_sum 13.000000" in text
+    assert 'arbius_gpu_tasks_total{gpu="1"} 1' in text and 'arbius_gpu_task_seconds_total{gpu="0"} 3.500' in text
