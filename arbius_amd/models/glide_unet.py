@@ -83,7 +83,7 @@ class SSResBlock(nn.Module):
         ss = self.emb(emb_act)                          # [B, 2C] = [scale | shift]
         # scale-shift norm + SiLU folded into one per-(b, c) affine table: conv2's prologue
         norm = self.norm2.table(h, mod=ss, one_plus=1.0, silu=True)
-        skip = self.skip(x) if self.skip is not None else x
+        skip = self.skip(x) if self.skip is not None else ops.materialize(x)
         return self.conv2(h, residual=skip, norm=norm)
 
 
@@ -189,7 +189,7 @@ class GlideUNet(nn.Module):
         h = self.mid_attn(h, ctx)
         h = self.mid2(h, emb_act)
         for blk in self.up:
-            h = blk.res(torch.cat([h, hs.pop()], dim=-1), emb_act)
+            h = blk.res(ops.cat_channels(h, hs.pop()), emb_act)
             if blk.attn is not None:
                 h = blk.attn(h, ctx)
             if blk.upsample is not None:

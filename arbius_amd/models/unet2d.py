@@ -177,7 +177,7 @@ class ResBlock(nn.Module):
         # GroupNorm+SiLU run as the convs' operand prologue (table of per-(b, c) affines);
         # time-embedding add and residual are fused into the epilogues.
         h = self.conv1(x, temb=temb_out, norm=self.norm1.table(x))
-        skip = self.shortcut(x) if self.shortcut is not None else x
+        skip = self.shortcut(x) if self.shortcut is not None else ops.materialize(x)
         return self.conv2(h, residual=skip, norm=self.norm2.table(h))
 
 
@@ -301,7 +301,7 @@ class UNet2DCondition(nn.Module):
         h = self.mid_res2(h, temb[self.mid_res2])
         for blk in self.up:
             for i, rb in enumerate(blk.resnets):
-                h = torch.cat([h, skips.pop()], dim=-1)
+                h = ops.cat_channels(h, skips.pop())      # read in place by GN stats/apply + shortcut
                 h = rb(h, temb[rb])
                 if len(blk.attns):
                     h = blk.attns[i](h, ctx)

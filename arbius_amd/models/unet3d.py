@@ -205,7 +205,7 @@ class UNet3DCondition(nn.Module):
         h = self._layer(self.mid_out, h, temb, ctx_f, frames)
         for blk in self.up:
             for m in blk.layers:
-                h = self._layer(m, torch.cat([h, skips.pop()], dim=-1), temb, ctx_f, frames)
+                h = self._layer(m, ops.cat_channels(h, skips.pop()), temb, ctx_f, frames)
             if blk.upsample is not None:
                 h = blk.upsample(h)
         return self.conv_out(h, norm=self.norm_out.table(h))

@@ -93,10 +93,12 @@ def _hip(t: torch.Tensor) -> bool:
 def linear(x, w, b=None, residual=None):
     """y = x @ w^T + b (+ residual).
 
-    GPU: with a residual (attention out-proj, FF down-proj, proj_out) the
-    implicit-GEMM kernel fuses bias + residual into its epilogue; plain
-    projections go to hipBLASLt (bias fused by the library)."""
-    if _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]) and (residual is not None or getattr(_TL, "pb", None)):
+    GPU: every linear whose K % 64 == 0 and N % 8 == 0 runs on the implicit-GEMM kernel (bias and
+    residual fused into its epilogue, pinned plans - so a task's bytes never depend on which
+    library algorithm a GEMM picks).  Library GEMMs (hipBLASLt) only for the other shapes: its
+    stream-K kernels spin on other workgroups of their own launch, and two of them replayed
+    concurrently on the two task streams of a GPU deadlocked (zeroscope, 2 streams)."""
+    if _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]):
         return _lib.gemm(x, w, b, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
     if residual is not None:
         x2 = x.reshape(-1, x.shape[-1])
@@ -129,6 +131,42 @@ def linear_geglu(x, w, b=None):
             _GEGLU_W[id(w)] = ent
         return _lib.gemm_geglu(x, ent[2], ent[3], plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
     return geglu(linear(x, w, b))
+
+
+class CatPair:
+    """The channel concat [a | b] of two channels-last tensors, NOT materialised: the UNet up-path
+    skip connection.  Its consumers (GroupNorm statistics, the GroupNorm table-apply pass and the
+    ResBlock shortcut conv) read both parts in place on the GPU, with bytes identical to reading the
+    concatenated tensor; anything else calls ``materialize()``."""
+    __slots__ = ("a", "b", "shape", "dtype", "device")
+
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+        self.shape = tuple(a.shape[:-1]) + (a.shape[-1] + b.shape[-1],)
+        self.dtype, self.device = a.dtype, a.device
+
+    @property
+    def is_cuda(self):
+        return self.a.is_cuda
+
+    def dim(self):
+        return len(self.shape)
+
+    def materialize(self):
+        return torch.cat([self.a, self.b], dim=-1)
+
+
+def cat_channels(a, b):
+    """[a | b] along the channel (last) dim: a lazy ``CatPair`` where the GPU kernels can read it in
+    place (bf16, a's channels % 64 == 0), else ``torch.cat``."""
+    if (_hip(a) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.shape[:-1] == b.shape[:-1]
+            and a.shape[-1] % 64 == 0 and b.shape[-1] % 8 == 0 and a.is_contiguous() and b.is_contiguous()):
+        return CatPair(a, b)
+    return torch.cat([a, b], dim=-1)
+
+
+def materialize(x):
+    return x.materialize() if isinstance(x, CatPair) else x
 
 
 class NormSpec:
@@ -164,6 +202,16 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
     (+bias, +temb[b, n] per-batch bias, +residual); ``norm = (table, silu)`` applies a
     GroupNorm(+SiLU) prologue from ``group_norm_table`` inside the conv's operand load."""
     kern_ok = (w.shape[1] in (1, 3) and w.shape[1] == w.shape[2]) or tuple(w.shape[1:3]) == (3, 1)
+    if isinstance(x, CatPair):
+        if (norm is not None and _hip(x.a) and not _NORM_PROLOGUE and kern_ok and x.shape[-1] % 64 == 0
+                and w.shape[0] % 8 == 0 and "gnapply" not in _EXP_SKIP):
+            table, nsilu = norm
+            x, norm = _lib.norm_table_apply(x.a, table, nsilu, x2=x.b), None     # reads both parts in place
+        elif norm is None and _hip(x.a) and kern_ok and x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
+            return _lib.conv2d_nhwc(x.a, w, b, padding, upsample, residual, temb, stride, x2=x.b,
+                                    plan_b=_canon_batch(x.shape[0]))
+        else:
+            x = x.materialize()
     if _hip(x) and kern_ok:
         table, nsilu = norm if norm is not None else (None, False)
         if table is not None and not _NORM_PROLOGUE and x.shape[-1] % 8 == 0:
@@ -282,6 +330,10 @@ def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
     """GroupNorm of x as a per-(batch, channel) affine table [B, C, 2] fp32 (scale, shift) for a
     consumer prologue (conv/GEMM); ``mod`` [B, 2C] folds the GLIDE scale-shift modulation
     (out = GN(x) * (mod[:, :C] + one_plus) + mod[:, C:])."""
+    if isinstance(x, CatPair):
+        if _hip(x.a) and "gnstats" not in _EXP_SKIP:
+            return _lib.group_norm_table(x.a, gamma, beta, groups, eps, mod, one_plus, x2=x.b)
+        x = x.materialize()
     if _hip(x):
         if "gnstats" in _EXP_SKIP:
             key = (x.shape[0], x.shape[-1])

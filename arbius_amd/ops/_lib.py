@@ -44,6 +44,12 @@ _SIGS = {
     "arb_convgru_gates": (c_int, [c_int] + [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_void_p]),
     "arb_sampler_step": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "arb_dwconv_f16": (c_int, [c_void_p] * 4 + [c_int] * 8 + [c_void_p]),
+    "arb_softmax_rows": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "arb_group_norm_table_cat": (c_int, [c_void_p] * 2 + [c_int] + [c_void_p] * 3 + [c_float] + [c_void_p] * 2
+                                 + [c_int] * 4 + [c_float, c_void_p]),
+    "arb_norm_table_apply_cat": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_long, c_int, c_int,
+                                         c_void_p]),
+    "arb_conv2d_nhwc_cat": (c_int, [c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int] * 11 + [c_void_p]),
 }
 
 
@@ -213,9 +219,30 @@ def temporal_attention(q, k, v, scale):
     return o
 
 
+def softmax_rows(s, scale):
+    """P = softmax(scale * S) over the last dim (csrc/elementwise.hip), S bf16 [..., N], N % 8 == 0."""
+    _bf16(s)
+    s = s.contiguous()
+    N = s.shape[-1]
+    p = torch.empty_like(s)
+    _check(_fn("arb_softmax_rows")(_p(s), _p(p), s.numel() // N, N, float(scale), _stream()), "softmax_rows")
+    return p
+
+
 def _large_head_attention(q, k, v, scale):
-    """Head dims > 160 (the single-head d=512 VAE mid-block attention): two
-    hipBLASLt GEMMs around an fp32 softmax.  Runs once per task."""
+    """Head dims > 160 (the single-head d = 512 VAE / MoVQ mid-block attention, once per task):
+    S = Q K^T on the implicit-GEMM kernel, the HIP row softmax, O = P V on the implicit-GEMM kernel
+    (per batch and head; V^T made contiguous once).  Shapes the GEMM does not tile (Nk or D not a
+    multiple of 64) take the library GEMMs around an fp32 softmax."""
+    B, Nq, H, D = q.shape
+    Nk = k.shape[1]
+    if D % 64 == 0 and Nk % 64 == 0:
+        o = torch.empty(B, Nq, H, D, dtype=q.dtype, device=q.device)
+        for b in range(B):
+            for h in range(H):
+                s = gemm(q[b, :, h], k[b, :, h].contiguous())                 # [Nq, Nk] = q k^T
+                o[b, :, h] = gemm(softmax_rows(s, scale), v[b, :, h].t().contiguous())
+        return o
     qf = q.transpose(1, 2)
     kf = k.transpose(1, 2)
     vf = v.transpose(1, 2)
@@ -296,8 +323,28 @@ def silu(x):
     return y
 
 
-def norm_table_apply(x, table, silu=False):
-    """x [B, *, C] * table[b, c].scale + .shift (+SiLU) - the unfused GroupNorm-table prologue."""
+def _cat_parts(x, x2):
+    """(x, x2) of a channel concat read in place: both contiguous, same leading dims, C1 % 64 == 0."""
+    _bf16(x, x2)
+    x, x2 = x.contiguous(), x2.contiguous()
+    if x.shape[:-1] != x2.shape[:-1] or x.shape[-1] % 64 or x2.shape[-1] % 8:
+        raise ValueError(f"channel concat: bad parts {tuple(x.shape)} | {tuple(x2.shape)}")
+    return x, x2
+
+
+def norm_table_apply(x, table, silu=False, x2=None):
+    """x [B, *, C] * table[b, c].scale + .shift (+SiLU) - the unfused GroupNorm-table prologue.
+    ``x2``: the channels [C1, C) of a concat [x | x2] read in place (the output is the concat)."""
+    if x2 is not None:
+        x, x2 = _cat_parts(x, x2)
+        B, C1, C = x.shape[0], x.shape[-1], x.shape[-1] + x2.shape[-1]
+        if tuple(table.shape) != (B, C, 2) or table.dtype != torch.float32:
+            raise ValueError(f"norm_table_apply: bad table {tuple(table.shape)}")
+        y = torch.empty(*x.shape[:-1], C, dtype=x.dtype, device=x.device)
+        _check(_fn("arb_norm_table_apply_cat")(_p(x), _p(x2), C1, _p(y), _p(table.contiguous()), B,
+                                               x.numel() // (B * C1), C, int(bool(silu)), _stream()),
+               "norm_table_apply_cat")
+        return y
     _bf16(x)
     x = x.contiguous()
     B, C = x.shape[0], x.shape[-1]
@@ -316,13 +363,18 @@ def conv_plan(B, H, W, Cin, Cout, k, pad, upsample, stride):
     return out[0], out[1]
 
 
-def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
+def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0, x2=None):
     """GroupNorm of x [B, *, C] as a per-(batch, channel) affine table [B, C, 2] fp32
-    (scale, shift) for a consumer prologue; ``mod`` [B, 2C] folds a scale-shift modulation."""
+    (scale, shift) for a consumer prologue; ``mod`` [B, 2C] folds a scale-shift modulation.
+    ``x2``: GroupNorm of the channel concat [x | x2], read in place (same bytes)."""
     _bf16(x, gamma, beta, mod)
+    C1 = 0
+    if x2 is not None:
+        x, x2 = _cat_parts(x, x2)
+        C1 = x.shape[-1]
     x = x.contiguous()
-    B, C = x.shape[0], x.shape[-1]
-    HW = x.numel() // (B * C)
+    B, C = x.shape[0], x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
+    HW = x.numel() // (B * x.shape[-1])
     if C % 8 or C // 8 > 512 or C % groups or groups > 256:
         raise ValueError(f"group_norm_table: unsupported C={C} G={groups}")
     if mod is not None:
@@ -331,17 +383,29 @@ def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0):
             raise ValueError("group_norm_table: mod must be [B, 2C]")
     ws = torch.empty(max(16, _fn("arb_group_norm_workspace")(B, HW, C, groups)), dtype=torch.uint8, device=x.device)
     table = torch.empty(B, C, 2, dtype=torch.float32, device=x.device)
+    if x2 is not None:
+        _check(_fn("arb_group_norm_table_cat")(_p(x), _p(x2), C1, _p(gamma), _p(beta), _p(mod), float(one_plus),
+                                               _p(ws), _p(table), B, HW, C, groups, float(eps), _stream()),
+               "group_norm_table_cat")
+        return table
     _check(_fn("arb_group_norm_table")(_p(x), _p(gamma), _p(beta), _p(mod), float(one_plus), _p(ws), _p(table), B,
                                        HW, C, groups, float(eps), _stream()), "group_norm_table")
     return table
 
 
 def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-1, split=-1, norm=None,
-                norm_silu=False, plan_b=None):
+                norm_silu=False, plan_b=None, x2=None):
     """Implicit-GEMM conv (csrc/conv.hip).  x [B,H,W,Cin], w [Cout,k,k,Cin] -> [B,Ho,Wo,Cout].
     Fused epilogue: + bias[n] + temb[b, n] + residual[m, n]; optional GroupNorm(+SiLU)
     prologue from a ``group_norm_table`` (the normalised x never hits HBM).  fp16 tensors run the
-    fp16 twin of the kernel (mfma f16; no norm prologue)."""
+    fp16 twin of the kernel (mfma f16; no norm prologue).  ``x2``: the input is the channel concat
+    [x | x2] read in place (bf16, no norm prologue; bytes equal the concatenated-input conv)."""
+    x1 = None
+    if x2 is not None:
+        if norm is not None:
+            raise ValueError("conv2d: no norm prologue on a concat input")
+        x1, x2 = _cat_parts(x, x2)
+        x = x1
     f16 = x.dtype == torch.float16
     if f16:
         for t in (w, b, residual, temb):
@@ -351,9 +415,12 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
             raise ValueError("conv2d fp16: no norm prologue")
     else:
         _bf16(x, w, b, residual, temb)
-    x = x.contiguous()
+    if x1 is None:
+        x = x.contiguous()
     w = w.contiguous()
     B, H, W, Cin = x.shape
+    if x1 is not None:
+        Cin += x2.shape[-1]
     Cout, kh, kw, Cin2 = w.shape
     temporal = (kh, kw) == (3, 1)      # (3,1,1) Conv3d over a [B, F, HW, C] view
     if Cin != Cin2 or not (kh == kw and kh in (1, 3) or temporal) or Cin % 64 or Cout % 8 or stride not in (1, 2):
@@ -385,6 +452,10 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     if f16:
         _check(_fn("arb_conv2d_nhwc_f16")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), *args,
                                           _stream()), "conv2d_f16")
+        return y
+    if x1 is not None:
+        _check(_fn("arb_conv2d_nhwc_cat")(_p(x1), _p(x2), x1.shape[-1], _p(w), _p(b), _p(temb), _p(residual), _p(y),
+                                          _p(ws), *args, _stream()), "conv2d_cat")
         return y
     _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), _p(norm), *args,
                                   int(bool(norm_silu)), _stream()), "conv2d")

@@ -49,6 +49,11 @@ struct ConvArgs {
   int tiles_n, tiles_total;
   int nsplit, m_fastest;
   int geglu = 0;        // GEGLU epilogue: W rows interleaved [value 8 | gate 8] per 16; out [M, N/2]
+  // Two channel sources (a UNet skip concat read in place): channels [0, C1) from x (row stride
+  // C1), [C1, Cin) from x2 (row stride Cin - C1); C1 % 64 == 0, so a K tile never straddles.
+  // Register-staged kernel only.
+  const bf16_t* x2 = nullptr;
+  int C1 = 0;
 };
 
 // ---- element type: EL = 0 bf16 (the diffusion models), EL = 1 fp16 (robust video matting).
@@ -280,10 +285,17 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
       int hi = xho[i] + wr, wi = xwo[i] + ws;
       const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
       if (p.upsample) { hi >>= 1; wi >>= 1; }
-      xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + cc * 8 : -1;
+      const int pix = (xb[i] * p.H + hi) * p.W + wi;
+      xoff[i] = ok ? (p.x2 ? pix : pix * p.Cin + cc * 8) : -1;   // dual source: the pixel index
     }
   };
   set_tap();
+  // activation chunk address of row i at channel offset wc (wave-uniform source select)
+  auto xaddr = [&](int i) -> const bf16_t* {
+    if (p.x2 == nullptr) return p.x + xoff[i] + wc;
+    return wc < p.C1 ? p.x + (size_t)xoff[i] * p.C1 + wc + cc * 8
+                     : p.x2 + (size_t)xoff[i] * (p.Cin - p.C1) + (wc - p.C1) + cc * 8;
+  };
 
   // Staging depth: small tiles (MFMA work per k-tile far below a load latency) keep two k-tiles
   // of loads in flight; large tiles keep one (their VGPR budget is spent on accumulators).
@@ -315,7 +327,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
       S.xv[i] = live && xoff[i] >= 0;
-      S.x[i] = ld16(S.xv[i] ? p.x + xoff[i] + wc : zp);
+      S.x[i] = ld16(S.xv[i] ? xaddr(i) : zp);
     }
     wk += BK;
     wc += BK;
@@ -411,7 +423,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
       const bool ok = xoff[i] >= 0;
-      rx[i] = ok ? ld16(p.x + xoff[i] + wc) : make_uint4(0, 0, 0, 0);
+      rx[i] = ok ? ld16(xaddr(i)) : make_uint4(0, 0, 0, 0);
       xv[i] = ok;
     }
     wk += BK;
@@ -1409,9 +1421,13 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
 template <int EL>
 static int conv_run(const void* x, const void* w, const void* bias, const void* temb, const void* res, void* out,
                     void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
-                    int stride, int cfg, int split, int norm_silu, hipStream_t stream, int geglu = 0) {
+                    int stride, int cfg, int split, int norm_silu, hipStream_t stream, int geglu = 0,
+                    const void* x2 = nullptr, int C1 = 0) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
+  if (x2 != nullptr && (EL != 0 || C1 <= 0 || C1 >= Cin || C1 % 64 != 0 || geglu)) return -1;
   ConvArgs a;
+  a.x2 = (const bf16_t*)x2;
+  a.C1 = C1;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = (const bf16_t*)bias; a.temb = (const bf16_t*)temb;
   a.res = (const bf16_t*)res; a.out = (bf16_t*)out; a.ws = (float*)ws;
   a.norm = (const float*)norm; a.norm_silu = norm_silu;
@@ -1425,6 +1441,14 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
   // The 8-wave / persistent families have no GroupNorm prologue: a normed call on a shape pinned to
   // one of them runs the register-staged 128x128 tile at the pinned split (same grid coverage).
   if (norm != nullptr && pl.cfg >= 20) pl = conv_plan(a.M, a.N, a.ktiles, kNumCfgs, is_persist(pl.cfg) ? 1 : pl.split);
+  // Dual-source reads exist in the register-staged kernel only: the same tile's register-staged
+  // twin (or the 128x128 one for the 8-wave / persistent families) at the same split - the
+  // per-output MFMA order and split-K slab order are those of the planned kernel, so the bytes are
+  // those of the concatenated-input conv.
+  if (a.x2 != nullptr) {
+    if (pl.cfg >= 20) pl = conv_plan(a.M, a.N, a.ktiles, kNumCfgs, is_persist(pl.cfg) ? 1 : pl.split);
+    else if (pl.cfg < kNumCfgs) pl.cfg += kNumCfgs;
+  }
   if (pl.split > 1 && ws == nullptr) return -3;
   if (pl.cfg >= 28) {   // 8-wave 3-stage LDS-DMA ring (bf16, no norm prologue)
     if (EL != 0 || a.norm != nullptr) return -4;
@@ -1478,6 +1502,16 @@ ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, cons
                             hipStream_t stream) {
   return conv_run<0>(x, w, bias, temb, res, out, ws, norm, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg, split,
                      norm_silu, stream);
+}
+
+// Conv over the channel concat [x | x2] without materialising it (UNet up-path skip connections):
+// x [B,H,W,C1], x2 [B,H,W,Cin-C1]; otherwise as arb_conv2d_nhwc (no norm prologue).
+ARB_API int arb_conv2d_nhwc_cat(const void* x, const void* x2, int C1, const void* w, const void* bias,
+                                const void* temb, const void* res, void* out, void* ws, int B, int H, int W, int Cin,
+                                int Cout, int k, int pad, int upsample, int stride, int cfg, int split,
+                                hipStream_t stream) {
+  return conv_run<0>(x, w, bias, temb, res, out, ws, nullptr, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg, split,
+                     0, stream, 0, x2, C1);
 }
 
 // fp16 twin (robust video matting): same plans and tiles on mfma_f32_16x16x32_f16, no norm prologue.

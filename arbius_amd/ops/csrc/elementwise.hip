@@ -34,9 +34,11 @@ __global__ void __launch_bounds__(256) silu_kernel(const bf16_t* __restrict__ x,
 // Unfused form of a GroupNorm-table prologue: y[b, p, c] = x * table[b, c].x + table[b, c].y
 // (+SiLU).  Used in front of the LDS-DMA conv variant, which stages operands straight into
 // LDS and so cannot transform them on the way in.
+// x2 != null: channels [C1, C) are read from x2 (the concat [x | x2] is written, never read, whole).
 __global__ void __launch_bounds__(256) norm_table_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                                const float2* __restrict__ table, long HW, int C,
-                                                               long total8, int silu) {
+                                                               long total8, int silu, const bf16_t* __restrict__ x2,
+                                                               int C1) {
   const int CV = C >> 3;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
     const long pix = i / CV;
@@ -44,7 +46,9 @@ __global__ void __launch_bounds__(256) norm_table_apply_kernel(const bf16_t* __r
     const long b = pix / HW;
     const float2* t = table + b * C + c;
     float f[8];
-    unpack8(ld16(x + i * 8), f);
+    const bf16_t* src = x2 == nullptr ? x + i * 8
+                                      : (c < C1 ? x + pix * C1 + c : x2 + pix * (C - C1) + (c - C1));
+    unpack8(ld16(src), f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float2 ss = t[e];
@@ -53,6 +57,47 @@ __global__ void __launch_bounds__(256) norm_table_apply_kernel(const bf16_t* __r
     }
     st16(y + i * 8, pack8(f));
   }
+}
+
+// Row softmax of a score matrix: P = softmax(scale * S) per row, S / P [R, N] bf16 (N % 8 == 0), fp32
+// math, one wave per row (three sweeps of the row: max, sum of exp, write; the row stays in L1/L2).
+// The middle launch of the large-head attention (d = 512 single-head VAE / MoVQ mid-block
+// attention): S = Q K^T and O = P V run on the implicit-GEMM kernel.  Fixed reduction order.
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const bf16_t* __restrict__ s, bf16_t* __restrict__ p,
+                                                           int R, int N, float scale) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const bf16_t* sr = s + (size_t)row * N;
+  bf16_t* pr = p + (size_t)row * N;
+  float m = -INFINITY;
+  for (int c = lane * 8; c < N; c += 512) {
+    float f[8];
+    unpack8(ld16(sr + c), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, f[e] * scale);
+  }
+  m = wave_max(m);
+  float sum = 0.f;
+  for (int c = lane * 8; c < N; c += 512) {
+    float f[8];
+    unpack8(ld16(sr + c), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum += __expf(f[e] * scale - m);
+  }
+  const float inv = 1.f / wave_sum(sum);
+  for (int c = lane * 8; c < N; c += 512) {
+    float f[8];
+    unpack8(ld16(sr + c), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = __expf(f[e] * scale - m) * inv;
+    st16(pr + c, pack8(f));
+  }
+}
+
+ARB_API int arb_softmax_rows(const void* s, void* p, int R, int N, float scale, hipStream_t stream) {
+  if (N % 8 != 0 || R <= 0) return -1;
+  softmax_rows_kernel<<<(R + 3) / 4, 256, 0, stream>>>((const bf16_t*)s, (bf16_t*)p, R, N, scale);
+  return (int)hipGetLastError();
 }
 
 static int grid_for(long work) {
@@ -79,6 +124,15 @@ ARB_API int arb_norm_table_apply(const void* x, void* y, const void* table, int 
   if (C % 8 != 0) return -1;
   const long total8 = (long)B * HW * (C / 8);
   norm_table_apply_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
-                                                                HW, C, total8, silu);
+                                                                HW, C, total8, silu, nullptr, 0);
+  return (int)hipGetLastError();
+}
+
+ARB_API int arb_norm_table_apply_cat(const void* x, const void* x2, int C1, void* y, const void* table, int B, long HW,
+                                     int C, int silu, hipStream_t stream) {
+  if (C % 8 != 0 || C1 <= 0 || C1 >= C || C1 % 8 != 0 || x2 == nullptr) return -1;
+  const long total8 = (long)B * HW * (C / 8);
+  norm_table_apply_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
+                                                                HW, C, total8, silu, (const bf16_t*)x2, C1);
   return (int)hipGetLastError();
 }

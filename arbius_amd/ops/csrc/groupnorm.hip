@@ -57,7 +57,7 @@ __host__ __device__ inline int gn_iters(int HW, int C) {
 // (v = t % NV, rl = t / NV).  NV >= 256: one row lane, thread owns vectors t, t+256 (VPT).
 template <int VPT, int GN_SRPT>
 __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict__ x, Stat* __restrict__ part,
-                                                       int HW, int C, int G) {
+                                                       int HW, int C, int G, const bf16_t* __restrict__ x2, int C1) {
   const int chunk = blockIdx.x, b = blockIdx.y, chunks = gridDim.x;
   const int NV = C >> 3;
   const int k = NV >= 256 ? 1 : 256 / NV;
@@ -68,7 +68,19 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
   __shared__ float sh_mean[256 * 8 * VPT];
   __shared__ float sh_m2[256 * 8 * VPT];
 
-  const bf16_t* base = x + ((size_t)b * HW) * C;
+  // Per channel vector: source tensor, row stride and channel offset.  x2 != null: the channels
+  // [C1, C) live in x2 (a skip concat read in place; C1 % 8 == 0, so a vector never straddles).
+  const bf16_t* sbase[VPT];
+  int sstride[VPT], scoff[VPT];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int ch = (v + 256 * j) * 8;
+    const bool second = x2 != nullptr && ch >= C1;
+    const int cs = x2 == nullptr ? C : (second ? C - C1 : C1);
+    sbase[j] = (second ? x2 : x) + (size_t)b * HW * cs;
+    sstride[j] = cs;
+    scoff[j] = second ? ch - C1 : ch;
+  }
   // The block walks ITER slabs of k*GN_SRPT rows (ITER from (HW, C) only: batch-invariant).  Per
   // slab each thread takes the EXACT (mean, M2) of its GN_SRPT rows per channel (two passes over
   // registers) and Chan-combines it into a running per-channel Stat; the next slab's loads are in
@@ -88,7 +100,7 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int j = 0; j < VPT; ++j) {
         const int vv = v + 256 * j;
-        dst[j][i] = (ok && vv < NV) ? ld16(base + (size_t)r * C + vv * 8) : make_uint4(0, 0, 0, 0);
+        dst[j][i] = (ok && vv < NV) ? ld16(sbase[j] + (size_t)r * sstride[j] + scoff[j]) : make_uint4(0, 0, 0, 0);
       }
     }
   };
@@ -293,16 +305,18 @@ static int gn_stat_chunks(int HW, int C) {
   return (HW + rows - 1) / rows;
 }
 
-static void launch_gn_stats(const void* x, Stat* part, int B, int HW, int C, int G, hipStream_t stream) {
+static void launch_gn_stats(const void* x, Stat* part, int B, int HW, int C, int G, hipStream_t stream,
+                            const void* x2 = nullptr, int C1 = 0) {
   dim3 grid(gn_stat_chunks(HW, C), B);
   const bool wide = C / 8 > 256, big = gn_srpt(HW, C) == 8;
   const bf16_t* xb = (const bf16_t*)x;
+  const bf16_t* xb2 = (const bf16_t*)x2;
   if (wide) {
-    if (big) gn_stats_kernel<2, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G);
-    else gn_stats_kernel<2, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G);
+    if (big) gn_stats_kernel<2, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1);
+    else gn_stats_kernel<2, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1);
   } else {
-    if (big) gn_stats_kernel<1, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G);
-    else gn_stats_kernel<1, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G);
+    if (big) gn_stats_kernel<1, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1);
+    else gn_stats_kernel<1, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1);
   }
 }
 
@@ -491,17 +505,35 @@ __global__ void __launch_bounds__(256) gn_table_kernel(const Stat* __restrict__ 
   }
 }
 
+static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma, const void* beta, const void* mod,
+                        float one_plus, void* workspace, void* table, int B, int HW, int C, int G, float eps,
+                        hipStream_t stream);
+
 ARB_API int arb_group_norm_table(const void* x, const void* gamma, const void* beta, const void* mod, float one_plus,
                                  void* workspace, void* table, int B, int HW, int C, int G, float eps,
                                  hipStream_t stream) {
+  return gn_table_run(x, nullptr, 0, gamma, beta, mod, one_plus, workspace, table, B, HW, C, G, eps, stream);
+}
+
+// GroupNorm table over the channel concat [x | x2] (x: C1 channels, x2: C - C1) without materialising it.
+ARB_API int arb_group_norm_table_cat(const void* x, const void* x2, int C1, const void* gamma, const void* beta,
+                                     const void* mod, float one_plus, void* workspace, void* table, int B, int HW,
+                                     int C, int G, float eps, hipStream_t stream) {
+  if (x2 == nullptr || C1 <= 0 || C1 >= C || C1 % 8 != 0) return -1;
+  return gn_table_run(x, x2, C1, gamma, beta, mod, one_plus, workspace, table, B, HW, C, G, eps, stream);
+}
+
+static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma, const void* beta, const void* mod,
+                        float one_plus, void* workspace, void* table, int B, int HW, int C, int G, float eps,
+                        hipStream_t stream) {
   if (C % 8 != 0 || C / 8 > 512 || C % G != 0 || G > 256) return -1;
-  if (gn_group_path(HW, C, G)) {
+  if (x2 == nullptr && gn_group_path(HW, C, G)) {
     launch_gn_group(x, (float2*)table, nullptr, gamma, beta, mod, one_plus, B, HW, C, G, eps, stream);
     return (int)hipGetLastError();
   }
   const int chunks = gn_stat_chunks(HW, C);
   Stat* part = (Stat*)workspace;
-  launch_gn_stats(x, part, B, HW, C, G, stream);
+  launch_gn_stats(x, part, B, HW, C, G, stream, x2, C1);
   gn_table_kernel<<<dim3(G, B), 256, 0, stream>>>(part, (float2*)table, (const bf16_t*)gamma, (const bf16_t*)beta,
                                                   (const bf16_t*)mod, one_plus, chunks, C, G, eps);
   return (int)hipGetLastError();

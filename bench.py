@@ -77,6 +77,10 @@ def _device_type(args) -> str:
 
 
 def run(args):
+    dump = float(os.environ.get("ARBIUS_BENCH_STACKDUMP", "0") or 0)
+    if dump > 0:        # diagnosis of a stalled run: every thread's Python stack to stderr periodically
+        import faulthandler
+        faulthandler.dump_traceback_later(dump, repeat=True, file=sys.stderr)
     import torch
 
     from arbius_amd import ops

@@ -170,11 +170,14 @@ def main():
                     help="time only the 8-wave cfgs (20-23) against the current plan; re-pin where they win")
     ap.add_argument("--merge", default=None, help="existing conv_plans.inc to keep entries from")
     ap.add_argument("--batch", type=int, default=2, help="SD UNet batch for shape collection (8 = groups of 4)")
+    ap.add_argument("--gemms-only", action="store_true", help="tune the linear (GEMM) shapes only")
     args = ap.parse_args()
     out_dir = args.out_dir
     os.makedirs(out_dir, exist_ok=True)
     dev = torch.device("cuda")
     convs, gemms = collect_shapes(tuple(args.models.split(",")), batch=args.batch)
+    if args.gemms_only:
+        convs = []
     mode = "big" if args.big_only else "legacy" if args.legacy_only else args.mode
     global CONC
     CONC = args.conc

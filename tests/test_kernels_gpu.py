@@ -253,6 +253,49 @@ def test_convgru_gates(cuda, N, C, H, W):
     assert _rel(hn, ref.convgru_gates2(c, h, z)) < 2e-3
 
 
+@pytest.mark.parametrize("B,H,W,C1,C2,Co", [(8, 64, 64, 320, 320, 320), (8, 32, 32, 640, 320, 640),
+                                             (8, 16, 16, 1280, 640, 1280), (2, 8, 8, 1280, 1280, 1280),
+                                             (2, 24, 24, 1536, 1152, 1536)])
+def test_skip_concat_read_in_place_is_bitwise(cuda, B, H, W, C1, C2, Co):
+    """UNet up-path [h | skip] read in place (ops.CatPair): GroupNorm table, table-apply, the 1x1
+    shortcut conv and a whole ResBlock are bitwise equal to the materialised-concat path."""
+    from arbius_amd.models.layers import init_weights
+    from arbius_amd.models.unet2d import ResBlock
+    torch.manual_seed(11)
+    a = torch.randn(B, H, W, C1, device=cuda).bfloat16()
+    b = (torch.randn(B, H, W, C2, device=cuda) * 2).bfloat16()
+    cat = torch.cat([a, b], -1)
+    pair = ops.cat_channels(a, b)
+    assert isinstance(pair, ops.CatPair)
+    g = (torch.rand(C1 + C2, device=cuda) + 0.5).bfloat16()
+    bt = torch.randn(C1 + C2, device=cuda).bfloat16()
+    t1, t2 = ops.group_norm_table(pair, g, bt, 32, 1e-5), ops.group_norm_table(cat, g, bt, 32, 1e-5)
+    assert torch.equal(t1, t2)
+    assert torch.equal(_lib.norm_table_apply(a, t1, True, x2=b), _lib.norm_table_apply(cat, t2, True))
+    w = (torch.randn(Co, 1, 1, C1 + C2, device=cuda) / math.sqrt(C1 + C2)).bfloat16()
+    bias = torch.randn(Co, device=cuda).bfloat16()
+    for pb in (None, 2):
+        with ops.plan_batch(pb) if pb else torch.no_grad():
+            assert torch.equal(ops.conv2d(pair, w, bias, padding=0), ops.conv2d(cat, w, bias, padding=0))
+    rb = init_weights(ResBlock(C1 + C2, Co, 4 * 64, 32, 1e-5), 3).to(cuda, torch.bfloat16)
+    temb = torch.randn(B, Co, device=cuda).bfloat16()
+    with torch.no_grad():
+        assert torch.equal(rb(pair, temb), rb(cat, temb))
+
+
+@pytest.mark.parametrize("B,N,D", [(1, 4096, 512), (2, 2880, 512), (1, 1024, 512), (1, 100, 512)])
+def test_large_head_attention(cuda, B, N, D):
+    """d = 512 single-head attention (VAE / MoVQ mid block): GEMM -> HIP row softmax -> GEMM."""
+    torch.manual_seed(10)
+    qkv = torch.randn(B, N, 3, 1, D, device=cuda).bfloat16()
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    scale = 1 / math.sqrt(D)
+    o = ops.attention(q, k, v)
+    r = ref.attention(q.float(), k.float(), v.float(), scale, False)
+    assert o.shape == r.shape and _rel(o, r) < 2e-2
+    assert torch.equal(o, ops.attention(q, k, v))
+
+
 @pytest.mark.parametrize("B,C,H,W,k,stride,dil,act", [
     (2, 72, 64, 64, 3, 2, 1, "relu"), (3, 120, 32, 30, 5, 1, 1, None), (2, 960, 16, 16, 5, 1, 2, "hs"),
     (1, 200, 17, 13, 3, 1, 1, "hs"), (4, 16, 135, 240, 3, 1, 1, "relu"), (2, 672, 33, 31, 5, 2, 1, "hs")])
