@@ -16,7 +16,7 @@ import os
 from typing import Callable, Dict, List, Tuple
 
 # bump on ANY change of output bytes (kernels, conv plans, sampler arithmetic, PNG/MP4 encoders)
-NUMERICS_VERSION = "r2.4-hip-large-head-attn-rvm-boxpool"
+NUMERICS_VERSION = "r2.5-all-linears-hip-gemm-video-plans"
 
 # Environment knobs that select a different kernel library, plan table, tiling or reference ops.
 # They exist for A/B measurement only; ``start`` refuses to mine with any of them set.
