@@ -139,6 +139,22 @@ def test_conv2d_all_tile_configs(cuda, cfg, split):
     assert _rel(y, ref_y) < 1e-2, (cfg, split, _rel(y, ref_y))
 
 
+@pytest.mark.parametrize("B,H,W,C,Co,k", [(8, 64, 64, 320, 320, 3), (2, 16, 16, 640, 1280, 1), (1, 9, 13, 128, 72, 3)])
+def test_conv_tile_families_bitwise_equal(cuda, B, H, W, C, Co, k):
+    """Every tile family (register-staged, LDS-DMA ring, 8-wave, 3-stage 8-wave) reduces each output
+    in the same MFMA order at split 1, so they are bitwise interchangeable - what lets the planner
+    remap a norm-prologue or two-source call onto the register-staged kernel without changing bytes."""
+    torch.manual_seed(12)
+    x = torch.randn(B, H, W, C, device=cuda).bfloat16()
+    w = (torch.randn(Co, k, k, C, device=cuda) / math.sqrt(k * k * C)).bfloat16()
+    b = torch.randn(Co, device=cuda).bfloat16()
+    pad = k // 2
+    ref_y = _lib.conv2d_nhwc(x, w, b, pad, False, None, None, 1, 10, 1)
+    for cfg in (0, 3, 5, 6, 13, 15, 16, 20, 21, 22, 28, 29, 31):
+        y = _lib.conv2d_nhwc(x, w, b, pad, False, None, None, 1, cfg, 1)
+        assert torch.equal(y, ref_y), cfg
+
+
 @pytest.mark.parametrize("cfg", [24, 25, 26, 27])
 @pytest.mark.parametrize("res", [False, True])
 def test_gemm_persistent_many_tiles(cuda, cfg, res):
