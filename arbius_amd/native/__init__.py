@@ -1,10 +1,11 @@
 """Native C++ CPU runtime of the node (``src/native.cpp``): keccak256, deterministic
-PNG, H.264 I_PCM payload, secp256k1 ECDSA.  Built in-tree by ``python -m arbius_amd.native.build``
+PNG, H.264 I_PCM payload and the CAVLC intra codec (``src/h264.cpp``), secp256k1 ECDSA.  Built in-tree by ``python -m arbius_amd.native.build``
 (``__graft_entry__.build()``); every function has a byte-identical Python
 reference that tests compare against.  When the extension is not built the
 names are absent and callers use their Python reference (``loaded`` is False)."""
 try:
-    from ._native import (keccak256, pcm_slice_body, png_encode, secp256k1_pubkey,  # noqa: F401
+    from ._native import (h264_decode, h264_decode_rgb, h264_encode_rgb, h264_encode_yuv, h264_parameter_sets,  # noqa: F401
+                          h264_tables_ok, keccak256, pcm_slice_body, png_encode, secp256k1_pubkey,
                           secp256k1_recover, secp256k1_sign, sha256)
     loaded = True
 except ImportError:  # not built (CPU-only checkout before build())

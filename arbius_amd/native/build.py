@@ -11,8 +11,8 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 SRC = HERE / "src" / "native.cpp"
-SOURCES = [SRC, HERE / "src" / "secp256k1.cpp"]
-HEADERS = [HERE / "src" / "secp256k1.h"]
+SOURCES = [SRC, HERE / "src" / "secp256k1.cpp", HERE / "src" / "h264.cpp"]
+HEADERS = [HERE / "src" / "secp256k1.h", HERE / "src" / "h264.h"]
 
 
 def target() -> Path:

@@ -14,13 +14,16 @@
 //
 // Everything is a pure function of its input (no time, no thread-count dependence:
 // each thread writes a disjoint, precomputed byte range).
+#include "h264.h"
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <zlib.h>
 
 #include "secp256k1.h"
 
 #include <algorithm>
+#include <functional>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
@@ -209,6 +212,157 @@ static py::bytes pcm_slice_body(py::array_t<uint8_t, py::array::c_style | py::ar
   return py::bytes(out);
 }
 
+
+// ------------------------------------------------------------------------------------ H.264 CAVLC
+// RGB -> 4:2:0 (the same integer BT.601 conversion as pcm_slice_body / mp4.rgb_to_yuv420) of an
+// H x W frame edge-replicated to H16 x W16 (whole macroblocks; the SPS crops it back)
+static void rgb_to_420(const uint8_t* src, int H, int W, int H16, int W16, uint8_t* y, uint8_t* cb, uint8_t* cr) {
+  auto px = [&](int r, int x) { return src + ((size_t)std::min(r, H - 1) * W + std::min(x, W - 1)) * 3; };
+  for (int r = 0; r < H16; ++r)
+    for (int x = 0; x < W16; ++x) {
+      const uint8_t* p = px(r, x);
+      y[(size_t)r * W16 + x] = clip1(((66 * p[0] + 129 * p[1] + 25 * p[2] + 128) >> 8) + 16);
+    }
+  for (int r = 0; r < H16 / 2; ++r)
+    for (int x = 0; x < W16 / 2; ++x) {
+      const uint8_t *a = px(2 * r, 2 * x), *b = px(2 * r, 2 * x + 1), *c = px(2 * r + 1, 2 * x), *d = px(2 * r + 1, 2 * x + 1);
+      const int rr = a[0] + b[0] + c[0] + d[0], g = a[1] + b[1] + c[1] + d[1], bl = a[2] + b[2] + c[2] + d[2];
+      cb[(size_t)r * (W16 / 2) + x] = clip1(((-38 * rr - 74 * g + 112 * bl + 512) >> 10) + 128);
+      cr[(size_t)r * (W16 / 2) + x] = clip1(((112 * rr - 94 * g - 18 * bl + 512) >> 10) + 128);
+    }
+}
+
+static void run_parallel(int n, int threads, const std::function<void(int)>& fn) {
+  std::vector<std::string> errors(n);
+  auto work = [&](int t, int nt) {
+    for (int i = t; i < n; i += nt) {
+      try {
+        fn(i);
+      } catch (const std::exception& e) {
+        errors[i] = e.what();
+      }
+    }
+  };
+  const int nt = std::max(1, std::min(threads, n));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work, t, nt);
+  work(0, nt);
+  for (auto& th : pool) th.join();
+  for (auto& e : errors)
+    if (!e.empty()) throw std::runtime_error(e);
+}
+
+// frames uint8 [F, H, W, 3] -> (sps, pps, [IDR NAL per frame]); frames are independent pictures,
+// so they are encoded in parallel (the output does not depend on the thread count).
+static py::tuple h264_encode_rgb(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> frames, int qp,
+                                 int threads) {
+  auto b = frames.request();
+  if (b.ndim != 4 || b.shape[3] != 3 || b.shape[0] < 1 || b.shape[1] < 1 || b.shape[2] < 1)
+    throw std::invalid_argument("h264_encode_rgb: frames [F, H, W, 3]");
+  const int F = (int)b.shape[0], H = (int)b.shape[1], W = (int)b.shape[2];
+  const int H16 = (H + 15) / 16 * 16, W16 = (W + 15) / 16 * 16;
+  const uint8_t* src = static_cast<const uint8_t*>(b.ptr);
+  std::vector<std::string> nals(F);
+  std::string sps, pps;
+  h264::parameter_sets(W, H, qp, sps, pps);
+  {
+    py::gil_scoped_release nogil;
+    run_parallel(F, threads, [&](int i) {
+      std::vector<uint8_t> y((size_t)H16 * W16), cb((size_t)H16 * W16 / 4), cr((size_t)H16 * W16 / 4);
+      rgb_to_420(src + (size_t)i * H * W * 3, H, W, H16, W16, y.data(), cb.data(), cr.data());
+      nals[i] = h264::encode_idr(y.data(), cb.data(), cr.data(), W16, H16, qp, i, nullptr, nullptr, nullptr);
+    });
+  }
+  py::list out;
+  for (auto& n : nals) out.append(py::bytes(n));
+  return py::make_tuple(py::bytes(sps), py::bytes(pps), out);
+}
+
+using u8arr = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+
+// One picture from 4:2:0 planes -> (IDR NAL, recon Y, recon Cb, recon Cr) (tests: recon == decoder output)
+static py::tuple h264_encode_yuv(u8arr y, u8arr cb, u8arr cr, int qp, int idr_pic_id) {
+  auto by = y.request(), bcb = cb.request(), bcr = cr.request();
+  if (by.ndim != 2 || bcb.ndim != 2 || bcr.ndim != 2) throw std::invalid_argument("h264_encode_yuv: 2-D planes");
+  const int H = (int)by.shape[0], W = (int)by.shape[1];
+  if (bcb.shape[0] != H / 2 || bcb.shape[1] != W / 2 || bcr.shape[0] != H / 2 || bcr.shape[1] != W / 2)
+    throw std::invalid_argument("h264_encode_yuv: chroma planes must be [H/2, W/2]");
+  u8arr ry({H, W}), rcb({H / 2, W / 2}), rcr({H / 2, W / 2});
+  std::string nal = h264::encode_idr(static_cast<const uint8_t*>(by.ptr), static_cast<const uint8_t*>(bcb.ptr),
+                                     static_cast<const uint8_t*>(bcr.ptr), W, H, qp, idr_pic_id, ry.mutable_data(),
+                                     rcb.mutable_data(), rcr.mutable_data());
+  return py::make_tuple(py::bytes(nal), ry, rcb, rcr);
+}
+
+static py::tuple h264_parameter_sets(int width, int height, int qp) {
+  std::string sps, pps;
+  h264::parameter_sets(width, height, qp, sps, pps);
+  return py::make_tuple(py::bytes(sps), py::bytes(pps));
+}
+
+// NAL units (no start codes) -> [(Y, Cb, Cr, (crop_w, crop_h))]; raises ValueError outside the subset
+static py::list h264_decode(const std::vector<std::string>& nals, int threads) {
+  std::vector<h264::Picture> pics;
+  {
+    py::gil_scoped_release nogil;
+    try {
+      pics = h264::decode(nals, threads);
+    } catch (const std::runtime_error& e) {
+      py::gil_scoped_acquire gil;
+      throw py::value_error(e.what());
+    }
+  }
+  py::list out;
+  for (auto& p : pics) {
+    u8arr y({p.h16, p.w16}), cb({p.h16 / 2, p.w16 / 2}), cr({p.h16 / 2, p.w16 / 2});
+    std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
+    std::memcpy(cb.mutable_data(), p.cb.data(), p.cb.size());
+    std::memcpy(cr.mutable_data(), p.cr.data(), p.cr.size());
+    out.append(py::make_tuple(y, cb, cr, py::make_tuple(p.crop_w, p.crop_h)));
+  }
+  return out;
+}
+
+// NAL units -> uint8 RGB [F, crop_h, crop_w, 3]: the integer BT.601 inverse of rgb_to_420 (the
+// reference is video_io.yuv420_to_rgb: nearest chroma upsampling, clipped).
+static u8arr h264_decode_rgb(const std::vector<std::string>& nals, int threads) {
+  std::vector<h264::Picture> pics;
+  {
+    py::gil_scoped_release nogil;
+    try {
+      pics = h264::decode(nals, threads);
+    } catch (const std::runtime_error& e) {
+      py::gil_scoped_acquire gil;
+      throw py::value_error(e.what());
+    }
+  }
+  if (pics.empty()) throw py::value_error("no pictures in the H.264 stream");
+  const int H = pics[0].crop_h, W = pics[0].crop_w;
+  for (auto& p : pics)
+    if (p.crop_h != H || p.crop_w != W) throw py::value_error("pictures of different sizes");
+  const int F = (int)pics.size();
+  u8arr out({F, H, W, 3});
+  uint8_t* dst = out.mutable_data();
+  {
+    py::gil_scoped_release nogil;
+    run_parallel(F, threads, [&](int i) {
+      const h264::Picture& p = pics[i];
+      uint8_t* o = dst + (size_t)i * H * W * 3;
+      for (int r = 0; r < H; ++r)
+        for (int x = 0; x < W; ++x) {
+          const int c = int(p.y[(size_t)r * p.w16 + x]) - 16;
+          const int d = int(p.cb[(size_t)(r / 2) * (p.w16 / 2) + x / 2]) - 128;
+          const int e = int(p.cr[(size_t)(r / 2) * (p.w16 / 2) + x / 2]) - 128;
+          uint8_t* q = o + ((size_t)r * W + x) * 3;
+          q[0] = (uint8_t)std::min(255, std::max(0, (298 * c + 409 * e + 128) >> 8));
+          q[1] = (uint8_t)std::min(255, std::max(0, (298 * c - 100 * d - 208 * e + 128) >> 8));
+          q[2] = (uint8_t)std::min(255, std::max(0, (298 * c + 516 * d + 128) >> 8));
+        }
+    });
+  }
+  return out;
+}
+
 static py::bytes as_bytes32(const py::bytes& b, const char* what) {
   std::string s = b;
   if (s.size() != 32) throw std::invalid_argument(std::string(what) + " must be 32 bytes");
@@ -257,9 +411,19 @@ PYBIND11_MODULE(_native, m) {
   m.def("secp256k1_pubkey", &py_secp_pubkey, "uncompressed public key X||Y");
   m.def("secp256k1_recover", &py_secp_recover, "ecrecover -> X||Y or None");
   m.def("sha256", &py_sha256, "SHA-256 (the RFC 6979 HMAC's hash; checked against hashlib)");
-  m.doc() = "arbius_amd native CPU runtime (keccak256, PNG, H.264 I_PCM payload)";
+  m.doc() = "arbius_amd native CPU runtime (keccak256, PNG, H.264 intra codec, secp256k1)";
   m.def("keccak256", &keccak256, "Ethereum keccak-256");
   m.def("png_encode", &png_encode, py::arg("img"), py::arg("level") = 6, "deterministic filter-0 PNG");
   m.def("pcm_slice_body", &pcm_slice_body, py::arg("frame"), py::arg("threads") = 8,
         "H.264 I_PCM macroblock payload of one RGB frame");
+  m.def("h264_encode_rgb", &h264_encode_rgb, py::arg("frames"), py::arg("qp"), py::arg("threads") = 8,
+        "H.264 CAVLC intra: RGB frames [F, H, W, 3] -> (sps, pps, [IDR NAL])");
+  m.def("h264_encode_yuv", &h264_encode_yuv, py::arg("y"), py::arg("cb"), py::arg("cr"), py::arg("qp"),
+        py::arg("idr_pic_id") = 0, "one 4:2:0 picture -> (IDR NAL, recon Y, Cb, Cr)");
+  m.def("h264_parameter_sets", &h264_parameter_sets, "(sps, pps) NALs for the CAVLC intra stream");
+  m.def("h264_decode", &h264_decode, py::arg("nals"), py::arg("threads") = 8,
+        "decode intra CAVLC / I_PCM NAL units -> [(Y, Cb, Cr, (w, h))]");
+  m.def("h264_decode_rgb", &h264_decode_rgb, py::arg("nals"), py::arg("threads") = 8,
+        "decode intra CAVLC / I_PCM NAL units -> uint8 RGB [F, H, W, 3] (cropped)");
+  m.def("h264_tables_ok", &h264::tables_prefix_free, "every CAVLC VLC table is prefix-free");
 }

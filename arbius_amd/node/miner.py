@@ -164,15 +164,26 @@ class Miner:
             return None
         for row in template.get("input", []):
             if row.get("type") == "file" and inp.get(row["variable"]):
-                from ..utils.video_io import VideoSourceError, check_source
+                from ..utils.video_io import UndecodableVideo, VideoSourceError, check_source, probe_video
+                loop = asyncio.get_running_loop()
                 try:
-                    await asyncio.get_running_loop().run_in_executor(None, check_source, inp[row["variable"]])
+                    await loop.run_in_executor(None, check_source, inp[row["variable"]])
                 except VideoSourceError as e:
                     # untrusted source this node will not read (local file, private address, plain
                     # http): skip - not invalid, other miners may legitimately read it
                     log.warning("Task (%s) input %s refused: %s", taskid, row["variable"], e)
                     self.metrics.inc("tasks_refused_source")
                     return None
+                try:
+                    await loop.run_in_executor(None, probe_video, inp[row["variable"]])
+                except UndecodableVideo as e:
+                    # outside this node's decoder (e.g. P/B-frame H.264 without ffmpeg): skip, not
+                    # invalid - a miner with a full decoder can solve it, so contesting would be wrong
+                    log.warning("Task (%s) input %s not decodable here: %s", taskid, row["variable"], e)
+                    self.metrics.inc("tasks_undecodable_input")
+                    return None
+                except Exception as e:  # noqa: BLE001 - fetch failure: the solve retries the fetch
+                    log.warning("Task (%s) input %s probe fetch failed: %r", taskid, row["variable"], e)
         inp["seed"] = taskid2seed(taskid)
         self.db.store_task_input(taskid, cid, inp)
         self.queue("pinTaskInput", 10, 0, True, {"taskid": taskid, "input": pre_str})

@@ -1,22 +1,22 @@
-"""Deterministic MP4 (H.264) writer for the video models' ``out-1.mp4``
-(templates zeroscopev2xl / damo / robust_video_matting, SURVEY.md §2.6(c,d)).
+"""Deterministic MP4 (H.264) writer / reader for the video models' ``out-1.mp4``
+(templates zeroscopev2xl / damo / robust_video_matting, SURVEY.md §2.6(c,d)) and their
+``input_video``.
 
 There is no ffmpeg/libx264 in the image and a solution CID must be a pure
-function of the frames, so the encoder is self-contained and bit-exact:
+function of the frames, so the codec is self-contained and bit-exact:
 
 * colour: RGB -> BT.601 limited-range YCbCr 4:2:0 in integer arithmetic
   (chroma = rounded 2x2 mean of the RGB samples, then the integer matrix);
-* bitstream: H.264 Constrained Baseline, every picture one IDR slice made of
-  I_PCM macroblocks (mb_type 25: raw samples, lossless w.r.t. the YCbCr
-  planes, decodable by every H.264 decoder).  Samples are clamped to
-  [1, 254], so the macroblock payload can never contain a start-code prefix
-  (``00 00 0x``) and only the slice header needs emulation prevention;
+* bitstream (default, ``codec="avc-intra"``): H.264 Constrained Baseline, every picture one
+  IDR slice of Intra_16x16 macroblocks coded with CAVLC at a fixed QP, deblocking disabled
+  (``native/src/h264.cpp``: the encoder's reconstruction IS every decoder's output).  Round 1
+  wrote raw I_PCM macroblocks (``codec="pcm"``, still available and still decodable): a
+  48-frame 1080p clip was ~149 MB per task pinned to IPFS; the CAVLC intra stream is 10-40x
+  smaller;
 * container: ftyp + moov (faststart) + mdat, fixed zero timestamps, AVCC
   4-byte NAL lengths, avcC with the SPS/PPS.
 
-The whole frame -> bytes path is numpy-vectorised (one concatenate per
-picture, no per-macroblock Python); odd sizes are padded to whole macroblocks
-with edge replication and cropped back in the SPS.
+Odd sizes are padded to whole macroblocks with edge replication and cropped back in the SPS.
 """
 from __future__ import annotations
 
@@ -26,6 +26,9 @@ from typing import List, Sequence, Tuple
 import numpy as np
 
 PROFILE_IDC, CONSTRAINT_FLAGS, LEVEL_IDC = 66, 0xC0, 51
+# fixed quantiser of the CAVLC intra stream (part of NUMERICS_VERSION: changing it changes CIDs)
+INTRA_QP = 20
+CODECS = ("avc-intra", "pcm")
 
 
 class _Bits:
@@ -80,7 +83,7 @@ def _nal(ref_idc: int, typ: int, payload: bytes) -> bytes:
     return bytes([(ref_idc << 5) | typ]) + payload
 
 
-def sps_pps(width: int, height: int) -> Tuple[bytes, bytes]:
+def sps_pps(width: int, height: int, qp: int = 26) -> Tuple[bytes, bytes]:
     mbw, mbh = (width + 15) // 16, (height + 15) // 16
     s = _Bits()
     s.u(8, PROFILE_IDC); s.u(8, CONSTRAINT_FLAGS); s.u(8, LEVEL_IDC)
@@ -106,7 +109,7 @@ def sps_pps(width: int, height: int) -> Tuple[bytes, bytes]:
     p.ue(0)               # num_slice_groups_minus1
     p.ue(0); p.ue(0)      # num_ref_idx_l0/l1_default_active_minus1
     p.u(1, 0); p.u(2, 0)  # weighted_pred_flag, weighted_bipred_idc
-    p.se(0); p.se(0); p.se(0)   # pic_init_qp/qs_minus26, chroma_qp_index_offset
+    p.se(qp - 26); p.se(0); p.se(0)   # pic_init_qp/qs_minus26, chroma_qp_index_offset
     p.u(1, 1)             # deblocking_filter_control_present_flag
     p.u(1, 0); p.u(1, 0)  # constrained_intra_pred_flag, redundant_pic_cnt_present_flag
     p.trailing()
@@ -182,7 +185,7 @@ def _full(typ: bytes, version: int, flags: int, *parts: bytes) -> bytes:
 _MATRIX = struct.pack(">9I", 0x10000, 0, 0, 0, 0x10000, 0, 0, 0, 0x40000000)
 
 
-def _moov(width, height, fps, sizes, sps, pps, mdat_offset) -> bytes:
+def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False) -> bytes:
     F = len(sizes)
     dur_ms = int(round(F * 1000 / fps))
     mvhd = _full(b"mvhd", 0, 0, struct.pack(">IIII", 0, 0, 1000, dur_ms), struct.pack(">IH", 0x10000, 0x100),
@@ -195,7 +198,7 @@ def _moov(width, height, fps, sizes, sps, pps, mdat_offset) -> bytes:
     dinf = _box(b"dinf", _full(b"dref", 0, 0, struct.pack(">I", 1), _full(b"url ", 0, 1)))
     avcc = _box(b"avcC", bytes([1, PROFILE_IDC, CONSTRAINT_FLAGS, LEVEL_IDC, 0xFF, 0xE1]),
                 struct.pack(">H", len(sps)), sps, b"\x01", struct.pack(">H", len(pps)), pps)
-    name = b"\x0bI_PCM H.264".ljust(32, b"\0")
+    name = (b"\x0bI_PCM H.264" if pcm else b"\x0fAVC intra CAVLC").ljust(32, b"\0")
     avc1 = _box(b"avc1", b"\0" * 6, struct.pack(">H", 1), b"\0" * 16, struct.pack(">HH", width, height),
                 struct.pack(">III", 0x480000, 0x480000, 0), struct.pack(">H", 1), name,
                 struct.pack(">Hh", 0x18, -1), avcc)
@@ -210,32 +213,42 @@ def _moov(width, height, fps, sizes, sps, pps, mdat_offset) -> bytes:
     return _box(b"moov", mvhd, _box(b"trak", tkhd, mdia))
 
 
-def encode_mp4(frames: Sequence[np.ndarray], fps: int) -> bytes:
+def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra", threads: int = 16) -> bytes:
     """uint8 RGB frames [H, W, 3] (all the same size) -> MP4 bytes (deterministic)."""
     frames = list(frames)
     if not frames:
         raise ValueError("encode_mp4: no frames")
+    if codec not in CODECS:
+        raise ValueError(f"encode_mp4: codec must be one of {CODECS}")
     H, W = frames[0].shape[:2]
     fps = max(1, int(fps))
-    sps, pps = sps_pps(W, H)
-    samples = []
-    for i, f in enumerate(frames):
+    for f in frames:
         if f.shape != (H, W, 3) or f.dtype != np.uint8:
             raise ValueError("encode_mp4: frames must be uint8 [H, W, 3] of one size")
-        nal = encode_idr_pcm(f, i)
-        samples.append(struct.pack(">I", len(nal)) + nal)
+    pcm = codec == "pcm"
+    if pcm:
+        sps, pps = sps_pps(W, H)
+        nals = [encode_idr_pcm(f, i) for i, f in enumerate(frames)]
+    else:
+        from .. import native
+        if not native.loaded:
+            raise RuntimeError("encode_mp4: the native runtime (H.264 intra encoder) is not built; "
+                               "run python -m arbius_amd.native.build")
+        sps, pps = sps_pps(W, H, INTRA_QP)
+        _, _, nals = native.h264_encode_rgb(np.stack(frames), INTRA_QP, threads)
+    samples = [struct.pack(">I", len(n)) + n for n in nals]
     sizes = [len(s) for s in samples]
     ftyp = _box(b"ftyp", b"isom", struct.pack(">I", 512), b"isomiso2avc1mp41")
-    moov_len = len(_moov(W, H, fps, sizes, sps, pps, 0))
+    moov_len = len(_moov(W, H, fps, sizes, sps, pps, 0, pcm))
     mdat_payload = sum(sizes)
     offset = len(ftyp) + moov_len + 8
-    moov = _moov(W, H, fps, sizes, sps, pps, offset)
+    moov = _moov(W, H, fps, sizes, sps, pps, offset, pcm)
     if 8 + mdat_payload > 0xFFFFFFFF:
         raise ValueError("encode_mp4: output above 4 GiB")
     return ftyp + moov + struct.pack(">I", 8 + mdat_payload) + b"mdat" + b"".join(samples)
 
 
-# ------------------------------------------------------------------------------------ reader (tests)
+# ------------------------------------------------------------------------------------ readers
 def _boxes(data: bytes, start: int = 0, end: int = None):
     end = len(data) if end is None else end
     i = start
@@ -283,3 +296,124 @@ def read_mp4_pcm(data: bytes, with_size: bool = False):
         crp = body[:, 322:386].reshape(mbh, mbw, 8, 8).transpose(0, 2, 1, 3).reshape(H16 // 2, W16 // 2)
         out.append((y, cbp, crp))
     return (fps, out, (W, H)) if with_size else (fps, out)
+
+
+def read_mp4_nals(data: bytes):
+    """Demux an MP4 with one avc1 track: (fps, [NAL bytes] = SPS, PPS, one slice NAL per sample
+    (4-byte AVCC lengths; every NAL of a sample), (W, H)).  Raises ValueError on other layouts."""
+    try:
+        top = {t: (a, b) for t, a, b in _boxes(data)}
+        ma, mb = top[b"moov"]
+
+        def find(path, a, b):
+            for t, x, y in _boxes(data, a, b):
+                if t == path[0]:
+                    if len(path) == 1:
+                        return x, y
+                    skip = {b"stsd": 8, b"avc1": 78, b"dref": 8}.get(path[0], 0)
+                    return find(path[1:], x + skip, y)
+            raise KeyError(path)
+
+        stbl = [b"trak", b"mdia", b"minf", b"stbl"]
+        ha, _ = find([b"trak", b"mdia", b"mdhd"], ma, mb)
+        ver = data[ha]
+        ts_off = ha + (20 if ver == 1 else 12)
+        timescale = struct.unpack(">I", data[ts_off:ts_off + 4])[0]
+        dur = (struct.unpack(">Q", data[ts_off + 4:ts_off + 12])[0] if ver == 1
+               else struct.unpack(">I", data[ts_off + 4:ts_off + 8])[0])
+        sa, _ = find(stbl + [b"stsz"], ma, mb)
+        const, n = struct.unpack(">II", data[sa + 4:sa + 12])
+        sizes = [const] * n if const else list(struct.unpack(">%dI" % n, data[sa + 12:sa + 12 + 4 * n]))
+        # chunk offsets (stco / co64) and samples-per-chunk runs (stsc)
+        try:
+            ca, _ = find(stbl + [b"stco"], ma, mb)
+            nc = struct.unpack(">I", data[ca + 4:ca + 8])[0]
+            chunks = list(struct.unpack(">%dI" % nc, data[ca + 8:ca + 8 + 4 * nc]))
+        except KeyError:
+            ca, _ = find(stbl + [b"co64"], ma, mb)
+            nc = struct.unpack(">I", data[ca + 4:ca + 8])[0]
+            chunks = list(struct.unpack(">%dQ" % nc, data[ca + 8:ca + 8 + 8 * nc]))
+        xa, _ = find(stbl + [b"stsc"], ma, mb)
+        ne = struct.unpack(">I", data[xa + 4:xa + 8])[0]
+        runs = [struct.unpack(">III", data[xa + 8 + 12 * i:xa + 20 + 12 * i]) for i in range(ne)]
+        va, vb = find(stbl + [b"stsd", b"avc1"], ma, mb)
+        W, H = struct.unpack(">HH", data[va + 24:va + 28])
+        ca_, _ = find([b"avcC"], va + 78, vb)
+        cfg = data[ca_:]
+        nsps = cfg[5] & 0x1F
+        i = 6
+        ps = []
+        for _ in range(nsps):
+            ln = struct.unpack(">H", cfg[i:i + 2])[0]
+            ps.append(bytes(cfg[i + 2:i + 2 + ln]))
+            i += 2 + ln
+        npps = cfg[i]
+        i += 1
+        for _ in range(npps):
+            ln = struct.unpack(">H", cfg[i:i + 2])[0]
+            ps.append(bytes(cfg[i + 2:i + 2 + ln]))
+            i += 2 + ln
+        nal_len = (cfg[4] & 3) + 1
+        nals = list(ps)
+        s = 0
+        for ci, off in enumerate(chunks):
+            per = next(r[1] for r in reversed(runs) if r[0] <= ci + 1)
+            for _ in range(per):
+                if s >= n:
+                    break
+                end, p = off + sizes[s], off
+                while p < end:
+                    ln = int.from_bytes(data[p:p + nal_len], "big")
+                    nals.append(bytes(data[p + nal_len:p + nal_len + ln]))
+                    p += nal_len + ln
+                off = end
+                s += 1
+        fps = int(round(n * timescale / dur)) if dur else 24
+        return max(1, fps), nals, (W, H)
+    except (KeyError, struct.error, IndexError, StopIteration) as e:
+        raise ValueError(f"not an MP4 with one H.264 (avc1) video track: {e!r}") from None
+
+
+def annexb_nals(data: bytes) -> List[bytes]:
+    """Split an Annex-B byte stream (00 00 01 / 00 00 00 01 start codes) into NAL units."""
+    out, i, n = [], 0, len(data)
+    starts = []
+    while True:
+        j = data.find(b"\x00\x00\x01", i)
+        if j < 0:
+            break
+        starts.append(j + 3)
+        i = j + 3
+    for k, st in enumerate(starts):
+        end = starts[k + 1] - 3 if k + 1 < len(starts) else n
+        nal = data[st:end]
+        while nal.endswith(b"\x00"):          # trailing_zero_8bits / next 4-byte start code
+            nal = nal[:-1]
+        if nal:
+            out.append(bytes(nal))
+    return out
+
+
+def _threads() -> int:
+    import os
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def decode_h264_rgb(nals: Sequence[bytes]) -> np.ndarray:
+    """NAL units -> uint8 RGB [F, H, W, 3] (cropped), native decoder + integer BT.601 inverse."""
+    from .. import native
+    if not native.loaded:
+        raise RuntimeError("the native runtime (H.264 decoder) is not built")
+    return native.h264_decode_rgb(list(nals), _threads())
+
+
+def decode_h264(nals: Sequence[bytes]):
+    """NAL units -> [(Y, Cb, Cr)] at macroblock-padded size, plus (crop_w, crop_h), through the
+    native intra decoder.  ValueError for streams outside its subset (P/B slices, CABAC, ...)."""
+    from .. import native
+    if not native.loaded:
+        raise RuntimeError("the native runtime (H.264 decoder) is not built")
+    pics = native.h264_decode(list(nals), _threads())
+    if not pics:
+        raise ValueError("no pictures in the H.264 stream")
+    return [(y, cb, cr) for y, cb, cr, _ in pics], pics[0][3]

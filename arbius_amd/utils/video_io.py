@@ -13,10 +13,13 @@ a URL / IPFS reference to a video, ``templates/robust_video_matting.json:6``).
 Local paths, ``file://`` and plain ``http://`` are refused (``VideoSourceError``), and every
 download is capped at ``MAX_VIDEO_BYTES``.
 
-Containers: MP4 written by ``utils/mp4.py`` (H.264 I_PCM, decoded natively and
-exactly), ``.npy`` uint8 [T, H, W, 3] (``allow_pickle=False``); anything else is
-decoded by an ``ffmpeg`` binary when one is on PATH (the image ships none -
-then the task fails loudly instead of guessing).
+Containers: MP4 (any single avc1 track) or a raw Annex-B H.264 stream, decoded by the native
+intra decoder (``native/src/h264.cpp``: CAVLC I slices - I_PCM / Intra_16x16 / Intra_4x4,
+deblocking off; exactly what ``utils/mp4.py`` writes), and ``.npy`` uint8 [T, H, W, 3]
+(``allow_pickle=False``).  Anything else (P/B frames, CABAC, in-loop deblocking) is decoded
+by an ``ffmpeg`` binary when one is on PATH; the image ships none, so ``probe`` rejects such
+inputs at hydration (``UndecodableVideo``: the node skips the task, it does not mark it
+invalid - a miner with a full decoder may solve it).
 """
 from __future__ import annotations
 
@@ -27,7 +30,7 @@ import re
 import shutil
 import subprocess
 import tempfile
-from typing import Tuple
+from typing import List, Tuple
 
 import numpy as np
 
@@ -129,28 +132,85 @@ def yuv420_to_rgb(y, cb, cr, H, W) -> np.ndarray:
     return np.clip(np.stack([r, g, b], -1), 0, 255).astype(np.uint8)
 
 
+class UndecodableVideo(ValueError):
+    """The input is not a video this node can decode (outside the native H.264 intra subset and
+    no ffmpeg): the task is skipped, never marked invalid - other miners may decode it."""
+
+
+def _ue(bits: str, i: int) -> Tuple[int, int]:
+    z = 0
+    while i < len(bits) and bits[i] == "0":
+        z += 1
+        i += 1
+    if i + z + 1 > len(bits):
+        raise UndecodableVideo("truncated slice header")
+    return int(bits[i:i + z + 1], 2) - 1, i + z + 1
+
+
+def _demux(data: bytes) -> Tuple[List[bytes], int]:
+    from .mp4 import annexb_nals, read_mp4_nals
+    if data[4:8] == b"ftyp":
+        try:
+            fps, nals, _ = read_mp4_nals(data)
+        except ValueError as e:
+            raise UndecodableVideo(str(e)) from None
+        return nals, fps
+    if data.startswith(b"\x00\x00\x01") or data.startswith(b"\x00\x00\x00\x01"):
+        return annexb_nals(data), 24          # raw Annex-B stream: no timing, template default
+    raise UndecodableVideo("input video is neither an MP4 nor an H.264 Annex-B stream")
+
+
+def probe(data: bytes) -> None:
+    """Cheap decodability check (hydration): container, then every slice header's slice_type
+    must be I, and the first picture must decode through the native intra decoder."""
+    if data[:6] == b"\x93NUMPY":
+        return
+    if shutil.which("ffmpeg"):
+        return
+    nals, _ = _demux(data)
+    first_pic, started, done = [], False, False
+    for n in nals:
+        typ = n[0] & 0x1F
+        if typ in (1, 5):
+            head = "".join(f"{b:08b}" for b in n[1:9].replace(b"\x00\x00\x03", b"\x00\x00"))
+            first_mb, i = _ue(head, 0)
+            slice_type, _ = _ue(head, i)
+            if slice_type % 5 != 2:
+                raise UndecodableVideo("input video has inter (P/B) slices: only intra H.264 decodes natively")
+            done = done or (started and first_mb == 0)
+            if not done:
+                first_pic.append(n)
+                started = True
+        elif not started:
+            first_pic.append(n)
+    from .mp4 import decode_h264
+    try:
+        decode_h264(first_pic)
+    except ValueError as e:
+        raise UndecodableVideo(str(e)) from None
+
+
 def decode(data: bytes) -> Tuple[np.ndarray, int]:
     if data[:6] == b"\x93NUMPY":
         arr = np.load(io.BytesIO(data), allow_pickle=False)
         return arr.astype(np.uint8), 24
-    if data[4:8] == b"ftyp":
-        try:
-            from .mp4 import read_mp4_pcm
-            fps, planes, (W, H) = read_mp4_pcm(data, with_size=True)
-            return np.stack([yuv420_to_rgb(y, cb, cr, H, W) for y, cb, cr in planes]), fps
-        except Exception:  # noqa: BLE001 - not our I_PCM layout: external decoder
-            pass
+    try:
+        nals, fps = _demux(data)
+        from .mp4 import decode_h264_rgb
+        return decode_h264_rgb(nals), fps
+    except ValueError as e:
+        native_err = e
     ff = shutil.which("ffmpeg")
     if ff is None:
-        raise RuntimeError("input video is not an I_PCM MP4 / .npy and no ffmpeg binary is available to decode it")
+        raise UndecodableVideo(f"native H.264 intra decoder: {native_err}; no ffmpeg binary for other streams")
     with tempfile.NamedTemporaryFile(suffix=".mp4") as f:
         f.write(data)
         f.flush()
-        probe = subprocess.run([ff, "-i", f.name], capture_output=True, text=True)
+        probe_out = subprocess.run([ff, "-i", f.name], capture_output=True, text=True)
         import re
-        m = re.search(r"(\d+)x(\d+)[, ].*?(\d+(?:\.\d+)?) fps", probe.stderr)
+        m = re.search(r"(\d+)x(\d+)[, ].*?(\d+(?:\.\d+)?) fps", probe_out.stderr)
         if not m:
-            raise RuntimeError("ffmpeg could not probe the input video")
+            raise UndecodableVideo("ffmpeg could not probe the input video")
         W, H, fps = int(m.group(1)), int(m.group(2)), float(m.group(3))
         raw = subprocess.run([ff, "-v", "error", "-i", f.name, "-f", "rawvideo", "-pix_fmt", "rgb24", "-"],
                              capture_output=True, check=True).stdout
@@ -159,3 +219,9 @@ def decode(data: bytes) -> Tuple[np.ndarray, int]:
 
 def load_video(ref: str) -> Tuple[np.ndarray, int]:
     return decode(fetch(ref))
+
+
+def probe_video(ref: str) -> None:
+    """Hydration-time check: the source is allowed AND decodable (raises VideoSourceError /
+    UndecodableVideo).  Fetch failures propagate as their own exceptions."""
+    probe(fetch(ref))

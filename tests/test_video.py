@@ -1,6 +1,11 @@
 """Video families (BASELINE config #4 zeroscopev2xl, damo) and the deterministic
-MP4 writer, on CPU: bitstream/container structure, lossless PCM round trip,
-tiny UNet3D pipeline determinism and a node round trip with out-1.mp4."""
+MP4 writer / H.264 intra codec, on CPU: bitstream/container structure, lossless PCM round
+trip, CAVLC intra encoder == decoder reconstruction, decodability probe, tiny UNet3D pipeline
+determinism and a node round trip with out-1.mp4.
+
+The CAVLC codec (``native/src/h264.cpp``) is checked against itself (encoder recon == decoder
+output), its VLC tables for prefix-freeness, and its rate/distortion for sanity; no third-party
+H.264 decoder exists in the image, so conformance against libavcodec is parity unpinned."""
 import asyncio
 import json
 
@@ -55,7 +60,7 @@ def test_emulation_prevention():
 def test_mp4_pcm_roundtrip_lossless_and_deterministic():
     rng = np.random.default_rng(0)
     frames = [rng.integers(0, 256, (40, 72, 3), dtype=np.uint8) for _ in range(4)]
-    a, b = encode_mp4(frames, 24), encode_mp4(frames, 24)
+    a, b = encode_mp4(frames, 24, codec="pcm"), encode_mp4(frames, 24, codec="pcm")
     assert a == b and a[4:8] == b"ftyp" and a[a.index(b"moov") - 4:].startswith(a[a.index(b"moov") - 4:][:4])
     fps, planes = read_mp4_pcm(a)
     assert fps == 24 and len(planes) == 4
@@ -96,3 +101,129 @@ def test_damo_tiny_through_node():
     row = json.loads(m.db.get_task_input(tid, e.tasks[tid].cid)["data"])
     sol = pool.solve_sync(model, tid, row)
     assert sol.files[0][0] == "out-1.mp4" and sol.cid == e.solutions[tid].cid
+
+
+# ------------------------------------------------------------------------------------ CAVLC intra codec
+def _test_picture(H=64, W=96, seed=0):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:H, 0:W]
+    y = ((xx * 2 + yy + 10 * np.sin(xx / 5.0)) % 256).astype(np.uint8)
+    y[H // 3:H // 3 + 20, W // 3:W // 3 + 30] = rng.integers(0, 256, (20, 30))
+    cb = ((xx[::2, ::2] + 100) % 256).astype(np.uint8)
+    cr = ((yy[::2, ::2] * 3 + 50) % 256).astype(np.uint8)
+    cr[:8, :8] = rng.integers(0, 256, (8, 8))
+    return y, cb, cr
+
+
+def test_h264_vlc_tables_prefix_free():
+    from arbius_amd import native
+    assert native.h264_tables_ok()
+
+
+def test_h264_parameter_sets_python_equals_native():
+    from arbius_amd import native
+    for w, h, qp in ((1920, 1080, 20), (96, 64, 26), (100, 50, 40)):
+        assert sps_pps(w, h, qp) == tuple(native.h264_parameter_sets(w, h, qp))
+
+
+def test_h264_intra_recon_is_decoder_output_every_qp():
+    from arbius_amd import native
+    y, cb, cr = _test_picture()
+    psnr, size = [], []
+    for qp in (4, 10, 20, 28, 36, 44, 51):     # (below ~4 Baseline level escapes clamp |level|)
+        nal, ry, rcb, rcr = native.h264_encode_yuv(y, cb, cr, qp, 1)
+        assert nal[0] == 0x65
+        sps, pps = native.h264_parameter_sets(96, 64, qp)
+        (dy, dcb, dcr, crop), = native.h264_decode([sps, pps, nal])
+        assert crop == (96, 64)
+        assert (dy == ry).all() and (dcb == rcb).all() and (dcr == rcr).all()
+        mse = np.mean((ry.astype(float) - y) ** 2)
+        psnr.append(10 * np.log10(255 ** 2 / max(mse, 1e-6)))
+        size.append(len(nal))
+    assert all(a > b for a, b in zip(psnr, psnr[1:])) and psnr[0] > 50 and psnr[2] > 40
+    assert all(a > b for a, b in zip(size, size[1:]))
+
+
+def test_h264_multi_slice_and_pcm_decode():
+    """I_PCM pictures (round-1 outputs) still decode losslessly through the native decoder."""
+    from arbius_amd.utils.mp4 import decode_h264, read_mp4_nals
+    rng = np.random.default_rng(5)
+    frames = [rng.integers(0, 256, (40, 72, 3), dtype=np.uint8) for _ in range(3)]
+    fps, nals, (W, H) = read_mp4_nals(encode_mp4(frames, 7, codec="pcm"))
+    planes, crop = decode_h264(nals)
+    assert fps == 7 and crop == (72, 40) and (W, H) == (72, 40)
+    for f, (y, cb, cr) in zip(frames, planes):
+        ey, ecb, ecr = rgb_to_yuv420(np.pad(f, ((0, 8), (0, 8), (0, 0)), mode="edge"))
+        assert (y == ey).all() and (cb == ecb).all() and (cr == ecr).all()
+
+
+def test_mp4_avc_intra_roundtrip_small_and_deterministic():
+    from arbius_amd.utils.video_io import decode, probe
+    yy, xx = np.mgrid[0:90, 0:160]
+    frames = [np.stack([(xx + 3 * t) % 256, (yy * 2 + t) % 256, ((xx + yy) // 2) % 256], -1).astype(np.uint8)
+              for t in range(6)]
+    a = encode_mp4(frames, 12)
+    assert a == encode_mp4(frames, 12, threads=1)          # thread count never changes bytes
+    pcm = encode_mp4(frames, 12, codec="pcm")
+    assert len(pcm) > 10 * len(a)
+    probe(a)
+    probe(pcm)
+    dec, fps = decode(a)
+    ref, _ = decode(pcm)                                  # lossless YCbCr -> RGB of the same frames
+    assert fps == 12 and dec.shape == (6, 90, 160, 3)
+    mse = np.mean((dec.astype(float) - ref) ** 2)
+    assert 10 * np.log10(255 ** 2 / mse) > 38
+
+
+def test_probe_rejects_streams_outside_the_intra_subset():
+    import pytest
+    from arbius_amd.utils.mp4 import _Bits, _ep
+    from arbius_amd.utils.video_io import UndecodableVideo, decode, probe
+    sps, pps = sps_pps(64, 64)
+    hdr = _Bits()
+    hdr.ue(0); hdr.ue(5); hdr.ue(0); hdr.u(4, 1)          # first_mb 0, slice_type P
+    hdr.trailing()
+    p_slice = b"\x41" + _ep(hdr.bytes())
+    stream = b"".join(b"\x00\x00\x00\x01" + n for n in (sps, pps, p_slice))
+    with pytest.raises(UndecodableVideo, match="inter"):
+        probe(stream)
+    with pytest.raises(UndecodableVideo):
+        decode(stream)
+    cabac = _Bits()
+    cabac.ue(0); cabac.ue(0); cabac.u(1, 1)               # entropy_coding_mode_flag = 1
+    cabac.trailing()
+    idr = encode_mp4([np.zeros((64, 64, 3), np.uint8)], 1)
+    from arbius_amd.utils.mp4 import read_mp4_nals
+    _, nals, _ = read_mp4_nals(idr)
+    bad = b"".join(b"\x00\x00\x01" + n for n in (nals[0], b"\x68" + _ep(cabac.bytes()), nals[2]))
+    with pytest.raises(UndecodableVideo, match="CABAC"):
+        probe(bad)
+    with pytest.raises(UndecodableVideo):
+        probe(b"not a video at all")
+    good = b"".join(b"\x00\x00\x00\x01" + n for n in nals)   # Annex-B of our own stream
+    probe(good)
+    assert decode(good)[0].shape == (1, 64, 64, 3)
+
+
+def test_undecodable_video_input_is_skipped_not_invalid():
+    """A task whose input_video this node cannot decode is skipped at hydration (metric), never
+    stored invalid (which would make the node contest a task other miners can solve)."""
+    import base64
+    from test_node_e2e import submit
+    e, tok, mid = make_world("robust_video_matting")
+    pool = LocalSolverPool("cpu", tiny=True)
+    m = make_miner(e, mid, pool, model="robust_video_matting")
+    src = "data:video/mp4;base64," + base64.b64encode(b"\x00\x00\x00\x01\x41garbage").decode()
+
+    async def go():
+        await m.boot()
+        await m.poll_events()
+        await m.drain()
+        tid = submit(e, mid, {"input_video": src, "output_type": "alpha-mask"})
+        await m.poll_events()
+        await m.drain()
+        return tid
+    tid = asyncio.run(go())
+    assert tid not in e.solutions
+    assert m.metrics.counters.get("tasks_undecodable_input", 0) == 1
+    assert not m.db.get_invalid_task(tid)
