@@ -1,5 +1,6 @@
 """Native C++ CPU runtime of the node (``src/native.cpp``): keccak256, deterministic
-PNG, H.264 I_PCM payload and the CAVLC intra codec (``src/h264.cpp``), secp256k1 ECDSA.  Built in-tree by ``python -m arbius_amd.native.build``
+PNG, H.264 I_PCM payload and the CAVLC intra codec (``src/h264.cpp``),
+secp256k1 ECDSA.  Built in-tree by ``python -m arbius_amd.native.build``
 (``__graft_entry__.build()``); every function has a byte-identical Python
 reference that tests compare against.  When the extension is not built the
 names are absent and callers use their Python reference (``loaded`` is False)."""

@@ -269,7 +269,8 @@ struct Tables {
     for (int t = 0; t < 4; ++t) coeff_token[t].build(16, kCoeffTokenLen[t], kCoeffTokenBits[t], 68);
     chroma_dc_token.build(8, kChromaDcTokenLen, kChromaDcTokenBits, 20);
     for (int t = 0; t < 15; ++t) total_zeros[t].build(9, kTotalZerosLen[t], kTotalZerosBits[t], 16 - t);
-    for (int t = 0; t < 3; ++t) chroma_dc_total_zeros[t].build(3, kChromaDcTotalZerosLen[t], kChromaDcTotalZerosBits[t], 4 - t);
+    for (int t = 0; t < 3; ++t)
+      chroma_dc_total_zeros[t].build(3, kChromaDcTotalZerosLen[t], kChromaDcTotalZerosBits[t], 4 - t);
     for (int t = 0; t < 7; ++t) run[t].build(11, kRunLen[t], kRunBits[t], t < 6 ? t + 2 : 15);
   }
 };
@@ -336,10 +337,11 @@ void hadamard4(const int* c, int* f) {  // H c H, H = [[1,1,1,1],[1,1,-1,-1],[1,
   }
 }
 
-// AC / non-DC scaling (8.5.12.1), qp >= 24 shifts left
+// AC / non-DC scaling (8.5.12.1), qp >= 24 shifts left (written as a multiply: the spec's << of a
+// negative value is x * 2^n, which C++17 leaves undefined; >> stays the arithmetic shift)
 inline int dequant(int c, int qp, int r) {
   const int ls = level_scale(qp % 6, r);
-  return qp >= 24 ? (c * ls) << (qp / 6 - 4) : (c * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
+  return qp >= 24 ? c * ls * (1 << (qp / 6 - 4)) : (c * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
 }
 
 // ------------------------------------------------------------------------------------ prediction
@@ -655,7 +657,7 @@ void recon_luma16(Frame& f, int mx, int my, const uint8_t* pred, const int* dc, 
     const int bx = kBlkX[blk], by = kBlkY[blk];
     const int fv = fdc[4 * by + bx];
     int d[16] = {0}, r[16];
-    d[0] = qp >= 36 ? (fv * ls) << (qp / 6 - 6) : (fv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+    d[0] = qp >= 36 ? fv * ls * (1 << (qp / 6 - 6)) : (fv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
     for (int k = 0; k < 15; ++k) {
       const int rp = kZigzag[k + 1];
       if (ac[blk][k]) d[rp] = dequant(ac[blk][k], qp, rp);
@@ -677,7 +679,7 @@ void recon_chroma(std::vector<uint8_t>& pl, int Wc, int mx, int my, const uint8_
   for (int blk = 0; blk < 4; ++blk) {
     const int bx = blk & 1, by = blk >> 1;
     int d[16] = {0}, r[16];
-    d[0] = ((fv[blk] * ls) << (qpc / 6)) >> 5;
+    d[0] = (fv[blk] * ls * (1 << (qpc / 6))) >> 5;
     for (int k = 0; k < 15; ++k) {
       const int rp = kZigzag[k + 1];
       if (ac[blk][k]) d[rp] = dequant(ac[blk][k], qpc, rp);
@@ -946,10 +948,14 @@ Sps parse_sps(BitReader& br) {
   if (profile == 100 || profile == 110 || profile == 122 || profile == 244 || profile == 44 || profile == 83 ||
       profile == 86 || profile == 118 || profile == 128)
     throw std::runtime_error("h264: High / scalable profiles are not supported (Constrained Baseline intra only)");
-  s.log2_max_frame_num = int(br.ue()) + 4;
-  s.poc_type = int(br.ue());
+  const uint32_t lmf = br.ue(), poc_type = br.ue();
+  if (lmf > 12 || poc_type > 2) throw std::runtime_error("h264: SPS field out of range");
+  s.log2_max_frame_num = int(lmf) + 4;
+  s.poc_type = int(poc_type);
   if (s.poc_type == 0) {
-    s.log2_max_poc_lsb = int(br.ue()) + 4;
+    const uint32_t lpl = br.ue();
+    if (lpl > 12) throw std::runtime_error("h264: SPS field out of range");
+    s.log2_max_poc_lsb = int(lpl) + 4;
   } else if (s.poc_type == 1) {
     s.delta_pic_order_always_zero = br.u(1);
     br.se();
@@ -959,17 +965,21 @@ Sps parse_sps(BitReader& br) {
   }
   br.ue();    // max_num_ref_frames
   br.u(1);    // gaps
-  s.mbw = int(br.ue()) + 1;
-  s.mbh = int(br.ue()) + 1;
+  const uint32_t mbw = br.ue(), mbh = br.ue();
+  if (mbw >= 512 || mbh >= 512) throw std::runtime_error("h264: picture too large");
+  s.mbw = int(mbw) + 1;
+  s.mbh = int(mbh) + 1;
   if (!br.u(1)) throw std::runtime_error("h264: interlaced (frame_mbs_only_flag = 0) is not supported");
   br.u(1);  // direct_8x8_inference_flag
   if (br.u(1)) {
-    s.crop_l = int(br.ue());
-    s.crop_r = int(br.ue());
-    s.crop_t = int(br.ue());
-    s.crop_b = int(br.ue());
+    const uint32_t l = br.ue(), r = br.ue(), t = br.ue(), b = br.ue();
+    if (2 * (uint64_t(l) + r) >= uint64_t(16) * s.mbw || 2 * (uint64_t(t) + b) >= uint64_t(16) * s.mbh)
+      throw std::runtime_error("h264: bad cropping window");
+    s.crop_l = int(l);
+    s.crop_r = int(r);
+    s.crop_t = int(t);
+    s.crop_b = int(b);
   }
-  if (s.mbw > 512 || s.mbh > 512) throw std::runtime_error("h264: picture too large");
   s.ok = true;
   return s;
 }
@@ -988,6 +998,8 @@ Pps parse_pps(BitReader& br) {
   p.init_qp = 26 + br.se();
   br.se();
   p.chroma_qp_offset = br.se();
+  if (p.init_qp < 0 || p.init_qp > 51 || p.chroma_qp_offset < -12 || p.chroma_qp_offset > 12)
+    throw std::runtime_error("h264: PPS field out of range");
   p.deblocking_control = br.u(1);
   br.u(1);  // constrained_intra_pred_flag (intra-only streams: no effect)
   p.redundant_pic_cnt = br.u(1);
@@ -1028,9 +1040,16 @@ void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, 
     }
   }
   int qp = pps.init_qp + br.se();
+  if (qp < 0 || qp > 51) throw std::runtime_error("h264: slice QP out of range");
+  auto qp_delta = [&](int q) {
+    const int d = br.se();
+    if (d < -26 || d > 25) throw std::runtime_error("h264: mb_qp_delta out of range");
+    return (q + d + 52) % 52;
+  };
   if (pps.deblocking_control) {
     const uint32_t idc = br.ue();
-    if (idc != 1) throw std::runtime_error("h264: in-loop deblocking is not supported (disable_deblocking_filter_idc != 1)");
+    if (idc != 1)
+      throw std::runtime_error("h264: in-loop deblocking is not supported (disable_deblocking_filter_idc != 1)");
   } else {
     throw std::runtime_error("h264: in-loop deblocking is not supported (no deblocking control in the PPS)");
   }
@@ -1063,7 +1082,7 @@ void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, 
       const int cbp_luma = mb_type >= 13 ? 15 : 0;
       const int cmode = int(br.ue());
       if (cmode > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
-      qp = (qp + br.se() + 52) % 52;
+      qp = qp_delta(qp);
       if ((mode == 0 && !nb.top) || (mode == 1 && !nb.left) || (mode == 3 && !(nb.top && nb.left && nb.topleft)))
         throw std::runtime_error("h264: Intra_16x16 mode uses unavailable samples");
       int dc[16], ac[16][15];
@@ -1125,7 +1144,7 @@ void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, 
       const uint32_t cbp_code = br.ue();
       if (cbp_code > 47) throw std::runtime_error("h264: bad coded_block_pattern");
       const int cbp = kIntraCbp[cbp_code], cbp_luma = cbp & 15, cbp_chroma = cbp >> 4;
-      if (cbp) qp = (qp + br.se() + 52) % 52;
+      if (cbp) qp = qp_delta(qp);
       int coef[16][16];
       std::memset(coef, 0, sizeof(coef));
       for (int blk = 0; blk < 16; ++blk) {

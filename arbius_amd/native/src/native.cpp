@@ -225,7 +225,8 @@ static void rgb_to_420(const uint8_t* src, int H, int W, int H16, int W16, uint8
     }
   for (int r = 0; r < H16 / 2; ++r)
     for (int x = 0; x < W16 / 2; ++x) {
-      const uint8_t *a = px(2 * r, 2 * x), *b = px(2 * r, 2 * x + 1), *c = px(2 * r + 1, 2 * x), *d = px(2 * r + 1, 2 * x + 1);
+      const uint8_t *a = px(2 * r, 2 * x), *b = px(2 * r, 2 * x + 1);
+      const uint8_t *c = px(2 * r + 1, 2 * x), *d = px(2 * r + 1, 2 * x + 1);
       const int rr = a[0] + b[0] + c[0] + d[0], g = a[1] + b[1] + c[1] + d[1], bl = a[2] + b[2] + c[2] + d[2];
       cb[(size_t)r * (W16 / 2) + x] = clip1(((-38 * rr - 74 * g + 112 * bl + 512) >> 10) + 128);
       cr[(size_t)r * (W16 / 2) + x] = clip1(((112 * rr - 94 * g - 18 * bl + 512) >> 10) + 128);

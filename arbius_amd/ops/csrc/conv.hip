@@ -829,6 +829,154 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
   }
 }
 
+// X-in-registers variant (cfg 32 + i), for the big-M SD level-0 convs (M = 32768 pixels at
+// lock-step batch 8).  The register-staged 160x128 tile is LDS-bound (profiles/pmc_r2_conv.md:
+// per K tile a CU moves 8 waves x (18 ds_read_b128 + 9 ds_write_b128) through LDS against 2 x 640
+// MFMA cycles per SIMD; 35 % of wave cycles issue-stalled, 32 % MFMA busy).  Here the activation
+// operand never touches LDS: the 16x16x32 MFMA B fragment is "lane = pixel l16, 8 consecutive k at
+// chunk g" = 16 contiguous channel bytes of one NHWC pixel, so every lane loads its fragments
+// straight from global memory into registers (global_load_dwordx4, NS-1 K tiles ahead).  Only the
+// weight tile goes through an NS-deep LDS-DMA ring shared by all WAVES waves, each wave owning
+// TMW x 16 pixels x all BN channels.  Per K tile and CU (BN 160, 8 waves, TMW 2): 160 ds_read_b128
+// + 24 KB of DMA writes against the same 2 x 640 MFMA cycles per SIMD - about half the LDS
+// traffic of the register-staged tile, and no VGPR->LDS store transfers at all.  NS = 2 (tile i+1
+// in flight during tile i): a third X register set spills at TMW = 2.  Per output the
+// MFMA sequence (k-tiles ascending, two k32 halves each) is that of the other non-split kernels,
+// so results are bitwise identical to them.  bf16, no split-K / norm prologue / dual source.
+template <int BN, int WAVES, int TMW, int NS>
+__global__ void __launch_bounds__(64 * WAVES, 1) conv_xreg_kernel(ConvArgs p) {
+  constexpr int EL = 0, BK = 64, NT = 64 * WAVES;
+  constexpr int BM = WAVES * TMW * 16;
+  constexpr int TN = BN / 16;
+  constexpr int WINS = BN / 8;                     // W DMA wave-instructions per stage (8 rows each)
+  constexpr int WCH = (WINS + WAVES - 1) / WAVES;  // per wave; the remainder target a dummy buffer
+  constexpr int LPT = WCH + 2 * TMW;               // vmcnt units per K tile per wave
+  constexpr int STAGE = BN * BK;                   // bf16 elements per W stage
+  constexpr int OROW = BN + 4;                     // epilogue fp32 staging row (epilogue_lds)
+  constexpr int EPI_ROWS = 64;
+  constexpr int S0 = STAGE > EPI_ROWS * OROW * 2 ? STAGE : EPI_ROWS * OROW * 2;
+  static_assert(BN % 16 == 0 && NS >= 2 && NS <= 3, "tile");
+  static_assert((size_t)(S0 + (NS - 1) * STAGE + 512) * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16_t lds0[S0];
+  __shared__ __attribute__((aligned(16))) bf16_t lds1[STAGE];
+  __shared__ __attribute__((aligned(16))) bf16_t lds2[NS > 2 ? STAGE : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t ldsd[512];   // dummy DMA target: zeros, never read
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  int split_idx, n0, m0;
+  tile_coords(p, BN, BM, split_idx, n0, m0);
+  const int nk = p.ktiles;
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  const bf16_t* zp = reinterpret_cast<const bf16_t*>(g_conv_zero_page);
+
+  // W tile: DMA instruction j = wave + WAVES * i fills stage rows 8j .. 8j+7, lane-linear; the
+  // source carries the XOR chunk swizzle (row r, position q holds logical chunk q ^ (r & 7)).
+  const int pos = lane & 7;
+  int woff[WCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) {
+    const int j = wave + WAVES * i;
+    const int row = 8 * j + (lane >> 3);
+    woff[i] = (j < WINS && n0 + row < p.N) ? (n0 + row) * p.K + ((pos ^ (row & 7)) << 3) : -1;
+  }
+  // X: this lane's pixel in each of the wave's TMW fragments
+  int xb[TMW], xho[TMW], xwo[TMW];
+  bool xok[TMW];
+  const int hw = p.Ho * p.Wo;
+#pragma unroll
+  for (int f = 0; f < TMW; ++f) {
+    const int m = m0 + (wave * TMW + f) * 16 + l16;
+    xok[f] = m < p.M;
+    const int mm = xok[f] ? m : 0;
+    xb[f] = mm / hw;
+    const int rem = mm - xb[f] * hw;
+    xho[f] = (rem / p.Wo) * p.stride - p.pad;
+    xwo[f] = (rem % p.Wo) * p.stride - p.padw;
+  }
+  int wk = 0, wc = 0, wr = 0, ws = 0;
+  int xoff[TMW];
+  auto set_tap = [&]() {
+#pragma unroll
+    for (int f = 0; f < TMW; ++f) {
+      int hi = xho[f] + wr, wi = xwo[f] + ws;
+      const bool ok = xok[f] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
+      if (p.upsample) { hi >>= 1; wi >>= 1; }
+      xoff[f] = ok ? ((xb[f] * p.H + hi) * p.W + wi) * p.Cin + g * 8 : -1;
+    }
+  };
+  set_tap();
+
+  uint4 xr[NS][TMW][2];
+  auto issue = [&](auto stage_c) {
+    constexpr int S = decltype(stage_c)::value;
+#pragma unroll
+    for (int f = 0; f < TMW; ++f)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) xr[S][f][kk] = ld16(xoff[f] >= 0 ? p.x + xoff[f] + wc + kk * 32 : zp);
+    bf16_t* sW = ring_stage<S>(lds0, lds1, lds2, lds2);
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int j = wave + WAVES * i;
+      const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
+      bf16_t* dst = j < WINS ? sW + 8 * j * BK : ldsd;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    }
+    wk += BK;
+    wc += BK;
+    if (wc == p.Cin) {
+      wc = 0;
+      if (++ws == p.kw) { ws = 0; ++wr; }
+      set_tap();
+    }
+  };
+
+  f32x4 acc[TN][TMW];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int f = 0; f < TMW; ++f) acc[a][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (0 < nk) issue(IC<0>());
+  if (NS > 2 && 1 < nk) issue(IC<1>());
+  auto step = [&](auto stage_c, int i) __attribute__((always_inline)) {
+    constexpr int S = decltype(stage_c)::value;
+    if (i + NS - 2 < nk) wait_vmcnt<(NS - 2) * LPT>();   // tile i (X regs + W DMA) landed
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();                       // every wave's W DMA of tile i is visible
+    if (i + NS - 1 < nk) issue(IC<(S + NS - 1) % NS>());  // refill the stage / set read at i-1
+    const bf16_t* sW = ring_stage<S>(lds0, lds1, lds2, lds2);
+    // both k32 halves of one 16-channel row block back to back on each accumulator: the
+    // per-accumulator MFMA order is unchanged (k ascending), and the accumulators stay in place
+    // (two separate k-half loops made hipcc ping-pong every accumulator through a second
+    // register set and spill at TMW = 2)
+    if constexpr (NT == 512) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < TN; ++a) {
+      const int row = a * 16 + l16;
+      const uint4 a0 = ld16(&sW[row * BK + ((g ^ (row & 7)) << 3)]);
+      const uint4 a1 = ld16(&sW[row * BK + (((4 + g) ^ (row & 7)) << 3)]);
+#pragma unroll
+      for (int f = 0; f < TMW; ++f) {
+        const f32x4 t = mma16<EL>(a0, xr[S][f][0], acc[a][f]);
+        acc[a][f] = mma16<EL>(a1, xr[S][f][1], t);
+      }
+    }
+    if constexpr (NT == 512) __builtin_amdgcn_s_setprio(0);
+  };
+  for (int i = 0; i < nk; i += NS) {
+    step(IC<0>(), i);
+    if (i + 1 >= nk) break;
+    step(IC<1>(), i + 1);
+    if constexpr (NS > 2) {
+      if (i + 2 >= nk) break;
+      step(IC<2 % NS>(), i + 2);
+    }
+  }
+  epilogue_lds<BN, BM, 1, WAVES, NT, EPI_ROWS * OROW, EL>(p, acc, reinterpret_cast<float*>(lds0), m0, n0);
+}
+
 // Persistent LDS-DMA variant for short-K GEMMs / 1x1 convs (K = 320..1280 on the UNet: the
 // transformer projections, GEGLU proj).  With 5-20 K-tiles per output tile, a one-tile-per-block
 // kernel spends most of its life in prologue latency and epilogue; here a grid of ~one block
@@ -1170,13 +1318,16 @@ static const std::vector<PinnedPlan>& env_plans() {
 }
 
 // cfg ids: 0..9 LDS-DMA 4-wave, 10..19 register-staged 4-wave, 20..23 8-wave LDS-DMA 2-stage,
-// 24..27 persistent short-K, 28..31 8-wave LDS-DMA 3-stage ring (two K-tiles in flight)
+// 24..27 persistent short-K, 28..31 8-wave LDS-DMA 3-stage ring (two K-tiles in flight),
+// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring)
 static inline bool is_persist(int cfg) { return cfg >= 24 && cfg < 28; }
+// 32..35 X-in-registers 8-wave tiles (weights through an LDS-DMA ring, activations straight to VGPRs)
+static inline bool is_xreg(int cfg) { return cfg >= 32 && cfg < 36; }
 
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
-  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 32))) {
-    if (is_persist(want_cfg)) return {want_cfg, 1, ktiles};   // persistent: no split-K
+  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 36))) {
+    if (is_persist(want_cfg) || is_xreg(want_cfg)) return {want_cfg, 1, ktiles};   // no split-K
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
     const int per = (ktiles + split - 1) / split;
@@ -1185,7 +1336,8 @@ static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split
   for (const PinnedPlan& pp : env_plans()) {
     if (pp.M == M && pp.N == N && pp.K == K) {
       const int per = (ktiles + pp.split - 1) / pp.split;
-      return {pp.cfg, is_persist(pp.cfg) ? 1 : (ktiles + per - 1) / per, is_persist(pp.cfg) ? ktiles : per};
+      const bool one = is_persist(pp.cfg) || is_xreg(pp.cfg);
+      return {pp.cfg, one ? 1 : (ktiles + per - 1) / per, one ? ktiles : per};
     }
   }
   for (const PinnedPlan& pp : kPinnedPlans) {
@@ -1331,6 +1483,21 @@ static void launch_persist(const ConvArgs& a, hipStream_t s) {
   conv_persist_kernel<BN, BM, WN, WM, NS><<<grid, 64 * WN * WM, 0, s>>>(p);
 }
 
+// X-in-registers tiles (cfg 32 + i): BN channels x WAVES * TMW * 16 pixels, no split-K.
+template <int BN, int WAVES, int TMW, int NS>
+static void launch_xreg(const ConvArgs& a, hipStream_t s) {
+  constexpr int BM = WAVES * TMW * 16;
+  ConvArgs p = a;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
+  p.nsplit = 1;
+  p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;
+  p.norm = nullptr;
+  p.counters = nullptr;
+  p.kt_per_split = p.ktiles;
+  conv_xreg_kernel<BN, WAVES, TMW, NS><<<p.tiles_total, 64 * WAVES, 0, s>>>(p);
+}
+
 // 8-wave LDS-DMA tiles (cfg 20 + i): two full K-tile stages, per-wave 128x64 / 160x64 outputs.
 struct BigCfg {
   int bn, bm;
@@ -1450,6 +1617,16 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
     else if (pl.cfg < kNumCfgs) pl.cfg += kNumCfgs;
   }
   if (pl.split > 1 && ws == nullptr) return -3;
+  if (is_xreg(pl.cfg)) {   // X-in-registers 8-wave tiles (bf16, no norm prologue / dual source / split)
+    if (EL != 0 || a.norm != nullptr) return -4;
+    switch (pl.cfg - 32) {
+      case 0: launch_xreg<160, 8, 2, 2>(a, stream); break;
+      case 1: launch_xreg<128, 8, 2, 2>(a, stream); break;
+      case 2: launch_xreg<160, 8, 1, 2>(a, stream); break;
+      default: launch_xreg<256, 8, 1, 2>(a, stream); break;
+    }
+    return (int)hipGetLastError();
+  }
   if (pl.cfg >= 28) {   // 8-wave 3-stage LDS-DMA ring (bf16, no norm prologue)
     if (EL != 0 || a.norm != nullptr) return -4;
     switch (pl.cfg - 28) {
@@ -1520,6 +1697,21 @@ ARB_API int arb_conv2d_nhwc_f16(const void* x, const void* w, const void* bias, 
                                 int upsample, int stride, int cfg, int split, hipStream_t stream) {
   return conv_run<1>(x, w, bias, temb, res, out, ws, nullptr, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg,
                      split, 0, stream);
+}
+
+// Tile family for the ACTUAL shape at a plan's split-K (solo tasks run the canonical batch-8 split;
+// at a fixed split every family reduces each output in the same order, so the family is a free,
+// bitwise-neutral choice - scripts/tune_family.py pins the fastest per shape).  Unknown: keep cfg.
+struct FamilyPlan {
+  int M, N, K, split, cfg;
+};
+#include "conv_family.inc"
+
+ARB_API int arb_conv_family(int M, int N, int K, int split, int cfg) {
+  if (std::getenv("ARB_NO_FAMILY") != nullptr) return cfg;
+  for (const FamilyPlan& fp : kFamilyPlans)
+    if (fp.M == M && fp.N == N && fp.K == K && fp.split == split) return fp.cfg;
+  return cfg;
 }
 
 ARB_API int arb_conv2d_plan(int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample, int stride,

@@ -45,6 +45,31 @@ for bad in (bytes(32), (S.N).to_bytes(32, "big")):
         raise SystemExit("accepted an invalid key")
     except ValueError:
         pass
+# H.264 intra codec: encoder / decoder round trip, then the decoder on corrupted (untrusted) input
+import numpy as np
+rng = np.random.default_rng(0)
+y = rng.integers(0, 256, (48, 64), dtype=np.uint8)
+cb = rng.integers(0, 256, (24, 32), dtype=np.uint8)
+cr = rng.integers(0, 256, (24, 32), dtype=np.uint8)
+for qp in (4, 20, 51):
+    nal, ry, rcb, rcr = N.h264_encode_yuv(y, cb, cr, qp, 0)
+    sps, pps = N.h264_parameter_sets(64, 48, qp)
+    (dy, dcb, dcr, _), = N.h264_decode([sps, pps, nal], 2)
+    assert (dy == ry).all() and (dcb == rcb).all() and (dcr == rcr).all()
+    for trial in range(200):
+        bad = bytearray(nal)
+        if trial % 2:
+            bad = bad[:rng.integers(1, len(bad))]
+        else:
+            for _ in range(3):
+                bad[rng.integers(1, len(bad))] ^= 1 << int(rng.integers(0, 8))
+        try:
+            N.h264_decode([sps, pps, bytes(bad)], 1)
+        except ValueError:
+            pass
+frames = rng.integers(0, 256, (3, 40, 72, 3), dtype=np.uint8)
+_, _, nals = N.h264_encode_rgb(frames, 24, 3)
+assert N.h264_decode_rgb([sps_ for sps_ in N.h264_parameter_sets(72, 40, 24)] + list(nals), 2).shape == (3, 40, 72, 3)
 print("sanitized native runtime: all entry points clean")
 '''
 
@@ -56,6 +81,7 @@ def main():
     flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
     cmd = ["g++", *flags, "-shared", "-fPIC", "-std=c++17", "-pthread", "-I", pybind11.get_include(),
            "-I", sysconfig.get_paths()["include"], os.path.join(SRC, "native.cpp"), os.path.join(SRC, "secp256k1.cpp"),
+           os.path.join(SRC, "h264.cpp"),
            "-lz", "-o", so]
     subprocess.run(cmd, check=True)
     asan = subprocess.check_output(["g++", "-print-file-name=libasan.so"], text=True).strip()

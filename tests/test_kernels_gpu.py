@@ -124,7 +124,7 @@ def test_gemm(cuda, M, K, N):
     assert _rel(y, x.float() @ w.float().t() + b.float() + r.float()) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(20)) + [20, 21, 22, 23, 24, 25, 26, 27])
+@pytest.mark.parametrize("cfg", list(range(20)) + [20, 21, 22, 23, 24, 25, 26, 27, 32, 33, 34, 35])
 @pytest.mark.parametrize("split", [1, 3])
 def test_conv2d_all_tile_configs(cuda, cfg, split):
     """Every tile config of both kernel variants (LDS-DMA ring / register staged) and split-K."""
@@ -155,6 +155,26 @@ def test_conv_tile_families_bitwise_equal(cuda, B, H, W, C, Co, k):
         assert torch.equal(y, ref_y), cfg
 
 
+@pytest.mark.parametrize("split", [2, 3])
+@pytest.mark.parametrize("B,H,W,C,Co,k", [(2, 32, 32, 640, 640, 3), (2, 8, 8, 1280, 1280, 3),
+                                          (2, 16, 16, 640, 1280, 1)])
+def test_conv_tile_families_bitwise_equal_at_split(cuda, split, B, H, W, C, Co, k):
+    """At a fixed split-K every family walks the same K range per slab in the same MFMA order and
+    the slabs are summed in slab order, so families stay bitwise interchangeable - what lets a solo
+    task run the canonical (batch-8) split on a tile family tuned for its own shape
+    (ops/csrc/conv_family.inc, scripts/tune_family.py)."""
+    torch.manual_seed(13)
+    x = torch.randn(B, H, W, C, device=cuda).bfloat16()
+    w = (torch.randn(Co, k, k, C, device=cuda) / math.sqrt(k * k * C)).bfloat16()
+    b = torch.randn(Co, device=cuda).bfloat16()
+    r = torch.randn(B, H, W, Co, device=cuda).bfloat16()
+    pad = k // 2
+    ref_y = _lib.conv2d_nhwc(x, w, b, pad, False, r, None, 1, 15, split)
+    for cfg in (0, 3, 4, 5, 10, 13, 14, 16, 20, 21, 22, 28, 29, 31):
+        y = _lib.conv2d_nhwc(x, w, b, pad, False, r, None, 1, cfg, split)
+        assert torch.equal(y, ref_y), cfg
+
+
 @pytest.mark.parametrize("cfg", [24, 25, 26, 27])
 @pytest.mark.parametrize("res", [False, True])
 def test_gemm_persistent_many_tiles(cuda, cfg, res):
@@ -174,7 +194,8 @@ def test_gemm_persistent_many_tiles(cuda, cfg, res):
 
 @pytest.mark.parametrize("M,K,N,cfg,split", [
     (8200, 320, 2560, -1, -1), (8200, 320, 2560, 15, 1), (8200, 320, 2560, 25, 1), (8200, 320, 2560, 21, 1),
-    (8200, 320, 2560, 0, 1), (512, 1280, 10240, 13, 3), (512, 1280, 10240, 22, 2), (300, 640, 5120, 3, 1)])
+    (8200, 320, 2560, 0, 1), (512, 1280, 10240, 13, 3), (512, 1280, 10240, 22, 2), (300, 640, 5120, 3, 1),
+    (8200, 320, 2560, 32, 1), (300, 640, 5120, 35, 1)])
 def test_gemm_geglu_bitwise_equals_unfused(cuda, M, K, N, cfg, split):
     """GEGLU in the GEMM epilogue (interleaved value/gate rows) == geglu(gemm(x, w, b)) bitwise,
     for register / LDS-DMA / 8-wave tiles, split-K (reduce kernel) and the persistent remap."""
@@ -188,6 +209,35 @@ def test_gemm_geglu_bitwise_equals_unfused(cuda, M, K, N, cfg, split):
     assert torch.equal(got, want)
     r = ref.geglu(x.float() @ w.float().t() + b.float())
     assert _rel(got, r) < 2e-2
+
+
+@pytest.mark.parametrize("cfg", [32, 33, 34, 35])
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,up,stride,res,temb", [
+    (8, 64, 64, 320, 320, 3, False, 1, True, False), (8, 64, 64, 640, 320, 3, False, 1, False, True),
+    (2, 37, 29, 320, 640, 1, False, 1, True, True), (2, 37, 29, 128, 1280, 3, False, 1, False, False),
+    (2, 16, 16, 320, 320, 3, True, 1, False, False), (3, 33, 35, 192, 200, 3, False, 2, True, False)])
+def test_conv2d_xreg_tiles_bitwise_equal_register_staged(cuda, cfg, B, H, W, Cin, Cout, k, up, stride, res, temb):
+    """X-in-registers tiles (activation fragments straight to VGPRs, weights through the LDS-DMA
+    ring): partial M / N tiles, upsample, stride 2, bias + temb + residual epilogue.  Same per-output
+    MFMA order as the register-staged kernel, so bitwise equal to it; and close to fp32."""
+    torch.manual_seed(21)
+    x = torch.randn(B, H, W, Cin, device=cuda).bfloat16()
+    w = (torch.randn(Cout, k, k, Cin, device=cuda) / math.sqrt(k * k * Cin)).bfloat16()
+    b = torch.randn(Cout, device=cuda).bfloat16()
+    pad = k // 2
+    Ho = ((2 * H if up else H) + 2 * pad - k) // stride + 1
+    Wo = ((2 * W if up else W) + 2 * pad - k) // stride + 1
+    r = torch.randn(B, Ho, Wo, Cout, device=cuda).bfloat16() if res else None
+    t = torch.randn(B, Cout, device=cuda).bfloat16() if temb else None
+    y = _lib.conv2d_nhwc(x, w, b, pad, up, r, t, stride, cfg, 1)
+    ref_y = ref.conv2d_nhwc(x.float(), w.float(), b.float(), stride, pad, up)
+    if res:
+        ref_y = ref_y + r.float()
+    if temb:
+        ref_y = ref_y + t.float()[:, None, None, :]
+    assert _rel(y, ref_y) < 1e-2
+    assert torch.equal(y, _lib.conv2d_nhwc(x, w, b, pad, up, r, t, stride, 15, 1))
+    assert torch.equal(y, _lib.conv2d_nhwc(x, w, b, pad, up, r, t, stride, cfg, 1))   # run to run
 
 
 @pytest.mark.parametrize("cfg", [20, 21, 22, 23])
