@@ -839,10 +839,11 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
 // weight tile goes through an NS-deep LDS-DMA ring shared by all WAVES waves, each wave owning
 // TMW x 16 pixels x all BN channels.  Per K tile and CU (BN 160, 8 waves, TMW 2): 160 ds_read_b128
 // + 24 KB of DMA writes against the same 2 x 640 MFMA cycles per SIMD - about half the LDS
-// traffic of the register-staged tile, and no VGPR->LDS store transfers at all.  NS = 2 (tile i+1
+// traffic of the register-staged tile, and no VGPR->LDS store transfers at all.  Split-K writes the
+// K range's fp32 slab (summed in slab order by splitk_reduce_kernel).  NS = 2 (tile i+1
 // in flight during tile i): a third X register set spills at TMW = 2.  Per output the
 // MFMA sequence (k-tiles ascending, two k32 halves each) is that of the other non-split kernels,
-// so results are bitwise identical to them.  bf16, no split-K / norm prologue / dual source.
+// so results are bitwise identical to them at every split.  bf16, no norm prologue / dual source.
 template <int BN, int WAVES, int TMW, int NS>
 __global__ void __launch_bounds__(64 * WAVES, 1) conv_xreg_kernel(ConvArgs p) {
   constexpr int EL = 0, BK = 64, NT = 64 * WAVES;
@@ -866,7 +867,9 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_xreg_kernel(ConvArgs p) {
   const int g = lane >> 4, l16 = lane & 15;
   int split_idx, n0, m0;
   tile_coords(p, BN, BM, split_idx, n0, m0);
-  const int nk = p.ktiles;
+  const bool split = p.nsplit > 1;   // split-K: fp32 slab of this K range, summed by splitk_reduce
+  const int kt0 = split ? split_idx * p.kt_per_split : 0;
+  const int nk = (split ? min(p.ktiles, kt0 + p.kt_per_split) : p.ktiles) - kt0;
   typedef __attribute__((address_space(1))) const void* gptr_t;
   typedef __attribute__((address_space(3))) void* lptr_t;
   const bf16_t* zp = reinterpret_cast<const bf16_t*>(g_conv_zero_page);
@@ -895,7 +898,7 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_xreg_kernel(ConvArgs p) {
     xho[f] = (rem / p.Wo) * p.stride - p.pad;
     xwo[f] = (rem % p.Wo) * p.stride - p.padw;
   }
-  int wk = 0, wc = 0, wr = 0, ws = 0;
+  int wk = kt0 * BK, wc = wk % p.Cin, wr = (wk / p.Cin) / p.kw, ws = (wk / p.Cin) % p.kw;
   int xoff[TMW];
   auto set_tap = [&]() {
 #pragma unroll
@@ -973,6 +976,21 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_xreg_kernel(ConvArgs p) {
       if (i + 2 >= nk) break;
       step(IC<2 % NS>(), i + 2);
     }
+  }
+  if (split) {
+#pragma unroll
+    for (int f = 0; f < TMW; ++f) {
+      const int m = m0 + (wave * TMW + f) * 16 + l16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int n = n0 + a * 16 + 4 * g;
+        if (n < p.N)
+          *reinterpret_cast<float4*>(p.ws + ((size_t)split_idx * p.M + m) * p.N + n) =
+              make_float4(acc[a][f][0], acc[a][f][1], acc[a][f][2], acc[a][f][3]);
+      }
+    }
+    return;
   }
   epilogue_lds<BN, BM, 1, WAVES, NT, EPI_ROWS * OROW, EL>(p, acc, reinterpret_cast<float*>(lds0), m0, n0);
 }
@@ -1327,7 +1345,7 @@ static inline bool is_xreg(int cfg) { return cfg >= 32 && cfg < 36; }
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
   if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 36))) {
-    if (is_persist(want_cfg) || is_xreg(want_cfg)) return {want_cfg, 1, ktiles};   // no split-K
+    if (is_persist(want_cfg)) return {want_cfg, 1, ktiles};   // persistent: no split-K
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
     const int per = (ktiles + split - 1) / split;
@@ -1336,8 +1354,7 @@ static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split
   for (const PinnedPlan& pp : env_plans()) {
     if (pp.M == M && pp.N == N && pp.K == K) {
       const int per = (ktiles + pp.split - 1) / pp.split;
-      const bool one = is_persist(pp.cfg) || is_xreg(pp.cfg);
-      return {pp.cfg, one ? 1 : (ktiles + per - 1) / per, one ? ktiles : per};
+      return {pp.cfg, is_persist(pp.cfg) ? 1 : (ktiles + per - 1) / per, is_persist(pp.cfg) ? ktiles : per};
     }
   }
   for (const PinnedPlan& pp : kPinnedPlans) {
@@ -1485,17 +1502,22 @@ static void launch_persist(const ConvArgs& a, hipStream_t s) {
 
 // X-in-registers tiles (cfg 32 + i): BN channels x WAVES * TMW * 16 pixels, no split-K.
 template <int BN, int WAVES, int TMW, int NS>
-static void launch_xreg(const ConvArgs& a, hipStream_t s) {
+static void launch_xreg(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   constexpr int BM = WAVES * TMW * 16;
   ConvArgs p = a;
   p.tiles_n = (p.N + BN - 1) / BN;
   p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
-  p.nsplit = 1;
+  p.nsplit = pl.split > 1 ? pl.split : 1;
   p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;
   p.norm = nullptr;
   p.counters = nullptr;
-  p.kt_per_split = p.ktiles;
-  conv_xreg_kernel<BN, WAVES, TMW, NS><<<p.tiles_total, 64 * WAVES, 0, s>>>(p);
+  p.kt_per_split = p.nsplit > 1 ? pl.kt_per_split : p.ktiles;
+  conv_xreg_kernel<BN, WAVES, TMW, NS><<<p.tiles_total * p.nsplit, 64 * WAVES, 0, s>>>(p);
+  if (p.nsplit > 1) {
+    long blocks = ((long)p.M * (p.N / 8) + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<0><<<(int)blocks, 256, 0, s>>>(p, p.nsplit);
+  }
 }
 
 // 8-wave LDS-DMA tiles (cfg 20 + i): two full K-tile stages, per-wave 128x64 / 160x64 outputs.
@@ -1617,13 +1639,13 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
     else if (pl.cfg < kNumCfgs) pl.cfg += kNumCfgs;
   }
   if (pl.split > 1 && ws == nullptr) return -3;
-  if (is_xreg(pl.cfg)) {   // X-in-registers 8-wave tiles (bf16, no norm prologue / dual source / split)
+  if (is_xreg(pl.cfg)) {   // X-in-registers 8-wave tiles (bf16, no norm prologue / dual source)
     if (EL != 0 || a.norm != nullptr) return -4;
     switch (pl.cfg - 32) {
-      case 0: launch_xreg<160, 8, 2, 2>(a, stream); break;
-      case 1: launch_xreg<128, 8, 2, 2>(a, stream); break;
-      case 2: launch_xreg<160, 8, 1, 2>(a, stream); break;
-      default: launch_xreg<256, 8, 1, 2>(a, stream); break;
+      case 0: launch_xreg<160, 8, 2, 2>(a, pl, stream); break;
+      case 1: launch_xreg<128, 8, 2, 2>(a, pl, stream); break;
+      case 2: launch_xreg<160, 8, 1, 2>(a, pl, stream); break;
+      default: launch_xreg<256, 8, 1, 2>(a, pl, stream); break;
     }
     return (int)hipGetLastError();
   }

@@ -170,7 +170,7 @@ def test_conv_tile_families_bitwise_equal_at_split(cuda, split, B, H, W, C, Co, 
     r = torch.randn(B, H, W, Co, device=cuda).bfloat16()
     pad = k // 2
     ref_y = _lib.conv2d_nhwc(x, w, b, pad, False, r, None, 1, 15, split)
-    for cfg in (0, 3, 4, 5, 10, 13, 14, 16, 20, 21, 22, 28, 29, 31):
+    for cfg in (0, 3, 4, 5, 10, 13, 14, 16, 20, 21, 22, 28, 29, 31, 32, 33, 34, 35):
         y = _lib.conv2d_nhwc(x, w, b, pad, False, r, None, 1, cfg, split)
         assert torch.equal(y, ref_y), cfg
 
