@@ -227,3 +227,161 @@ def test_undecodable_video_input_is_skipped_not_invalid():
     assert tid not in e.solutions
     assert m.metrics.counters.get("tasks_undecodable_input", 0) == 1
     assert not m.db.get_invalid_task(tid)
+
+
+# ---- Intra_4x4 decode path, independent of the native encoder: an I_PCM macroblock with random
+# samples followed by I_NxN macroblocks with zero residual (cbp 0), so every decoded sample is a
+# chain of 4x4 predictions (all 9 modes, top-right substitution, predicted-mode signalling)
+def _p4(top, left, tl, mode):
+    """Intra_4x4 prediction (H.264 8.3.1.2) from p[-1,-1] = tl, p[0..7,-1] = top, p[-1,0..3] = left."""
+    def P(x, y):
+        if y == -1:
+            return tl if x == -1 else top[x]
+        return left[y]
+    out = np.zeros((4, 4), np.int64)
+    for y in range(4):
+        for x in range(4):
+            if mode == 0:
+                v = P(x, -1)
+            elif mode == 1:
+                v = P(-1, y)
+            elif mode == 2:
+                v = None
+            elif mode == 3:
+                v = (P(6, -1) + 3 * P(7, -1) + 2) >> 2 if x == y == 3 else \
+                    (P(x + y, -1) + 2 * P(x + y + 1, -1) + P(x + y + 2, -1) + 2) >> 2
+            elif mode == 4:
+                if x > y:
+                    v = (P(x - y - 2, -1) + 2 * P(x - y - 1, -1) + P(x - y, -1) + 2) >> 2
+                elif x < y:
+                    v = (P(-1, y - x - 2) + 2 * P(-1, y - x - 1) + P(-1, y - x) + 2) >> 2
+                else:
+                    v = (P(0, -1) + 2 * P(-1, -1) + P(-1, 0) + 2) >> 2
+            elif mode == 5:
+                z = 2 * x - y
+                if z in (0, 2, 4, 6):
+                    v = (P(x - (y >> 1) - 1, -1) + P(x - (y >> 1), -1) + 1) >> 1
+                elif z in (1, 3, 5):
+                    v = (P(x - (y >> 1) - 2, -1) + 2 * P(x - (y >> 1) - 1, -1) + P(x - (y >> 1), -1) + 2) >> 2
+                elif z == -1:
+                    v = (P(-1, 0) + 2 * P(-1, -1) + P(0, -1) + 2) >> 2
+                else:
+                    v = (P(-1, y - 1) + 2 * P(-1, y - 2) + P(-1, y - 3) + 2) >> 2
+            elif mode == 6:
+                z = 2 * y - x
+                if z in (0, 2, 4, 6):
+                    v = (P(-1, y - (x >> 1) - 1) + P(-1, y - (x >> 1)) + 1) >> 1
+                elif z in (1, 3, 5):
+                    v = (P(-1, y - (x >> 1) - 2) + 2 * P(-1, y - (x >> 1) - 1) + P(-1, y - (x >> 1)) + 2) >> 2
+                elif z == -1:
+                    v = (P(-1, 0) + 2 * P(-1, -1) + P(0, -1) + 2) >> 2
+                else:
+                    v = (P(x - 1, -1) + 2 * P(x - 2, -1) + P(x - 3, -1) + 2) >> 2
+            elif mode == 7:
+                v = (P(x + (y >> 1), -1) + P(x + (y >> 1) + 1, -1) + 1) >> 1 if y % 2 == 0 else \
+                    (P(x + (y >> 1), -1) + 2 * P(x + (y >> 1) + 1, -1) + P(x + (y >> 1) + 2, -1) + 2) >> 2
+            else:
+                z = x + 2 * y
+                if z in (0, 2, 4):
+                    v = (P(-1, y + (x >> 1)) + P(-1, y + (x >> 1) + 1) + 1) >> 1
+                elif z in (1, 3):
+                    v = (P(-1, y + (x >> 1)) + 2 * P(-1, y + (x >> 1) + 1) + P(-1, y + (x >> 1) + 2) + 2) >> 2
+                elif z == 5:
+                    v = (P(-1, 2) + 3 * P(-1, 3) + 2) >> 2
+                else:
+                    v = P(-1, 3)
+            out[y, x] = v if v is not None else 0
+    return out
+
+
+def test_intra4x4_decode_matches_independent_prediction_chain():
+    from arbius_amd.utils.mp4 import _Bits, _ep, decode_h264
+    rng = np.random.default_rng(9)
+    W = H = 32
+    Y = np.zeros((H, W), np.int64)
+    Cb = np.zeros((H // 2, W // 2), np.int64)
+    Cr = np.zeros((H // 2, W // 2), np.int64)
+    pcm_y = rng.integers(1, 255, (16, 16))
+    pcm_c = rng.integers(1, 255, (2, 8, 8))
+    blk_xy = [(0, 0), (1, 0), (0, 1), (1, 1), (2, 0), (3, 0), (2, 1), (3, 1),
+              (0, 2), (1, 2), (0, 3), (1, 3), (2, 2), (3, 2), (2, 3), (3, 3)]
+    modes = {}                      # (bx, by) in 4x4-block units -> mode (I_NxN macroblocks only)
+    bits = _Bits()
+    bits.ue(0); bits.ue(7); bits.ue(0); bits.u(4, 0); bits.ue(0); bits.u(1, 0); bits.u(1, 0)
+    bits.se(0); bits.ue(1)          # slice header: qp delta 0, deblocking off
+    used = set()
+    for mb in range(4):
+        mx, my = mb % 2, mb // 2
+        if mb == 0:
+            bits.ue(25)
+            bits.align_zero()
+            for v in pcm_y.ravel():
+                bits.u(8, int(v))
+            for c in range(2):
+                for v in pcm_c[c].ravel():
+                    bits.u(8, int(v))
+            Y[:16, :16] = pcm_y
+            Cb[:8, :8], Cr[:8, :8] = pcm_c
+            continue
+        bits.ue(0)                  # I_NxN
+        for k, (lx, ly) in enumerate(blk_xy):
+            bx, by = 4 * mx + lx, 4 * my + ly
+            x0, y0 = 4 * bx, 4 * by
+            has_l = bx > 0
+            has_t = by > 0
+            has_tl = has_l and has_t
+            if ly == 0:
+                has_tr = by > 0 and bx + 1 < 8 and (lx < 3 or mx + 1 < 2)
+            elif lx == 3:
+                has_tr = False
+            else:
+                has_tr = blk_xy.index((lx + 1, ly - 1)) < k
+            ok = [m for m in range(9) if not ((m in (0, 3, 7) and not has_t) or (m in (1, 8) and not has_l)
+                                               or (m in (4, 5, 6) and not has_tl))]
+            m = ok[(3 * mb + k) % len(ok)]
+            used.add(m)
+            if has_l and has_t:
+                ma, mbm = modes.get((bx - 1, by), 2), modes.get((bx, by - 1), 2)
+                pred = min(ma, mbm)
+            else:
+                pred = 2
+            if m == pred:
+                bits.u(1, 1)
+            else:
+                bits.u(1, 0)
+                bits.u(3, m if m < pred else m - 1)
+            modes[(bx, by)] = m
+            top = [int(Y[y0 - 1, x0 + i]) if has_t else 0 for i in range(4)]
+            top += [int(Y[y0 - 1, x0 + i]) if has_tr else top[3] for i in range(4, 8)]
+            left = [int(Y[y0 + i, x0 - 1]) if has_l else 0 for i in range(4)]
+            tl = int(Y[y0 - 1, x0 - 1]) if has_tl else 0
+            if m == 2:
+                s = (sum(top[:4]) if has_t else 0) + (sum(left) if has_l else 0)
+                n = 4 * (has_t + has_l)
+                dc = (s + n // 2) // n if n else 128
+                Y[y0:y0 + 4, x0:x0 + 4] = dc
+            else:
+                Y[y0:y0 + 4, x0:x0 + 4] = _p4(top, left, tl, m)
+        bits.ue(0)                  # intra_chroma_pred_mode DC
+        bits.ue(3)                  # coded_block_pattern me(v): codeNum 3 -> cbp 0 (no mb_qp_delta)
+        for C in (Cb, Cr):          # chroma DC prediction (8.3.4, 4:2:0), no residual
+            cx, cy = 8 * mx, 8 * my
+            for by4 in range(2):
+                for bx4 in range(2):
+                    t = C[cy - 1, cx + 4 * bx4:cx + 4 * bx4 + 4].sum() if my else None
+                    l_ = C[cy + 4 * by4:cy + 4 * by4 + 4, cx - 1].sum() if mx else None
+                    if (bx4, by4) in ((0, 0), (1, 1)):
+                        v = (t + l_ + 4) >> 3 if t is not None and l_ is not None else \
+                            (l_ + 2) >> 2 if l_ is not None else (t + 2) >> 2 if t is not None else 128
+                    elif (bx4, by4) == (1, 0):
+                        v = (t + 2) >> 2 if t is not None else (l_ + 2) >> 2 if l_ is not None else 128
+                    else:
+                        v = (l_ + 2) >> 2 if l_ is not None else (t + 2) >> 2 if t is not None else 128
+                    C[cy + 4 * by4:cy + 4 * by4 + 4, cx + 4 * bx4:cx + 4 * bx4 + 4] = v
+    bits.trailing()
+    assert used == set(range(9))
+    sps, pps = sps_pps(W, H)
+    nal = bytes([0x65]) + _ep(bits.bytes())
+    [(y, cb, cr)], crop = decode_h264([sps, pps, nal])
+    assert crop == (W, H)
+    assert (y == Y).all() and (cb == Cb).all() and (cr == Cr).all()
