@@ -445,7 +445,7 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
         if norm.dtype != torch.float32 or tuple(norm.shape) != (B, Cin, 2) or not norm.is_contiguous():
             raise ValueError("conv2d norm table must be contiguous fp32 [B, Cin, 2]")
     kcode = 31 if temporal else kh
-    if plan_b and plan_b != B and cfg < 0:   # batch-invariant: the canonical batch's plan
+    if plan_b and cfg < 0:   # batch-invariant: the canonical batch's plan
         cfg, split = conv_plan(plan_b, H, W, Cin, Cout, kcode, padding, upsample, stride)
         # ... at its split-K, on the tile family tuned for the actual shape (bitwise-neutral)
         cfg = _fn("arb_conv_family")(B * Ho * Wo, Cout, kh * kw * Cin, split, cfg)
@@ -475,7 +475,7 @@ def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None):
     M = x2.shape[0]
     if K % 64 or N % 8 or w.shape[1] != K:
         raise ValueError(f"gemm: unsupported K={K} N={N}")
-    if plan_batch and plan_batch[1] and plan_batch[1] != plan_batch[0] and cfg < 0:
+    if plan_batch and plan_batch[1] and cfg < 0:
         cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
         cfg = _fn("arb_conv_family")(M, N, K, split, cfg)
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
@@ -498,7 +498,7 @@ def gemm_geglu(x, w_il, b_il=None, cfg=-1, split=-1, plan_batch=None):
     M = x2.shape[0]
     if K % 64 or N % 16 or w_il.shape[1] != K:
         raise ValueError(f"gemm_geglu: unsupported K={K} N={N}")
-    if plan_batch and plan_batch[1] and plan_batch[1] != plan_batch[0] and cfg < 0:
+    if plan_batch and plan_batch[1] and cfg < 0:
         cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
         cfg = _fn("arb_conv_family")(M, N, K, split, cfg)
     y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)

@@ -11,7 +11,11 @@ chip; this tuner times every family at the canonical split on the solo shapes, c
 candidate bitwise against the canonical plan's own output, and writes the winners as
 ``csrc/conv_family.inc`` ({M, N, K, split, cfg}).
 
-    python scripts/tune_family.py OUT_FILE [--batch 2]
+    python scripts/tune_family.py OUT_FILE [--batch 2] [--conc 1] [--merge conv_family.inc]
+
+With ``--batch 8 --conc 2`` the same search runs on the lock-step group shapes (canonical plan =
+their own plan) with two concurrent copies, i.e. the family that keeps the most throughput while
+the other task stream shares the GPU - again without moving a bit.
 """
 import argparse
 import math
@@ -33,10 +37,20 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--canon", type=int, default=8)
+    ap.add_argument("--conc", type=int, default=1, help="time CONC concurrent copies (2 = the two task streams)")
+    ap.add_argument("--merge", default=None, help="existing conv_family.inc whose entries are kept")
     a = ap.parse_args()
+    import scripts.autotune_conv as at
+    at.CONC = a.conc
     dev = torch.device("cuda")
     convs, gemms = collect_shapes(("sd15",), 512, a.batch)
-    rows = {}
+    rows, kept = {}, {}
+    if a.merge and os.path.exists(a.merge):
+        for line in open(a.merge):
+            line = line.strip()
+            if line.startswith("{") and line.endswith("},") and not line.startswith("{0,"):
+                M, N, K, sp, c = (int(v) for v in line[1:-2].split(","))
+                kept[(M, N, K, sp)] = c
     torch.manual_seed(0)
     for (B, H, W, C, Co, kh, kw, pad, up, stride) in convs:
         if B != a.batch or kh != kw:
@@ -96,6 +110,10 @@ def main():
         rows[key] = best[1]
         print(f"gemm M={M} N={N} K={K} split={sp}: canonical cfg {cfg0} {base:.1f} us -> cfg {best[1]} "
               f"{best[0]:.1f} us", flush=True)
+    for k, c in kept.items():
+        if k in rows and rows[k] != c:
+            print(f"# key {k} re-tuned: {c} -> {rows[k]}", flush=True)
+        rows.setdefault(k, c)
     with open(a.out, "w") as f:
         f.write("// Generated by scripts/tune_family.py on MI355X: tile family for the ACTUAL (solo) shape at the\n"
                 "// canonical split-K {M, N, K, split, cfg}.  Bitwise equal to the canonical plan's kernel.\n"
