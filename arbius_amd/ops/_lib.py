@@ -38,7 +38,7 @@ _SIGS = {
     "arb_group_norm_table": (c_int, [c_void_p] * 4 + [c_float] + [c_void_p] * 2 + [c_int] * 4 + [c_float, c_void_p]),
     "arb_conv2d_workspace": (c_size_t, [c_int] * 11),
     "arb_conv2d_plan": (c_int, [c_int] * 9 + [c_void_p]),
-    "arb_conv_family": (c_int, [c_int] * 5),
+    "arb_conv_family": (c_int, [c_int] * 6),
     "arb_gemm_bias_res": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_void_p]),
     "arb_gemm_geglu": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p]),
     "arb_temporal_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_void_p]),
@@ -448,7 +448,7 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     if plan_b and cfg < 0:   # batch-invariant: the canonical batch's plan
         cfg, split = conv_plan(plan_b, H, W, Cin, Cout, kcode, padding, upsample, stride)
         # ... at its split-K, on the tile family tuned for the actual shape (bitwise-neutral)
-        cfg = _fn("arb_conv_family")(B * Ho * Wo, Cout, kh * kw * Cin, split, cfg)
+        cfg = _fn("arb_conv_family")(B * Ho * Wo, Cout, kh * kw * Cin, split, plan_b // B if plan_b % B == 0 else 0, cfg)
     args = (B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
@@ -477,7 +477,7 @@ def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None):
         raise ValueError(f"gemm: unsupported K={K} N={N}")
     if plan_batch and plan_batch[1] and cfg < 0:
         cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
-        cfg = _fn("arb_conv_family")(M, N, K, split, cfg)
+        cfg = _fn("arb_conv_family")(M, N, K, split, plan_batch[1] // plan_batch[0], cfg)
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
@@ -500,7 +500,7 @@ def gemm_geglu(x, w_il, b_il=None, cfg=-1, split=-1, plan_batch=None):
         raise ValueError(f"gemm_geglu: unsupported K={K} N={N}")
     if plan_batch and plan_batch[1] and cfg < 0:
         cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
-        cfg = _fn("arb_conv_family")(M, N, K, split, cfg)
+        cfg = _fn("arb_conv_family")(M, N, K, split, plan_batch[1] // plan_batch[0], cfg)
     y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None

@@ -1724,15 +1724,17 @@ ARB_API int arb_conv2d_nhwc_f16(const void* x, const void* w, const void* bias, 
 // Tile family for the ACTUAL shape at a plan's split-K (solo tasks run the canonical batch-8 split;
 // at a fixed split every family reduces each output in the same order, so the family is a free,
 // bitwise-neutral choice - scripts/tune_family.py pins the fastest per shape).  Unknown: keep cfg.
+// ratio = canonical batch / actual batch (4: a solo task under the batch-8 plans; 1: a lock-step
+// group of 4 on its own plans, tuned with the second task stream running concurrently).
 struct FamilyPlan {
-  int M, N, K, split, cfg;
+  int M, N, K, split, ratio, cfg;
 };
 #include "conv_family.inc"
 
-ARB_API int arb_conv_family(int M, int N, int K, int split, int cfg) {
+ARB_API int arb_conv_family(int M, int N, int K, int split, int ratio, int cfg) {
   if (std::getenv("ARB_NO_FAMILY") != nullptr) return cfg;
   for (const FamilyPlan& fp : kFamilyPlans)
-    if (fp.M == M && fp.N == N && fp.K == K && fp.split == split) return fp.cfg;
+    if (fp.M == M && fp.N == N && fp.K == K && fp.split == split && fp.ratio == ratio) return fp.cfg;
   return cfg;
 }
 

@@ -49,8 +49,8 @@ def main():
         for line in open(a.merge):
             line = line.strip()
             if line.startswith("{") and line.endswith("},") and not line.startswith("{0,"):
-                M, N, K, sp, c = (int(v) for v in line[1:-2].split(","))
-                kept[(M, N, K, sp)] = c
+                M, N, K, sp, r, c = (int(v) for v in line[1:-2].split(","))
+                kept[(M, N, K, sp, r)] = c
     torch.manual_seed(0)
     for (B, H, W, C, Co, kh, kw, pad, up, stride) in convs:
         if B != a.batch or kh != kw:
@@ -62,7 +62,7 @@ def main():
         Hl, Wl = (2 * H, 2 * W) if up else (H, W)
         M = B * ((Hl + 2 * pad - kh) // stride + 1) * ((Wl + 2 * pad - kw) // stride + 1)
         K = kh * kw * C
-        key = (M, Co, K, sp)
+        key = (M, Co, K, sp, a.canon // a.batch)
         if key in rows:
             continue
         ref = _lib.conv2d_nhwc(x, w, b, pad, up, None, None, stride, cfg0, sp)
@@ -89,7 +89,7 @@ def main():
         b = torch.randn(N, device=dev).bfloat16()
         r = torch.randn(M, N, device=dev).bfloat16() if res else None
         cfg0, sp = _lib.conv_plan(1, 1, M * a.canon // a.batch, K, N, 1, 0, 0, 1)
-        key = (M, N, K, sp)
+        key = (M, N, K, sp, a.canon // a.batch)
         if key in rows:
             continue
         ref = _lib.gemm(x, w, b, r, cfg0, sp)
@@ -116,10 +116,11 @@ def main():
         rows.setdefault(k, c)
     with open(a.out, "w") as f:
         f.write("// Generated by scripts/tune_family.py on MI355X: tile family for the ACTUAL (solo) shape at the\n"
-                "// canonical split-K {M, N, K, split, cfg}.  Bitwise equal to the canonical plan's kernel.\n"
+                "// canonical split-K {M, N, K, split, canonical/actual batch, cfg}.  Bitwise equal to the canonical\n"
+                "// plan's kernel.\n"
                 "static const FamilyPlan kFamilyPlans[] = {\n")
-        for (M, N, K, sp), cfg in sorted(rows.items()):
-            f.write(f"    {{{M}, {N}, {K}, {sp}, {cfg}}},\n")
+        for (M, N, K, sp, r), cfg in sorted(rows.items()):
+            f.write(f"    {{{M}, {N}, {K}, {sp}, {r}, {cfg}}},\n")
         f.write("};\n")
 
 
