@@ -39,11 +39,13 @@ def main():
     ap.add_argument("--canon", type=int, default=8)
     ap.add_argument("--conc", type=int, default=1, help="time CONC concurrent copies (2 = the two task streams)")
     ap.add_argument("--merge", default=None, help="existing conv_family.inc whose entries are kept")
+    ap.add_argument("--models", default="sd15", help="comma list: sd15,kandinsky2")
+    ap.add_argument("--res", type=int, default=512)
     a = ap.parse_args()
     import scripts.autotune_conv as at
     at.CONC = a.conc
     dev = torch.device("cuda")
-    convs, gemms = collect_shapes(("sd15",), 512, a.batch)
+    convs, gemms = collect_shapes(tuple(a.models.split(",")), a.res, a.batch)
     rows, kept = {}, {}
     if a.merge and os.path.exists(a.merge):
         for line in open(a.merge):
