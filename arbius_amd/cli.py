@@ -216,6 +216,20 @@ async def _operator(a, c):
             h = cid if isinstance(cid, str) else "0x" + cid.hex()
             out["solution_cid"] = cid_hex_to_str(h)
         print(json.dumps(out, indent=1))
+    elif a.cmd == "deploy":
+        from .chain.deploy import deploy
+        print(json.dumps(await deploy(c, a.artifact, [_arg(x) for x in a.args])))
+    elif a.cmd == "deploy-core":
+        # contract/scripts/003-deploy-core-basic.ts: Engine behind a transparent proxy + free kandinsky2
+        from .chain.deploy import deploy_core
+        from .node.models import template_bytes
+        tpl = None if a.no_model else (Path(a.template).read_bytes() if os.path.exists(a.template)
+                                       else template_bytes(a.template))
+        rec = await deploy_core(c, a.engine_artifact, a.proxy_artifact, a.token or c.token_address,
+                                a.treasury, tpl)
+        if a.out:
+            Path(a.out).write_text(json.dumps(rec, indent=2))
+        print(json.dumps(rec, indent=1))
     elif a.cmd == "pinata-gc":
         from .ipfs.pin import pinata_gc
         print(json.dumps(await pinata_gc(_cfg(a.config).ipfs.pinata.jwt)))
@@ -261,6 +275,18 @@ def main(argv=None):
         p.add_argument("--governor", default=None)
     p = sub.add_parser("call")
     p.add_argument("to"); p.add_argument("sig"); p.add_argument("rets"); p.add_argument("args", nargs="*")
+    p.add_argument("-c", "--config", default="MiningConfig.json")
+    p = sub.add_parser("deploy", help="contract creation from a compiled Hardhat artifact")
+    p.add_argument("artifact"); p.add_argument("args", nargs="*")
+    p.add_argument("-c", "--config", default="MiningConfig.json")
+    p = sub.add_parser("deploy-core", help="003-deploy-core-basic: Engine proxy + free mineable model")
+    p.add_argument("--engine-artifact", required=True)
+    p.add_argument("--proxy-artifact", required=True, help="TransparentUpgradeableProxy artifact")
+    p.add_argument("--token", default=None, help="BaseToken address (default: the config's)")
+    p.add_argument("--treasury", default=None)
+    p.add_argument("--template", default="kandinsky2")
+    p.add_argument("--no-model", action="store_true")
+    p.add_argument("--out", default=None, help="write the deployment record (scripts/config.json analog)")
     p.add_argument("-c", "--config", default="MiningConfig.json")
     p = sub.add_parser("send")
     p.add_argument("to"); p.add_argument("sig"); p.add_argument("args", nargs="*")

@@ -29,6 +29,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..utils.progress import beat
+from .graphs import PipelineBase
 
 CL = torch.channels_last
 GREEN = (120 / 255, 255 / 255, 155 / 255)     # RVM's green-screen background
@@ -313,7 +314,11 @@ class MattingNetwork(nn.Module):
         return _ubt(fgr, B), _ubt(pha, B), rec
 
 
-class RVMPipeline:
+class RVMPipeline(PipelineBase):
+    """Clip-level matting.  ``fork()`` (PipelineBase) shares the weights and owns a private HIP
+    stream, so the node / bench can matte one clip on the GPU while another clip's MP4 is encoded
+    and hashed on the CPU; every clip's kernels and their order are those of a solo run (bitwise)."""
+
     def __init__(self, cfg: RVMConfig = None, device="cpu", dtype=None, weight_seed: int = 0, init=True, **_):
         self.cfg = cfg = cfg or RVMConfig()
         self.device = torch.device(device)
@@ -327,12 +332,19 @@ class RVMPipeline:
         self.net.to(device=self.device, dtype=dtype, memory_format=CL).eval()
         self.timings = {}
 
+    def _reset_graphs(self):
+        pass                        # eager launches (the recurrent state is per clip): nothing to re-capture
+
     def modules(self):
         return {"net": self.net}
 
     @torch.no_grad()
     def __call__(self, frames: np.ndarray, output_type: str = "green-screen") -> np.ndarray:
         """frames uint8 [T, H, W, 3] -> uint8 [T, H, W, 3] (composite / alpha / foreground)."""
+        with self._stream_ctx():
+            return self._matte(frames, output_type)
+
+    def _matte(self, frames: np.ndarray, output_type: str) -> np.ndarray:
         t0 = time.perf_counter()
         T, H, W, _ = frames.shape
         ratio = min(1.0, self.cfg.max_side / max(H, W))

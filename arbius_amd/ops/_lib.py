@@ -448,7 +448,8 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     if plan_b and cfg < 0:   # batch-invariant: the canonical batch's plan
         cfg, split = conv_plan(plan_b, H, W, Cin, Cout, kcode, padding, upsample, stride)
         # ... at its split-K, on the tile family tuned for the actual shape (bitwise-neutral)
-        cfg = _fn("arb_conv_family")(B * Ho * Wo, Cout, kh * kw * Cin, split, plan_b // B if plan_b % B == 0 else 0, cfg)
+        ratio = plan_b // B if plan_b % B == 0 else 0
+        cfg = _fn("arb_conv_family")(B * Ho * Wo, Cout, kh * kw * Cin, split, ratio, cfg)
     args = (B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None

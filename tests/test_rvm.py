@@ -107,3 +107,28 @@ def test_miner_skips_task_with_refused_video_source():
     tid = asyncio.run(go())
     assert pool.calls == [] and m.db.get_invalid_task(tid) is None
     assert m.metrics.counters.get("tasks_refused_source") == 1
+
+
+@pytest.mark.gpu
+def test_rvm_forks_concurrent_bitwise_equal_solo():
+    """Two forks (shared weights, private HIP streams) matting different clips on two threads give
+    exactly the solo outputs - what lets the node overlap one clip's matting with another's encode."""
+    import threading
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    pipe = RVMPipeline(RVMConfig(), device="cuda")
+    rng = np.random.default_rng(4)
+    clips = [rng.integers(0, 256, (6, 144, 256, 3), dtype=np.uint8) for _ in range(2)]
+    solo = [pipe(c, "green-screen") for c in clips]
+    forks = [pipe.fork(), pipe.fork()]
+    out = [None, None]
+
+    def run(i):
+        out[i] = forks[i](clips[i], "green-screen")
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert all((a == b).all() for a, b in zip(out, solo))
