@@ -33,15 +33,23 @@ namespace {
 // ------------------------------------------------------------------------------------ bit I/O
 struct BitWriter {
   std::string out;
-  uint64_t acc = 0;
-  int n = 0;
+  uint64_t acc = 0;   // pending bits: the low n bits of acc, MSB first
+  int n = 0;          // < 32 between calls: full 32-bit words are flushed as they complete
   void put(uint32_t v, int len) {  // len <= 32
     if (len == 0) return;
     acc = (acc << len) | (len == 32 ? v : (v & ((1u << len) - 1)));
     n += len;
+    if (n >= 32) {
+      n -= 32;
+      const uint32_t w = uint32_t(acc >> n);
+      const char b[4] = {char(w >> 24), char(w >> 16), char(w >> 8), char(w)};
+      out.append(b, 4);
+    }
+  }
+  void flush_bytes() {
     while (n >= 8) {
-      out.push_back(char((acc >> (n - 8)) & 0xFF));
       n -= 8;
+      out.push_back(char((acc >> n) & 0xFF));
     }
   }
   void ue(uint32_t v) {
@@ -53,11 +61,12 @@ struct BitWriter {
   void se(int v) { ue(v > 0 ? 2u * v - 1 : 2u * uint32_t(-v)); }
   void trailing() {  // rbsp_trailing_bits
     put(1, 1);
-    if (n) put(0, 8 - n);
+    if (n & 7) put(0, 8 - (n & 7));
+    flush_bytes();
   }
-  bool aligned() const { return n == 0; }
+  bool aligned() const { return (n & 7) == 0; }
   void align_zero() {
-    if (n) put(0, 8 - n);
+    if (n & 7) put(0, 8 - (n & 7));
   }
 };
 
@@ -113,16 +122,29 @@ struct BitReader {
 };
 
 std::string add_emulation_prevention(const std::string& rbsp) {
+  // copy runs up to each 00 00 pair (rare in coded data), then apply the 00 00 0x -> 00 00 03 0x rule
   std::string out;
   out.reserve(rbsp.size() + rbsp.size() / 64 + 4);
+  const char* p = rbsp.data();
+  const size_t n = rbsp.size();
+  size_t i = 0;
   int zeros = 0;
-  for (unsigned char b : rbsp) {
+  while (i < n) {
+    if (zeros == 0) {   // fast path: jump to the next zero byte
+      const void* z = std::memchr(p + i, 0, n - i);
+      const size_t j = z ? size_t(static_cast<const char*>(z) - p) : n;
+      out.append(p + i, j - i);
+      i = j;
+      if (i == n) break;
+    }
+    const unsigned char b = static_cast<unsigned char>(p[i]);
     if (zeros >= 2 && b <= 3) {
       out.push_back(3);
       zeros = 0;
     }
     out.push_back(char(b));
     zeros = b == 0 ? zeros + 1 : 0;
+    ++i;
   }
   return out;
 }
@@ -500,17 +522,19 @@ void pred4(const int* t, const int* l, int mode, bool has_top, bool has_left, in
 
 // ------------------------------------------------------------------------------------ CAVLC
 void write_block(BitWriter& bw, const int* coef, int max_num, int nC) {
-  int levels[16], runs[16], tc = 0, last = -1;
-  for (int i = 0; i < max_num; ++i)
-    if (coef[i]) last = i;
-  for (int i = last; i >= 0; --i) {
-    if (!coef[i]) continue;
-    levels[tc] = coef[i];
-    int r = 0;
-    for (int k = i - 1; k >= 0 && !coef[k]; --k) ++r;
-    runs[tc] = r;
-    ++tc;
+  int levels[16], runs[16], tc = 0, last = max_num - 1;
+  while (last >= 0 && !coef[last]) --last;
+  int zeros = 0;
+  for (int i = last; i >= 0; --i) {   // reverse scan: runs[k] = zeros just below level k
+    if (coef[i]) {
+      if (tc) runs[tc - 1] = zeros;
+      levels[tc++] = coef[i];
+      zeros = 0;
+    } else {
+      ++zeros;
+    }
   }
+  if (tc) runs[tc - 1] = zeros;
   const int total_zeros = last + 1 - tc;
   int t1 = 0;
   while (t1 < tc && t1 < 3 && (levels[t1] == 1 || levels[t1] == -1)) ++t1;
@@ -521,31 +545,30 @@ void write_block(BitWriter& bw, const int* coef, int max_num, int nC) {
     bw.put(kCoeffTokenBits[t][tc * 4 + t1], kCoeffTokenLen[t][tc * 4 + t1]);
   }
   if (tc == 0) return;
-  for (int k = 0; k < t1; ++k) bw.put(levels[k] < 0, 1);
+  uint32_t signs = 0;
+  for (int k = 0; k < t1; ++k) signs = (signs << 1) | uint32_t(levels[k] < 0);
+  bw.put(signs, t1);
   int sl = (tc > 10 && t1 < 3) ? 1 : 0;
   for (int k = t1; k < tc; ++k) {
     const int lv = levels[k];
     int code = lv > 0 ? 2 * lv - 2 : -2 * lv - 1;
     if (k == t1 && t1 < 3) code -= 2;
+    // level_prefix (leading zeros + 1) and level_suffix written as one field
     if (sl == 0) {
       if (code < 14) {
         bw.put(1, code + 1);
       } else if (code < 30) {
-        bw.put(1, 15);
-        bw.put(code - 14, 4);
+        bw.put(16 | uint32_t(code - 14), 19);
       } else {
         if (code - 30 >= 4096) throw std::logic_error("h264: level out of range");
-        bw.put(1, 16);
-        bw.put(code - 30, 12);
+        bw.put(4096 | uint32_t(code - 30), 28);
       }
     } else {
       if (code < (15 << sl)) {
-        bw.put(1, (code >> sl) + 1);
-        bw.put(code & ((1 << sl) - 1), sl);
+        bw.put((1u << sl) | uint32_t(code & ((1 << sl) - 1)), (code >> sl) + 1 + sl);
       } else {
         if (code - (15 << sl) >= 4096) throw std::logic_error("h264: level out of range");
-        bw.put(1, 16);
-        bw.put(code - (15 << sl), 12);
+        bw.put(4096 | uint32_t(code - (15 << sl)), 28);
       }
     }
     if (sl == 0) sl = 1;
