@@ -200,9 +200,22 @@ def run(args):
     sync()
     t0 = time.perf_counter()
     last = None
-    for i in range(args.steps):
-        last = one_step(i)
-        progress(f"step {i} done")
+    if ex is None:
+        for i in range(args.steps):
+            last = one_step(i)
+            progress(f"step {i} done")
+    else:
+        # C free-running task slots (as the node's scheduler runs them): each fork solves its K
+        # tasks back to back, so one slot's CPU tail (PNG / MP4 encode + CID) overlaps the other
+        # slots' GPU work instead of every slot idling the GPU at a per-step join.  Same K x C tasks.
+        def run_slot(j):
+            r = None
+            for i in range(args.steps):
+                r = one_task(i * C + j, forks[j])
+                progress(f"slot {j} task {i} done")
+            return r
+        futs = [ex.submit(run_slot, j) for j in range(C)]
+        last = [f.result() for f in futs][-1]
     sync()
     D.barrier(dev)
     elapsed = time.perf_counter() - t0
