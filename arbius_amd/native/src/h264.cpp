@@ -989,7 +989,8 @@ Sps parse_sps(BitReader& br) {
   br.ue();    // max_num_ref_frames
   br.u(1);    // gaps
   const uint32_t mbw = br.ue(), mbh = br.ue();
-  if (mbw >= 512 || mbh >= 512) throw std::runtime_error("h264: picture too large");
+  if (mbw >= 256 || mbh >= 256 || (uint64_t(mbw) + 1) * (mbh + 1) > 36864)   // <= 4096 x 2304 (level 5.1)
+    throw std::runtime_error("h264: picture too large");
   s.mbw = int(mbw) + 1;
   s.mbh = int(mbh) + 1;
   if (!br.u(1)) throw std::runtime_error("h264: interlaced (frame_mbs_only_flag = 0) is not supported");
@@ -1280,6 +1281,11 @@ std::vector<Picture> decode(const std::vector<std::string>& nals, int threads) {
       throw std::runtime_error("h264: unsupported NAL unit type " + std::to_string(type));
     }
   }
+  // untrusted input: a few bits per macroblock can declare huge pictures, so bound what decoding
+  // may allocate (4K per picture via the SPS limits, 2^31 luma samples - ~3.2 GB of 4:2:0 - in total)
+  uint64_t samples = 0;
+  for (const Job& j : jobs) samples += uint64_t(j.sps.mbw) * j.sps.mbh * 256;
+  if (samples > (uint64_t(1) << 31)) throw std::runtime_error("h264: video too large to decode");
   std::vector<Picture> out(jobs.size());
   std::vector<std::string> errors(jobs.size());
   auto work = [&](int t, int nt) {

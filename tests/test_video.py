@@ -385,3 +385,17 @@ def test_intra4x4_decode_matches_independent_prediction_chain():
     [(y, cb, cr)], crop = decode_h264([sps, pps, nal])
     assert crop == (W, H)
     assert (y == Y).all() and (cb == Cb).all() and (cr == Cr).all()
+
+
+def test_decoder_refuses_oversized_pictures():
+    """A few bits per macroblock can declare huge pictures: the decoder caps picture size (4K) and
+    the total decoded samples before allocating (untrusted input_video)."""
+    import pytest
+    from arbius_amd import native
+    from arbius_amd.utils.mp4 import _Bits, _ep
+    s = _Bits()
+    s.u(8, 66); s.u(8, 0xC0); s.u(8, 51); s.ue(0); s.ue(0); s.ue(2); s.ue(1); s.u(1, 0)
+    s.ue(299); s.ue(10)                    # 4800 x 176: wider than 4096
+    s.u(1, 1); s.u(1, 1); s.u(1, 0); s.u(1, 0); s.trailing()
+    with pytest.raises(ValueError, match="too large"):
+        native.h264_decode([b"\x67" + _ep(s.bytes())])
