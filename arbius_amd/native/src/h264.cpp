@@ -717,7 +717,7 @@ void recon_chroma(std::vector<uint8_t>& pl, int Wc, int mx, int my, const uint8_
 // ------------------------------------------------------------------------------------ encoder
 inline int quant(int w, int mf, int f, int qbits) {
   const int a = w < 0 ? -w : w;
-  int z = int((int64_t(a) * mf + f) >> qbits);
+  int z = (a * mf + f) >> qbits;   // |w| * mf < 2^31 for 8-bit residuals (luma DC: 32640 x 13107)
   z = std::min(z, 2047);
   return w < 0 ? -z : z;
 }
