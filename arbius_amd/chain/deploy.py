@@ -6,8 +6,12 @@ The EngineV1 implementation disables initializers in its constructor
 ``upgrades.deployProxy`` does (``003-deploy-core-basic.ts:20-26``):
 
 1. deploy the Engine implementation (contract creation, no constructor arguments);
-2. deploy a TransparentUpgradeableProxy(implementation, admin, initialize(baseToken, treasury)) -
-   the proxy's constructor runs the initializer in the proxy's storage;
+2. deploy a ProxyAdmin owned by the deployer (or use ``proxy_admin=`` an existing one), then a
+   TransparentUpgradeableProxy(implementation, proxyAdmin, initialize(baseToken, treasury)) - the
+   proxy's constructor runs the initializer in the proxy's storage.  The admin must NOT be the
+   deployer's own address: OZ 4.9's transparent proxy refuses to forward any call from its admin
+   ("admin cannot fallback to proxy target"), so the deployer's registerModel below would revert -
+   ``upgrades.deployProxy`` uses a ProxyAdmin contract for the same reason;
 3. ``registerModel(0x..01, 0, kandinsky2 template)`` on the proxy and ``setSolutionMineableRate(id,
    1e18)`` (``deployFreeMineableModel``, ``:60-100``);
 4. write the deployment record (the reference rewrites ``scripts/config.json``).
@@ -23,7 +27,9 @@ import json
 from pathlib import Path
 from typing import Any, Dict, List, Sequence, Tuple
 
+from ..ipfs.unixfs import onchain_cid
 from ..utils.keccak import keccak256
+from ..utils.protocol import hash_model
 from . import abi
 from .tx import rlp_encode
 
@@ -92,24 +98,37 @@ async def deploy(client, artifact, args: Sequence[Any] = (), gas: int = 8_000_00
 
 
 async def deploy_core(client, engine_artifact, proxy_artifact, base_token: str, treasury: str = None,
-                      template: bytes = None, rate: int = 10 ** 18) -> Dict[str, Any]:
-    """003-deploy-core-basic: Engine behind a transparent proxy + one free mineable model."""
+                      template: bytes = None, rate: int = 10 ** 18, proxy_admin_artifact=None,
+                      proxy_admin: str = None) -> Dict[str, Any]:
+    """003-deploy-core-basic: Engine behind a transparent proxy + one free mineable model.
+
+    Exactly one of ``proxy_admin_artifact`` (a ProxyAdmin to deploy, owned by the deployer) and
+    ``proxy_admin`` (an existing admin contract) is required; the deployer itself is refused as admin."""
+    if (proxy_admin_artifact is None) == (proxy_admin is None):
+        raise ValueError("deploy_core needs exactly one of proxy_admin_artifact / proxy_admin")
+    if proxy_admin is not None and proxy_admin.lower() == client.address.lower():
+        raise ValueError("the proxy admin must not be the deployer: OZ transparent proxies do not forward "
+                         "the admin's calls, so the deployer's registerModel would revert")
     treasury = treasury or client.address
     impl = await deploy(client, engine_artifact)
+    if proxy_admin_artifact is not None:
+        # OZ 4.x ProxyAdmin: no constructor arguments, owner = msg.sender; OZ 5.x: ProxyAdmin(initialOwner)
+        admin_abi, _ = load_artifact(proxy_admin_artifact)
+        admin_args = [client.address] if constructor_types(admin_abi) == ["address"] else []
+        proxy_admin = (await deploy(client, proxy_admin_artifact, admin_args))["address"]
     init = abi.encode_call("initialize(address,address)", base_token, treasury)
-    proxy = await deploy(client, proxy_artifact, [impl["address"], client.address, init])
+    proxy = await deploy(client, proxy_artifact, [impl["address"], proxy_admin, init])
     engine = proxy["address"]
     out: Dict[str, Any] = {"baseTokenAddress": base_token, "engineAddress": engine,
-                           "engineImplementation": impl["address"], "proxyAdmin": client.address, "models": {}}
+                           "engineImplementation": impl["address"], "proxyAdmin": proxy_admin, "models": {}}
     if template is not None:
-        cid = (await client.call_sig(engine, "generateIPFSCID(bytes)", ["bytes"], template))[0]
-        mid = (await client.call_sig(engine, "hashModel((address,uint256,uint256,bytes),address)", ["bytes32"],
-                                     (FREE_MODEL_ADDR, 0, rate, cid), client.address))[0]
+        # both ids are pure functions (EngineV1.sol:409-424), so compute them here rather than eth_call:
+        # hashModel(Model{fee, addr, rate, cid}, sender) = keccak(abi.encode(sender, addr, fee, cid))
+        cid_hex = "0x" + onchain_cid(template).hex()
+        mid_hex = hash_model(client.address, FREE_MODEL_ADDR, 0, cid_hex)
         await client.send_sig(engine, "registerModel(address,uint256,bytes)", FREE_MODEL_ADDR, 0, template,
                               gas=3_000_000)
-        await client.send_sig(engine, "setSolutionMineableRate(bytes32,uint256)", mid, rate)
-        mid_hex = mid if isinstance(mid, str) else "0x" + bytes(mid).hex()
-        cid_hex = cid if isinstance(cid, str) else "0x" + bytes(cid).hex()
+        await client.send_sig(engine, "setSolutionMineableRate(bytes32,uint256)", mid_hex, rate)
         out["models"]["kandinsky2"] = {"id": mid_hex, "mineable": True,
                                        "params": {"addr": FREE_MODEL_ADDR, "fee": "0", "rate": str(rate),
                                                   "cid": cid_hex}}

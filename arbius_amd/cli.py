@@ -226,7 +226,8 @@ async def _operator(a, c):
         tpl = None if a.no_model else (Path(a.template).read_bytes() if os.path.exists(a.template)
                                        else template_bytes(a.template))
         rec = await deploy_core(c, a.engine_artifact, a.proxy_artifact, a.token or c.token_address,
-                                a.treasury, tpl)
+                                a.treasury, tpl, proxy_admin_artifact=a.proxy_admin_artifact,
+                                proxy_admin=a.proxy_admin)
         if a.out:
             Path(a.out).write_text(json.dumps(rec, indent=2))
         print(json.dumps(rec, indent=1))
@@ -282,6 +283,9 @@ def main(argv=None):
     p = sub.add_parser("deploy-core", help="003-deploy-core-basic: Engine proxy + free mineable model")
     p.add_argument("--engine-artifact", required=True)
     p.add_argument("--proxy-artifact", required=True, help="TransparentUpgradeableProxy artifact")
+    g = p.add_mutually_exclusive_group(required=True)
+    g.add_argument("--proxy-admin-artifact", help="ProxyAdmin artifact (deployed, owned by the deployer)")
+    g.add_argument("--proxy-admin", help="existing ProxyAdmin contract address")
     p.add_argument("--token", default=None, help="BaseToken address (default: the config's)")
     p.add_argument("--treasury", default=None)
     p.add_argument("--template", default="kandinsky2")

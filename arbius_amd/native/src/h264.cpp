@@ -1011,7 +1011,8 @@ Sps parse_sps(BitReader& br) {
 Pps parse_pps(BitReader& br) {
   Pps p;
   if (br.ue() != 0) throw std::runtime_error("h264: only pic_parameter_set_id 0 is supported");
-  p.sps_id = int(br.ue());
+  if (br.ue() != 0) throw std::runtime_error("h264: only seq_parameter_set_id 0 is supported");
+  p.sps_id = 0;
   if (br.u(1)) throw std::runtime_error("h264: CABAC is not supported");
   p.bottom_field_pic_order = br.u(1);
   if (br.ue() != 0) throw std::runtime_error("h264: slice groups (FMO) are not supported");
@@ -1019,9 +1020,12 @@ Pps parse_pps(BitReader& br) {
   br.ue();
   br.u(1);
   br.u(2);
-  p.init_qp = 26 + br.se();
+  const int64_t init_qp = 26 + int64_t(br.se());   // int64: a hostile se() must not overflow
   br.se();
-  p.chroma_qp_offset = br.se();
+  const int64_t cqo = br.se();
+  if (init_qp < 0 || init_qp > 51 || cqo < -12 || cqo > 12) throw std::runtime_error("h264: PPS field out of range");
+  p.init_qp = int(init_qp);
+  p.chroma_qp_offset = int(cqo);
   if (p.init_qp < 0 || p.init_qp > 51 || p.chroma_qp_offset < -12 || p.chroma_qp_offset > 12)
     throw std::runtime_error("h264: PPS field out of range");
   p.deblocking_control = br.u(1);
@@ -1034,8 +1038,11 @@ Pps parse_pps(BitReader& br) {
 
 void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, const Pps& pps, Frame& f,
                   int slice_id) {
-  const int first_mb = int(br.ue());
-  const int slice_type = int(br.ue()) % 5;
+  // untrusted input: range-check every exp-golomb value as uint32 before it becomes an index
+  const uint32_t first_mb_u = br.ue();
+  if (first_mb_u >= uint32_t(f.mbw) * uint32_t(f.mbh)) throw std::runtime_error("h264: first_mb_in_slice out of range");
+  const int first_mb = int(first_mb_u);
+  const int slice_type = int(br.ue() % 5);
   if (slice_type != 2) throw std::runtime_error("h264: only I slices are supported (no P/B/SP/SI)");
   br.ue();  // pps id
   br.u(sps.log2_max_frame_num);
@@ -1063,8 +1070,9 @@ void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, 
       }
     }
   }
-  int qp = pps.init_qp + br.se();
-  if (qp < 0 || qp > 51) throw std::runtime_error("h264: slice QP out of range");
+  const int64_t qp0 = pps.init_qp + int64_t(br.se());
+  if (qp0 < 0 || qp0 > 51) throw std::runtime_error("h264: slice QP out of range");
+  int qp = int(qp0);
   auto qp_delta = [&](int q) {
     const int d = br.se();
     if (d < -26 || d > 25) throw std::runtime_error("h264: mb_qp_delta out of range");
@@ -1104,8 +1112,9 @@ void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, 
     } else if (mb_type >= 1 && mb_type <= 24) {  // I_16x16
       const int mode = int(mb_type - 1) % 4, cbp_chroma = (int(mb_type - 1) / 4) % 3;
       const int cbp_luma = mb_type >= 13 ? 15 : 0;
-      const int cmode = int(br.ue());
-      if (cmode > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
+      const uint32_t cmode_u = br.ue();
+      if (cmode_u > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
+      const int cmode = int(cmode_u);
       qp = qp_delta(qp);
       if ((mode == 0 && !nb.top) || (mode == 1 && !nb.left) || (mode == 3 && !(nb.top && nb.left && nb.topleft)))
         throw std::runtime_error("h264: Intra_16x16 mode uses unavailable samples");
@@ -1163,8 +1172,9 @@ void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, 
         modes[blk] = m;
         f.i4mode[size_t(by) * 4 * f.mbw + bx] = int8_t(m);
       }
-      const int cmode = int(br.ue());
-      if (cmode > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
+      const uint32_t cmode_u = br.ue();
+      if (cmode_u > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
+      const int cmode = int(cmode_u);
       const uint32_t cbp_code = br.ue();
       if (cbp_code > 47) throw std::runtime_error("h264: bad coded_block_pattern");
       const int cbp = kIntraCbp[cbp_code], cbp_luma = cbp & 15, cbp_chroma = cbp >> 4;

@@ -67,6 +67,29 @@ for qp in (4, 20, 51):
             N.h264_decode([sps, pps, bytes(bad)], 1)
         except ValueError:
             pass
+# hand-made hostile slices: exp-golomb values with 31 leading zeros (>= 2^31) in every field that
+# becomes an index (first_mb_in_slice, intra_chroma_pred_mode, slice QP delta)
+def ue(v):
+    x = v + 1
+    return "0" * (x.bit_length() - 1) + format(x, "b")
+def se(v):
+    return ue(2 * v - 1 if v > 0 else -2 * v)
+def nal(bits):
+    bits += "1"
+    bits += "0" * (-len(bits) % 8)
+    return bytes([0x65]) + int(bits, 2).to_bytes(len(bits) // 8, "big")
+BIG = (1 << 32) - 2
+head = lambda first=0, qpd=0: ue(first) + ue(7) + ue(0) + "0000" + ue(0) + "00" + se(qpd) + ue(1)
+hostile = [nal(head(first=BIG)), nal(head(first=(1 << 31) + 5)), nal(head(qpd=(1 << 31) - 1)),
+           nal(head() + ue(3) + ue(BIG) + se(0)),               # I_16x16 DC, chroma mode 2^32-2
+           nal(head() + ue(0) + "1" * 16 + ue((1 << 31) + 1) + ue(0))]   # I_NxN, chroma mode >= 2^31
+sps, pps = N.h264_parameter_sets(64, 48, 20)
+for h in hostile:
+    try:
+        N.h264_decode([sps, pps, h], 1)
+        raise SystemExit("accepted a hostile slice")
+    except ValueError:
+        pass
 frames = rng.integers(0, 256, (3, 40, 72, 3), dtype=np.uint8)
 _, _, nals = N.h264_encode_rgb(frames, 24, 3)
 assert N.h264_decode_rgb([sps_ for sps_ in N.h264_parameter_sets(72, 40, 24)] + list(nals), 2).shape == (3, 40, 72, 3)

@@ -10,6 +10,8 @@ from arbius_amd.chain import abi
 from arbius_amd.chain.deploy import FREE_MODEL_ADDR, create_address, creation_data, deploy, deploy_core
 from arbius_amd.chain.rpc import RpcChainClient as RpcClient
 from arbius_amd.chain.tx import decode_raw_tx
+from arbius_amd.ipfs.unixfs import onchain_cid
+from arbius_amd.utils.keccak import keccak256
 
 KEY = "0x" + "42" * 32
 
@@ -51,12 +53,7 @@ class _Chain:
             return f["hash"]
         if method == "eth_getTransactionReceipt":
             return self.last
-        if method == "eth_call":
-            data = bytes.fromhex(params[0]["data"][2:])
-            if data[:4] == abi.selector("generateIPFSCID(bytes)"):
-                return "0x" + abi.encode(["bytes"], [b"\x12\x20" + b"\x11" * 32]).hex()
-            return "0x" + abi.encode(["bytes32"], [b"\x77" * 32]).hex()
-        raise AssertionError(method)
+        raise AssertionError(f"unexpected JSON-RPC call {method}")   # no eth_call: ids are computed locally
 
 
 def _client(chain):
@@ -79,26 +76,49 @@ def test_contract_creation_tx(tmp_path):
         creation_data(json.loads(art.read_text())["abi"], code, [1])
 
 
-def test_deploy_core_flow(tmp_path):
-    """impl -> TransparentUpgradeableProxy(impl, admin, initialize(token, treasury)) -> registerModel ->
-    setSolutionMineableRate, each signed by the deployer, nonces consecutive."""
+def _proxy_artifacts(tmp_path):
     eng = _artifact(tmp_path, "EngineV1", [])
     prx = _artifact(tmp_path, "TransparentUpgradeableProxy",
                     [{"name": "_logic", "type": "address"}, {"name": "admin_", "type": "address"},
                      {"name": "_data", "type": "bytes"}])
+    adm = _artifact(tmp_path, "ProxyAdmin", [])            # OZ 4.9: owner = msg.sender
+    return eng, prx, adm
+
+
+def test_deploy_core_flow(tmp_path):
+    """impl -> ProxyAdmin -> TransparentUpgradeableProxy(impl, proxyAdmin, initialize(token, treasury)) ->
+    registerModel -> setSolutionMineableRate, each signed by the deployer, nonces consecutive."""
+    eng, prx, adm = _proxy_artifacts(tmp_path)
     chain = _Chain()
     c = _client(chain)
     token = "0x" + "ab" * 20
-    rec = asyncio.run(deploy_core(c, eng, prx, token, template=b'{"meta": {}}'))
+    tpl = b'{"meta": {}}'
+    rec = asyncio.run(deploy_core(c, eng, prx, token, template=tpl, proxy_admin_artifact=adm))
     kinds = [f["to"] for f, _ in chain.raw]
-    impl, proxy = create_address(c.address, 0), create_address(c.address, 1)
-    assert kinds == ["0x", "0x", proxy, proxy]
-    assert [f["nonce"] for f, _ in chain.raw] == [0, 1, 2, 3]
+    impl, admin, proxy = (create_address(c.address, n) for n in range(3))
+    assert kinds == ["0x", "0x", "0x", proxy, proxy]
+    assert [f["nonce"] for f, _ in chain.raw] == [0, 1, 2, 3, 4]
     init = abi.encode_call("initialize(address,address)", token, c.address)
-    assert chain.raw[1][0]["data"].endswith(abi.encode(["address", "address", "bytes"], [impl, c.address, init]))
-    reg = abi.decode_call("registerModel(address,uint256,bytes)", chain.raw[2][0]["data"])
-    assert reg[0].lower() == FREE_MODEL_ADDR and reg[1] == 0 and reg[2] == "0x" + b'{"meta": {}}'.hex()
-    rate = abi.decode_call("setSolutionMineableRate(bytes32,uint256)", chain.raw[3][0]["data"])
+    assert chain.raw[2][0]["data"].endswith(abi.encode(["address", "address", "bytes"], [impl, admin, init]))
+    # the transparent proxy never forwards its admin's calls: the admin must not be the tx sender
+    assert admin.lower() != c.address.lower() and rec["proxyAdmin"] == admin
+    reg = abi.decode_call("registerModel(address,uint256,bytes)", chain.raw[3][0]["data"])
+    assert reg[0].lower() == FREE_MODEL_ADDR and reg[1] == 0 and reg[2] == "0x" + tpl.hex()
+    rate = abi.decode_call("setSolutionMineableRate(bytes32,uint256)", chain.raw[4][0]["data"])
     assert rate[1] == 10 ** 18
     assert rec["engineAddress"] == proxy and rec["engineImplementation"] == impl
-    assert rec["models"]["kandinsky2"]["id"] == "0x" + "77" * 32
+    # EngineV1.hashModel(Model{fee, addr, rate, cid}, sender) = keccak(abi.encode(sender, addr, fee, cid))
+    cid = onchain_cid(tpl)
+    want = "0x" + keccak256(abi.encode(["address", "address", "uint256", "bytes"],
+                                       [c.address, FREE_MODEL_ADDR, 0, cid])).hex()
+    assert rec["models"]["kandinsky2"]["id"] == want
+    assert "0x" + bytes(rate[0]).hex() == want if not isinstance(rate[0], str) else rate[0] == want
+
+
+def test_deploy_core_refuses_deployer_as_admin(tmp_path):
+    eng, prx, _ = _proxy_artifacts(tmp_path)
+    c = _client(_Chain())
+    with pytest.raises(ValueError, match="must not be the deployer"):
+        asyncio.run(deploy_core(c, eng, prx, "0x" + "ab" * 20, proxy_admin=c.address))
+    with pytest.raises(ValueError, match="exactly one"):
+        asyncio.run(deploy_core(c, eng, prx, "0x" + "ab" * 20))
