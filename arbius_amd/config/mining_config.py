@@ -94,7 +94,8 @@ class MI355XConfig(_Base):
     mock_chain: bool = False              # in-process MockEngine (testing / plumbing config)
     selftest: bool = True                 # boot CID self-test (index.ts:981-1001)
     selftest_table: Optional[str] = None  # override of config/selftest.json
-    workers_per_gpu: int = 1              # concurrent task streams per GPU (pipeline forks)
+    workers_per_gpu: int = 2              # concurrent task streams per GPU (pipeline forks): the benched
+                                          # default (bench.py --concurrent 2); 1 = latency mode
     lockstep_group: int = 4               # queued compatible SD tasks solved per stream in ONE batch
                                           # (batch-invariant plans: same CIDs as solo; a lone task
                                           # never waits for company)

@@ -73,7 +73,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
             backend = "nccl" if device_type == "cuda" else "gloo"
             kw = {"device_id": dev} if device_type == "cuda" else {}
-            dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+            dist.init_process_group(backend, rank=rank, world_size=world, timeout=D.pg_timeout(), **kw)
         pipes = {}
         bstats = {"bytes": 0, "seconds": 0.0}
         from ..utils import progress
@@ -85,6 +85,9 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                                   init=src and not weights_dir, weights_dir=weights_dir if src else None,
                                   tokenizer_dir=weights_dir)
             if group and world > 1:
+                if (os.environ.get("ARBIUS_FAULT_INJECTION") == "1"
+                        and os.environ.get("ARBIUS_FAULT_BCAST_DIE_RANK") == str(rank)):
+                    os._exit(17)                    # test hook: a rank lost in the middle of the broadcast
                 st = D.broadcast_modules(pipe.modules().values())
                 bstats["bytes"] += st["bytes"]
                 bstats["seconds"] += st["seconds"]
@@ -128,7 +131,9 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
         threads = [threading.Thread(target=slot_loop, args=(k,), daemon=True) for k in range(streams)]
         for t in threads:
             t.start()
-        out_q.put(("ready", rank, bstats))
+        world_info = D.world_info(dev) if group and world > 1 else {"backend": "none", "world_size": 1}
+        log.info("worker %d ready: %s", rank, world_info)
+        out_q.put(("ready", rank, dict(bstats, world=world_info)))
         while True:
             msg = in_q.get()
             if msg is None:
@@ -139,11 +144,10 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
         for t in threads:
             t.join()
     finally:
-        if group and world > 1 and dist.is_initialized():
-            try:
-                dist.destroy_process_group()
-            except Exception:  # noqa: BLE001
-                pass
+        # bounded: with a dead peer destroy_process_group can block forever, and a worker that never
+        # exits would stall the pool's shutdown (close() joins it)
+        if group and world > 1 and dist.is_initialized() and not D.shutdown(timeout=15.0):
+            os._exit(0)
 
 
 class MultiGPUSolverPool:
@@ -175,13 +179,32 @@ class MultiGPUSolverPool:
         self.futures: Dict[int, asyncio.Future] = {}
         self._ids = itertools.count(1)
         self.broadcast_stats = {}
+        self.world = None                        # the process group the workers formed (rank 0's view)
         self.restarts = 0
         port = _free_port()
         for r in range(n):
             self._spawn(r, port, group=True)
-        ready = 0
+        try:
+            self._await_ready(start_timeout)
+        except BaseException:
+            # one rank lost during start (e.g. mid-broadcast) leaves its peers blocked in a collective
+            # until the process-group timeout: take every worker down now, then fail loudly
+            self._kill_all()
+            raise
+        self.idle.sort()
+        self._pump_task = None
+
+    def _kill_all(self):
+        for p in self.procs:
+            if p is not None and p.is_alive():
+                p.kill()
+        for p in self.procs:
+            if p is not None:
+                p.join(10)
+
+    def _await_ready(self, start_timeout: float):
         t0 = time.time()
-        pending = set(range(n))
+        pending = set(range(self.n))
         while pending:
             if time.time() - t0 > start_timeout:
                 raise TimeoutError("GPU workers did not start")
@@ -197,8 +220,7 @@ class MultiGPUSolverPool:
                     pending.discard(rank)
                     self.idle.extend([rank] * self.streams * self.lockstep)
                     self.broadcast_stats[rank] = payload
-        self.idle.sort()
-        self._pump_task = None
+                    self.world = payload.get("world")
 
     def hardware(self) -> str:
         from ..node.pool import hardware_id

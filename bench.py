@@ -56,6 +56,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--tiny", action="store_true", help="tiny config (CPU plumbing check only)")
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu (gloo ranks)")
+    ap.add_argument("--node", action="store_true",
+                    help="whole-node mode: tasks flow through the node's own stack (MockEngine events -> "
+                         "orchestrator -> solver pool -> commit/submit); one process, N GPU worker processes")
     args = ap.parse_args(argv)
     k2 = args.model == "kandinsky2"
     vid = args.model in ("zeroscopev2xl", "damo")
@@ -110,6 +113,11 @@ def run(args):
                           weights_dir=args.weights_dir if src else None,
                           tokenizer_dir=args.weights_dir,
                           use_graphs=(dev.type == "cuda" and not args.no_graphs))
+    winfo = D.world_info(dev)
+    if rank == 0:
+        print(f"[bench] world: {json.dumps(winfo)}", file=sys.stderr, flush=True)
+    if os.environ.get("ARBIUS_FAULT_INJECTION") == "1" and os.environ.get("ARBIUS_FAULT_BCAST_DIE_RANK") == str(rank):
+        os._exit(17)        # test hook: a rank lost right before / during the weight broadcast
     bstats = D.broadcast_modules(pipe.modules().values())
     if hasattr(pipe, "_reset_graphs"):
         pipe._reset_graphs()
@@ -273,6 +281,7 @@ def run(args):
             "stage_s": {k: round(v, 4) for k, v in (last.timings.items() if last else [])},
             "weight_broadcast": {"bytes": int(max(v[2] for v in per_rank)), "seconds": round(bstats["seconds"], 4),
                                  "backend": D.backend_name()},
+            "world": winfo,
             "init_s": round(t_init, 2),
             "native_kernels_loaded": ops.native_loaded(),
             "reference_ops": bool(args.reference_ops),
@@ -281,6 +290,52 @@ def run(args):
     if ex is not None:
         ex.shutdown()
     D.shutdown()
+
+
+def run_node(args):
+    """``--node``: the node as shipped (arbius_amd/node/nodebench.py) instead of bare pipeline loops."""
+    from arbius_amd import ops
+    from arbius_amd.node.nodebench import run_node_bench
+    dev = _device_type(args)
+    device = "cuda:0" if dev == "cuda" else "cpu"
+    if args.reference_ops:
+        ops.set_reference_ops(True)
+    r = run_node_bench(args, device)
+    per_step_ms = r["elapsed_s"] * 1000.0 / args.steps
+    k2 = args.model == "kandinsky2"
+    out = {
+        "metric": "tasks_solved_per_hour",
+        "value": round(r["tasks"] * 3600.0 / r["elapsed_s"], 2),
+        "unit": "tasks/hour",
+        "n_gpus": args.gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(per_step_ms, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if dev == "cuda" else "fp32",
+        "data": "synthetic prompts submitted to an in-process MockEngine, random-init weights" + (
+            " (TINY)" if args.tiny else ""),
+        "config": {"model": args.model + (" TINY" if args.tiny else ""), "mode": "node",
+                   "global_batch": r["capacity"], "seq_len": (args.res // 8) * (args.height // 8),
+                   "resolution": args.res, "denoise_steps": args.denoise_steps,
+                   "scheduler": "p_sampler" if k2 else args.scheduler, "cfg_batch": 2,
+                   "streams_per_gpu": args.concurrent, "lockstep_group": args.group,
+                   "parallelism": f"dp{args.gpus}",
+                   "parallelism_detail": "node stack: event poll -> task/solve jobs -> solver pool -> "
+                                         "commit/submit; pool slots = GPUs x streams x lock-step group"},
+        "p50_task_latency_ms": round(r["p50_s"] * 1000.0, 2),
+        "p90_task_latency_ms": round(r["p90_s"] * 1000.0, 2),
+        "tasks_timed": r["tasks"],
+        "pool_capacity": r["capacity"],
+        "pins_ok": r["pins_ok"],
+        "jobs": r["jobs"],
+        "stage_p50_s": r["stage_p50_s"],
+        "init_s": round(r["init_s"], 2),
+        "native_kernels_loaded": ops.native_loaded(),
+    }
+    print(json.dumps(out), flush=True)
 
 
 def _free_port() -> int:
@@ -328,6 +383,10 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
     launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if args.node:
+        if launched > 1:
+            raise SystemExit("--node runs the whole node in ONE process (it spawns its GPU workers): no torchrun")
+        return run_node(args)
     if launched == 0 and args.gpus > 1:
         sys.exit(spawn(argv, args.gpus))
     run(args)

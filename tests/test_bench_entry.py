@@ -52,3 +52,28 @@ def test_bench_gpus_must_match_launcher_world():
     env = {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29599"}
     r = _run(["--gpus", "2", *TINY], env=env)
     assert r.returncode != 0 and "--gpus 2" in (r.stderr + r.stdout)
+
+
+@pytest.mark.timeout(900)
+def test_node_bench_through_the_node_stack_gloo():
+    """``--node``: tasks are submitted to the MockEngine and solved by the orchestrator + a 2-worker
+    MultiGPUSolverPool (gloo ranks, weights broadcast); every solution is accepted on chain."""
+    r = _run(["--node", "--gpus", "2", "--device", "cpu", "--tiny", "--steps", "2", "--warmup", "0",
+              "--denoise-steps", "2", "--res", "128", "--scheduler", "DDIM", "--concurrent", "1", "--group", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r.stdout)
+    assert d["config"]["mode"] == "node" and d["n_gpus"] == 2 and d["pool_capacity"] == 2
+    assert d["tasks_timed"] == 4 and d["pins_ok"]
+    assert d["jobs"]["jobs_ok_solve"] == 4 and d["jobs"]["jobs_ok_task"] == 4
+    assert d["p50_task_latency_ms"] > 0
+    assert d["value"] == pytest.approx(4 * 3600e3 / (2 * d["ms_per_step"]), rel=1e-3)
+
+
+@pytest.mark.timeout(300)
+def test_bench_exits_nonzero_when_a_rank_dies_in_the_broadcast():
+    import time
+    t0 = time.time()
+    r = _run(["--gpus", "2", *TINY], env={"ARBIUS_FAULT_INJECTION": "1", "ARBIUS_FAULT_BCAST_DIE_RANK": "1",
+                                          "WORLD_SIZE": "0"}, timeout=240)
+    assert r.returncode != 0
+    assert time.time() - t0 < 200

@@ -65,3 +65,31 @@ def test_two_task_streams_per_worker():
             await pool.close()
 
     asyncio.run(go())
+
+
+@pytest.mark.timeout(300)
+def test_pool_start_fails_fast_when_a_rank_dies_in_the_broadcast(monkeypatch):
+    """A worker lost in the middle of the weight broadcast: the pool kills its peers (blocked in the
+    collective) and raises within seconds, instead of hanging until the process-group timeout."""
+    import time
+    monkeypatch.setenv("ARBIUS_FAULT_INJECTION", "1")
+    monkeypatch.setenv("ARBIUS_FAULT_BCAST_DIE_RANK", "1")
+    monkeypatch.setenv("ARBIUS_DIST_TIMEOUT_S", "600")
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="died during start"):
+        MultiGPUSolverPool(2, ["anythingv3"], device_type="cpu", tiny=True)
+    assert time.time() - t0 < 120
+
+
+@pytest.mark.timeout(300)
+def test_pool_reports_the_formed_world_and_closes():
+    async def go():
+        pool = MultiGPUSolverPool(2, ["anythingv3"], device_type="cpu", tiny=True)
+        try:
+            assert pool.world["backend"] == "gloo" and pool.world["world_size"] == 2
+            assert len(pool.world["ranks"]) == 2
+        finally:
+            await pool.close()
+        assert not any(p.is_alive() for p in pool.procs)
+
+    asyncio.run(go())
