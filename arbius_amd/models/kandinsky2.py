@@ -36,7 +36,7 @@ from .graphs import GraphCache, PipelineBase
 from .layers import Linear, init_weights
 from .movq import MoVQConfig, MoVQDecoder
 from .prior import PriorConfig, PriorTransformer
-from .schedulers import GaussianDiffusion, GroupSampler, TaskSampler
+from .schedulers import K2_SCHEDULERS, GaussianDiffusion, GroupSampler, TaskSampler, k2_decoder_scheduler
 from .tokenizer import CLIPTokenizer
 from .xlmr import MCLIPText, XLMRConfig, XLMRTokenizer
 
@@ -51,7 +51,7 @@ class Kandinsky2Config:
     num_steps: int = 100
     guidance_scale: float = 4.0
     prior_cf_scale: float = 4.0
-    prior_steps: int = 5
+    prior_steps: str = "5"          # template type "string" (guided-diffusion respacing spec)
     latent_clamp: float = 2.0      # denoised_fn clamp(-2, 2)
 
     @staticmethod
@@ -105,51 +105,73 @@ class Kandinsky2Pipeline(PipelineBase):
                 "clip_proj": self.clip_proj, "xlmr": self.xlmr, "buffers": self.buffers}
 
     # ------------------------------------------------------------------------------------------
+    def settings(self, inp: dict) -> dict:
+        """A task's sampling settings: the template inputs (docs/src/pages/register-model.mdx:141-185:
+        num_inference_steps, guidance_scale, scheduler, prior_cf_scale, prior_steps) over the hidden
+        defaults of the mainnet template (templates/kandinsky2.json exposes only prompt / size)."""
+        cfg = self.cfg
+        sched = str(inp.get("scheduler", "p_sampler"))
+        if sched not in K2_SCHEDULERS:
+            raise ValueError(f"kandinsky2: unknown scheduler {sched!r}")
+        prior_steps = inp.get("prior_steps", cfg.prior_steps)
+        return {"steps": int(inp.get("num_inference_steps", cfg.num_steps)),
+                "guidance": float(inp.get("guidance_scale", cfg.guidance_scale)),
+                "scheduler": sched,
+                "prior_cf_scale": float(inp.get("prior_cf_scale", cfg.prior_cf_scale)),
+                "prior_steps": str(prior_steps).strip()}
+
     def _clip_len(self, ids):
         eos = ids[-1]
         return ids.index(eos) + 1
 
     @torch.no_grad()
-    def encode_clip(self, prompt: str):
-        ids = [self.clip_tok(prompt), self.clip_tok("")]
-        lens = [self._clip_len(i) for i in ids]
-        hidden, pooled = self.clip(torch.tensor(ids, dtype=torch.long, device=self.device))
-        return hidden, self.clip_proj(pooled), lens
+    def encode_text(self, prompts: List[str]):
+        """Both text towers for k prompts in ONE batch of 2k sequences (rows 2i / 2i+1 = prompt i /
+        the empty prompt), under batch-invariant plans: each row's bytes are its solo bytes.
+        -> CLIP hidden [2k,77,w], CLIP pooled (projected) [2k,d], CLIP lengths, XLM-R full [2k,77,W],
+        XLM-R pooled [2k,proj]."""
+        texts = [t for p in prompts for t in (p, "")]
+        cids = [self.clip_tok(t) for t in texts]
+        lens = [self._clip_len(i) for i in cids]
+        xt = [self.xlmr_tok(t) for t in texts]
+        with ops.plan_batch(1):
+            hidden, pooled = self.clip(torch.tensor(cids, dtype=torch.long, device=self.device))
+            pooled = self.clip_proj(pooled)
+            full, xpooled = self.xlmr(torch.tensor([i for i, _ in xt], dtype=torch.long, device=self.device),
+                                      [n for _, n in xt])
+        return hidden, pooled, lens, full, xpooled
+
+    def _prior_stats(self):
+        return self.prior.clip_std.float(), self.prior.clip_mean.float()
 
     @torch.no_grad()
-    def encode_xlmr(self, prompt: str):
-        full, pooled = [], []
-        for text in (prompt, ""):
-            ids, n = self.xlmr_tok(text)
-            f, p = self.xlmr(torch.tensor([ids], dtype=torch.long, device=self.device), n)
-            full.append(f)
-            pooled.append(p)
-        return torch.cat(full), torch.cat(pooled)
-
-    @torch.no_grad()
-    def sample_prior(self, hidden, pooled, lens, gen, steps: int, cf_scale: float):
+    def sample_prior(self, hidden, pooled, lens, gens, steps, cf_scales: List[float]):
+        """The diffusion prior of k tasks as ONE batch of 2k padded sequences per step (fused CFG +
+        x0-pred p_sample per task, each with its own generator) -> image embeddings [k, d]."""
+        k = len(gens)
         d = self.cfg.prior.clip_dim
         sched = GaussianDiffusion(steps, schedule="cosine", predict="x0", learned_var=False)
-        x = torch.randn((1, d), generator=gen, dtype=torch.float32)
-        ts = TaskSampler(sched, x.view(d // 4, 4), gen, self.device)
-        xin = torch.empty((d // 4, 4), dtype=self.dtype, device=self.device)
+        tasks = [TaskSampler(sched, torch.randn((1, d), generator=g, dtype=torch.float32).view(d // 4, 4), g,
+                             self.device) for g in gens]
+        xin = torch.empty((2 * k, d), dtype=self.dtype, device=self.device)
 
-        def rows(k, out):     # out = (cond, uncond) prior outputs [1, d]
-            return (None if out is None else out[1].reshape(-1, 4), None if out is None else out[0].reshape(-1, 4),
-                    xin, None)
+        def rows(i, out):     # out = prior outputs [2k, d]: rows 2i / 2i+1 = (cond, uncond)
+            return (None if out is None else out[2 * i + 1].reshape(-1, 4),
+                    None if out is None else out[2 * i].reshape(-1, 4),
+                    xin[2 * i].view(-1, 4), xin[2 * i + 1].view(-1, 4))
 
-        samp = GroupSampler([ts], [float(cf_scale)], xin, rows)
+        samp = GroupSampler(tasks, [float(c) for c in cf_scales], xin, rows)
         samp.write_input(0)
+        layout = self.prior.layout(lens, self.device)
         for i, t in enumerate(sched.timesteps):
             beat()
-            xv = xin.view(1, d)
-            c = self.prior(xv, t, hidden[0:1], pooled[0:1], lens[0]).contiguous()
-            u = self.prior(xv, t, hidden[1:2], pooled[1:2], lens[1]).contiguous()
-            samp.step(i, (c, u))
-        x = ts.x.view(1, d)
-        return (x * self.prior.clip_std.float() + self.prior.clip_mean.float()).to(self.dtype)
+            with ops.plan_batch(2):
+                out = self.prior(xin, t, hidden, pooled, lens, layout).contiguous()
+            samp.step(i, out)
+        std, mean = self._prior_stats()
+        return torch.stack([(ts.x.view(d) * std + mean) for ts in tasks]).to(self.dtype)
 
-    def _group_sampler(self, tasks, h, w):
+    def _group_sampler(self, tasks, h, w, guidance: List[float]):
         """k decoder tasks on one batch-2k GLIDE UNet input: rows 2k / 2k+1 = (cond, uncond); the
         cond row's channels 4..7 are the learned variance of p_sample."""
         zc = self.cfg.unet.in_channels
@@ -159,97 +181,73 @@ class Kandinsky2Pipeline(PipelineBase):
             return (None if out is None else out[2 * k + 1], None if out is None else out[2 * k],
                     xin[2 * k], xin[2 * k + 1])
 
-        samp = GroupSampler(tasks, [float(self.cfg.guidance_scale)] * len(tasks), xin, rows)
+        samp = GroupSampler(tasks, [float(g) for g in guidance], xin, rows)
         samp.write_input(0)
         return samp
 
     @torch.no_grad()
     def __call__(self, prompt: str, width: int = 768, height: int = 768, seed: int = 0,
                  num_inference_steps: Optional[int] = None, guidance_scale: Optional[float] = None,
-                 prior_cf_scale: Optional[float] = None, prior_steps: Optional[int] = None):
-        with self._stream_ctx():
-            return self._run(prompt, width, height, seed, num_inference_steps, guidance_scale, prior_cf_scale,
-                             prior_steps)
-
-    def _run(self, prompt, width, height, seed, num_inference_steps, guidance_scale, prior_cf_scale, prior_steps):
-        cfg = self.cfg
-        steps = num_inference_steps or cfg.num_steps
-        g = cfg.guidance_scale if guidance_scale is None else guidance_scale
-        sync = self._sync
-        t0 = time.perf_counter()
-        gen = torch.Generator(device="cpu").manual_seed(int(seed))
-        hidden, pooled, lens = self.encode_clip(prompt)
-        img_emb = self.sample_prior(hidden, pooled, lens, gen, prior_steps or cfg.prior_steps,
-                                    cfg.prior_cf_scale if prior_cf_scale is None else prior_cf_scale)
-        text_full, text_pooled = self.encode_xlmr(prompt)
-        img_embs = torch.cat([img_emb, self.buffers.zero_img_emb[None].to(self.dtype)])
-        sync()
-        t1 = time.perf_counter()
-        h, w = height // 8, width // 8
-        zc = cfg.unet.in_channels
-        x = torch.randn((1, zc, h, w), generator=gen, dtype=torch.float32).permute(0, 2, 3, 1).contiguous()
-        sched = GaussianDiffusion(steps, schedule="linear", predict="eps", learned_var=True, clamp=cfg.latent_clamp)
-        ts = TaskSampler(sched, x, gen, self.device)
-        samp = self._group_sampler([ts], h, w)
-        samp.g = [float(g)]
-        tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
-        for i, t in enumerate(sched.timesteps):
-            beat()
-            tbuf.fill_(float(t))
-            with ops.plan_batch(2):      # batch-invariant plans: solo == lock-step group bytes
-                out = self._unet(samp.xin, tbuf, text_full, text_pooled, img_embs)
-            samp.step(i, out)            # ONE fused CFG + p_sample launch (learned variance, clamp)
-        sync()
-        t2 = time.perf_counter()
-        img = self.decode(ts.x)
-        sync()
-        t3 = time.perf_counter()
-        self.timings = {"text_prior_s": t1 - t0, "denoise_s": t2 - t1, "movq_s": t3 - t2}
-        return img
+                 prior_cf_scale: Optional[float] = None, prior_steps=None, scheduler: str = "p_sampler"):
+        inp = {"prompt": prompt, "width": width, "height": height, "seed": seed, "scheduler": scheduler}
+        for k, v in (("num_inference_steps", num_inference_steps), ("guidance_scale", guidance_scale),
+                     ("prior_cf_scale", prior_cf_scale), ("prior_steps", prior_steps)):
+            if v is not None:
+                inp[k] = v
+        return self.run_group([inp])[0]
 
     @torch.no_grad()
     def run_group(self, inps: List[dict]) -> List[np.ndarray]:
-        """Lock-step solve of k tasks of one resolution: text encoders, prior, noise, sampler and
-        MoVQ per task; every GLIDE UNet step runs the k (cond, uncond) pairs as one batch-2k
-        launch sequence under batch-invariant plans (bitwise the solo outputs)."""
+        """Lock-step solve of k tasks of one resolution / step count / scheduler (a solo task is
+        k = 1, the same code): both text towers and the prior run as one batch per step, every
+        GLIDE UNet step runs the k (cond, uncond) pairs as one batch-2k launch sequence, all under
+        batch-invariant plans (bitwise the solo outputs); guidance, prior_cf_scale, noise and MoVQ
+        are per task.  Tasks whose prior_steps differ run their priors as separate batches."""
         sizes = {(int(i.get("width", 768)), int(i.get("height", 768))) for i in inps}
         if len(sizes) != 1:
             raise ValueError(f"run_group needs one resolution, got {sorted(sizes)}")
         width, height = sizes.pop()
+        st = [self.settings(i) for i in inps]
+        if len({(s["steps"], s["scheduler"]) for s in st}) != 1:
+            raise ValueError("run_group needs one step count and scheduler")
         cfg = self.cfg
         with self._stream_ctx():
             sync = self._sync
             t0 = time.perf_counter()
-            gens, xs, tf, tp, ie = [], [], [], [], []
+            k = len(inps)
+            gens = [torch.Generator(device="cpu").manual_seed(int(i["seed"])) for i in inps]
+            hidden, pooled, lens, text_full, text_pooled = self.encode_text([i["prompt"] for i in inps])
+            img = [None] * k
+            for ps in sorted({s["prior_steps"] for s in st}):
+                sel = [j for j in range(k) if st[j]["prior_steps"] == ps]
+                r = [r for j in sel for r in (2 * j, 2 * j + 1)]
+                steps = int(ps) if ps.isdigit() else ps
+                emb = self.sample_prior(hidden[r], pooled[r], [lens[x] for x in r], [gens[j] for j in sel], steps,
+                                        [st[j]["prior_cf_scale"] for j in sel])
+                for q, j in enumerate(sel):
+                    img[j] = emb[q]
+            zero = self.buffers.zero_img_emb.to(self.dtype)
+            img_embs = torch.stack([e for j in range(k) for e in (img[j], zero)])
             h, w = height // 8, width // 8
             zc = cfg.unet.in_channels
-            for inp in inps:
-                gen = torch.Generator(device="cpu").manual_seed(int(inp["seed"]))
-                hidden, pooled, lens = self.encode_clip(inp["prompt"])
-                img_emb = self.sample_prior(hidden, pooled, lens, gen, cfg.prior_steps, cfg.prior_cf_scale)
-                text_full, text_pooled = self.encode_xlmr(inp["prompt"])
-                tf.append(text_full)
-                tp.append(text_pooled)
-                ie.append(torch.cat([img_emb, self.buffers.zero_img_emb[None].to(self.dtype)]))
-                x = torch.randn((1, zc, h, w), generator=gen, dtype=torch.float32).permute(0, 2, 3, 1).contiguous()
-                sched = GaussianDiffusion(cfg.num_steps, schedule="linear", predict="eps", learned_var=True,
-                                          clamp=cfg.latent_clamp)
-                xs.append(TaskSampler(sched, x, gen, self.device))    # draws this task's noise now
-                gens.append(gen)
-            text_full, text_pooled, img_embs = torch.cat(tf), torch.cat(tp), torch.cat(ie)
+            tasks = []
+            for j in range(k):
+                x = torch.randn((1, zc, h, w), generator=gens[j], dtype=torch.float32).permute(0, 2, 3, 1).contiguous()
+                sched = k2_decoder_scheduler(st[j]["scheduler"], st[j]["steps"], cfg.latent_clamp)
+                tasks.append(TaskSampler(sched, x, gens[j], self.device))    # draws this task's noise now
             sync()
             t1 = time.perf_counter()
-            samp = self._group_sampler(xs, h, w)
+            samp = self._group_sampler(tasks, h, w, [s["guidance"] for s in st])
             tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
-            for i, t in enumerate(xs[0].sched.timesteps):
+            for i, t in enumerate(tasks[0].sched.timesteps):
                 beat()
                 tbuf.fill_(float(t))
-                with ops.plan_batch(2):
+                with ops.plan_batch(2):      # batch-invariant plans: solo == lock-step group bytes
                     out = self._unet(samp.xin, tbuf, text_full, text_pooled, img_embs)
-                samp.step(i, out)
+                samp.step(i, out)            # ONE fused CFG + sampler launch for the group
             sync()
             t2 = time.perf_counter()
-            imgs = [self.decode(ts.x) for ts in xs]
+            imgs = [self.decode(ts.x) for ts in tasks]
             sync()
             self.timings = {"text_prior_s": t1 - t0, "denoise_s": t2 - t1, "movq_s": time.perf_counter() - t2}
             return imgs
@@ -261,11 +259,11 @@ class Kandinsky2Pipeline(PipelineBase):
         return img.cpu().numpy()
 
     def solve(self, inp: dict):
-        """Template inputs (prompt, width, height, seed) -> ``out-1.png`` solution."""
+        """Template inputs (prompt, width, height, seed + the documented sampling inputs) ->
+        ``out-1.png`` solution."""
         from ..node.solver import solve_files
         t0 = time.perf_counter()
-        img = self(prompt=inp["prompt"], width=int(inp.get("width", 768)), height=int(inp.get("height", 768)),
-                   seed=int(inp["seed"]))
+        img = self.run_group([inp])[0]
         t1 = time.perf_counter()
         png = encode_png(img, 6)
         tm = dict(self.timings)

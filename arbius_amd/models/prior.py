@@ -7,9 +7,12 @@ with learned positional embeddings indexed by the ORIGINAL positions (text
 positions 0..76, then 77..80), causal attention, final LN and an output
 projection of the query token -> predicted x_0 in the normalised CLIP space.
 
-Padding keys of the reference's mask are removed from the sequence instead
-of masked: with causal attention and the pads masked as keys, the real
-tokens' outputs are identical, and the last token is the only one read.
+Padding: the reference masks the padding keys of the text.  Here every sequence
+is laid out as [its n real text tokens | pooled | time | x_t | query | pads] and
+padded to a fixed 81 tokens: under causal attention no real token ever sees a
+trailing pad, so the pads need no mask, and every sequence of a lock-step group
+(any mix of prompt lengths, cond and uncond rows) runs in ONE batch with static
+shapes; the query token n+3 of each row is read.
 """
 from __future__ import annotations
 
@@ -84,16 +87,32 @@ class PriorTransformer(nn.Module):
         self.pos.data.normal_(0, 0.01, generator=gen)
         self.query.data.normal_(0, 0.01, generator=gen)
 
-    def forward(self, x_t, t, text_states, text_pooled, n: int):
-        """x_t [1,d] (normalised), t scalar, text_states [1,77,d], text_pooled [1,d], n real tokens."""
+    def layout(self, ns, device):
+        """Gather map of the padded sequences: token j of row b comes from source slot idx[b, j] of
+        [text 0..76 | pooled, time, x_t, query | zero], and the query sits at n_b + 3."""
+        ctx = self.cfg.text_ctx
+        L = ctx + 4
+        j = torch.arange(L, device=device)[None]
+        n = torch.tensor([int(v) for v in ns], device=device)[:, None]
+        idx = torch.where(j < n, j, torch.where(j < n + 4, ctx + (j - n), torch.full_like(j, L)))
+        return idx, (n[:, 0] + 3)
+
+    def forward(self, x_t, t, text_states, text_pooled, ns, layout=None):
+        """x_t [B,d] (normalised), t scalar, text_states [B,77,d], text_pooled [B,d], ns[b] = real
+        text tokens of row b -> predicted x_0 [B,d].  ``layout``: a cached ``self.layout(ns)``."""
         w = self.cfg.width
+        B = x_t.shape[0]
+        idx, q = layout if layout is not None else self.layout(ns, x_t.device)
         tt = torch.tensor([float(t)], device=x_t.device)
         temb = self.time2(ops.silu(self.time1(timestep_embedding(tt, w).to(x_t.dtype))))
-        seq = torch.cat([self.text_enc_proj(text_states[:, :n]), self.text_emb_proj(text_pooled)[:, None],
-                         temb[:, None], self.img_proj(x_t)[:, None], self.query.to(x_t.dtype)[None, None]], dim=1)
-        ctx = self.cfg.text_ctx
-        pos = torch.cat([self.pos[:n], self.pos[ctx:ctx + 4]], dim=0)
-        h = seq + pos[None].to(seq.dtype)
+        src = torch.cat([self.text_enc_proj(text_states), self.text_emb_proj(text_pooled)[:, None],
+                         temb[:, None].expand(B, 1, w), self.img_proj(x_t)[:, None],
+                         self.query.to(x_t.dtype)[None, None].expand(B, 1, w),
+                         torch.zeros(B, 1, w, dtype=x_t.dtype, device=x_t.device)], dim=1)
+        pos = torch.cat([self.pos, torch.zeros(1, w, dtype=self.pos.dtype, device=self.pos.device)]).to(x_t.dtype)
+        g = idx[:, :, None].expand(B, idx.shape[1], w)
+        h = torch.gather(src, 1, g) + pos[idx]
         for blk in self.blocks:
             h = blk(h)
-        return self.out_proj(self.final_ln(h[:, -1:]))[:, 0]
+        last = h[torch.arange(B, device=h.device), q][:, None]
+        return self.out_proj(self.final_ln(last))[:, 0]

@@ -98,18 +98,31 @@ class Scheduler:
         return [int(v) for v in (np.arange(0, self.steps) * ratio).round()[::-1] + offset]
 
 
+def ldm_uniform_timesteps(n_train: int, steps: int) -> List[int]:
+    """latent-diffusion ``make_ddim_timesteps("uniform")``: range(0, n_train, n_train // steps) + 1,
+    ascending (more than ``steps`` entries when ``steps`` does not divide ``n_train``, as there)."""
+    c = max(1, n_train // steps)
+    ts = [t + 1 for t in range(0, n_train, c)]
+    if ts[-1] >= n_train:
+        raise ValueError(f"{steps} steps over {n_train} training steps: timestep {ts[-1]} out of range")
+    return ts
+
+
 class DDIM(Scheduler):
+    """DDIM (eta 0 by default).  ``timesteps_asc``: an explicit ascending timestep list (the
+    latent-diffusion uniform discretisation of the Kandinsky 2 ``ddim_sampler``); the previous
+    alpha of the first (smallest) timestep is alphas_cumprod[0] in both conventions."""
     name = "DDIM"
 
-    def __init__(self, steps, eta=0.0, **kw):
+    def __init__(self, steps, eta=0.0, timesteps_asc: Optional[List[int]] = None, **kw):
         super().__init__(steps, **kw)
         self.eta = eta
-        self.timesteps = self._leading(1)
+        self.timesteps = list(timesteps_asc[::-1]) if timesteps_asc is not None else self._leading(1)
         self.ratio = self.n_train // steps
 
     def _plan(self, i):
         t = self.timesteps[i]
-        tp = t - self.ratio
+        tp = self.timesteps[i + 1] if i + 1 < len(self.timesteps) else -1
         a_t = float(self.ac[t])
         a_p = float(self.ac[tp]) if tp >= 0 else float(self.ac[0])
         var = (1 - a_p) / (1 - a_t) * (1 - a_t / a_p)
@@ -223,16 +236,20 @@ class DPMSolverMultistep(Scheduler):
 
 
 class PNDM(Scheduler):
-    """PLMS (PNDM with skip_prk_steps, SD default config)."""
+    """PLMS (PNDM with skip_prk_steps, SD default config).  Also the latent-diffusion PLMSSampler of
+    the Kandinsky 2 ``plms_sampler``: its first step (e_t, a DDIM probe to t_next, e = (e_t +
+    e_t_next) / 2 from the original x) and the 2/3/4-step Adams-Bashforth weights are this
+    schedule's counter-0/1 pair and ets history, and its DDIM update equals PNDM's formula (eq. 9)
+    algebraically.  ``timesteps_asc``: an explicit uniform ascending list (stride = ratio)."""
     name = "PNDM"
 
-    def __init__(self, steps, **kw):
+    def __init__(self, steps, timesteps_asc: Optional[List[int]] = None, **kw):
         super().__init__(steps, **kw)
-        base = self._leading(1)[::-1]  # ascending
+        base = list(timesteps_asc) if timesteps_asc is not None else self._leading(1)[::-1]  # ascending
         ts = np.array(base)
         plms = np.concatenate([ts[:-1], ts[-2:-1], ts[-1:]])[::-1]
         self.timesteps = [int(v) for v in plms]
-        self.ratio = self.n_train // steps
+        self.ratio = int(ts[1] - ts[0]) if len(ts) > 1 else self.n_train // steps
 
     def _prev_coefs(self, t, tp):
         a_t = float(self.ac[t])
@@ -266,13 +283,33 @@ class PNDM(Scheduler):
         return out
 
 
-def space_timesteps(n_train: int, steps: int) -> List[int]:
-    """Evenly strided subset of the training timesteps (guided-diffusion
-    ``space_timesteps(n, "K")`` with one section): round(i * (n-1)/(K-1))."""
-    if steps == 1:
-        return [0]
-    stride = (n_train - 1) / (steps - 1)
-    return sorted({int(round(i * stride)) for i in range(steps)})
+def space_timesteps(n_train: int, spec) -> List[int]:
+    """guided-diffusion ``space_timesteps`` (the respacing of Kandinsky 2's ``p_sampler`` and of its
+    prior's ``prior_steps`` string): an int / "K" (one section), "K1,K2,..." (equal sections, the
+    first ``n % len`` one step longer, each strided by accumulating (size-1)/(K-1) and rounding),
+    or "ddimK" (the stride i with len(range(0, n, i)) == K)."""
+    if isinstance(spec, str) and spec.startswith("ddim"):
+        want = int(spec[len("ddim"):])
+        for i in range(1, n_train):
+            if len(range(0, n_train, i)) == want:
+                return list(range(0, n_train, i))
+        raise ValueError(f"cannot create exactly {want} steps with an integer stride")
+    counts = [int(x) for x in str(spec).split(",")] if isinstance(spec, str) else [int(spec)]
+    if not counts or any(c < 1 for c in counts):
+        raise ValueError(f"bad respacing {spec!r}")
+    size_per, extra = divmod(n_train, len(counts))
+    start, out = 0, []
+    for i, count in enumerate(counts):
+        size = size_per + (1 if i < extra else 0)
+        if size < count:
+            raise ValueError(f"cannot divide a section of {size} steps into {count}")
+        frac = 1.0 if count <= 1 else (size - 1) / (count - 1)
+        cur = 0.0
+        for _ in range(count):
+            out.append(start + round(cur))
+            cur += frac
+        start += size
+    return sorted(set(out))
 
 
 class GaussianDiffusion(Scheduler):
@@ -290,7 +327,7 @@ class GaussianDiffusion(Scheduler):
     def __init__(self, steps, n_train=1000, schedule="linear", beta_start=0.0001, beta_end=0.02,
                  predict="eps", learned_var=True, clamp=None):
         full = sd_alphas_cumprod(n_train, beta_start, beta_end, schedule)
-        use = space_timesteps(n_train, steps)
+        use = space_timesteps(n_train, steps)    # int, "K", "K1,K2", "ddimK"
         ac = full[use]
         super().__init__(len(use), n_train, ac)
         ac_prev = np.concatenate([[1.0], ac[:-1]])
@@ -328,6 +365,25 @@ SCHEDULERS = {
     "KLMS": LMSDiscrete,
     "p_sampler": GaussianDiffusion,
 }
+
+
+# Kandinsky 2 template ``scheduler`` enum (docs/src/pages/register-model.mdx:141-185):
+# p_sampler = respaced ancestral p_sample (learned variance, clamp); ddim_sampler / plms_sampler =
+# the latent-diffusion samplers over the FULL 1000-step linear schedule with uniform timesteps,
+# eps = the UNet's first 4 channels, no clamp.  The template lists "pims_sampler": taken as PLMS.
+K2_SCHEDULERS = ("p_sampler", "ddim_sampler", "pims_sampler", "plms_sampler")
+
+
+def k2_decoder_scheduler(name: str, steps: int, clamp: float = 2.0) -> Scheduler:
+    if name == "p_sampler":
+        return GaussianDiffusion(steps, schedule="linear", predict="eps", learned_var=True, clamp=clamp)
+    ac = sd_alphas_cumprod(1000, 0.0001, 0.02, "linear")
+    ts = ldm_uniform_timesteps(1000, steps)
+    if name == "ddim_sampler":
+        return DDIM(steps, timesteps_asc=ts, alphas_cumprod=ac)
+    if name in ("pims_sampler", "plms_sampler"):
+        return PNDM(steps, timesteps_asc=ts, alphas_cumprod=ac)
+    raise ValueError(f"unknown Kandinsky 2 scheduler {name!r}; choices {K2_SCHEDULERS}")
 
 
 def make_scheduler(name: str, steps: int) -> Scheduler:

@@ -89,11 +89,24 @@ class XLMRLayer(nn.Module):
         self.fc2 = Linear(cfg.mlp, cfg.width)
         self.ln2 = LayerNorm(cfg.width, cfg.eps)
 
-    def forward(self, x, n: int):
+    def forward(self, x, ns: List[int]):
+        """x [B, 77, C]; ns[b] = real tokens of sequence b (its keys / values are sliced to them;
+        sequences of equal length share one attention launch)."""
         B, N, C = x.shape
         H = self.heads
         qkv = self.qkv(x).view(B, N, 3, H, C // H)
-        o = ops.attention(qkv[:, :, 0], qkv[:, :n, 1], qkv[:, :n, 2])
+        if len(set(ns)) == 1:
+            o = ops.attention(qkv[:, :, 0], qkv[:, :ns[0], 1], qkv[:, :ns[0], 2])
+        else:
+            o = torch.empty(B, N, H, C // H, dtype=x.dtype, device=x.device)
+            for n in sorted(set(ns)):
+                rows = [b for b in range(B) if ns[b] == n]
+                i0, i1 = rows[0], rows[-1] + 1
+                if rows == list(range(i0, i1)):          # contiguous run: views, no gather
+                    o[i0:i1] = ops.attention(qkv[i0:i1, :, 0], qkv[i0:i1, :n, 1], qkv[i0:i1, :n, 2])
+                else:
+                    for b in rows:
+                        o[b:b + 1] = ops.attention(qkv[b:b + 1, :, 0], qkv[b:b + 1, :n, 1], qkv[b:b + 1, :n, 2])
         x = self.ln1(self.out(o.reshape(B, N, C), residual=x))
         h = torch.nn.functional.gelu(self.fc1(x))
         return self.ln2(self.fc2(h, residual=x))
@@ -111,14 +124,18 @@ class MCLIPText(nn.Module):
         self.layers = nn.ModuleList([XLMRLayer(cfg) for _ in range(cfg.layers)])
         self.proj = Linear(cfg.width, cfg.proj_dim)
 
-    def forward(self, ids: torch.Tensor, n: int):
-        """One sequence: ids [1, 77], n = real length -> (full [1,77,W], pooled [1,proj])."""
-        L = ids.shape[1]
-        pos = torch.arange(L, device=ids.device)
-        pos = torch.where(pos < n, pos + 2, torch.full_like(pos, 1))   # pad positions use padding_idx
-        x = self.tok(ids) + self.pos(pos)[None] + self.tok_type.weight[0]
+    def forward(self, ids: torch.Tensor, ns):
+        """ids [B, 77], ns = real length of each sequence (an int: every row) -> (full [B,77,W],
+        pooled [B,proj]).  Row-wise arithmetic only (GEMM plans under ``ops.plan_batch``), so a
+        sequence's outputs do not depend on the other rows of the batch."""
+        B, L = ids.shape
+        ns = [int(ns)] * B if isinstance(ns, int) else [int(n) for n in ns]
+        pos = torch.arange(L, device=ids.device)[None].expand(B, L)
+        lim = torch.tensor(ns, device=ids.device)[:, None]
+        pos = torch.where(pos < lim, pos + 2, torch.ones_like(pos))   # pad positions use padding_idx
+        x = self.tok(ids) + self.pos(pos) + self.tok_type.weight[0]
         x = self.ln(x)
         for layer in self.layers:
-            x = layer(x, n)
-        pooled = x[:, :n].float().mean(dim=1).to(x.dtype)
+            x = layer(x, ns)
+        pooled = torch.stack([x[b, :n].float().mean(dim=0) for b, n in enumerate(ns)]).to(x.dtype)
         return x, self.proj(pooled)

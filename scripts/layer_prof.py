@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from arbius_amd.ops import _lib  # noqa: E402
 
 REC = []
+SLEEP_CYCLES = 400_000
 WRAPPED = ("conv2d_nhwc", "gemm", "gemm_geglu", "group_norm_table", "norm_table_apply", "layer_norm",
            "flash_attention", "group_norm_nhwc", "group_norm_mod_nhwc", "softmax_rows", "sampler_step", "silu",
            "geglu", "temporal_attention")
@@ -48,6 +49,9 @@ def wrap():
 
         def g(*a, __f=f, __n=name, **k):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            # keep the GPU busy while the host enqueues (start event, op, end event): the events then
+            # bracket GPU execution only, not the host's launch gaps of an eager run
+            torch.cuda._sleep(SLEEP_CYCLES)
             s.record()
             r = __f(*a, **k)
             e.record()

@@ -6,6 +6,7 @@ import json
 import math
 
 import numpy as np
+import pytest
 import torch
 
 from arbius_amd import ops
@@ -95,7 +96,7 @@ def test_prior_pad_removal_equals_causal_plus_padding_mask():
     d, n = cfg.clip_dim, 6
     torch.manual_seed(0)
     xt, states, pooled = torch.randn(1, d), torch.randn(1, 77, d), torch.randn(1, d)
-    got = p(xt, 500, states, pooled, n)
+    got = p(xt, 500, states, pooled, [n])
     # reference: full 81-token sequence, causal mask AND text-padding mask
     from arbius_amd.models.layers import timestep_embedding
     w = cfg.width
@@ -114,6 +115,45 @@ def test_prior_pad_removal_equals_causal_plus_padding_mask():
         h = blk.fc2(torch.nn.functional.gelu(blk.fc1(blk.ln2(h))), residual=h)
     ref = p.out_proj(p.final_ln(h[:, -1]))
     assert torch.allclose(got, ref, atol=1e-5)
+
+
+def test_prior_batched_rows_with_different_lengths_equal_solo():
+    """Rows padded to 81 tokens with trailing pads: a batch of sequences of different prompt lengths
+    gives each row its solo result (causal attention never reaches a trailing pad)."""
+    cfg = PriorConfig.tiny()
+    p = init_weights(torch.nn.ModuleDict({"p": PriorTransformer(cfg)}), 3)["p"].eval()
+    d = cfg.clip_dim
+    torch.manual_seed(1)
+    xt, states, pooled = torch.randn(3, d), torch.randn(3, 77, d), torch.randn(3, d)
+    ns = [4, 11, 77]
+    got = p(xt, 250, states, pooled, ns)
+    for b, n in enumerate(ns):
+        solo = p(xt[b:b + 1], 250, states[b:b + 1], pooled[b:b + 1], [n])
+        assert torch.allclose(got[b:b + 1], solo, atol=1e-5)
+
+
+def test_k2_template_surface_and_group_on_cpu():
+    """The documented Kandinsky 2 inputs (num_inference_steps, guidance_scale, scheduler in
+    {p_sampler, ddim_sampler, pims_sampler}, prior_cf_scale, prior_steps) change the output; a
+    lock-step group with mixed guidance / prior settings matches the solo solves."""
+    pipe = Kandinsky2Pipeline(Kandinsky2Config.tiny(), device="cpu")
+    base = {"prompt": "arbius test cat", "width": 64, "height": 64, "seed": 7, "num_inference_steps": 4}
+    outs = {}
+    for key, val in (("scheduler", "p_sampler"), ("scheduler", "ddim_sampler"), ("scheduler", "pims_sampler"),
+                     ("guidance_scale", 9.0), ("prior_cf_scale", 1), ("prior_steps", "3")):
+        outs[(key, val)] = pipe.run_group([dict(base, **{key: val})])[0]
+    ref = outs[("scheduler", "p_sampler")]
+    for k, v in outs.items():
+        if k != ("scheduler", "p_sampler"):
+            assert not (v == ref).all(), k
+    with pytest.raises(ValueError):
+        pipe.run_group([dict(base, scheduler="euler")])
+    inps = [dict(base, prompt=f"cat {i}", seed=20 + i, guidance_scale=4.0 + i, prior_cf_scale=1 + i,
+                 prior_steps="3" if i == 1 else "5", scheduler="ddim_sampler") for i in range(3)]
+    grp = pipe.run_group(inps)
+    for inp, g in zip(inps, grp):
+        solo = pipe.run_group([inp])[0]
+        assert np.abs(solo.astype(int) - g.astype(int)).max() <= 1
 
 
 def test_kandinsky_tiny_deterministic():
