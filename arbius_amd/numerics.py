@@ -85,6 +85,49 @@ def golden_cases(device) -> List[Tuple[str, Callable[[], object]]]:
             raise AssertionError(f"lock-step/stream CIDs differ from solo: {grouped} vs {solo}")
         return grouped
 
+    def sd_group(k):
+        """one stream, a lock-step group of k (k = 2, 3: the batch-4 / batch-6 tile-family entries of
+        csrc/conv_family.inc) - every CID must equal its solo CID (also pinned by name)."""
+        def f():
+            base = pipe("anythingv3")
+            grouped = [s.cid for s in solve_images(base, SD_GROUP[:k])]
+            solo = [solve_image(base, i).cid for i in SD_GROUP[:k]]
+            if grouped != solo:
+                raise AssertionError(f"lock-step group of {k} differs from solo: {grouped} vs {solo}")
+            return grouped
+        return f
+
+    def sd_template_default():
+        """anythingv3's template defaults (templates/anythingv3.json: 768^2, 20 steps, guidance 12,
+        DPMSolverMultistep) with the template's default negative prompt."""
+        from .node.models import hydrate_input, load_template
+        inp, err, msg = hydrate_input({"prompt": "arbius test cat"}, load_template("anythingv3"))
+        if err:
+            raise AssertionError(msg)
+        inp["seed"] = 1337
+        return solve_image(pipe("anythingv3"), inp).cid
+
+    def k2_group2():
+        """Kandinsky2 768^2, a lock-step group of 2 with different guidance / prior settings: batched
+        text towers + prior + batch-4 GLIDE UNet launches; CIDs equal the solo solves."""
+        from .node.solver import solve_images as group_solve
+        p = pipe("kandinsky2")
+        inps = [{"prompt": f"arbius test cat {j}", "width": 768, "height": 768, "seed": 4000 + j,
+                 "num_inference_steps": 2, "prior_steps": "2", "guidance_scale": 4.0 + j, "prior_cf_scale": 4 - j}
+                for j in range(2)]
+        grouped = [s.cid for s in group_solve(p, inps)]
+        solo = [p.solve(i).cid for i in inps]
+        if grouped != solo:
+            raise AssertionError(f"K2 lock-step group differs from solo: {grouped} vs {solo}")
+        return grouped
+
+    def k2_sampler(name):
+        def f():
+            return pipe("kandinsky2").solve({"prompt": "arbius test cat", "width": 768, "height": 768, "seed": 1337,
+                                             "num_inference_steps": 3, "prior_steps": "2",
+                                             "scheduler": name}).cid
+        return f
+
     def sd_sched(s):
         return lambda: solve_image(pipe("anythingv3"), _sd_inp("arbius test cat", 42, 256, 3, s, 7.0)).cid
 
@@ -121,6 +164,33 @@ def golden_cases(device) -> List[Tuple[str, Callable[[], object]]]:
 
     cases = [("sd15_512_dpm4_solo", sd_solo), ("sd15_512_dpm4_2streams_group4", sd_group_streams)]
     cases += [(f"sd15_256_{s}_3", sd_sched(s)) for s in SD_SCHEDULERS]
+    cases += [("sd15_512_dpm4_group2", sd_group(2)), ("sd15_512_dpm4_group3", sd_group(3)),
+              ("sd15_768_dpm20_template_default", sd_template_default)]
+    cases += [("kandinsky2_768_group2", k2_group2)]
+    cases += [(f"kandinsky2_768_{n}_3", k2_sampler(n)) for n in ("ddim_sampler", "pims_sampler")]
     cases += [("kandinsky2_768_2+2", k2), ("zeroscopev2xl_256x256x8_2", video("zeroscopev2xl")),
               ("damo_256x256x8_2", video("damo")), ("rvm_320x180x8", rvm)]
     return cases
+
+
+def selftest_cids(device, names=("kandinsky2", "anythingv3")) -> Dict[str, str]:
+    """The boot self-test tasks of ``config/selftest.json`` solved exactly as ``Miner.self_test``
+    does (template hydration + the task's seed + ``solve_task``) -> {model: CID}."""
+    import json
+    from pathlib import Path
+
+    from .models.registry import build_pipeline
+    from .node.models import Model, hydrate_input, load_template
+    from .node.solver import solve_task
+    table = json.loads((Path(__file__).resolve().parent / "config" / "selftest.json").read_text())
+    out = {}
+    for name in names:
+        tpl = load_template(name)
+        inp, err, msg = hydrate_input(dict(table[name]["input"]), tpl)
+        if err:
+            raise ValueError(f"self test input of {name}: {msg}")
+        inp["seed"] = table[name]["input"]["seed"]
+        pipe = build_pipeline(name, device=device)
+        out[name] = solve_task(Model("0x0", name, tpl), pipe, inp).cid
+        del pipe
+    return out

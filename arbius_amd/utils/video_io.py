@@ -43,24 +43,35 @@ class VideoSourceError(ValueError):
     """``input_video`` names a source this node refuses to read (local file, private address...)."""
 
 
-def _public_host(host: str) -> bool:
-    """True when every address ``host`` resolves to is public unicast."""
+def _is_public(addr: str) -> bool:
     import ipaddress
+    ip = ipaddress.ip_address(addr.split("%")[0])
+    if getattr(ip, "ipv4_mapped", None):
+        ip = ip.ipv4_mapped
+    return not (ip.is_private or ip.is_loopback or ip.is_link_local or ip.is_multicast or ip.is_reserved
+                or ip.is_unspecified or not ip.is_global)
+
+
+def resolve_public(host: str, port: int = 443) -> List[str]:
+    """Every address ``host`` resolves to, or [] unless ALL of them are public unicast."""
     import socket
     try:
-        infos = socket.getaddrinfo(host, 443, proto=socket.IPPROTO_TCP)
+        infos = socket.getaddrinfo(host, port, proto=socket.IPPROTO_TCP)
     except OSError:
-        return False
-    if not infos:
-        return False
+        return []
+    addrs = []
     for info in infos:
-        ip = ipaddress.ip_address(info[4][0].split("%")[0])
-        if getattr(ip, "ipv4_mapped", None):
-            ip = ip.ipv4_mapped
-        if (ip.is_private or ip.is_loopback or ip.is_link_local or ip.is_multicast or ip.is_reserved
-                or ip.is_unspecified or not ip.is_global):
-            return False
-    return True
+        a = info[4][0]
+        if not _is_public(a):
+            return []
+        if a not in addrs:
+            addrs.append(a)
+    return addrs
+
+
+def _public_host(host: str) -> bool:
+    """True when every address ``host`` resolves to is public unicast."""
+    return bool(resolve_public(host))
 
 
 def check_source(ref: str) -> str:
@@ -85,37 +96,106 @@ def check_source(ref: str) -> str:
     return "https"
 
 
+def _read_capped(r) -> bytes:
+    buf = bytearray()
+    for chunk in r.iter_bytes():
+        buf += chunk
+        if len(buf) > MAX_VIDEO_BYTES:
+            raise VideoSourceError("input video exceeds MAX_VIDEO_BYTES")
+    return bytes(buf)
+
+
+def pinned_request(url: str):
+    """(url to connect to, Host header, TLS server name): the host is resolved ONCE, every address
+    must be public, and the connection goes to that validated address - no second resolution by the
+    HTTP client, so DNS rebinding between the check and the connect cannot reach a private address.
+    TLS SNI and certificate verification still use the hostname."""
+    from urllib.parse import urlsplit, urlunsplit
+    u = urlsplit(url)
+    port = u.port or 443
+    addrs = resolve_public(u.hostname, port)
+    if not addrs:
+        raise VideoSourceError(f"host {u.hostname} resolves to a non-public address")
+    ip = addrs[0]
+    netloc = (f"[{ip}]" if ":" in ip else ip) + (f":{u.port}" if u.port else "")
+    host_hdr = u.hostname + (f":{u.port}" if u.port else "")
+    return urlunsplit((u.scheme, netloc, u.path or "/", u.query, "")), host_hdr, u.hostname
+
+
 def _get(url: str, max_redirects: int = 3) -> bytes:
     import httpx
     for _ in range(max_redirects + 1):
-        with httpx.stream("GET", url, timeout=120.0, follow_redirects=False) as r:
-            if r.status_code in (301, 302, 303, 307, 308):
-                nxt = str(r.url.join(r.headers.get("location", "")))
-                check_source(nxt)                  # every hop must pass the same policy
-                url = nxt
-                continue
-            r.raise_for_status()
-            buf = bytearray()
-            for chunk in r.iter_bytes():
-                buf += chunk
-                if len(buf) > MAX_VIDEO_BYTES:
-                    raise VideoSourceError("input video exceeds MAX_VIDEO_BYTES")
-            return bytes(buf)
+        target, host_hdr, sni = pinned_request(url)
+        with httpx.Client(timeout=120.0, follow_redirects=False) as cl:
+            req = cl.build_request("GET", target, headers={"Host": host_hdr}, extensions={"sni_hostname": sni})
+            r = cl.send(req, stream=True)
+            try:
+                if r.status_code in (301, 302, 303, 307, 308):
+                    from urllib.parse import urljoin
+                    nxt = urljoin(url, r.headers.get("location", ""))
+                    check_source(nxt)              # every hop must pass the same policy
+                    url = nxt
+                    continue
+                r.raise_for_status()
+                return _read_capped(r)
+            finally:
+                r.close()
     raise VideoSourceError("too many redirects")
+
+
+# Fetched inputs are cached on disk between hydration (``probe_video``) and the solve
+# (``load_video``, possibly in a GPU worker process): one download per task input.
+_CACHE_DIR = os.environ.get("ARBIUS_VIDEO_CACHE") or os.path.join(tempfile.gettempdir(), "arbius_video_cache")
+_CACHE_KEEP = 16
+
+
+def _cache_path(ref: str) -> str:
+    import hashlib
+    return os.path.join(_CACHE_DIR, hashlib.sha256(ref.encode()).hexdigest())
+
+
+def _cache_get(ref: str):
+    p = _cache_path(ref)
+    try:
+        with open(p, "rb") as f:
+            data = f.read(MAX_VIDEO_BYTES + 1)
+        os.utime(p)
+        return data if len(data) <= MAX_VIDEO_BYTES else None
+    except OSError:
+        return None
+
+
+def _cache_put(ref: str, data: bytes):
+    try:
+        os.makedirs(_CACHE_DIR, exist_ok=True)
+        tmp = _cache_path(ref) + f".{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, _cache_path(ref))
+        ents = sorted((os.path.getmtime(os.path.join(_CACHE_DIR, e)), e) for e in os.listdir(_CACHE_DIR)
+                      if not e.endswith(".tmp"))
+        for _, e in ents[:-_CACHE_KEEP]:
+            os.unlink(os.path.join(_CACHE_DIR, e))
+    except OSError:
+        pass
 
 
 def fetch(ref: str) -> bytes:
     kind = check_source(ref)
     if kind == "data":
         data = base64.b64decode(ref.split(",", 1)[1])
-    elif kind == "https":
-        data = _get(ref)
     else:
-        import httpx
-        gw = os.environ.get("ARBIUS_IPFS_GATEWAY", "http://127.0.0.1:8080")   # operator-configured
-        r = httpx.get(f"{gw.rstrip('/')}/ipfs/{ref.replace('ipfs://', '')}", timeout=120.0)
-        r.raise_for_status()
-        data = r.content
+        data = _cache_get(ref)
+        if data is None:
+            if kind == "https":
+                data = _get(ref)
+            else:
+                import httpx
+                gw = os.environ.get("ARBIUS_IPFS_GATEWAY", "http://127.0.0.1:8080")   # operator-configured
+                with httpx.stream("GET", f"{gw.rstrip('/')}/ipfs/{ref.replace('ipfs://', '')}", timeout=120.0) as r:
+                    r.raise_for_status()
+                    data = _read_capped(r)                 # capped while streaming, never read whole first
+            _cache_put(ref, data)
     if len(data) > MAX_VIDEO_BYTES:
         raise VideoSourceError("input video exceeds MAX_VIDEO_BYTES")
     return data

@@ -33,22 +33,9 @@ def main():
         out["seconds"][name] = round(time.perf_counter() - t0, 2)
         print(name, out["cases"][name], flush=True)
     if a.selftest:
-        from arbius_amd.models.registry import build_pipeline
-        from arbius_amd.node.models import hydrate_input, load_template
-        from arbius_amd.node.solver import solve_task
-        from arbius_amd.node.models import Model
-        table = json.load(open(os.path.join(os.path.dirname(__file__), "..", "arbius_amd", "config", "selftest.json")))
-        out["selftest"] = {}
-        for name in ("kandinsky2", "anythingv3"):
-            tpl = load_template(name)
-            inp, err, msg = hydrate_input(dict(table[name]["input"]), tpl)
-            assert not err, msg
-            inp["seed"] = table[name]["input"]["seed"]
-            pipe = build_pipeline(name, device=dev)
-            out["selftest"][name] = solve_task(Model("0x0", name, tpl), pipe, inp).cid
-            print("selftest", name, out["selftest"][name], flush=True)
-            del pipe
-            torch.cuda.empty_cache()
+        from arbius_amd.numerics import selftest_cids
+        out["selftest"] = selftest_cids(dev)
+        print("selftest", out["selftest"], flush=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
 

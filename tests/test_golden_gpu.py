@@ -34,3 +34,19 @@ def test_golden_cid(cases, name):
     assert got == GOLDEN["cases"][name], (
         f"{name}: output bytes changed under NUMERICS_VERSION {NUMERICS_VERSION} "
         f"(got {got}, pinned {GOLDEN['cases'][name]}): bump the version and re-pin")
+
+
+def test_boot_selftest_table_matches_this_gpu(cuda):
+    """Every config/selftest.json task recomputed on this GPU equals its pinned gfx950 value (the
+    node refuses to start on a mismatch, miner/src/index.ts:981-1001)."""
+    import torch
+    from pathlib import Path
+
+    from arbius_amd.node.pool import hardware_id
+    from arbius_amd.numerics import selftest_cids
+    table = json.loads((Path(__file__).resolve().parents[1] / "arbius_amd" / "config" / "selftest.json").read_text())
+    assert table["numerics_version"] == NUMERICS_VERSION, "re-pin config/selftest.json (scripts/pin_goldens.py)"
+    key = f"{hardware_id(torch.device('cuda', 0))}/random-init-seed0"
+    got = selftest_cids(cuda)
+    for name, cid in got.items():
+        assert table[name]["expected"].get(key) == cid, f"self test {name}: got {cid}, pinned {table[name]['expected']}"

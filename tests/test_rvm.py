@@ -132,3 +132,62 @@ def test_rvm_forks_concurrent_bitwise_equal_solo():
     for t in ts:
         t.join()
     assert all((a == b).all() for a, b in zip(out, solo))
+
+
+def test_https_fetch_connects_to_the_validated_address(monkeypatch):
+    """DNS rebinding: the host is resolved once, every address must be public, and the request goes
+    to that address (Host header + TLS SNI carry the name) - the client never re-resolves."""
+    import socket
+
+    from arbius_amd.utils import video_io as V
+    calls = []
+
+    def fake(host, port, *a, **k):
+        calls.append(host)
+        return [(socket.AF_INET, socket.SOCK_STREAM, 6, "", ("93.184.216.34", port))]
+    monkeypatch.setattr(socket, "getaddrinfo", fake)
+    target, host, sni = V.pinned_request("https://videos.example.com:8443/a/clip.mp4?x=1")
+    assert target == "https://93.184.216.34:8443/a/clip.mp4?x=1"
+    assert host == "videos.example.com:8443" and sni == "videos.example.com" and calls == ["videos.example.com"]
+
+    def mixed(host, port, *a, **k):
+        return [(socket.AF_INET, socket.SOCK_STREAM, 6, "", ("93.184.216.34", port)),
+                (socket.AF_INET, socket.SOCK_STREAM, 6, "", ("10.0.0.5", port))]
+    monkeypatch.setattr(socket, "getaddrinfo", mixed)
+    with pytest.raises(V.VideoSourceError):
+        V.pinned_request("https://videos.example.com/a.mp4")
+
+
+def test_gateway_fetch_is_capped_while_streaming_and_cached(monkeypatch, tmp_path):
+    import http.server
+    import threading
+
+    from arbius_amd.utils import video_io as V
+    hits = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            hits.append(self.path)
+            body = b"\0" * (4096 if "big" not in self.path else 1 << 20)
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    try:
+        monkeypatch.setenv("ARBIUS_IPFS_GATEWAY", f"http://127.0.0.1:{srv.server_address[1]}")
+        monkeypatch.setattr(V, "_CACHE_DIR", str(tmp_path / "cache"))
+        monkeypatch.setattr(V, "MAX_VIDEO_BYTES", 64 << 10)
+        cid = "QmYwAPJzv5CZsnA625s3Xf2nemtYgPpHdWEz79ojWnPbdG"
+        assert len(V.fetch(cid)) == 4096
+        assert len(V.fetch("ipfs://" + cid)) == 4096 and len(V.fetch(cid)) == 4096
+        assert len(hits) == 2            # "ipfs://X" and "X" are two refs; the repeat came from the cache
+        with pytest.raises(V.VideoSourceError):
+            V.fetch(cid + "/big")
+    finally:
+        srv.shutdown()
