@@ -102,6 +102,14 @@ class LayerNorm(nn.Module):
     def forward(self, x):
         return ops.layer_norm(x, self.weight, self.bias, self.eps)
 
+    def linear(self, x, lin: "Linear", residual=None):
+        """lin(self(x)) with this LayerNorm folded into the GEMM (ops.ln_linear)."""
+        return ops.ln_linear(x, self.weight, self.bias, self.eps, lin.weight, lin.bias, residual=residual)
+
+    def linear_geglu(self, x, lin: "Linear"):
+        """GEGLU projection of self(x) with this LayerNorm folded in (ops.ln_linear_geglu)."""
+        return ops.ln_linear_geglu(x, self.weight, self.bias, self.eps, lin.weight, lin.bias)
+
 
 class Embedding(nn.Module):
     def __init__(self, n, dim):

@@ -57,10 +57,10 @@ class PriorBlock(nn.Module):
     def forward(self, x):
         B, N, C = x.shape
         H = self.heads
-        qkv = self.qkv(self.ln1(x)).view(B, N, 3, H, C // H)
+        qkv = self.ln1.linear(x, self.qkv).view(B, N, 3, H, C // H)   # LayerNorm folded into QKV
         o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
         x = self.out(o.reshape(B, N, C), residual=x)
-        return self.fc2(torch.nn.functional.gelu(self.fc1(self.ln2(x))), residual=x)
+        return self.fc2(torch.nn.functional.gelu(self.ln2.linear(x, self.fc1)), residual=x)
 
 
 class PriorTransformer(nn.Module):

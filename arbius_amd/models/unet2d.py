@@ -59,10 +59,11 @@ class SelfAttention(nn.Module):
         self.to_qkv = Linear(dim, 3 * dim, bias=False)
         self.to_out = Linear(dim, dim)
 
-    def forward(self, x, residual):
+    def forward(self, x, residual, ln=None):
+        """``ln``: the block's LayerNorm of x, folded into the QKV GEMM (x is then its input)."""
         B, N, C = x.shape
         H = self.heads
-        qkv = self.to_qkv(x).view(B, N, 3, H, C // H)
+        qkv = (ln.linear(x, self.to_qkv) if ln is not None else self.to_qkv(x)).view(B, N, 3, H, C // H)
         o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])
         return self.to_out(o.reshape(B, N, C), residual=residual)
 
@@ -100,10 +101,10 @@ class CrossAttention(nn.Module):
     def context_kv(self, ctx):
         return self.to_kv(ctx)
 
-    def forward(self, x, ctx, residual):
+    def forward(self, x, ctx, residual, ln=None):
         B, N, C = x.shape
         H = self.heads
-        q = self.to_q(x).view(B, N, H, C // H)
+        q = (ln.linear(x, self.to_q) if ln is not None else self.to_q(x)).view(B, N, H, C // H)
         mode = getattr(_KV, "mode", None)
         if mode == "consume":
             kv = _KV.table[id(self)]
@@ -124,9 +125,11 @@ class FeedForward(nn.Module):
         self.proj = Linear(dim, 2 * mult * dim)
         self.out = Linear(mult * dim, dim)
 
-    def forward(self, x, residual):
-        # GEGLU fused into the projection GEMM's epilogue on the GPU (ops.linear_geglu)
-        return self.out(ops.linear_geglu(x, self.proj.weight, self.proj.bias), residual=residual)
+    def forward(self, x, residual, ln=None):
+        # GEGLU fused into the projection GEMM's epilogue on the GPU (ops.linear_geglu); ``ln``: the
+        # block's LayerNorm of x folded into the same GEMM
+        h = ln.linear_geglu(x, self.proj) if ln is not None else ops.linear_geglu(x, self.proj.weight, self.proj.bias)
+        return self.out(h, residual=residual)
 
 
 class BasicTransformerBlock(nn.Module):
@@ -140,9 +143,10 @@ class BasicTransformerBlock(nn.Module):
         self.ff = FeedForward(dim)
 
     def forward(self, h, ctx):
-        h = self.attn1(self.norm1(h), residual=h)
-        h = self.attn2(self.norm2(h), ctx, residual=h)
-        h = self.ff(self.norm3(h), residual=h)
+        # pre-LN: each LayerNorm feeds only its GEMM, so it is folded into that GEMM (ops.ln_linear)
+        h = self.attn1(h, residual=h, ln=self.norm1)
+        h = self.attn2(h, ctx, residual=h, ln=self.norm2)
+        h = self.ff(h, residual=h, ln=self.norm3)
         return h
 
 

@@ -92,8 +92,8 @@ class TemporalTransformer(nn.Module):
         self.ff = FeedForward(inner)
         self.proj_out = Linear(inner, c)
 
-    def _attn(self, h, qkv_l, out_l, B, F, P):
-        qkv = qkv_l(h).view(B, F, P, 3, self.heads, self.hd)
+    def _attn(self, h, ln, qkv_l, out_l, B, F, P):
+        qkv = ln.linear(h, qkv_l).view(B, F, P, 3, self.heads, self.hd)     # LayerNorm folded into QKV
         o = ops.temporal_attention(qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2])
         return o.view(B * F * P, -1)
 
@@ -102,9 +102,9 @@ class TemporalTransformer(nn.Module):
         B, P = BF // frames, H * W
         h = self.proj_in.forward_norm(x.view(B, frames * P, C), self.norm.table(x.view(B, frames * P, C)))
         h = h.view(BF * P, -1)
-        h = self.out1(self._attn(self.norm1(h), self.qkv1, self.out1, B, frames, P), residual=h)
-        h = self.out2(self._attn(self.norm2(h), self.qkv2, self.out2, B, frames, P), residual=h)
-        h = self.ff(self.norm3(h), residual=h)
+        h = self.out1(self._attn(h, self.norm1, self.qkv1, self.out1, B, frames, P), residual=h)
+        h = self.out2(self._attn(h, self.norm2, self.qkv2, self.out2, B, frames, P), residual=h)
+        h = self.ff(h, residual=h, ln=self.norm3)
         return self.proj_out(h, residual=x.view(BF * P, C)).view(BF, H, W, C)
 
 

@@ -133,6 +133,60 @@ def linear_geglu(x, w, b=None):
     return geglu(linear(x, w, b))
 
 
+_LN_FOLD = {}   # (id(ln weight), id(linear weight), geglu) -> folded tensors (weakly keyed, version-stamped)
+
+
+def ln_fold(gamma, beta, w, b, geglu=False):
+    """Fold LayerNorm(gamma, beta) into the following linear (w [N, K], b [N] or None):
+    LN(x) w^T + b = rstd (x W'^T - mean wsum) + b' with W' = bf16(w * gamma) (per column k),
+    wsum[n] = sum_k W'[n, k] (fp32, of the rounded W' - so the mean term cancels exactly as the
+    GEMM sees it) and b' = bf16(b + w beta).  ``geglu``: rows interleaved for the GEGLU epilogue.
+    Cached per live (gamma, w) pair; recomputed when either changes."""
+    key = (id(gamma), id(w), bool(geglu))
+    stamp = (gamma.data_ptr(), gamma._version, beta.data_ptr(), beta._version, w.data_ptr(), w._version,
+             None if b is None else (b.data_ptr(), b._version))
+    ent = _LN_FOLD.get(key)
+    if ent is not None and ent[0]() is gamma and ent[1]() is w and ent[2] == stamp:
+        return ent[3]
+    with torch.no_grad():
+        wf = (w.float() * gamma.float()[None, :]).to(w.dtype)
+        wsum = wf.double().sum(dim=1).float()
+        bf = w.double() @ beta.double()
+        if b is not None:
+            bf = bf + b.double()
+        bf = bf.to(w.dtype)
+        if geglu:
+            wf, bf = _lib.interleave_geglu(wf), _lib.interleave_geglu(bf)
+            wsum = _lib.interleave_geglu(wsum)
+        out = (wf.contiguous(), bf.contiguous(), wsum.contiguous())
+    _LN_FOLD[key] = (weakref.ref(gamma), weakref.ref(w), stamp, out)
+    return out
+
+
+def _ln_fold_ok(x, w, geglu):
+    return (_hip(x) and x.dtype == torch.bfloat16 and _gemm_ok(x.shape[-1], w.shape[0]) and x.shape[-1] <= 2048
+            and (not geglu or w.shape[0] % 16 == 0) and "lnfold" not in _EXP_SKIP)
+
+
+def ln_linear(x, gamma, beta, eps, w, b=None, residual=None):
+    """linear(LayerNorm(x)) - on the GPU the LayerNorm is folded into the GEMM's epilogue (one
+    row-stats pass over x, no normalised tensor in HBM)."""
+    if _ln_fold_ok(x, w, False):
+        wf, bf, wsum = ln_fold(gamma, beta, w, b)
+        rs = _lib.row_stats(x, eps)
+        return _lib.gemm_ln(x, wf, bf, wsum, rs, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
+    return linear(layer_norm(x, gamma, beta, eps), w, b, residual)
+
+
+def ln_linear_geglu(x, gamma, beta, eps, w, b=None):
+    """linear_geglu(LayerNorm(x)) with the LayerNorm folded in (see ``ln_linear``)."""
+    if _GEGLU_FUSED and _ln_fold_ok(x, w, True):
+        wf, bf, wsum = ln_fold(gamma, beta, w, b, geglu=True)
+        rs = _lib.row_stats(x, eps)
+        return _lib.gemm_ln(x, wf, bf, wsum, rs, geglu=True, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
+    return linear_geglu(layer_norm(x, gamma, beta, eps), w, b)
+
+
 class CatPair:
     """The channel concat [a | b] of two channels-last tensors, NOT materialised: the UNet up-path
     skip connection.  Its consumers (GroupNorm statistics, the GroupNorm table-apply pass and the

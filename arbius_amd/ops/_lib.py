@@ -51,6 +51,8 @@ _SIGS = {
     "arb_norm_table_apply_cat": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_long, c_int, c_int,
                                          c_void_p]),
     "arb_conv2d_nhwc_cat": (c_int, [c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int] * 11 + [c_void_p]),
+    "arb_row_stats": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "arb_gemm_ln": (c_int, [c_void_p] * 8 + [c_int] * 6 + [c_void_p]),
 }
 
 
@@ -508,6 +510,44 @@ def gemm_geglu(x, w_il, b_il=None, cfg=-1, split=-1, plan_batch=None):
     _check(_fn("arb_gemm_geglu")(_p(x2), _p(w_il.contiguous()), _p(b_il), _p(y), _p(ws), M, N, K, int(cfg),
                                  int(split), _stream()), "gemm_geglu")
     return y.reshape(*x.shape[:-1], N // 2)
+
+
+def row_stats(x, eps):
+    """(mean, rstd) per row of x [..., C] (csrc/norm.hip, the LayerNorm kernel's arithmetic) -> fp32
+    [M, 2] - the statistics of a LayerNorm folded into the following GEMM."""
+    _bf16(x)
+    x = x.contiguous()
+    C = x.shape[-1]
+    if C % 8 or C > 2048:
+        raise ValueError(f"row_stats: unsupported C={C}")
+    M = x.numel() // C
+    rs = torch.empty(M, 2, dtype=torch.float32, device=x.device)
+    _check(_fn("arb_row_stats")(_p(x), _p(rs), M, C, float(eps), _stream()), "row_stats")
+    return rs
+
+
+def gemm_ln(x, w, b, wsum, rs, residual=None, geglu=False, cfg=-1, split=-1, plan_batch=None):
+    """LayerNorm folded into a GEMM: x is the LN INPUT, ``w`` / ``b`` / ``wsum`` from ``ops.ln_fold``,
+    ``rs`` = ``row_stats(x)``.  out = rstd (x w^T - mean wsum) + b (+ residual | GEGLU, out N/2)."""
+    _bf16(x, w, b, residual)
+    K = x.shape[-1]
+    N = w.shape[0]
+    x2 = x.reshape(-1, K).contiguous()
+    M = x2.shape[0]
+    if K % 64 or N % (16 if geglu else 8) or w.shape[1] != K or tuple(rs.shape) != (M, 2) or wsum.numel() != N:
+        raise ValueError(f"gemm_ln: unsupported M={M} K={K} N={N}")
+    if rs.dtype != torch.float32 or wsum.dtype != torch.float32 or not rs.is_contiguous() or not wsum.is_contiguous():
+        raise ValueError("gemm_ln: row stats / wsum must be contiguous fp32")
+    if plan_batch and plan_batch[1] and cfg < 0:
+        cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
+        cfg = _fn("arb_conv_family")(M, N, K, split, plan_batch[1] // plan_batch[0], cfg)
+    y = torch.empty(M, N // 2 if geglu else N, dtype=x.dtype, device=x.device)
+    r2 = residual.reshape(M, N).contiguous() if residual is not None else None
+    ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
+    _check(_fn("arb_gemm_ln")(_p(x2), _p(w.contiguous()), _p(b), _p(r2), _p(y), _p(ws), _p(rs), _p(wsum), M, N, K,
+                              int(cfg), int(split), int(bool(geglu)), _stream()), "gemm_ln")
+    return y.reshape(*x.shape[:-1], y.shape[-1])
 
 
 def interleave_geglu(t):

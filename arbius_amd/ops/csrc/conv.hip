@@ -49,6 +49,11 @@ struct ConvArgs {
   int tiles_n, tiles_total;
   int nsplit, m_fastest;
   int geglu = 0;        // GEGLU epilogue: W rows interleaved [value 8 | gate 8] per 16; out [M, N/2]
+  // LayerNorm folded into this GEMM (x is the RAW LN input, W = W_orig * gamma per column):
+  //   out = rstd_m * (acc - mean_m * wsum_n) + bias' (+ ...),  rowstat[m] = (mean, rstd),
+  //   wsum[n] = sum_k W[n, k] (fp32, of the bf16 folded weights), bias' = bias + W_orig beta.
+  const float2* rowstat = nullptr;
+  const float* wsum = nullptr;
   // Two channel sources (a UNet skip concat read in place): channels [0, C1) from x (row stride
   // C1), [C1, Cin) from x2 (row stride Cin - C1); C1 % 64 == 0, so a K tile never straddles.
   // Register-staged kernel only.
@@ -123,6 +128,24 @@ __device__ __forceinline__ void tile_coords(const ConvArgs& p, int BN, int BM, i
   }
 }
 
+// LN fold (ConvArgs::rowstat): v[e] <- rstd * (v[e] - mean * wsum[n + e]) for 8 / 4 channels.
+__device__ __forceinline__ void ln_fold8(const ConvArgs& p, int m, int n, float (&v)[8]) {
+  const float2 rs = p.rowstat[m];
+  const float4 w0 = *reinterpret_cast<const float4*>(p.wsum + n), w1 = *reinterpret_cast<const float4*>(p.wsum + n + 4);
+  const float ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = rs.y * (v[e] - rs.x * ws[e]);
+}
+__device__ __forceinline__ void ln_fold4(const ConvArgs& p, int m, int n, float& v0, float& v1, float& v2,
+                                         float& v3) {
+  const float2 rs = p.rowstat[m];
+  const float4 w = *reinterpret_cast<const float4*>(p.wsum + n);
+  v0 = rs.y * (v0 - rs.x * w.x);
+  v1 = rs.y * (v1 - rs.x * w.y);
+  v2 = rs.y * (v2 - rs.x * w.z);
+  v3 = rs.y * (v3 - rs.x * w.w);
+}
+
 // Largest row block (a power-of-two fraction of BM, >= 16) whose fp32 staging fits LDSF floats.
 template <int BM, int OROW, int LDSF>
 constexpr int epi_rows() {
@@ -179,6 +202,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&ac
         const f32x4 g1 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch + 12]);
         float va[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
         float vg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        if (p.rowstat) {
+          ln_fold8(p, m, n, va);
+          ln_fold8(p, m, n + 8, vg);
+        }
         if (p.bias) {
           float t[8];
           unpack8e<EL>(ld16(p.bias + n), t);
@@ -202,6 +229,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&ac
       const f32x4 s1 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch + 4]);
       float v[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
       float t[8];
+      if (p.rowstat) ln_fold8(p, m, n, v);
       if (p.bias) {
         unpack8e<EL>(ld16(p.bias + n), t);
 #pragma unroll
@@ -503,6 +531,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
   // ---- epilogue: lane holds out[m][n .. n+3]
   const int hw = p.Ho * p.Wo;
   auto emit = [&](int m, int n, float v0, float v1, float v2, float v3) {
+    if (p.rowstat) ln_fold4(p, m, n, v0, v1, v2, v3);
     if (p.bias) {
       const uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
       v0 += lo16<EL>(bv.x); v1 += hi16<EL>(bv.x);
@@ -806,6 +835,7 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
         *reinterpret_cast<float4*>(p.ws + ((size_t)split_idx * p.M + m) * p.N + n) = make_float4(v0, v1, v2, v3);
         continue;
       }
+      if (p.rowstat) ln_fold4(p, m, n, v0, v1, v2, v3);
       if (p.bias) {
         const uint2 bv = *reinterpret_cast<const uint2*>(p.bias + n);
         v0 += lo16<EL>(bv.x); v1 += hi16<EL>(bv.x);
@@ -1183,6 +1213,7 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_persist_kernel(ConvArgs 
         float v0 = acc[a][b][0], v1 = acc[a][b][1], v2 = acc[a][b][2], v3 = acc[a][b][3];
         acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
         if (m >= p.M || n >= p.N) continue;
+        if (p.rowstat) ln_fold4(p, m, n, v0, v1, v2, v3);
         const uint2 bv = *reinterpret_cast<const uint2*>(&sB[nl]);
         v0 += lo16<EL>(bv.x); v1 += hi16<EL>(bv.x);
         v2 += lo16<EL>(bv.y); v3 += hi16<EL>(bv.y);
@@ -1239,6 +1270,15 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
           v[4 * q] += a.x; v[4 * q + 1] += a.y; v[4 * q + 2] += a.z; v[4 * q + 3] += a.w;
         }
       }
+      if (p.rowstat) {
+        float a[8], b[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { a[e] = v[e]; b[e] = v[8 + e]; }
+        ln_fold8(p, m, n, a);
+        ln_fold8(p, m, n + 8, b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { v[e] = a[e]; v[8 + e] = b[e]; }
+      }
       if (p.bias) {
         float t[8];
         unpack8e<EL>(ld16(p.bias + n), t);
@@ -1272,6 +1312,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
       v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
     }
     float t[8];
+    if (p.rowstat) ln_fold8(p, m, n, v);
     if (p.bias) {
       unpack8e<EL>(ld16(p.bias + n), t);
 #pragma unroll
@@ -1611,7 +1652,8 @@ template <int EL>
 static int conv_run(const void* x, const void* w, const void* bias, const void* temb, const void* res, void* out,
                     void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
                     int stride, int cfg, int split, int norm_silu, hipStream_t stream, int geglu = 0,
-                    const void* x2 = nullptr, int C1 = 0) {
+                    const void* x2 = nullptr, int C1 = 0, const void* rowstat = nullptr,
+                    const void* wsum = nullptr) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
   if (x2 != nullptr && (EL != 0 || C1 <= 0 || C1 >= Cin || C1 % 64 != 0 || geglu)) return -1;
   ConvArgs a;
@@ -1622,6 +1664,9 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
   a.norm = (const float*)norm; a.norm_silu = norm_silu;
   conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
   a.geglu = geglu;
+  a.rowstat = (const float2*)rowstat;
+  a.wsum = (const float*)wsum;
+  if ((rowstat == nullptr) != (wsum == nullptr) || (rowstat && (norm != nullptr || x2 != nullptr))) return -1;
   ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
   if (geglu) {
     if (Cout % 16 != 0 || temb != nullptr || res != nullptr || norm != nullptr) return -1;
@@ -1760,4 +1805,16 @@ ARB_API int arb_gemm_geglu(const void* x, const void* w, const void* bias, void*
 ARB_API int arb_gemm_bias_res(const void* x, const void* w, const void* bias, const void* res, void* out, void* ws,
                               int M, int N, int K, int cfg, int split, hipStream_t stream) {
   return arb_conv2d_nhwc(x, w, bias, nullptr, res, out, ws, nullptr, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, 0, stream);
+}
+
+// GEMM with a LayerNorm folded in (see ConvArgs::rowstat): x is the LN's INPUT [M, K], w the
+// gamma-scaled weights, bias the beta-folded bias, rowstat[m] = (mean, rstd) of x's row m
+// (arb_row_stats), wsum[n] = sum_k w[n, k] in fp32.  geglu: w / bias / wsum interleaved as for
+// arb_gemm_geglu, out [M, N/2].  The normalised activation never exists in memory.
+ARB_API int arb_gemm_ln(const void* x, const void* w, const void* bias, const void* res, void* out, void* ws,
+                        const void* rowstat, const void* wsum, int M, int N, int K, int cfg, int split, int geglu,
+                        hipStream_t stream) {
+  if (rowstat == nullptr || wsum == nullptr || (geglu && res != nullptr)) return -1;
+  return conv_run<0>(x, w, bias, nullptr, res, out, ws, nullptr, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, 0, stream,
+                     geglu, nullptr, 0, rowstat, wsum);
 }

@@ -525,3 +525,31 @@ def test_fused_sampler_hip_vs_fp32_reference(cuda, name):
         assert torch.allclose(x, y, rtol=1e-4, atol=1e-4 * max(1.0, y.abs().max().item())), (x - y).abs().max()
     for x, y in zip(ai[:-1], bi[:-1]):
         assert (x - y).abs().max() <= 0.02 * max(1.0, y.abs().max().item())   # one bf16 ulp at most
+
+
+@pytest.mark.parametrize("M,K,N,geglu,res", [(8 * 4096, 320, 960, False, False), (8 * 1024, 640, 640, False, False),
+                                             (8 * 256, 1280, 10240, True, False), (2 * 77, 768, 3072, False, False),
+                                             (300, 320, 2560, True, False), (1000, 1280, 1280, False, True)])
+@pytest.mark.parametrize("cfg,split", [(-1, -1), (10, 1), (12, 3), (24, 1), (5, 2), (32, 1)])
+def test_gemm_with_folded_layer_norm(cuda, M, K, N, geglu, res, cfg, split):
+    """LayerNorm folded into the GEMM epilogue (row stats + gamma-scaled weights + wsum) against the
+    fp32 reference LN -> linear (-> GEGLU), on every epilogue path: planned, register-staged,
+    split-K reduce, persistent, LDS-DMA + split, X-in-registers."""
+    from arbius_amd import ops
+    torch.manual_seed(7)
+    x = (torch.randn(M, K, device=cuda) * 3 + 1.5).bfloat16()        # offset mean: the fold must cancel it
+    g = (torch.rand(K, device=cuda) + 0.5).bfloat16()
+    be = (torch.randn(K, device=cuda) * 0.2).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    r = torch.randn(M, N, device=cuda).bfloat16() if res else None
+    wf, bf, wsum = ops.ln_fold(g, be, w, b, geglu=geglu)
+    rs = _lib.row_stats(x, 1e-5)
+    y = _lib.gemm_ln(x, wf, bf, wsum, rs, r, geglu=geglu, cfg=cfg, split=split)
+    h = ref.layer_norm(x.float(), g.float(), be.float(), 1e-5) @ w.float().t() + b.float()
+    if geglu:
+        h = ref.geglu(h)
+    if res:
+        h = h + r.float()
+    assert _rel(y, h) < 1.5e-2, _rel(y, h)
+    assert torch.equal(y, _lib.gemm_ln(x, wf, bf, wsum, rs, r, geglu=geglu, cfg=cfg, split=split))   # bitwise rerun
