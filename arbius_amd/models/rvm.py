@@ -333,7 +333,9 @@ class RVMPipeline(PipelineBase):
         self.timings = {}
 
     def _reset_graphs(self):
-        pass                        # eager launches (the recurrent state is per clip): nothing to re-capture
+        # eager launches (the recurrent state is per clip): nothing to re-capture; a fork gets its OWN
+        # pinned staging buffers (they are written while the fork's previous chunk is in flight)
+        self._pin = {}
 
     def modules(self):
         return {"net": self.net}
@@ -344,10 +346,68 @@ class RVMPipeline(PipelineBase):
         with self._stream_ctx():
             return self._matte(frames, output_type)
 
+    def _fast_ok(self, ratio) -> bool:
+        return (self.device.type == "cuda" and self.dtype == torch.float16 and ratio < 1.0 and not ops.reference_ops()
+                and self.net.backbone.features[0].conv.out_channels == 16)
+
+    def _pinned(self, key, nbytes):
+        """Reusable page-locked host staging buffers (async H2D / D2H), per pipeline fork."""
+        bufs = self.__dict__.setdefault("_pin", {})     # per fork: fork() -> _reset_graphs() -> {}
+        b = bufs.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+            bufs[key] = b
+        return b[:nbytes]
+
+    def _matte_fast(self, frames: np.ndarray, output_type: str, ratio: float) -> np.ndarray:
+        """HIP fast path (models/rvm_fast.py): uint8 chunks in through pinned double buffers (async
+        H2D), uint8 composites out the same way; chunk i+1's upload and chunk i-1's download overlap
+        chunk i's kernels.  Bytes are those of the fast path, bitwise, for any chunk timing."""
+        from .rvm_fast import FastMatting
+        if getattr(self, "_fast", None) is None:
+            self._fast = FastMatting(self.net)
+        T, H, W, _ = frames.shape
+        n = self.cfg.chunk
+        res = np.empty((T, H, W, 3), dtype=np.uint8)
+        stream = torch.cuda.current_stream(self.device)
+        rec = [None] * 4
+        pending = []                      # (event, pinned out view, target slice)
+        ups = []
+        for j, i in enumerate(range(0, T, n)):
+            beat()
+            t = min(n, T - i)
+            nb = t * H * W * 3
+            st = self._pinned(("in", j % 2), n * H * W * 3)[:nb]
+            if len(ups) >= 2:
+                ups[-2].synchronize()     # the staging buffer's previous upload has been consumed
+            st.copy_(torch.from_numpy(np.ascontiguousarray(frames[i:i + t]).reshape(-1)))
+            dev = st.to(self.device, non_blocking=True).view(t, H, W, 3)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            ups.append(ev)
+            out, rec = self._fast(dev, rec, ratio, output_type, GREEN)
+            ob = self._pinned(("out", j % 2), n * H * W * 3)[:nb]
+            if len(pending) >= 2:         # the staging buffer's previous download must be drained first
+                e, v, sl = pending.pop(0)
+                e.synchronize()
+                res[sl] = v.numpy().reshape(res[sl].shape)
+            ob.copy_(out.view(-1), non_blocking=True)
+            e = torch.cuda.Event()
+            e.record(stream)
+            pending.append((e, ob, slice(i, i + t)))
+        for e, v, sl in pending:
+            e.synchronize()
+            res[sl] = v.numpy().reshape(res[sl].shape)
+        return res
+
     def _matte(self, frames: np.ndarray, output_type: str) -> np.ndarray:
         t0 = time.perf_counter()
         T, H, W, _ = frames.shape
         ratio = min(1.0, self.cfg.max_side / max(H, W))
+        if self._fast_ok(ratio):
+            res = self._matte_fast(frames, output_type, ratio)
+            self.timings = {"matting_s": time.perf_counter() - t0}
+            return res
         rec = [None] * 4
         out = []
         green = torch.tensor(GREEN, dtype=self.dtype, device=self.device).view(1, 3, 1, 1)

@@ -163,8 +163,17 @@ def ln_fold(gamma, beta, w, b, geglu=False):
     return out
 
 
+# Rows up to which the LayerNorm fold pays: it replaces the LN pass (read + write x) by a row-stats
+# pass (read x) but adds ~2 FMAs + the weight-sum loads per output element to the GEMM epilogue.
+# Measured per call on MI355X (r3, eager): text encoders / prior / UNet level 2 (<= 2048 rows) win
+# (CLIP [2,77,768]: 21 vs 27 us), the 8k-32k-row level-0/1 projections lose (GEGLU [32768, 320 ->
+# 2560]: 159 + 13 vs 137 + 17 us) - the epilogue of those short-K GEMMs is already their bottleneck.
+LN_FOLD_MAX_ROWS = 2048
+
+
 def _ln_fold_ok(x, w, geglu):
     return (_hip(x) and x.dtype == torch.bfloat16 and _gemm_ok(x.shape[-1], w.shape[0]) and x.shape[-1] <= 2048
+            and x.numel() // x.shape[-1] <= LN_FOLD_MAX_ROWS
             and (not geglu or w.shape[0] % 16 == 0) and "lnfold" not in _EXP_SKIP)
 
 

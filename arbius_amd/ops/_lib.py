@@ -52,6 +52,17 @@ _SIGS = {
                                          c_void_p]),
     "arb_conv2d_nhwc_cat": (c_int, [c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int] * 11 + [c_void_p]),
     "arb_row_stats": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "arb_conv2d_ex": (c_int, [c_void_p] * 7 + [c_int] * 13 + [c_void_p]),
+    "arb_rvm_resize_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
+    "arb_rvm_stem": (c_int, [c_void_p] * 3 + [c_int] * 3 + [c_void_p]),
+    "arb_rvm_pool3": (c_int, [c_void_p] * 4 + [c_int] * 3 + [c_void_p]),
+    "arb_rvm_upcat": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p] + [c_int] * 4
+                      + [c_void_p]),
+    "arb_rvm_pack": (c_int, [c_void_p, c_int, c_void_p, c_long, c_int, c_int, c_void_p, c_int, c_long, c_void_p]),
+    "arb_rvm_gru_out": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_int,
+                                c_void_p, c_long, c_int, c_long, c_int, c_void_p]),
+    "arb_rvm_dgf": (c_int, [c_void_p] * 7 + [c_int] * 6 + [c_float] * 3 + [c_void_p]),
+    "arb_rvm_args_sizes": (c_size_t, [c_int]),
     "arb_gemm_ln": (c_int, [c_void_p] * 8 + [c_int] * 6 + [c_void_p]),
 }
 
@@ -607,3 +618,120 @@ def sampler_step(tasks):
         r.flags = (int(bool(a["store_x0"])) | int(bool(a["store_cur"])) << 1 | int(a["learned"] is not None) << 2
                    | int(a["clamp"] is not None) << 3 | int(bool(a["read_p"])) << 4)
     _check(_fn("arb_sampler_step")(ctypes.cast(arr, c_void_p), len(tasks), n_pix, cout, _stream()), "sampler_step")
+
+
+# --------------------------------------------------------------------------- general conv entry
+def conv_ex(x, w_pad, b, k, stride=1, pad=None, act=0, residual=None, cfg=-1, split=-1):
+    """Implicit-GEMM conv on NHWC ``x`` [B,H,W,Cx] with Cx % 8 == 0 (NOT necessarily % 64: the kernel
+    reads zeros for the channels up to the next multiple of 64 - no padded copy of x).  ``w_pad``
+    [Cout, k, k, Cpad] zero-padded (Cpad = Cx rounded up to 64), Cout % 8 == 0; act 0/1/2 = none /
+    ReLU / hardswish fused into the epilogue (after bias and residual).  bf16 or fp16."""
+    f16 = x.dtype == torch.float16
+    if not f16:
+        _bf16(x, w_pad, b, residual)
+    for t in (w_pad, b, residual):
+        if t is not None and t.dtype != x.dtype:
+            raise TypeError("conv_ex: operands must share the activation dtype")
+    x = x.contiguous()
+    B, H, W, Cx = x.shape
+    Cout, kh, kw, Cp = w_pad.shape
+    pad = k // 2 if pad is None else pad
+    if Cx % 8 or Cp != -(-Cx // 64) * 64 or Cout % 8 or kh != k or kw != k or k not in (1, 3) or stride not in (1, 2):
+        raise ValueError(f"conv_ex: unsupported x={tuple(x.shape)} w={tuple(w_pad.shape)}")
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    y = torch.empty(B, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    if residual is not None:
+        residual = residual.contiguous()
+        if tuple(residual.shape) != tuple(y.shape):
+            raise ValueError("conv_ex: residual shape")
+    if b is not None and b.numel() != Cout:
+        raise ValueError("conv_ex: bias size")
+    ws_bytes = _fn("arb_conv2d_workspace")(B, H, W, Cp, Cout, k, pad, 0, stride, int(cfg), int(split))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
+    _check(_fn("arb_conv2d_ex")(_p(x), _p(w_pad.contiguous()), _p(b), None, _p(residual), _p(y), _p(ws), B, H, W, Cx,
+                                Cout, k, pad, 0, stride, int(cfg), int(split), int(act), int(f16), _stream()),
+           "conv_ex")
+    return y
+
+
+# --------------------------------------------------------------------------- RVM fused passes
+def _f16(*ts):
+    for t in ts:
+        if t is not None and (t.dtype != torch.float16 or not t.is_contiguous()):
+            raise TypeError("RVM kernels take contiguous fp16 tensors")
+
+
+def rvm_resize_u8(frames, h, w):
+    """uint8 [T,H,W,3] -> fp16 [T,h,w,3] = bilinear(frames / 255) (align_corners=False, size given)."""
+    if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[-1] != 3 or not frames.is_contiguous():
+        raise TypeError("rvm_resize_u8: contiguous uint8 [T,H,W,3]")
+    T, H, W, _ = frames.shape
+    out = torch.empty(T, h, w, 3, dtype=torch.float16, device=frames.device)
+    _check(_fn("arb_rvm_resize_u8")(_p(frames), _p(out), T, H, W, h, w, _stream()), "rvm_resize_u8")
+    return out
+
+
+def rvm_stem(small, args_blob):
+    """3x3 s2 conv 3 -> 16 on the normalised source + bias + hardswish -> fp16 [T, ceil(h/2), ceil(w/2), 16]."""
+    _f16(small)
+    T, h, w, _ = small.shape
+    out = torch.empty(T, (h + 1) // 2, (w + 1) // 2, 16, dtype=torch.float16, device=small.device)
+    _check(_fn("arb_rvm_stem")(_p(small), _p(out), ctypes.c_char_p(args_blob), T, h, w, _stream()), "rvm_stem")
+    return out
+
+
+def rvm_pool3(s0):
+    _f16(s0)
+    T, h, w, _ = s0.shape
+    dims = []
+    for _ in range(3):
+        h, w = (h + 1) // 2, (w + 1) // 2
+        dims.append((h, w))
+    s1, s2, s3 = (torch.empty(T, hh, ww, 3, dtype=torch.float16, device=s0.device) for hh, ww in dims)
+    _check(_fn("arb_rvm_pool3")(_p(s0), _p(s1), _p(s2), _p(s3), T, s0.shape[1], s0.shape[2], _stream()), "rvm_pool3")
+    return s1, s2, s3
+
+
+def rvm_upcat(x, f, s, Cd):
+    """[up2x(x)[:H,:W] | f | s | zeros] -> fp16 [T,H,W,Cd]; (H, W) = s's spatial size; f may be None."""
+    _f16(x, f, s)
+    T, H, W, cs = s.shape
+    cf = f.shape[-1] if f is not None else 0
+    out = torch.empty(T, H, W, Cd, dtype=torch.float16, device=s.device)
+    _check(_fn("arb_rvm_upcat")(_p(x), x.shape[1], x.shape[2], x.shape[3], _p(f), cf, _p(s), cs, _p(out), T, H, W, Cd,
+                                _stream()), "rvm_upcat")
+    return out
+
+
+def rvm_pack(buf, a, aoff, CA, b, CB):
+    """buf [P, bs] rows <- [a[:, aoff:aoff+CA] | b (or zeros)]; a [P, as] rows."""
+    _f16(buf, b)
+    P = buf.numel() // buf.shape[-1]
+    _check(_fn("arb_rvm_pack")(_p(buf), buf.shape[-1], _p(a), a.stride(-2) if a.dim() > 1 else a.shape[-1], aoff, CA,
+                               _p(b), CB, P, _stream()), "rvm_pack")
+
+
+def rvm_gru_out(cc, h, z, out, oc, buf=None, nx=None, noff=0):
+    """h <- (1 - z) h + z tanh(cc[..., :C]) in place; out[p, oc:oc+C] <- h'; buf <- [nx[p, noff:+C] | h']."""
+    C = h.shape[-1]
+    P = h.numel() // C
+    _check(_fn("arb_rvm_gru_out")(_p(cc), cc.shape[-1], _p(h), _p(z), _p(out), out.shape[-1], oc, _p(buf),
+                                  buf.shape[-1] if buf is not None else 0, _p(nx),
+                                  nx.shape[-1] if nx is not None else 0, noff, P, C, _stream()), "rvm_gru_out")
+
+
+def rvm_dgf(hid, small, args_dev, frames, mode, green):
+    """Projection head + deep guided filter + composite -> uint8 [T,H,W,3] at the frames' resolution."""
+    _f16(hid, small)
+    T, h, w, _ = small.shape
+    H, W = frames.shape[1], frames.shape[2]
+    xy = torch.empty(T * h * w * 8, dtype=torch.float32, device=hid.device)
+    ab = torch.empty_like(xy)
+    out = torch.empty(T, H, W, 3, dtype=torch.uint8, device=hid.device)
+    _check(_fn("arb_rvm_dgf")(_p(hid), _p(small), _p(args_dev), _p(xy), _p(ab), _p(frames), _p(out), T, H, W, h, w,
+                              int(mode), float(green[0]), float(green[1]), float(green[2]), _stream()), "rvm_dgf")
+    return out
+
+
+def rvm_args_size(which: int) -> int:
+    return int(_fn("arb_rvm_args_sizes")(which))

@@ -54,6 +54,11 @@ struct ConvArgs {
   //   wsum[n] = sum_k W[n, k] (fp32, of the bf16 folded weights), bias' = bias + W_orig beta.
   const float2* rowstat = nullptr;
   const float* wsum = nullptr;
+  // Channel padding without a padded copy (register-staged kernels): x holds Cx channels per pixel
+  // (row stride Cx, Cx % 8 == 0), the K walk runs over Cin = Cx rounded up to 64 per tap, chunks
+  // at channel >= Cx read zeros; w is [N, kh, kw, Cin] zero-padded.  Cx == Cin otherwise.
+  int Cx = 0;
+  int act = 0;          // epilogue activation after bias / temb / residual: 1 ReLU, 2 hardswish
   // Two channel sources (a UNet skip concat read in place): channels [0, C1) from x (row stride
   // C1), [C1, Cin) from x2 (row stride Cin - C1); C1 % 64 == 0, so a K tile never straddles.
   // Register-staged kernel only.
@@ -126,6 +131,12 @@ __device__ __forceinline__ void tile_coords(const ConvArgs& p, int BN, int BM, i
     m0 = (rest % tiles_m) * BM;
     sp = rest / tiles_m;
   }
+}
+
+__device__ __forceinline__ float act_f(int act, float v) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+  return v;
 }
 
 // LN fold (ConvArgs::rowstat): v[e] <- rstd * (v[e] - mean * wsum[n + e]) for 8 / 4 channels.
@@ -245,6 +256,10 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&ac
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += t[e];
       }
+      if (p.act) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = act_f(p.act, v[e]);
+      }
       st16(p.out + (size_t)m * p.N + n, pack8e<EL>(v));
     }
   }
@@ -314,7 +329,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
       const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
       if (p.upsample) { hi >>= 1; wi >>= 1; }
       const int pix = (xb[i] * p.H + hi) * p.W + wi;
-      xoff[i] = ok ? (p.x2 ? pix : pix * p.Cin + cc * 8) : -1;   // dual source: the pixel index
+      xoff[i] = ok ? (p.x2 ? pix : pix * p.Cx + cc * 8) : -1;    // dual source: the pixel index
     }
   };
   set_tap();
@@ -352,9 +367,10 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
     S.lc = wc + cc * 8;
 #pragma unroll
     for (int i = 0; i < WCH; ++i) S.w[i] = ld16(live && woff[i] >= 0 ? p.w + woff[i] + wk : zp);
+    const bool cin_ok = wc + cc * 8 < p.Cx;           // padded channels read zeros
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
-      S.xv[i] = live && xoff[i] >= 0;
+      S.xv[i] = live && xoff[i] >= 0 && cin_ok;
       S.x[i] = ld16(S.xv[i] ? xaddr(i) : zp);
     }
     wk += BK;
@@ -448,9 +464,10 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
 #pragma unroll
     for (int i = 0; i < WCH; ++i)
       rw[i] = woff[i] >= 0 ? ld16(p.w + woff[i] + wk) : make_uint4(0, 0, 0, 0);
+    const bool cin_ok = wc + cc * 8 < p.Cx;           // padded channels read zeros
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
-      const bool ok = xoff[i] >= 0;
+      const bool ok = xoff[i] >= 0 && cin_ok;
       rx[i] = ok ? ld16(xaddr(i)) : make_uint4(0, 0, 0, 0);
       xv[i] = ok;
     }
@@ -547,6 +564,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
       v0 += lo16<EL>(rv.x); v1 += hi16<EL>(rv.x);
       v2 += lo16<EL>(rv.y); v3 += hi16<EL>(rv.y);
     }
+    if (p.act) { v0 = act_f(p.act, v0); v1 = act_f(p.act, v1); v2 = act_f(p.act, v2); v3 = act_f(p.act, v3); }
     uint2 o;
     o.x = enc16<EL>(v0) | (enc16<EL>(v1) << 16);
     o.y = enc16<EL>(v2) | (enc16<EL>(v3) << 16);
@@ -1227,6 +1245,7 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_persist_kernel(ConvArgs 
           v0 += lo16<EL>(rv.x); v1 += hi16<EL>(rv.x);
           v2 += lo16<EL>(rv.y); v3 += hi16<EL>(rv.y);
         }
+        if (p.act) { v0 = act_f(p.act, v0); v1 = act_f(p.act, v1); v2 = act_f(p.act, v2); v3 = act_f(p.act, v3); }
         uint2 o;
         o.x = enc16<EL>(v0) | (enc16<EL>(v1) << 16);
         o.y = enc16<EL>(v2) | (enc16<EL>(v3) << 16);
@@ -1327,6 +1346,10 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
       unpack8e<EL>(ld16(p.res + (size_t)m * p.N + n), t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    if (p.act) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = act_f(p.act, v[e]);
     }
     st16(p.out + (size_t)m * p.N + n, pack8e<EL>(v));
   }
@@ -1503,7 +1526,7 @@ static size_t slab_bytes(int split, int M, int N) {
 static void conv_geom(ConvArgs& a, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
                       int stride) {
   const int kh = k == 31 ? 3 : k, kw = k == 31 ? 1 : k, padw = k == 31 ? 0 : pad;
-  a.B = B; a.H = H; a.W = W; a.Cin = Cin;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cx = Cin;
   a.Hl = upsample ? 2 * H : H; a.Wl = upsample ? 2 * W : W;
   a.Ho = (a.Hl + 2 * pad - kh) / stride + 1; a.Wo = (a.Wl + 2 * padw - kw) / stride + 1;
   a.N = Cout; a.K = kh * kw * Cin; a.M = B * a.Ho * a.Wo;
@@ -1653,8 +1676,11 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
                     void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
                     int stride, int cfg, int split, int norm_silu, hipStream_t stream, int geglu = 0,
                     const void* x2 = nullptr, int C1 = 0, const void* rowstat = nullptr,
-                    const void* wsum = nullptr) {
+                    const void* wsum = nullptr, int cx = 0, int act = 0) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
+  if (cx == 0) cx = Cin;
+  if (cx % 8 != 0 || cx > Cin || Cin - cx >= 64 || act < 0 || act > 2) return -1;
+  if (cx != Cin && (norm != nullptr || x2 != nullptr || rowstat != nullptr)) return -1;
   if (x2 != nullptr && (EL != 0 || C1 <= 0 || C1 >= Cin || C1 % 64 != 0 || geglu)) return -1;
   ConvArgs a;
   a.x2 = (const bf16_t*)x2;
@@ -1666,6 +1692,8 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
   a.geglu = geglu;
   a.rowstat = (const float2*)rowstat;
   a.wsum = (const float*)wsum;
+  a.Cx = cx;
+  a.act = act;
   if ((rowstat == nullptr) != (wsum == nullptr) || (rowstat && (norm != nullptr || x2 != nullptr))) return -1;
   ConvPlan pl = conv_plan(a.M, a.N, a.ktiles, cfg, split);
   if (geglu) {
@@ -1679,7 +1707,8 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
   // twin (or the 128x128 one for the 8-wave / persistent families) at the same split - the
   // per-output MFMA order and split-K slab order are those of the planned kernel, so the bytes are
   // those of the concatenated-input conv.
-  if (a.x2 != nullptr) {
+  // Padded channels (Cx < Cin) are masked in the register-staged kernels only: same remap.
+  if (a.x2 != nullptr || a.Cx != a.Cin) {
     if (pl.cfg >= 20) pl = conv_plan(a.M, a.N, a.ktiles, kNumCfgs, is_persist(pl.cfg) ? 1 : pl.split);
     else if (pl.cfg < kNumCfgs) pl.cfg += kNumCfgs;
   }
@@ -1817,4 +1846,18 @@ ARB_API int arb_gemm_ln(const void* x, const void* w, const void* bias, const vo
   if (rowstat == nullptr || wsum == nullptr || (geglu && res != nullptr)) return -1;
   return conv_run<0>(x, w, bias, nullptr, res, out, ws, nullptr, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, 0, stream,
                      geglu, nullptr, 0, rowstat, wsum);
+}
+
+// General entry: x has Cx channels per pixel (Cx % 8 == 0; the K walk pads to Cin = Cx rounded up to
+// 64 and reads zeros for the padded channels - no padded copy of x), w is [Cout, k, k, Cin]
+// zero-padded; act 0/1/2 = none / ReLU / hardswish in the epilogue; f16 selects the fp16 twin.
+ARB_API int arb_conv2d_ex(const void* x, const void* w, const void* bias, const void* temb, const void* res, void* out,
+                          void* ws, int B, int H, int W, int Cx, int Cout, int k, int pad, int upsample, int stride,
+                          int cfg, int split, int act, int f16, hipStream_t stream) {
+  const int Cin = (Cx + 63) / 64 * 64;
+  if (f16)
+    return conv_run<1>(x, w, bias, temb, res, out, ws, nullptr, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg,
+                       split, 0, stream, 0, nullptr, 0, nullptr, nullptr, Cx, act);
+  return conv_run<0>(x, w, bias, temb, res, out, ws, nullptr, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg, split,
+                     0, stream, 0, nullptr, 0, nullptr, nullptr, Cx, act);
 }

@@ -44,14 +44,10 @@ __device__ __forceinline__ Stat chan_combine(Stat a, Stat b) {
 // ~64 KB of rows per block and at least 16 blocks per image.  Small images: one 4-row slab per
 // block (as many blocks as possible: these calls are latency-bound).
 __host__ __device__ inline int gn_srpt(int HW, int C) { return (long)HW * C >= (1L << 20) ? 8 : 4; }
-__host__ __device__ inline int gn_iters(int HW, int C) {
-  const int NV = C >> 3, k = NV >= 256 ? 1 : 256 / NV, srpt = gn_srpt(HW, C);
-  if (srpt == 4) return 1;
-  int it = (32768 / C) / (k * srpt);
-  const int cap = HW / (k * srpt * 16);
-  if (it > cap) it = cap;
-  return it < 1 ? 1 : (it > 16 ? 16 : it);
-}
+// One slab per block: the stats pass is bandwidth / latency bound, so it wants as many blocks in
+// flight as possible (SD level 0 at batch 8: 688 blocks of ~30 KB instead of 344 of ~61 KB); the
+// finalize / table combine of the extra partials costs far less than the idle CUs did.
+__host__ __device__ inline int gn_iters(int HW, int C) { return 1; }
 
 // Thread geometry: NV = C/8 channel vectors.  NV < 256: k = 256/NV row lanes, thread
 // (v = t % NV, rl = t / NV).  NV >= 256: one row lane, thread owns vectors t, t+256 (VPT).
@@ -339,11 +335,15 @@ template <int CWMAX, int U>
 __global__ void __launch_bounds__(GN_GROUP_THREADS) gn_group_kernel(
     const bf16_t* __restrict__ x, float2* __restrict__ table, float2* __restrict__ stats,
     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta, const bf16_t* __restrict__ mod,
-    float one_plus, int HW, int C, int G, float eps) {
+    float one_plus, int HW, int C, int G, float eps, const bf16_t* __restrict__ x2, int C1) {
   const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   const int Cg = C / G, Cw = Cg >> 1;                 // Cg even (C % 8 == 0, checked by the host)
-  const uint32_t* base = reinterpret_cast<const uint32_t*>(x + (size_t)b * HW * C + (size_t)g * Cg);
-  const int rowd = C >> 1;                           // row stride in dwords
+  // channels [0, C1) from x (row stride C1), [C1, C) from x2 (a skip concat read in place; C1 even, so
+  // a dword never straddles); C1 == C without x2
+  const int g0 = g * Cg;
+  const uint32_t* base1 = reinterpret_cast<const uint32_t*>(x + (size_t)b * HW * C1);
+  const uint32_t* base2 = x2 ? reinterpret_cast<const uint32_t*>(x2 + (size_t)b * HW * (C - C1)) : nullptr;
+  const int rowd1 = C1 >> 1, rowd2 = (C - C1) >> 1;   // row strides in dwords
   Stat acc = {0.f, 0.f, 0.f, 0.f};
   for (int r0 = 0; r0 < HW; r0 += U * GN_GROUP_THREADS) {
     uint32_t w[U][CWMAX];
@@ -352,7 +352,11 @@ __global__ void __launch_bounds__(GN_GROUP_THREADS) gn_group_kernel(
       const int r = r0 + u * GN_GROUP_THREADS + t;
 #pragma unroll
       for (int j = 0; j < CWMAX; ++j)
-        if (j < Cw) w[u][j] = r < HW ? base[(size_t)r * rowd + j] : 0u;
+        if (j < Cw) {
+          const int c = g0 + 2 * j;
+          w[u][j] = r >= HW ? 0u
+                    : c < C1 ? base1[(size_t)r * rowd1 + (c >> 1)] : base2[(size_t)r * rowd2 + ((c - C1) >> 1)];
+        }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -400,25 +404,32 @@ __global__ void __launch_bounds__(GN_GROUP_THREADS) gn_group_kernel(
   }
 }
 
+// One block per (group, image) building the table directly: opt-in (ARB_GN_GROUP=1: HW <= 256 only,
+// 2: every eligible shape).  Measured slower than stats + table at every SD1.5 level (r3: 36 vs 14 us
+// at [8, 16, 16, 1280], 30 vs 12 us at [8, 8, 8, 1280]; r2: 2.5 % end to end used everywhere) - the
+// 1024-thread blocks walk whole groups with most lanes idle.  Batch-invariant either way; reads a
+// skip concat in place like the slab path.
 static bool gn_group_path(int HW, int C, int G) {
   static const int mode = [] {
-    const char* e = std::getenv("ARB_GN_GROUP");   // opt-in: measured 2.5% slower end to end on
-    return e ? std::atoi(e) : 0;                    // SD1.5 c2g4 (G x B blocks leave CUs idle)
+    const char* e = std::getenv("ARB_GN_GROUP");
+    return e ? std::atoi(e) : 0;
   }();
   const int Cg = C / G;
-  return mode != 0 && Cg % 2 == 0 && Cg <= 64 && (long)HW * Cg <= GN_GROUP_MAX;
+  if (mode == 0 || Cg % 2 != 0 || Cg > 64 || (long)HW * Cg > GN_GROUP_MAX) return false;
+  return mode == 2 || HW <= 256;
 }
 
 // table != null: affine table; else stats (mean, rstd)
 static void launch_gn_group(const void* x, float2* table, float2* stats, const void* gamma, const void* beta,
                             const void* mod, float one_plus, int B, int HW, int C, int G, float eps,
-                            hipStream_t stream) {
+                            hipStream_t stream, const void* x2 = nullptr, int C1 = 0) {
+  if (x2 == nullptr) C1 = C;
   const int Cw = C / G / 2;
   dim3 grid(G, B);
 #define GN_GROUP_LAUNCH(CW, U)                                                                                   \
   gn_group_kernel<CW, U><<<grid, GN_GROUP_THREADS, 0, stream>>>((const bf16_t*)x, table, stats, (const bf16_t*)gamma, \
                                                                 (const bf16_t*)beta, (const bf16_t*)mod, one_plus, HW, \
-                                                                C, G, eps)
+                                                                C, G, eps, (const bf16_t*)x2, C1)
   if (Cw <= 8) GN_GROUP_LAUNCH(8, 4);
   else if (Cw <= 20) GN_GROUP_LAUNCH(20, 2);
   else GN_GROUP_LAUNCH(32, 1);
@@ -527,8 +538,8 @@ static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma
                         float one_plus, void* workspace, void* table, int B, int HW, int C, int G, float eps,
                         hipStream_t stream) {
   if (C % 8 != 0 || C / 8 > 512 || C % G != 0 || G > 256) return -1;
-  if (x2 == nullptr && gn_group_path(HW, C, G)) {
-    launch_gn_group(x, (float2*)table, nullptr, gamma, beta, mod, one_plus, B, HW, C, G, eps, stream);
+  if (gn_group_path(HW, C, G)) {   // same path (and bits) with or without the concat read in place
+    launch_gn_group(x, (float2*)table, nullptr, gamma, beta, mod, one_plus, B, HW, C, G, eps, stream, x2, C1);
     return (int)hipGetLastError();
   }
   const int chunks = gn_stat_chunks(HW, C);

@@ -21,7 +21,7 @@ REC = []
 SLEEP_CYCLES = 400_000
 WRAPPED = ("conv2d_nhwc", "gemm", "gemm_geglu", "group_norm_table", "norm_table_apply", "layer_norm",
            "flash_attention", "group_norm_nhwc", "group_norm_mod_nhwc", "softmax_rows", "sampler_step", "silu",
-           "geglu", "temporal_attention")
+           "geglu", "temporal_attention", "gemm_ln", "row_stats")
 
 
 def _key(name, a, k):
@@ -32,7 +32,7 @@ def _key(name, a, k):
         return (sh(x), sh(w), "s%d" % k.get("stride", a[7] if len(a) > 7 else 1),
                 "up" if (a[4] if len(a) > 4 else k.get("upsample")) else "", "cat" if k.get("x2") is not None else "",
                 "norm" if k.get("norm") is not None else "")
-    if name in ("gemm", "gemm_geglu"):
+    if name in ("gemm", "gemm_geglu", "gemm_ln"):
         return (sh(a[0]), sh(a[1]))
     if name == "flash_attention":
         return (sh(a[0]), sh(a[1]), "prefix" if (a[5] if len(a) > 5 else k.get("kv_prefix")) is not None else "")
