@@ -18,8 +18,7 @@ stays the CPU reference and the small-input path.
 """
 from __future__ import annotations
 
-import ctypes
-from typing import Dict, List, Optional
+from typing import Dict
 
 import numpy as np
 import torch
@@ -149,7 +148,8 @@ class FastMatting:
         r4 = self.gru_inplace(dec.decode4.gru, f4, rec[0])
         out = [r4]
         x = f4
-        for ub, f, s, r in ((dec.decode3, f3, s3, rec[1]), (dec.decode2, f2, s2, rec[2]), (dec.decode1, f1, s1, rec[3])):
+        stages = ((dec.decode3, f3, s3, rec[1]), (dec.decode2, f2, s2, rec[2]), (dec.decode1, f1, s1, rec[3]))
+        for ub, f, s, r in stages:
             cat = _lib.rvm_upcat(x, f, s, _r8(x.shape[-1] + f.shape[-1] + 3))
             x = self.conv(cat, ub.conv.conv, "relu")
             out.append(self.gru_inplace(ub.gru.gru, x, r))

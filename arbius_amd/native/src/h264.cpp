@@ -22,8 +22,10 @@
 #include "h264.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
+#include <utility>
 #include <thread>
 #include <stdexcept>
 
@@ -101,6 +103,13 @@ struct BitReader {
     pos += len;
   }
   uint32_t ue() {
+    const uint32_t w = peek(24);
+    if (w >= (1u << 12)) {                 // fewer than 12 leading zeros: the whole code is in w
+      const int lz = __builtin_clz(w) - 8, len = 2 * lz + 1;
+      if (pos + size_t(len) > nbits) throw std::runtime_error("h264: bitstream overrun");
+      pos += size_t(len);
+      return (w >> (24 - len)) - 1;
+    }
     int lz = 0;
     while (u(1) == 0) {
       if (++lz > 31) throw std::runtime_error("h264: bad exp-golomb code");
@@ -634,9 +643,16 @@ int read_block(BitReader& br, int* coef, int max_num, int nC) {
 struct Frame {
   int mbw, mbh, W, H;
   std::vector<uint8_t> y, cb, cr;
-  std::vector<uint8_t> tc_y, tc_cb, tc_cr;   // TotalCoeff per 4x4 block (nC prediction)
+  std::vector<uint8_t> tc_y, tc_cb, tc_cr;   // TotalCoeff per 4x4 block (nC prediction, deblocking bS 2)
   std::vector<int> slice;                    // slice id per macroblock (-1: not decoded yet)
   std::vector<int8_t> i4mode;                // Intra4x4PredMode per 4x4 block, -1 = not I_NxN
+  // inter state per 4x4 luma block: motion vector (quarter samples), ref_idx (-1: intra / none)
+  // and the identity of the reference picture (deblocking compares pictures, not indices)
+  std::vector<int16_t> mvx, mvy;
+  std::vector<int8_t> ref;
+  std::vector<int> refpic;
+  std::vector<uint8_t> intra, mbqp;          // per macroblock: intra flag, QP_Y (0 for I_PCM)
+  bool constrained_intra = false;            // PPS constrained_intra_pred_flag
   Frame(int mbw_, int mbh_) : mbw(mbw_), mbh(mbh_), W(16 * mbw_), H(16 * mbh_) {
     y.assign(size_t(W) * H, 0);
     cb.assign(size_t(W / 2) * (H / 2), 0);
@@ -646,16 +662,27 @@ struct Frame {
     tc_cr.assign(tc_cb.size(), 0);
     slice.assign(size_t(mbw) * mbh, -1);
     i4mode.assign(tc_y.size(), -1);
+    mvx.assign(tc_y.size(), 0);
+    mvy.assign(tc_y.size(), 0);
+    ref.assign(tc_y.size(), -1);
+    refpic.assign(tc_y.size(), -1);
+    intra.assign(size_t(mbw) * mbh, 1);
+    mbqp.assign(size_t(mbw) * mbh, 0);
   }
   bool avail(int mx, int my, int cur_slice) const {
     return mx >= 0 && my >= 0 && mx < mbw && my < mbh && slice[size_t(my) * mbw + mx] == cur_slice;
   }
+  // neighbour availability for INTRA prediction: with constrained_intra_pred, inter neighbours
+  // do not count (8.3.1.2 / 8.3.3 / 8.3.4)
+  bool avail_intra(int mx, int my, int cur_slice) const {
+    return avail(mx, my, cur_slice) && (!constrained_intra || intra[size_t(my) * mbw + mx]);
+  }
   Nb nb(int mx, int my, int s) const {
     Nb n;
-    n.left = avail(mx - 1, my, s);
-    n.top = avail(mx, my - 1, s);
-    n.topleft = avail(mx - 1, my - 1, s);
-    n.topright = avail(mx + 1, my - 1, s);
+    n.left = avail_intra(mx - 1, my, s);
+    n.top = avail_intra(mx, my - 1, s);
+    n.topleft = avail_intra(mx - 1, my - 1, s);
+    n.topright = avail_intra(mx + 1, my - 1, s);
     return n;
   }
   // nC for a 4x4 block at (bx, by) in block units of a plane with `per` blocks per MB side
@@ -714,6 +741,463 @@ void recon_chroma(std::vector<uint8_t>& pl, int Wc, int mx, int my, const uint8_
   }
 }
 
+// ------------------------------------------------------------------------------------ inter (P) tools
+// coded_block_pattern me(v) for Inter macroblocks (Table 9-4), codeNum -> cbp
+const uint8_t kInterCbp[48] = {0,  16, 1,  2,  4,  8,  32, 3,  5,  10, 12, 15, 47, 7,  11, 13,
+                               14, 6,  9,  31, 35, 37, 42, 44, 33, 34, 36, 40, 39, 43, 45, 46,
+                               17, 18, 20, 24, 19, 21, 26, 28, 23, 27, 29, 30, 22, 25, 38, 41};
+
+inline int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
+
+// Luma inter prediction (8.4.2.2.1) of a w x h block whose top-left integer position is (x0, y0),
+// motion vector (mvx, mvy) in quarter samples; reference samples outside the picture are the
+// nearest edge sample.  The half-sample values b / h / j come from the unclipped 6-tap sums of a
+// (w + 5) x (h + 5) window; quarter samples average the two nearest (8-251..8-261).
+void mc_luma(const Frame& r, int x0, int y0, int mvx, int mvy, int w, int h, uint8_t* out, int ostride) {
+  const int xi = x0 + (mvx >> 2), yi = y0 + (mvy >> 2), xf = mvx & 3, yf = mvy & 3;
+  if (xf == 0 && yf == 0) {                         // full-sample vector: a (clamped) copy
+    if (xi >= 0 && yi >= 0 && xi + w <= r.W && yi + h <= r.H) {
+      for (int j = 0; j < h; ++j) std::memcpy(out + j * ostride, r.y.data() + size_t(yi + j) * r.W + xi, size_t(w));
+    } else {
+      for (int j = 0; j < h; ++j) {
+        const uint8_t* row = r.y.data() + size_t(std::clamp(yi + j, 0, r.H - 1)) * r.W;
+        for (int i = 0; i < w; ++i) out[j * ostride + i] = row[std::clamp(xi + i, 0, r.W - 1)];
+      }
+    }
+    return;
+  }
+  int win[21][22];                                  // rows yi-2 .. yi+h+2, cols xi-2 .. xi+w+3
+  if (xi - 2 >= 0 && yi - 2 >= 0 && xi + w + 3 < r.W && yi + h + 2 < r.H) {
+    for (int j = 0; j < h + 5; ++j) {
+      const uint8_t* row = r.y.data() + size_t(yi - 2 + j) * r.W + xi - 2;
+      for (int i = 0; i < w + 6; ++i) win[j][i] = row[i];
+    }
+  } else {
+    for (int j = 0; j < h + 5; ++j) {
+      const uint8_t* row = r.y.data() + size_t(std::clamp(yi - 2 + j, 0, r.H - 1)) * r.W;
+      for (int i = 0; i < w + 6; ++i) win[j][i] = row[std::clamp(xi - 2 + i, 0, r.W - 1)];
+    }
+  }
+  const int cs = yf * 4 + xf;
+  const bool use_b = cs == 1 || cs == 2 || cs == 3 || cs == 5 || cs == 6 || cs == 7 || cs >= 13;
+  const bool use_j = cs == 6 || cs == 9 || cs == 10 || cs == 11 || cs == 14;
+  const bool use_h =
+      cs == 4 || cs == 5 || cs == 7 || cs == 8 || cs == 9 || cs == 11 || cs == 12 || cs == 13 || cs == 15;
+  auto clip = [](int v) { return v < 0 ? 0 : v > 255 ? 255 : v; };
+  // b1[j][i]: unclipped horizontal half sample (i + 1/2, j - 2) for window rows j = 0 .. h+4
+  int b1[21][16], bq[17][16], hq[16][17], jq[16][16];
+  if (use_b || use_j) {
+    const int j0 = use_j ? 0 : 2, j1 = use_j ? h + 5 : h + 3;
+    for (int j = j0; j < j1; ++j)
+      for (int i = 0; i < w; ++i)
+        b1[j][i] = tap6(win[j][i], win[j][i + 1], win[j][i + 2], win[j][i + 3], win[j][i + 4], win[j][i + 5]);
+    for (int j = 0; j <= h; ++j)                    // b at rows 0 .. h (row h: the "s" samples below)
+      for (int i = 0; i < w; ++i) bq[j][i] = clip((b1[j + 2][i] + 16) >> 5);
+  }
+  if (use_h)
+    for (int j = 0; j < h; ++j)                     // h at cols 0 .. w (col w: the "m" samples right)
+      for (int i = 0; i <= w; ++i)
+        hq[j][i] = clip((tap6(win[j][i + 2], win[j + 1][i + 2], win[j + 2][i + 2], win[j + 3][i + 2], win[j + 4][i + 2],
+                              win[j + 5][i + 2]) + 16) >> 5);
+  if (use_j)
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i)
+        jq[j][i] =
+            clip((tap6(b1[j][i], b1[j + 1][i], b1[j + 2][i], b1[j + 3][i], b1[j + 4][i], b1[j + 5][i]) + 512) >> 10);
+  auto G = [&](int i, int j) { return win[j + 2][i + 2]; };
+  auto run = [&](auto fn) {
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) out[j * ostride + i] = uint8_t(fn(i, j));
+  };
+  switch (cs) {
+    case 1: run([&](int i, int j) { return (G(i, j) + bq[j][i] + 1) >> 1; }); break;            // a
+    case 2: run([&](int i, int j) { return bq[j][i]; }); break;                                   // b
+    case 3: run([&](int i, int j) { return (G(i + 1, j) + bq[j][i] + 1) >> 1; }); break;        // c
+    case 4: run([&](int i, int j) { return (G(i, j) + hq[j][i] + 1) >> 1; }); break;            // d
+    case 5: run([&](int i, int j) { return (bq[j][i] + hq[j][i] + 1) >> 1; }); break;           // e
+    case 6: run([&](int i, int j) { return (bq[j][i] + jq[j][i] + 1) >> 1; }); break;           // f
+    case 7: run([&](int i, int j) { return (bq[j][i] + hq[j][i + 1] + 1) >> 1; }); break;       // g
+    case 8: run([&](int i, int j) { return hq[j][i]; }); break;                                   // h
+    case 9: run([&](int i, int j) { return (hq[j][i] + jq[j][i] + 1) >> 1; }); break;           // i
+    case 10: run([&](int i, int j) { return jq[j][i]; }); break;                                  // j
+    case 11: run([&](int i, int j) { return (jq[j][i] + hq[j][i + 1] + 1) >> 1; }); break;      // k
+    case 12: run([&](int i, int j) { return (G(i, j + 1) + hq[j][i] + 1) >> 1; }); break;       // n
+    case 13: run([&](int i, int j) { return (hq[j][i] + bq[j + 1][i] + 1) >> 1; }); break;      // p
+    case 14: run([&](int i, int j) { return (jq[j][i] + bq[j + 1][i] + 1) >> 1; }); break;      // q
+    default: run([&](int i, int j) { return (hq[j][i + 1] + bq[j + 1][i] + 1) >> 1; }); break; // r
+  }
+}
+
+// Chroma inter prediction (8.4.2.2.2), 4:2:0 frame: eighth-sample bilinear, vector = the luma one
+void mc_chroma(const std::vector<uint8_t>& pl, int Wc, int Hc, int x0, int y0, int mvx, int mvy, int w, int h,
+               uint8_t* out, int ostride) {
+  const int xi = x0 + (mvx >> 3), yi = y0 + (mvy >> 3), xf = mvx & 7, yf = mvy & 7;
+  auto P = [&](int x, int y) { return int(pl[size_t(std::clamp(y, 0, Hc - 1)) * Wc + std::clamp(x, 0, Wc - 1)]); };
+  for (int j = 0; j < h; ++j)
+    for (int i = 0; i < w; ++i) {
+      const int x = xi + i, y = yi + j;
+      out[j * ostride + i] = uint8_t(((8 - xf) * (8 - yf) * P(x, y) + xf * (8 - yf) * P(x + 1, y) +
+                                      (8 - xf) * yf * P(x, y + 1) + xf * yf * P(x + 1, y + 1) + 32) >> 6);
+    }
+}
+
+// Motion vector prediction (8.4.1.3) inside macroblock (mx, my).  `done` marks the 4x4 blocks of the
+// current macroblock whose motion is already known (partitions decoded earlier in the macroblock).
+struct MvPred {
+  const Frame& f;
+  int mx, my, slice;
+  uint16_t done = 0;
+  struct N {
+    bool avail;
+    int ref, x, y;
+  };
+  N at(int bx, int by) const {            // 4x4 block (bx, by) in MB-relative 4x4 units
+    N n{false, -1, 0, 0};
+    if (bx >= 0 && bx < 4 && by >= 0 && by < 4) {
+      if (!(done >> (by * 4 + bx) & 1)) return n;
+    } else {
+      const int nmx = mx + (bx < 0 ? -1 : bx > 3 ? 1 : 0), nmy = my + (by < 0 ? -1 : by > 3 ? 1 : 0);
+      if (by >= 0 && by < 4 && bx > 3) return n;             // right neighbour: not decoded yet
+      if (by > 3) return n;
+      if (!f.avail(nmx, nmy, slice)) return n;
+    }
+    const int gx = 4 * mx + bx, gy = 4 * my + by;
+    const size_t i = size_t(gy) * 4 * f.mbw + gx;
+    n.avail = true;
+    n.ref = f.ref[i];
+    if (n.ref >= 0) {
+      n.x = f.mvx[i];
+      n.y = f.mvy[i];
+    }
+    return n;
+  }
+  static int med(int a, int b, int c) { return std::max(std::min(a, b), std::min(std::max(a, b), c)); }
+  // shape: 0 generic, 1 16x8 upper, 2 16x8 lower, 3 8x16 left, 4 8x16 right
+  void pred(int bx, int by, int bw, int ref, int shape, int& px, int& py) const {
+    N A = at(bx - 1, by), Bn = at(bx, by - 1), C = at(bx + bw, by - 1);
+    if (!C.avail) C = at(bx - 1, by - 1);
+    if (shape == 1 && Bn.ref == ref) { px = Bn.x; py = Bn.y; return; }
+    if (shape == 2 && A.ref == ref) { px = A.x; py = A.y; return; }
+    if (shape == 3 && A.ref == ref) { px = A.x; py = A.y; return; }
+    if (shape == 4 && C.ref == ref) { px = C.x; py = C.y; return; }
+    if (!Bn.avail && !C.avail && A.avail) Bn = C = A;
+    const int m = (A.ref == ref) + (Bn.ref == ref) + (C.ref == ref);
+    if (m == 1) {
+      const N& s = A.ref == ref ? A : Bn.ref == ref ? Bn : C;
+      px = s.x;
+      py = s.y;
+      return;
+    }
+    px = med(A.x, Bn.x, C.x);
+    py = med(A.y, Bn.y, C.y);
+  }
+  void skip(int& px, int& py) const {    // P_Skip (8.4.1.1)
+    const N A = at(-1, 0), Bn = at(0, -1);
+    if (!A.avail || !Bn.avail || (A.ref == 0 && A.x == 0 && A.y == 0) || (Bn.ref == 0 && Bn.x == 0 && Bn.y == 0)) {
+      px = py = 0;
+      return;
+    }
+    pred(0, 0, 4, 0, 0, px, py);
+  }
+};
+
+// Assign one (sub-)partition's motion (4x4-block rectangle) and mark it known for later predictions
+inline void set_motion(Frame& f, MvPred& mp, int mx, int my, int bx, int by, int bw, int bh, int ref, int refpic,
+                       int mvx, int mvy) {
+  for (int y = by; y < by + bh; ++y)
+    for (int x = bx; x < bx + bw; ++x) {
+      const size_t i = size_t(4 * my + y) * 4 * f.mbw + 4 * mx + x;
+      f.ref[i] = int8_t(ref);
+      f.refpic[i] = refpic;
+      f.mvx[i] = int16_t(mvx);
+      f.mvy[i] = int16_t(mvy);
+      mp.done |= uint16_t(1u << (y * 4 + x));
+    }
+}
+
+// Residual of an inter / Intra_4x4-style macroblock: coef[blk][16] in scan order (blkIdx order)
+void recon_luma4x4(Frame& f, int mx, int my, const uint8_t* pred, const int (*coef)[16], int qp) {
+  for (int blk = 0; blk < 16; ++blk) {
+    const int bx = kBlkX[blk], by = kBlkY[blk];
+    int d[16] = {0}, r[16] = {0};
+    bool any = false;
+    for (int k = 0; k < 16; ++k)
+      if (coef[blk][k]) {
+        const int rp = kZigzag[k];
+        d[rp] = dequant(coef[blk][k], qp, rp);
+        any = true;
+      }
+    if (any) inv4x4(d, r);
+    uint8_t* dst = f.y.data() + size_t(my * 16 + 4 * by) * f.W + mx * 16 + 4 * bx;
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) dst[y * f.W + x] = clip255(pred[16 * (4 * by + y) + 4 * bx + x] + r[4 * y + x]);
+  }
+}
+
+// ------------------------------------------------------------------------------------ deblocking (8.7)
+const uint8_t kAlpha[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   4,   4,
+                            5,  6,  7,  8,  9,  10, 12, 13, 15, 17, 20, 22,  25,  28,  32,  36,  40,  45,
+                            50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
+const uint8_t kBeta[52] = {0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  0,  0,  2,  2,
+                           2, 3, 3, 3, 3, 4, 4, 4, 6,  6,  7,  7,  8,  8,  9,  9,  10, 10,
+                           11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
+const uint8_t kTc0[52][3] = {
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1},
+    {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1},
+    {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 2, 3}, {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4},
+    {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11},
+    {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
+
+struct SliceDb {           // per-slice deblocking controls
+  int idc = 1, offa = 0, offb = 0;
+};
+
+// one edge position: p[i] = *(p0 - i * step) (i = 0..3), q[i] = *(q0 + i * step)
+inline void filter_px(uint8_t* q0, int step, int bS, int alpha, int beta, int tc0, bool luma) {
+  const int p0 = q0[-step], p1 = q0[-2 * step], q0v = q0[0], q1 = q0[step];
+  if (!(std::abs(p0 - q0v) < alpha && std::abs(p1 - p0) < beta && std::abs(q1 - q0v) < beta)) return;
+  if (bS < 4) {
+    int tc = tc0;
+    int ap = 0, aq = 0, p2 = 0, q2 = 0;
+    if (luma) {
+      p2 = q0[-3 * step];
+      q2 = q0[2 * step];
+      ap = std::abs(p2 - p0);
+      aq = std::abs(q2 - q0v);
+      tc += (ap < beta) + (aq < beta);
+    } else {
+      tc += 1;
+    }
+    const int delta = std::clamp((((q0v - p0) * 4) + (p1 - q1) + 4) >> 3, -tc, tc);
+    q0[-step] = clip255(p0 + delta);
+    q0[0] = clip255(q0v - delta);
+    if (luma) {
+      if (ap < beta) q0[-2 * step] = uint8_t(p1 + std::clamp((p2 + ((p0 + q0v + 1) >> 1) - (p1 * 2)) >> 1, -tc0, tc0));
+      if (aq < beta) q0[step] = uint8_t(q1 + std::clamp((q2 + ((p0 + q0v + 1) >> 1) - (q1 * 2)) >> 1, -tc0, tc0));
+    }
+    return;
+  }
+  if (!luma) {
+    q0[-step] = uint8_t((2 * p1 + p0 + q1 + 2) >> 2);
+    q0[0] = uint8_t((2 * q1 + q0v + p1 + 2) >> 2);
+    return;
+  }
+  const int p2 = q0[-3 * step], p3 = q0[-4 * step], q2 = q0[2 * step], q3 = q0[3 * step];
+  const int ap = std::abs(p2 - p0), aq = std::abs(q2 - q0v);
+  const bool strong = std::abs(p0 - q0v) < ((alpha >> 2) + 2);
+  if (ap < beta && strong) {
+    q0[-step] = uint8_t((p2 + 2 * p1 + 2 * p0 + 2 * q0v + q1 + 4) >> 3);
+    q0[-2 * step] = uint8_t((p2 + p1 + p0 + q0v + 2) >> 2);
+    q0[-3 * step] = uint8_t((2 * p3 + 3 * p2 + p1 + p0 + q0v + 4) >> 3);
+  } else {
+    q0[-step] = uint8_t((2 * p1 + p0 + q1 + 2) >> 2);
+  }
+  if (aq < beta && strong) {
+    q0[0] = uint8_t((p1 + 2 * p0 + 2 * q0v + 2 * q1 + q2 + 4) >> 3);
+    q0[step] = uint8_t((p0 + q0v + q1 + q2 + 2) >> 2);
+    q0[2 * step] = uint8_t((2 * q3 + 3 * q2 + q1 + q0v + p0 + 4) >> 3);
+  } else {
+    q0[0] = uint8_t((2 * q1 + q0v + p1 + 2) >> 2);
+  }
+}
+
+// boundary strength between 4x4 luma blocks p and q (absolute 4x4 coordinates)
+inline int bs_of(const Frame& f, int pbx, int pby, int qbx, int qby, bool mb_edge) {
+  const int pm = (pby / 4) * f.mbw + pbx / 4, qm = (qby / 4) * f.mbw + qbx / 4;
+  if (f.intra[pm] || f.intra[qm]) return mb_edge ? 4 : 3;
+  const size_t pi = size_t(pby) * 4 * f.mbw + pbx, qi = size_t(qby) * 4 * f.mbw + qbx;
+  if (f.tc_y[pi] || f.tc_y[qi]) return 2;
+  if (f.refpic[pi] != f.refpic[qi] || std::abs(f.mvx[pi] - f.mvx[qi]) >= 4 || std::abs(f.mvy[pi] - f.mvy[qi]) >= 4)
+    return 1;
+  return 0;
+}
+
+// The in-loop deblocking filter over a whole decoded picture, macroblocks in raster order (luma,
+// then chroma; vertical edges, then horizontal ones), on the unfiltered reconstruction.
+void deblock(Frame& f, const std::vector<SliceDb>& sl, int chroma_qp_offset, int threads) {
+  const int Wc = f.W / 2;
+  auto filter_mb = [&](int mx, int my) {
+      const int mb = my * f.mbw + mx, sid = f.slice[mb];
+      const SliceDb& d = sl[sid];
+      if (d.idc == 1) return;
+      const bool left = mx > 0 && (d.idc != 2 || f.slice[mb - 1] == sid);
+      const bool top = my > 0 && (d.idc != 2 || f.slice[mb - f.mbw] == sid);
+      for (int dir = 0; dir < 2; ++dir) {                   // 0: vertical edges, 1: horizontal edges
+        for (int e = 0; e < 4; ++e) {
+          if (e == 0 && !(dir == 0 ? left : top)) continue;
+          int bS[4];
+          bool any = false;
+          for (int k = 0; k < 4; ++k) {
+            const int qbx = 4 * mx + (dir == 0 ? e : k), qby = 4 * my + (dir == 0 ? k : e);
+            const int pbx = dir == 0 ? qbx - 1 : qbx, pby = dir == 0 ? qby : qby - 1;
+            bS[k] = bs_of(f, pbx, pby, qbx, qby, e == 0);
+            any |= bS[k] != 0;
+          }
+          if (!any) continue;
+          const int pmb = e == 0 ? (dir == 0 ? mb - 1 : mb - f.mbw) : mb;
+          const int qpav = (f.mbqp[pmb] + f.mbqp[mb] + 1) >> 1;
+          const int ia = std::clamp(qpav + d.offa, 0, 51), ib = std::clamp(qpav + d.offb, 0, 51);
+          const int alpha = kAlpha[ia], beta = kBeta[ib];
+          // luma: 16 samples along the edge
+          for (int k = 0; k < 16; ++k) {
+            const int bsk = bS[k / 4];
+            if (!bsk) continue;
+            const int x = 16 * mx + (dir == 0 ? 4 * e : k), y = 16 * my + (dir == 0 ? k : 4 * e);
+            filter_px(f.y.data() + size_t(y) * f.W + x, dir == 0 ? 1 : f.W, bsk, alpha, beta,
+                      bsk < 4 ? kTc0[ia][bsk - 1] : 0, true);
+          }
+          // chroma: the luma edges 0 and 8 map to chroma edges 0 and 4
+          if (e & 1) continue;
+          const int qpp = kChromaQp[std::clamp(f.mbqp[pmb] + chroma_qp_offset, 0, 51)];
+          const int qpq = kChromaQp[std::clamp(f.mbqp[mb] + chroma_qp_offset, 0, 51)];
+          const int qpc = (qpp + qpq + 1) >> 1;
+          const int ca = std::clamp(qpc + d.offa, 0, 51), cbb = std::clamp(qpc + d.offb, 0, 51);
+          for (std::vector<uint8_t>* pl : {&f.cb, &f.cr})
+            for (int k = 0; k < 8; ++k) {
+              const int bsk = bS[k / 2];
+              if (!bsk) continue;
+              const int x = 8 * mx + (dir == 0 ? 2 * e : k), y = 8 * my + (dir == 0 ? k : 2 * e);
+              filter_px(pl->data() + size_t(y) * Wc + x, dir == 0 ? 1 : Wc, bsk, kAlpha[ca], kBeta[cbb],
+                        bsk < 4 ? kTc0[ca][bsk - 1] : 0, false);
+            }
+        }
+      }
+  };
+  // Raster order, or a wavefront over macroblock rows: a macroblock's edges touch samples that the
+  // macroblocks left of it and up to one column right of it in the row above filter first, so
+  // row y may filter column x once row y-1 has finished column x+1 - the same result as raster order.
+  if (threads <= 1 || f.mbh < 2) {
+    for (int my = 0; my < f.mbh; ++my)
+      for (int mx = 0; mx < f.mbw; ++mx) filter_mb(mx, my);
+    return;
+  }
+  std::vector<std::atomic<int>> progress(static_cast<size_t>(f.mbh));
+  for (auto& a : progress) a.store(0);
+  const int nt = std::min(threads, f.mbh);
+  auto worker = [&](int t) {
+    for (int my = t; my < f.mbh; my += nt)
+      for (int mx = 0; mx < f.mbw; ++mx) {
+        if (my > 0) {
+          const int need = std::min(f.mbw, mx + 2);
+          while (progress[size_t(my - 1)].load(std::memory_order_acquire) < need) std::this_thread::yield();
+        }
+        filter_mb(mx, my);
+        progress[size_t(my)].store(mx + 1, std::memory_order_release);
+      }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(worker, t);
+  worker(0);
+  for (auto& th : pool) th.join();
+}
+
+struct RefPic {                   // a decoded, deblocked picture in the DPB
+  std::shared_ptr<const Frame> f;
+  int id = -1, frame_num = 0;
+};
+
+// RefPicList0 of a P slice (8.2.4.2.1 + 8.2.4.3.1): short-term references by descending PicNum,
+// then the modifications, truncated to num_ref_idx_l0_active (missing entries stay empty)
+std::vector<RefPic> ref_list0(const std::vector<RefPic>& dpb, int cur, int max_fn,
+                              const std::vector<std::pair<int, int>>& mods, int n_active) {
+  auto picnum = [&](const RefPic& r) { return r.frame_num > cur ? r.frame_num - max_fn : r.frame_num; };
+  std::vector<RefPic> list = dpb;
+  std::stable_sort(list.begin(), list.end(), [&](const RefPic& a, const RefPic& b) { return picnum(a) > picnum(b); });
+  int pred = cur;
+  for (size_t m = 0; m < mods.size(); ++m) {
+    const int diff = mods[m].second + 1;
+    int nowrap = mods[m].first == 0 ? pred - diff : pred + diff;
+    if (nowrap < 0) nowrap += max_fn;
+    if (nowrap >= max_fn) nowrap -= max_fn;
+    pred = nowrap;
+    const int pn = nowrap > cur ? nowrap - max_fn : nowrap;
+    auto it = std::find_if(list.begin(), list.end(), [&](const RefPic& r) { return picnum(r) == pn; });
+    if (it == list.end()) throw std::runtime_error("h264: reference list modification names no picture");
+    const RefPic r = *it;
+    list.erase(it);
+    list.insert(list.begin() + std::ptrdiff_t(std::min(m, list.size())), r);
+  }
+  list.resize(size_t(n_active));
+  return list;
+}
+
+// Reference marking after a reference picture (8.2.5.3 sliding window / 8.2.5.4 MMCO 1 and 5);
+// the picture then joins the DPB.  Returns the frame_num later pictures continue from.
+int mark_reference(std::vector<RefPic>& dpb, RefPic pic, int max_fn, int max_refs, bool adaptive,
+                   const std::vector<std::pair<int, int>>& mmco) {
+  const int cur = pic.frame_num;
+  auto picnum = [&](const RefPic& r) { return r.frame_num > cur ? r.frame_num - max_fn : r.frame_num; };
+  bool cleared = false;
+  if (adaptive) {
+    for (const auto& op : mmco) {
+      if (op.first == 1) {
+        const int pn = cur - (op.second + 1);
+        dpb.erase(std::remove_if(dpb.begin(), dpb.end(), [&](const RefPic& r) { return picnum(r) == pn; }), dpb.end());
+      } else {
+        dpb.clear();
+        cleared = true;
+      }
+    }
+  } else if (int(dpb.size()) >= max_refs) {
+    dpb.erase(std::min_element(dpb.begin(), dpb.end(),
+                               [&](const RefPic& a, const RefPic& b) { return picnum(a) < picnum(b); }));
+  }
+  if (int(dpb.size()) >= max_refs) throw std::runtime_error("h264: too many reference pictures");
+  if (cleared) pic.frame_num = 0;
+  dpb.push_back(pic);
+  return pic.frame_num;
+}
+
+void mark_intra(Frame& f, int mx, int my) {
+  for (int y = 0; y < 4; ++y)
+    for (int x = 0; x < 4; ++x) {
+      const size_t i = size_t(4 * my + y) * 4 * f.mbw + 4 * mx + x;
+      f.ref[i] = -1;
+      f.refpic[i] = -1;
+      f.mvx[i] = f.mvy[i] = 0;
+    }
+  f.intra[size_t(my) * f.mbw + mx] = 1;
+}
+
+// inter prediction of the whole macroblock from its (already assigned) 4x4 motion
+void predict_inter(const Frame& f, const std::vector<RefPic>& list, int mx, int my, uint8_t* py, uint8_t* pcb,
+                   uint8_t* pcr) {
+  // every sample depends only on its position and its block's (ref, mv), so runs of equal motion
+  // are predicted as one larger block: 16x16, else per 8x8 quadrant, else per 4x4
+  auto idx = [&](int bx, int by) { return size_t(4 * my + by) * 4 * f.mbw + 4 * mx + bx; };
+  auto same = [&](int bx, int by, int n) {
+    const size_t a = idx(bx, by);
+    for (int y = by; y < by + n; ++y)
+      for (int x = bx; x < bx + n; ++x) {
+        const size_t b = idx(x, y);
+        if (f.ref[b] != f.ref[a] || f.mvx[b] != f.mvx[a] || f.mvy[b] != f.mvy[a]) return false;
+      }
+    return true;
+  };
+  auto block = [&](int bx, int by, int n) {
+    const size_t i = idx(bx, by);
+    const Frame& r = *list[size_t(f.ref[i])].f;
+    mc_luma(r, 16 * mx + 4 * bx, 16 * my + 4 * by, f.mvx[i], f.mvy[i], 4 * n, 4 * n, py + 16 * 4 * by + 4 * bx, 16);
+    mc_chroma(r.cb, r.W / 2, r.H / 2, 8 * mx + 2 * bx, 8 * my + 2 * by, f.mvx[i], f.mvy[i], 2 * n, 2 * n,
+              pcb + 8 * 2 * by + 2 * bx, 8);
+    mc_chroma(r.cr, r.W / 2, r.H / 2, 8 * mx + 2 * bx, 8 * my + 2 * by, f.mvx[i], f.mvy[i], 2 * n, 2 * n,
+              pcr + 8 * 2 * by + 2 * bx, 8);
+  };
+  if (same(0, 0, 4)) {
+    block(0, 0, 4);
+    return;
+  }
+  for (int q = 0; q < 4; ++q) {
+    const int qx = 2 * (q & 1), qy = 2 * (q >> 1);
+    if (same(qx, qy, 2)) {
+      block(qx, qy, 2);
+      continue;
+    }
+    for (int k = 0; k < 4; ++k) block(qx + (k & 1), qy + (k >> 1), 1);
+  }
+}
+
 // ------------------------------------------------------------------------------------ encoder
 inline int quant(int w, int mf, int f, int qbits) {
   const int a = w < 0 ? -w : w;
@@ -730,8 +1214,8 @@ int sad(const uint8_t* src, int stride, const uint8_t* pred, int n) {
 }
 
 void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, const uint8_t* scr, int mx, int my,
-               int qp) {
-  const Nb nb = f.nb(mx, my, 0);
+               int qp, int slice_id = 0, int type_offset = 0) {
+  const Nb nb = f.nb(mx, my, slice_id);
   const int W = f.W, Wc = f.W / 2;
   // ---- luma mode
   uint8_t pred[256], best[256];
@@ -818,15 +1302,15 @@ void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, c
   const int cbp_chroma = c_any_ac ? 2 : c_any_dc ? 1 : 0;
   if (cbp_chroma < 2) std::memset(cac, 0, sizeof(cac));
   // ---- syntax
-  bw.ue(1 + mode + 4 * cbp_chroma + (cbp_luma ? 12 : 0));
+  bw.ue(type_offset + 1 + mode + 4 * cbp_chroma + (cbp_luma ? 12 : 0));
   bw.ue(cmode);
   bw.se(0);  // mb_qp_delta
-  write_block(bw, dc, 16, f.nc(f.tc_y, 4 * mx, 4 * my, 4, 0));
+  write_block(bw, dc, 16, f.nc(f.tc_y, 4 * mx, 4 * my, 4, slice_id));
   for (int blk = 0; blk < 16; ++blk) {
     const int bx = 4 * mx + kBlkX[blk], by = 4 * my + kBlkY[blk];
     int tc = 0;
     if (cbp_luma) {
-      write_block(bw, ac[blk], 15, f.nc(f.tc_y, bx, by, 4, 0));
+      write_block(bw, ac[blk], 15, f.nc(f.tc_y, bx, by, 4, slice_id));
       for (int k = 0; k < 15; ++k) tc += ac[blk][k] != 0;
     }
     f.tc_y[size_t(by) * 4 * f.mbw + bx] = uint8_t(tc);
@@ -839,19 +1323,453 @@ void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, c
       const int bx = 2 * mx + (blk & 1), by = 2 * my + (blk >> 1);
       int tc = 0;
       if (cbp_chroma == 2) {
-        write_block(bw, cac[c][blk], 15, f.nc(tcs, bx, by, 2, 0));
+        write_block(bw, cac[c][blk], 15, f.nc(tcs, bx, by, 2, slice_id));
         for (int k = 0; k < 15; ++k) tc += cac[c][blk][k] != 0;
       }
       tcs[size_t(by) * 2 * f.mbw + bx] = uint8_t(tc);
     }
   }
   // ---- reconstruction (the decoder's output)
-  f.slice[size_t(my) * f.mbw + mx] = 0;
+  // (slice-parallel callers pre-set the slice ids: no write then, so other slices may read them)
+  if (f.slice[size_t(my) * f.mbw + mx] != slice_id) f.slice[size_t(my) * f.mbw + mx] = slice_id;
+  f.mbqp[size_t(my) * f.mbw + mx] = uint8_t(qp);
+  for (int b = 0; b < 16; ++b) f.i4mode[size_t(4 * my + b / 4) * 4 * f.mbw + 4 * mx + b % 4] = -1;
   recon_luma16(f, mx, my, best, dc, ac, qp);
   for (int c = 0; c < 2; ++c) recon_chroma(*cpl[c], Wc, mx, my, cpred[c], cdc[c], cac[c], qpc);
 }
 
-void write_sps(BitWriter& s, int width, int height) {
+
+// ------------------------------------------------------------------------------------ P encoder
+const int kLambda16[52] = {4,   4,   5,   5,   6,   7,   7,   8,   9,   10,  12,  13,  15,  17,  19,  21,  23,  26,
+                           30,  33,  37,  42,  47,  53,  59,  66,  74,  83,  94,  105, 118, 132, 149, 167, 187, 210,
+                           236, 265, 297, 334, 375, 421, 472, 530, 595, 668, 749, 841, 944, 1060, 1189, 1335};
+
+inline int ue_bits(uint32_t v) {
+  int n = 0;
+  for (uint32_t x = v + 1; x > 1; x >>= 1) ++n;
+  return 2 * n + 1;
+}
+inline int se_bits(int v) { return ue_bits(v > 0 ? uint32_t(2 * v - 1) : uint32_t(-2 * v)); }
+
+template <class Fn>
+void parallel_for(int n, int threads, Fn fn) {
+  const int nt = std::max(1, std::min(threads, n));
+  std::vector<std::thread> pool;
+  std::vector<std::string> errs(static_cast<size_t>(nt));
+  auto work = [&](int t) {
+    try {
+      for (int i = t; i < n; i += nt) fn(i);
+    } catch (const std::exception& e) {
+      errs[size_t(t)] = e.what();
+    }
+  };
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw std::runtime_error(e);
+}
+
+// Half-sample planes of a reference picture with a `pad`-sample margin (the decoder's clamped-
+// coordinate 6-tap values, so quarter samples from them equal mc_luma's): motion search only.
+struct HalfPel {
+  int W = 0, H = 0, pad = 0, stride = 0;
+  std::vector<uint8_t> g, b, h, j;
+  void build(const Frame& r, int pad_, int threads) {
+    W = r.W;
+    H = r.H;
+    pad = pad_;
+    stride = W + 2 * pad;
+    const int rows = H + 2 * pad;
+    // edge-replicated copy with 3 more samples of margin: every tap is a plain load, and rows or
+    // columns outside the picture equal the clamped ones (so do the sums built from them)
+    const int e = pad + 3, es = W + 2 * e, erows = H + 2 * e;
+    std::vector<uint8_t> ext(size_t(es) * erows);
+    for (int yy = 0; yy < erows; ++yy) {
+      const uint8_t* src = r.y.data() + size_t(std::clamp(yy - e, 0, H - 1)) * W;
+      uint8_t* d = ext.data() + size_t(yy) * es;
+      std::memset(d, src[0], size_t(e));
+      std::memcpy(d + e, src, size_t(W));
+      std::memset(d + e + W, src[W - 1], size_t(e));
+    }
+    auto X = [&](int x, int y) { return int(ext[size_t(y + e) * es + x + e]); };
+    g.assign(size_t(stride) * rows, 0);
+    b = h = j = g;
+    auto clip = [](int v) { return uint8_t(v < 0 ? 0 : v > 255 ? 255 : v); };
+    // unclipped horizontal sums for rows -pad-2 .. H+pad+2 (j's vertical taps reach 3 rows out)
+    const int b1rows = rows + 5;
+    std::vector<int> b1(size_t(stride) * b1rows);
+    const int bands = std::max(1, threads) * 4;
+    parallel_for(bands, threads, [&](int t) {
+      for (int k = t * b1rows / bands; k < (t + 1) * b1rows / bands; ++k) {
+        const int yy = k - pad - 2;
+        int* o = b1.data() + size_t(k) * stride;
+        for (int xx = -pad; xx < W + pad; ++xx)
+          o[xx + pad] = tap6(X(xx - 2, yy), X(xx - 1, yy), X(xx, yy), X(xx + 1, yy), X(xx + 2, yy), X(xx + 3, yy));
+      }
+    });
+    parallel_for(bands, threads, [&](int t) {
+      for (int yy = -pad + t * rows / bands; yy < -pad + (t + 1) * rows / bands; ++yy) {
+        const int* r0 = b1.data() + size_t(yy + pad) * stride;   // b1 row yy - 2
+        const size_t o0 = size_t(yy + pad) * stride;
+        for (int xx = -pad; xx < W + pad; ++xx) {
+          const size_t o = o0 + xx + pad;
+          const int c = xx + pad;
+          g[o] = uint8_t(X(xx, yy));
+          b[o] = clip((r0[2 * stride + c] + 16) >> 5);
+          h[o] = clip(
+              (tap6(X(xx, yy - 2), X(xx, yy - 1), X(xx, yy), X(xx, yy + 1), X(xx, yy + 2), X(xx, yy + 3)) + 16) >> 5);
+          j[o] = clip((tap6(r0[c], r0[stride + c], r0[2 * stride + c], r0[3 * stride + c], r0[4 * stride + c],
+                            r0[5 * stride + c]) + 512) >> 10);
+        }
+      }
+    });
+  }
+  // SAD of the 16x16 source block against the prediction at integer position (x0, y0) + quarter
+  // vector (mvx, mvy): every quarter sample is the rounded mean of two planes (8-250..8-261; full
+  // and half positions average a plane with itself).  The caller keeps the block in the margin.
+  int sad16(const uint8_t* src, int sstride, int x0, int y0, int mvx, int mvy) const {
+    const int X0 = x0 + (mvx >> 2), Y0 = y0 + (mvy >> 2), cs = (mvy & 3) * 4 + (mvx & 3);
+    struct Pair { char a; int ax, ay; char b; int bx, by; };
+    static const Pair kCases[16] = {{'g', 0, 0, 'g', 0, 0}, {'g', 0, 0, 'b', 0, 0}, {'b', 0, 0, 'b', 0, 0},
+                                    {'g', 1, 0, 'b', 0, 0}, {'g', 0, 0, 'h', 0, 0}, {'b', 0, 0, 'h', 0, 0},
+                                    {'b', 0, 0, 'j', 0, 0}, {'b', 0, 0, 'h', 1, 0}, {'h', 0, 0, 'h', 0, 0},
+                                    {'h', 0, 0, 'j', 0, 0}, {'j', 0, 0, 'j', 0, 0}, {'j', 0, 0, 'h', 1, 0},
+                                    {'g', 0, 1, 'h', 0, 0}, {'h', 0, 0, 'b', 0, 1}, {'j', 0, 0, 'b', 0, 1},
+                                    {'h', 1, 0, 'b', 0, 1}};
+    const Pair& pc = kCases[cs];
+    auto plane = [&](char c) -> const std::vector<uint8_t>& { return c == 'g' ? g : c == 'b' ? b : c == 'h' ? h : j; };
+    const uint8_t* A = plane(pc.a).data() + size_t(Y0 + pc.ay + pad) * stride + X0 + pc.ax + pad;
+    const uint8_t* B = plane(pc.b).data() + size_t(Y0 + pc.by + pad) * stride + X0 + pc.bx + pad;
+    int s = 0;
+    for (int yy = 0; yy < 16; ++yy) {
+      const uint8_t* a = A + size_t(yy) * stride;
+      const uint8_t* bb = B + size_t(yy) * stride;
+      const uint8_t* q = src + size_t(yy) * sstride;
+      for (int xx = 0; xx < 16; ++xx) s += std::abs(int(q[xx]) - ((int(a[xx]) + int(bb[xx]) + 1) >> 1));
+    }
+    return s;
+  }
+};
+
+struct Lcg {                   // deterministic decisions of the scripted (decoder-coverage) mode
+  uint32_t s;
+  uint32_t next() {
+    s = s * 1664525u + 1013904223u;
+    return s >> 8;
+  }
+  int below(int n) { return int(next() % uint32_t(n)); }
+};
+
+// residual of an inter macroblock -> levels (inter dead zone 1/6), cbp; returns cbp
+int quant_inter(const uint8_t* sy, int W, const uint8_t* const* csrc, int Wc, const uint8_t* py,
+                const uint8_t (*pc)[64],
+                int qp, int qpc, int (*coef)[16], int (*cdc)[4], int (*cac)[4][15]) {
+  const int qp6 = qp % 6, qbits = 15 + qp / 6, fq = (1 << qbits) / 6;
+  int cbp = 0;
+  for (int blk = 0; blk < 16; ++blk) {
+    const int bx = kBlkX[blk], by = kBlkY[blk];
+    int res[16], w[16];
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x)
+        res[4 * y + x] = int(sy[(4 * by + y) * W + 4 * bx + x]) - int(py[16 * (4 * by + y) + 4 * bx + x]);
+    fwd4x4(res, w);
+    bool any = false;
+    for (int k = 0; k < 16; ++k) {
+      const int rp = kZigzag[k];
+      coef[blk][k] = quant(w[rp], kMF[qp6][pos_class(rp)], fq, qbits);
+      any |= coef[blk][k] != 0;
+    }
+    if (any) cbp |= 1 << (blk / 4);
+  }
+  for (int blk = 0; blk < 16; ++blk)
+    if (!(cbp & (1 << (blk / 4)))) std::memset(coef[blk], 0, sizeof(int) * 16);
+  const int qc6 = qpc % 6, qcbits = 15 + qpc / 6, fqc = (1 << qcbits) / 6;
+  bool c_dc = false, c_ac = false;
+  for (int c = 0; c < 2; ++c) {
+    int Wb[4][16];
+    for (int blk = 0; blk < 4; ++blk) {
+      const int bx = blk & 1, by = blk >> 1;
+      int res[16];
+      for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x)
+          res[4 * y + x] = int(csrc[c][(4 * by + y) * Wc + 4 * bx + x]) - int(pc[c][8 * (4 * by + y) + 4 * bx + x]);
+      fwd4x4(res, Wb[blk]);
+      for (int k = 0; k < 15; ++k) {
+        const int rp = kZigzag[k + 1];
+        cac[c][blk][k] = quant(Wb[blk][rp], kMF[qc6][pos_class(rp)], fqc, qcbits);
+        c_ac |= cac[c][blk][k] != 0;
+      }
+    }
+    const int d0 = Wb[0][0], d1 = Wb[1][0], d2 = Wb[2][0], d3 = Wb[3][0];
+    const int hd[4] = {d0 + d1 + d2 + d3, d0 - d1 + d2 - d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3};
+    for (int k = 0; k < 4; ++k) {
+      cdc[c][k] = quant(hd[k], kMF[qc6][0], 2 * fqc, qcbits + 1);
+      c_dc |= cdc[c][k] != 0;
+    }
+  }
+  const int cbp_chroma = c_ac ? 2 : c_dc ? 1 : 0;
+  if (cbp_chroma < 2) std::memset(cac, 0, sizeof(int) * 120);
+  if (cbp_chroma == 0) std::memset(cdc, 0, sizeof(int) * 8);
+  return cbp | (cbp_chroma << 4);
+}
+
+// cbp -> me(v) codeNum for inter macroblocks
+int inter_cbp_code(int cbp) {
+  for (int k = 0; k < 48; ++k)
+    if (kInterCbp[k] == cbp) return k;
+  return 0;
+}
+
+// residual syntax of an inter macroblock (the cbp, qp delta and blocks) + TotalCoeff bookkeeping
+void write_inter_residual(BitWriter& bw, Frame& f, int mx, int my, int cbp, int qp_delta, const int (*coef)[16],
+                          const int (*cdc)[4], const int (*cac)[4][15], int slice_id) {
+  bw.ue(uint32_t(inter_cbp_code(cbp)));
+  if (cbp) bw.se(qp_delta);
+  for (int blk = 0; blk < 16; ++blk) {
+    const int bx = 4 * mx + kBlkX[blk], by = 4 * my + kBlkY[blk];
+    int tc = 0;
+    if (cbp & (1 << (blk / 4))) {
+      write_block(bw, coef[blk], 16, f.nc(f.tc_y, bx, by, 4, slice_id));
+      for (int k = 0; k < 16; ++k) tc += coef[blk][k] != 0;
+    }
+    f.tc_y[size_t(by) * 4 * f.mbw + bx] = uint8_t(tc);
+  }
+  if (cbp >> 4)
+    for (int c = 0; c < 2; ++c) write_block(bw, cdc[c], 4, -1);
+  for (int c = 0; c < 2; ++c) {
+    std::vector<uint8_t>& tcs = c ? f.tc_cr : f.tc_cb;
+    for (int blk = 0; blk < 4; ++blk) {
+      const int bx = 2 * mx + (blk & 1), by = 2 * my + (blk >> 1);
+      int tc = 0;
+      if ((cbp >> 4) == 2) {
+        write_block(bw, cac[c][blk], 15, f.nc(tcs, bx, by, 2, slice_id));
+        for (int k = 0; k < 15; ++k) tc += cac[c][blk][k] != 0;
+      }
+      tcs[size_t(by) * 2 * f.mbw + bx] = uint8_t(tc);
+    }
+  }
+}
+
+struct PEncCtx {
+  const uint8_t *y, *cb, *cr;
+  int qp;
+  const std::vector<RefPic>& list;             // RefPicList0 as the decoder will build it
+  const std::vector<const HalfPel*>& hp;       // half-sample planes per list entry (production search)
+  uint32_t seed;                                // 0: production decisions; else scripted
+};
+
+// prediction of a macroblock from its assigned motion into py / pc (the decoder's own MC)
+void inter_pred_mb(const Frame& f, const std::vector<RefPic>& list, int mx, int my, bool uniform, uint8_t* py,
+                   uint8_t (*pc)[64]) {
+  if (uniform) {
+    const size_t i = size_t(4 * my) * 4 * f.mbw + 4 * mx;
+    const Frame& r = *list[size_t(f.ref[i])].f;
+    mc_luma(r, 16 * mx, 16 * my, f.mvx[i], f.mvy[i], 16, 16, py, 16);
+    mc_chroma(r.cb, r.W / 2, r.H / 2, 8 * mx, 8 * my, f.mvx[i], f.mvy[i], 8, 8, pc[0], 8);
+    mc_chroma(r.cr, r.W / 2, r.H / 2, 8 * mx, 8 * my, f.mvx[i], f.mvy[i], 8, 8, pc[1], 8);
+  } else {
+    predict_inter(f, list, mx, my, py, pc[0], pc[1]);
+  }
+}
+
+// Production motion search for one 16x16 macroblock (ref 0): integer diamond around the predictor
+// and zero, then half- and quarter-sample refinement; cost = SAD + lambda * mvd bits.
+void search16(const PEncCtx& c, const Frame& f, int mx, int my, int pmx, int pmy, int& bmx, int& bmy) {
+  const HalfPel& hp = *c.hp[0];
+  const int W = f.W, x0 = 16 * mx, y0 = 16 * my, lam = kLambda16[c.qp];
+  const uint8_t* src = c.y + size_t(y0) * W + x0;
+  const int lo_x = 4 * (-x0 - hp.pad + 2), hi_x = 4 * (W + hp.pad - 19 - x0);
+  const int lo_y = 4 * (-y0 - hp.pad + 2), hi_y = 4 * (f.H + hp.pad - 19 - y0);
+  auto cost = [&](int vx, int vy) {
+    if (vx < lo_x || vx > hi_x || vy < lo_y || vy > hi_y) return 1 << 30;
+    return hp.sad16(src, W, x0, y0, vx, vy) * 16 + lam * (se_bits(vx - pmx) + se_bits(vy - pmy));
+  };
+  int best = 1 << 30;
+  auto consider = [&](int vx, int vy) {
+    const int cst = cost(vx, vy);
+    if (cst < best) {
+      best = cst;
+      bmx = vx;
+      bmy = vy;
+    }
+  };
+  bmx = bmy = 0;
+  consider(0, 0);
+  consider(pmx & ~3, pmy & ~3);
+  for (int it = 0; it < 24; ++it) {                    // integer small diamond
+    const int cx = bmx, cy = bmy;
+    for (const auto& d : {std::pair<int, int>{-4, 0}, {4, 0}, {0, -4}, {0, 4}}) consider(cx + d.first, cy + d.second);
+    if (cx == bmx && cy == bmy) break;
+  }
+  for (int step : {2, 1}) {                             // half, then quarter samples
+    const int cx = bmx, cy = bmy;
+    for (int dy = -step; dy <= step; dy += step)
+      for (int dx = -step; dx <= step; dx += step)
+        if (dx || dy) consider(cx + dx, cy + dy);
+  }
+}
+
+// One P slice (macroblocks [first, last)) into bw; updates f (motion, recon before deblocking)
+void encode_p_slice_data(BitWriter& bw, Frame& f, const PEncCtx& c, int first, int last, int slice_id, Lcg& rng) {
+  const int W = f.W, Wc = f.W / 2, nref = int(c.list.size());
+  int qp = c.qp, run = 0;
+  for (int mb = first; mb < last; ++mb) {
+    const int mx = mb % f.mbw, my = mb / f.mbw;
+    const uint8_t* sy = c.y + size_t(16 * my) * W + 16 * mx;
+    const uint8_t* csrc[2] = {c.cb + size_t(8 * my) * Wc + 8 * mx, c.cr + size_t(8 * my) * Wc + 8 * mx};
+    MvPred mp{f, mx, my, slice_id};
+    int coef[16][16], cdc[2][4], cac[2][4][15];
+    uint8_t py[256], pc[2][64];
+    int kind;                   // 0 skip, 1 16x16, 2 16x8, 3 8x16, 4 8x8, 5 8x8ref0, 6 intra
+    if (c.seed) {
+      const int r = rng.below(16);
+      kind = r < 3 ? 0 : r < 6 ? 1 : r < 8 ? 2 : r < 10 ? 3 : r < 13 ? 4 : r < 14 ? (nref > 1 ? 5 : 4) : 6;
+    } else {
+      kind = -1;
+    }
+    // ---- production: skip test, then search; intra when clearly better
+    int smx = 0, smy = 0;
+    mp.skip(smx, smy);
+    if (kind < 0) {
+      set_motion(f, mp, mx, my, 0, 0, 4, 4, 0, c.list[0].id, smx, smy);
+      inter_pred_mb(f, c.list, mx, my, true, py, pc);
+      const int qpc = kChromaQp[qp];
+      const int cbp = quant_inter(sy, W, csrc, Wc, py, pc, qp, qpc, coef, cdc, cac);
+      if (cbp == 0) {
+        kind = 0;
+      } else {
+        mp.done = 0;
+        int pmx, pmy, bmx, bmy;
+        mp.pred(0, 0, 4, 0, 0, pmx, pmy);
+        search16(c, f, mx, my, pmx, pmy, bmx, bmy);
+        set_motion(f, mp, mx, my, 0, 0, 4, 4, 0, c.list[0].id, bmx, bmy);
+        inter_pred_mb(f, c.list, mx, my, true, py, pc);
+        const int inter_sad = sad(sy, W, py, 16);
+        // intra 16x16 DC / V / H / plane estimate on the current (unfiltered) reconstruction
+        const Nb nb = f.nb(mx, my, slice_id);
+        int intra_sad = 1 << 30;
+        uint8_t ip[256];
+        for (int m : {0, 1, 2, 3}) {
+          if ((m == 0 && !nb.top) || (m == 1 && !nb.left) || (m == 3 && !(nb.top && nb.left && nb.topleft))) continue;
+          pred16(f.y.data(), W, mx * 16, my * 16, nb, m, ip);
+          intra_sad = std::min(intra_sad, sad(sy, W, ip, 16));
+        }
+        kind = intra_sad + 16 * 24 < inter_sad ? 6 : 1;
+      }
+    }
+    if (kind == 0) {                                     // P_Skip
+      mp.done = 0;
+      set_motion(f, mp, mx, my, 0, 0, 4, 4, 0, c.list[0].id, smx, smy);
+      inter_pred_mb(f, c.list, mx, my, true, py, pc);
+      std::memset(coef, 0, sizeof(coef));
+      std::memset(cdc, 0, sizeof(cdc));
+      std::memset(cac, 0, sizeof(cac));
+      for (int b = 0; b < 16; ++b) {
+        const size_t i = size_t(4 * my + b / 4) * 4 * f.mbw + 4 * mx + b % 4;
+        f.tc_y[i] = 0;
+        f.i4mode[i] = -1;
+      }
+      for (int b = 0; b < 4; ++b) {
+        const size_t i = size_t(2 * my + b / 2) * 2 * f.mbw + 2 * mx + b % 2;
+        f.tc_cb[i] = f.tc_cr[i] = 0;
+      }
+      recon_luma4x4(f, mx, my, py, coef, qp);
+      const int qpc = kChromaQp[qp];
+      for (int cc = 0; cc < 2; ++cc) recon_chroma(cc ? f.cr : f.cb, Wc, mx, my, pc[cc], cdc[cc], cac[cc], qpc);
+      f.intra[mb] = 0;
+      f.mbqp[mb] = uint8_t(qp);
+      ++run;
+      continue;
+    }
+    bw.ue(uint32_t(run));
+    run = 0;
+    if (kind == 6) {                                     // Intra_16x16 in a P slice (mb_type 5 + I type)
+      mark_intra(f, mx, my);
+      encode_mb(bw, f, c.y, c.cb, c.cr, mx, my, qp, slice_id, 5);
+      continue;
+    }
+    // ---- inter syntax: partitions, then refs, then mvds (motion assigned in decoding order)
+    mp.done = 0;
+    const int mb_type = kind - 1;                        // 0 16x16, 1 16x8, 2 8x16, 3 8x8, 4 8x8ref0
+    bw.ue(uint32_t(mb_type));
+    auto rnd_mv = [&](int p) { return p + rng.below(97) - 48; };
+    auto clamp_mv = [&](int v, int lo, int hi) { return std::clamp(v, lo, hi); };
+    if (mb_type <= 2) {
+      const int np = mb_type == 0 ? 1 : 2;
+      int refs[2] = {0, 0};
+      if (c.seed)
+        for (int p = 0; p < np; ++p) refs[p] = rng.below(nref);
+      if (nref > 1)
+        for (int p = 0; p < np; ++p) {
+          if (nref == 2) bw.put(refs[p] ? 0u : 1u, 1);
+          else bw.ue(uint32_t(refs[p]));
+        }
+      for (int p = 0; p < np; ++p) {
+        int bx = 0, by = 0, bwid = 4, bh = 4, shape = 0;
+        if (mb_type == 1) { by = 2 * p; bh = 2; shape = 1 + p; }
+        if (mb_type == 2) { bx = 2 * p; bwid = 2; shape = 3 + p; }
+        int pmx, pmy, vx, vy;
+        mp.pred(bx, by, bwid, refs[p], shape, pmx, pmy);
+        if (c.seed) {
+          vx = clamp_mv(rnd_mv(pmx), -4 * (16 * mx + 40), 4 * (W - 16 * mx + 24));
+          vy = clamp_mv(rnd_mv(pmy), -4 * (16 * my + 40), 4 * (f.H - 16 * my + 24));
+        } else {
+          vx = f.mvx[size_t(4 * my) * 4 * f.mbw + 4 * mx];   // the searched vector (kept by set_motion)
+          vy = f.mvy[size_t(4 * my) * 4 * f.mbw + 4 * mx];
+        }
+        bw.se(vx - pmx);
+        bw.se(vy - pmy);
+        set_motion(f, mp, mx, my, bx, by, bwid, bh, refs[p], c.list[size_t(refs[p])].id, vx, vy);
+      }
+    } else {
+      int sub[4], refs[4] = {0, 0, 0, 0};
+      for (int s = 0; s < 4; ++s) {
+        sub[s] = rng.below(4);
+        bw.ue(uint32_t(sub[s]));
+      }
+      if (mb_type == 3 && nref > 1)
+        for (int s = 0; s < 4; ++s) {
+          refs[s] = rng.below(nref);
+          if (nref == 2) bw.put(refs[s] ? 0u : 1u, 1);
+          else bw.ue(uint32_t(refs[s]));
+        }
+      for (int s = 0; s < 4; ++s) {
+        const int sx = 2 * (s & 1), sy2 = 2 * (s >> 1);
+        const int n = sub[s] == 0 ? 1 : sub[s] == 3 ? 4 : 2;
+        const int pw = sub[s] == 0 || sub[s] == 1 ? 2 : 1, ph = sub[s] == 0 || sub[s] == 2 ? 2 : 1;
+        for (int k = 0; k < n; ++k) {
+          const int bx = sx + (sub[s] == 2 || sub[s] == 3 ? (k & 1) : 0);
+          const int by = sy2 + (sub[s] == 1 ? k : sub[s] == 3 ? (k >> 1) : 0);
+          int pmx, pmy;
+          mp.pred(bx, by, pw, refs[s], 0, pmx, pmy);
+          const int vx = clamp_mv(rnd_mv(pmx), -4 * (16 * mx + 40), 4 * (W - 16 * mx + 24));
+          const int vy = clamp_mv(rnd_mv(pmy), -4 * (16 * my + 40), 4 * (f.H - 16 * my + 24));
+          bw.se(vx - pmx);
+          bw.se(vy - pmy);
+          set_motion(f, mp, mx, my, bx, by, pw, ph, refs[s], c.list[size_t(refs[s])].id, vx, vy);
+        }
+      }
+    }
+    int qp_delta = 0;
+    inter_pred_mb(f, c.list, mx, my, mb_type == 0, py, pc);
+    if (c.seed) qp_delta = rng.below(4) == 0 ? rng.below(9) - 4 : 0;
+    int qpm = std::clamp(qp + qp_delta, 0, 51);
+    int cbp = quant_inter(sy, W, csrc, Wc, py, pc, qpm, kChromaQp[qpm], coef, cdc, cac);
+    if (!cbp) qpm = qp;                                  // no mb_qp_delta without residual
+    write_inter_residual(bw, f, mx, my, cbp, qpm - qp, coef, cdc, cac, slice_id);
+    qp = qpm;
+    for (int b = 0; b < 16; ++b) f.i4mode[size_t(4 * my + b / 4) * 4 * f.mbw + 4 * mx + b % 4] = -1;
+    recon_luma4x4(f, mx, my, py, coef, qp);
+    const int qpc = kChromaQp[qp];
+    for (int cc = 0; cc < 2; ++cc) recon_chroma(cc ? f.cr : f.cb, Wc, mx, my, pc[cc], cdc[cc], cac[cc], qpc);
+    f.intra[mb] = 0;
+    f.mbqp[mb] = uint8_t(qp);
+  }
+  if (run) bw.ue(uint32_t(run));
+}
+
+void write_sps(BitWriter& s, int width, int height, int max_refs = 1) {
   const int mbw = (width + 15) / 16, mbh = (height + 15) / 16;
   s.put(66, 8);    // profile_idc: Baseline
   s.put(0xC0, 8);  // constraint_set0/1 -> Constrained Baseline
@@ -859,7 +1777,7 @@ void write_sps(BitWriter& s, int width, int height) {
   s.ue(0);         // seq_parameter_set_id
   s.ue(0);         // log2_max_frame_num_minus4
   s.ue(2);         // pic_order_cnt_type
-  s.ue(1);         // max_num_ref_frames
+  s.ue(uint32_t(max_refs));  // max_num_ref_frames
   s.put(0, 1);     // gaps_in_frame_num_value_allowed_flag
   s.ue(mbw - 1);
   s.ue(mbh - 1);
@@ -881,9 +1799,10 @@ void write_sps(BitWriter& s, int width, int height) {
 
 }  // namespace
 
-void parameter_sets(int width, int height, int qp, std::string& sps, std::string& pps) {
+void parameter_sets(int width, int height, int qp, std::string& sps, std::string& pps, int max_refs) {
+  if (max_refs < 1 || max_refs > 16) throw std::invalid_argument("h264: max_refs must be in [1, 16]");
   BitWriter s;
-  write_sps(s, width, height);
+  write_sps(s, width, height, max_refs);
   sps = std::string(1, char(0x67)) + add_emulation_prevention(s.out);
   BitWriter p;
   p.ue(0);  // pic_parameter_set_id
@@ -931,6 +1850,162 @@ std::string encode_idr(const uint8_t* y, const uint8_t* cb, const uint8_t* cr, i
   return std::string(1, char(0x65)) + add_emulation_prevention(bw.out);
 }
 
+namespace {
+
+void write_slice_header(BitWriter& bw, int first_mb, bool idr, bool p, int frame_num, int idr_pic_id, int nal_ref_idc,
+                        int nref_active, const std::vector<std::pair<int, int>>& mods, const SliceDb& db) {
+  bw.ue(uint32_t(first_mb));
+  bw.ue(p ? 5 : 7);                    // slice_type: every slice of the picture has this type
+  bw.ue(0);                            // pic_parameter_set_id
+  bw.put(uint32_t(frame_num) & 15u, 4);
+  if (idr) bw.ue(uint32_t(idr_pic_id & 1));
+  if (p) {
+    if (nref_active != 1) {
+      bw.put(1, 1);                    // num_ref_idx_active_override_flag
+      bw.ue(uint32_t(nref_active - 1));
+    } else {
+      bw.put(0, 1);
+    }
+    bw.put(mods.empty() ? 0u : 1u, 1);  // ref_pic_list_modification_flag_l0
+    if (!mods.empty()) {
+      for (const auto& m : mods) {
+        bw.ue(uint32_t(m.first));
+        bw.ue(uint32_t(m.second));
+      }
+      bw.ue(3);
+    }
+  }
+  if (nal_ref_idc) {
+    if (idr) {
+      bw.put(0, 1);                    // no_output_of_prior_pics_flag
+      bw.put(0, 1);                    // long_term_reference_flag
+    } else {
+      bw.put(0, 1);                    // adaptive_ref_pic_marking_mode_flag: sliding window
+    }
+  }
+  bw.se(0);                            // slice_qp_delta
+  bw.ue(uint32_t(db.idc));
+  if (db.idc != 1) {
+    bw.se(db.offa / 2);
+    bw.se(db.offb / 2);
+  }
+}
+
+}  // namespace
+
+std::vector<EncodedPicture> encode_stream(int F, int W, int H, const StreamOptions& o, const LoadFn& load) {
+  if (W % 16 || H % 16 || W <= 0 || H <= 0) throw std::invalid_argument("h264: W, H must be positive multiples of 16");
+  if (o.qp < 0 || o.qp > 51) throw std::invalid_argument("h264: qp must be in [0, 51]");
+  if (o.gop < 1 || o.max_refs < 1 || o.max_refs > 16 || o.rows_per_slice < 1)
+    throw std::invalid_argument("h264: bad stream options");
+  const int mbw = W / 16, mbh = H / 16, nmb = mbw * mbh, max_fn = 16;
+  std::vector<EncodedPicture> out(static_cast<size_t>(F));
+  std::vector<RefPic> dpb;
+  std::vector<std::pair<int, std::shared_ptr<HalfPel>>> planes;   // RefPic id -> half-sample planes
+  std::vector<uint8_t> y(size_t(W) * H), cb(size_t(W) * H / 4), cr(cb.size());
+  Lcg rng{o.seed * 2654435761u + 12345u};
+  int prev_ref_fn = 0, next_id = 1, gop_idx = -1;
+  for (int i = 0; i < F; ++i) {
+    load(i, y.data(), cb.data(), cr.data());
+    const bool idr = i % o.gop == 0;
+    if (idr) {
+      ++gop_idx;
+      dpb.clear();
+      planes.clear();
+      prev_ref_fn = 0;
+    }
+    const int frame_num = idr ? 0 : (prev_ref_fn + 1) % max_fn;
+    const int nal_ref_idc = idr ? 3 : (o.seed && rng.below(5) == 0) ? 0 : 2;
+    auto f = std::make_shared<Frame>(mbw, mbh);
+    // slices: production = fixed bands of MB rows (a function of the size only); scripted = random cuts
+    std::vector<int> cuts{0};
+    if (o.seed) {
+      const int extra = rng.below(3);
+      for (int k = 0; k < extra; ++k) cuts.push_back(1 + rng.below(std::max(1, nmb - 1)));
+      std::sort(cuts.begin(), cuts.end());
+      cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    } else {
+      for (int r = o.rows_per_slice; r < mbh; r += o.rows_per_slice) cuts.push_back(r * mbw);
+    }
+    cuts.push_back(nmb);
+    const int ns = int(cuts.size()) - 1;
+    for (int sl = 0; sl < ns; ++sl)
+      for (int m = cuts[size_t(sl)]; m < cuts[size_t(sl) + 1]; ++m) f->slice[size_t(m)] = sl;
+    std::vector<SliceDb> dbs(static_cast<size_t>(ns));
+    std::vector<std::vector<std::pair<int, int>>> mods(static_cast<size_t>(ns));
+    std::vector<int> nactive(static_cast<size_t>(ns), 1);
+    std::vector<uint32_t> seeds(static_cast<size_t>(ns), 0);
+    for (int sl = 0; sl < ns; ++sl) {
+      if (o.seed) {
+        dbs[size_t(sl)] = SliceDb{rng.below(3), 2 * (rng.below(5) - 2), 2 * (rng.below(5) - 2)};
+        seeds[size_t(sl)] = rng.next() | 1u;
+        if (!idr) {
+          nactive[size_t(sl)] = 1 + rng.below(int(dpb.size()));
+          if (dpb.size() >= 2 && rng.below(2)) {
+            // move the second most recent reference to the front
+            std::vector<RefPic> l = ref_list0(dpb, frame_num, max_fn, {}, int(dpb.size()));
+            const int pn = l[1].frame_num > frame_num ? l[1].frame_num - max_fn : l[1].frame_num;
+            mods[size_t(sl)].emplace_back(0, frame_num - pn - 1);
+          }
+        }
+      } else {
+        dbs[size_t(sl)] = SliceDb{0, 0, 0};
+      }
+    }
+    std::vector<std::string> nals(static_cast<size_t>(ns));
+    std::vector<std::vector<RefPic>> lists(static_cast<size_t>(ns));
+    std::vector<std::vector<const HalfPel*>> hps(static_cast<size_t>(ns));
+    if (!idr) {
+      for (int sl = 0; sl < ns; ++sl) {
+        lists[size_t(sl)] = ref_list0(dpb, frame_num, max_fn, mods[size_t(sl)], nactive[size_t(sl)]);
+        for (const RefPic& r : lists[size_t(sl)])
+          for (auto& pp : planes)
+            if (pp.first == r.id) hps[size_t(sl)].push_back(pp.second.get());
+      }
+    }
+    parallel_for(ns, o.threads, [&](int sl) {
+      BitWriter bw;
+      write_slice_header(bw, cuts[size_t(sl)], idr, !idr, frame_num, gop_idx, nal_ref_idc, nactive[size_t(sl)],
+                         mods[size_t(sl)], dbs[size_t(sl)]);
+      if (idr) {
+        for (int m = cuts[size_t(sl)]; m < cuts[size_t(sl) + 1]; ++m)
+          encode_mb(bw, *f, y.data(), cb.data(), cr.data(), m % mbw, m / mbw, o.qp, sl, 0);
+      } else {
+        Lcg srng{seeds[size_t(sl)]};
+        const PEncCtx c{y.data(), cb.data(), cr.data(), o.qp, lists[size_t(sl)], hps[size_t(sl)], o.seed};
+        encode_p_slice_data(bw, *f, c, cuts[size_t(sl)], cuts[size_t(sl) + 1], sl, srng);
+      }
+      bw.trailing();
+      const char hdr = char(idr ? 0x65 : (nal_ref_idc << 5) | 1);
+      nals[size_t(sl)] = std::string(1, hdr) + add_emulation_prevention(bw.out);
+    });
+    deblock(*f, dbs, 0, o.threads);
+    EncodedPicture& ep = out[size_t(i)];
+    ep.nals = std::move(nals);
+    if (o.keep_recon) {
+      ep.y = f->y;
+      ep.cb = f->cb;
+      ep.cr = f->cr;
+    }
+    if (nal_ref_idc) {
+      const int id = next_id++;
+      prev_ref_fn = mark_reference(dpb, RefPic{f, id, frame_num}, max_fn, o.max_refs, false, {});
+      planes.erase(std::remove_if(planes.begin(), planes.end(),
+                                  [&](const std::pair<int, std::shared_ptr<HalfPel>>& pp) {
+                                    return std::none_of(dpb.begin(), dpb.end(),
+                                                         [&](const RefPic& r) { return r.id == pp.first; });
+                                  }),
+                   planes.end());
+      if (!o.seed) {                       // production search reads half-sample planes of ref 0
+        auto hp = std::make_shared<HalfPel>();
+        hp->build(*f, 32, o.threads);
+        planes.emplace_back(id, hp);
+      }
+    }
+  }
+  return out;
+}
+
 bool tables_prefix_free() {
   try {
     (void)tables();
@@ -951,14 +2026,15 @@ namespace {
 
 struct Sps {
   bool ok = false;
-  int mbw = 0, mbh = 0, log2_max_frame_num = 4, poc_type = 0, log2_max_poc_lsb = 4;
-  bool delta_pic_order_always_zero = false;
+  int mbw = 0, mbh = 0, log2_max_frame_num = 4, poc_type = 0, log2_max_poc_lsb = 4, max_refs = 1;
+  bool delta_pic_order_always_zero = false, gaps_allowed = false;
   int crop_l = 0, crop_r = 0, crop_t = 0, crop_b = 0;
 };
 struct Pps {
   bool ok = false;
-  int sps_id = 0, init_qp = 26, chroma_qp_offset = 0;
+  int sps_id = 0, init_qp = 26, chroma_qp_offset = 0, num_ref_default = 1;
   bool bottom_field_pic_order = false, deblocking_control = false, redundant_pic_cnt = false;
+  bool weighted_pred = false, constrained_intra = false;
 };
 
 Sps parse_sps(BitReader& br) {
@@ -970,7 +2046,7 @@ Sps parse_sps(BitReader& br) {
   if (id != 0) throw std::runtime_error("h264: only seq_parameter_set_id 0 is supported");
   if (profile == 100 || profile == 110 || profile == 122 || profile == 244 || profile == 44 || profile == 83 ||
       profile == 86 || profile == 118 || profile == 128)
-    throw std::runtime_error("h264: High / scalable profiles are not supported (Constrained Baseline intra only)");
+    throw std::runtime_error("h264: High / scalable profiles are not supported (Baseline only)");
   const uint32_t lmf = br.ue(), poc_type = br.ue();
   if (lmf > 12 || poc_type > 2) throw std::runtime_error("h264: SPS field out of range");
   s.log2_max_frame_num = int(lmf) + 4;
@@ -984,10 +2060,13 @@ Sps parse_sps(BitReader& br) {
     br.se();
     br.se();
     const uint32_t n = br.ue();
+    if (n > 255) throw std::runtime_error("h264: SPS field out of range");
     for (uint32_t i = 0; i < n; ++i) br.se();
   }
-  br.ue();    // max_num_ref_frames
-  br.u(1);    // gaps
+  const uint32_t refs = br.ue();
+  if (refs > 16) throw std::runtime_error("h264: max_num_ref_frames out of range");
+  s.max_refs = std::max(1, int(refs));
+  s.gaps_allowed = br.u(1);
   const uint32_t mbw = br.ue(), mbh = br.ue();
   if (mbw >= 256 || mbh >= 256 || (uint64_t(mbw) + 1) * (mbh + 1) > 36864)   // <= 4096 x 2304 (level 5.1)
     throw std::runtime_error("h264: picture too large");
@@ -1016,9 +2095,11 @@ Pps parse_pps(BitReader& br) {
   if (br.u(1)) throw std::runtime_error("h264: CABAC is not supported");
   p.bottom_field_pic_order = br.u(1);
   if (br.ue() != 0) throw std::runtime_error("h264: slice groups (FMO) are not supported");
+  const uint32_t l0 = br.ue();
   br.ue();
-  br.ue();
-  br.u(1);
+  if (l0 > 31) throw std::runtime_error("h264: PPS field out of range");
+  p.num_ref_default = int(l0) + 1;
+  p.weighted_pred = br.u(1);
   br.u(2);
   const int64_t init_qp = 26 + int64_t(br.se());   // int64: a hostile se() must not overflow
   br.se();
@@ -1026,26 +2107,38 @@ Pps parse_pps(BitReader& br) {
   if (init_qp < 0 || init_qp > 51 || cqo < -12 || cqo > 12) throw std::runtime_error("h264: PPS field out of range");
   p.init_qp = int(init_qp);
   p.chroma_qp_offset = int(cqo);
-  if (p.init_qp < 0 || p.init_qp > 51 || p.chroma_qp_offset < -12 || p.chroma_qp_offset > 12)
-    throw std::runtime_error("h264: PPS field out of range");
   p.deblocking_control = br.u(1);
-  br.u(1);  // constrained_intra_pred_flag (intra-only streams: no effect)
+  p.constrained_intra = br.u(1);
   p.redundant_pic_cnt = br.u(1);
   if (br.more_rbsp_data()) throw std::runtime_error("h264: PPS extensions (8x8 transform) are not supported");
   p.ok = true;
   return p;
 }
 
-void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, const Pps& pps, Frame& f,
-                  int slice_id) {
+// Parsed slice header (7.3.3) - the part the picture level needs before the macroblocks
+struct SliceHdr {
+  int first_mb = 0, slice_type = 2, frame_num = 0, nal_type = 5, nal_ref_idc = 0;
+  int num_ref_active = 1, qp = 26;
+  SliceDb db;
+  std::vector<std::pair<int, int>> list_mods;    // (modification_of_pic_nums_idc, abs_diff_pic_num_minus1)
+  std::vector<std::pair<int, int>> mmco;         // (op, difference_of_pic_nums_minus1)
+  bool adaptive_marking = false;
+};
+
+SliceHdr parse_slice_header(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, const Pps& pps, int nmb) {
+  SliceHdr h;
+  h.nal_type = nal_type;
+  h.nal_ref_idc = nal_ref_idc;
   // untrusted input: range-check every exp-golomb value as uint32 before it becomes an index
   const uint32_t first_mb_u = br.ue();
-  if (first_mb_u >= uint32_t(f.mbw) * uint32_t(f.mbh)) throw std::runtime_error("h264: first_mb_in_slice out of range");
-  const int first_mb = int(first_mb_u);
-  const int slice_type = int(br.ue() % 5);
-  if (slice_type != 2) throw std::runtime_error("h264: only I slices are supported (no P/B/SP/SI)");
-  br.ue();  // pps id
-  br.u(sps.log2_max_frame_num);
+  if (first_mb_u >= uint32_t(nmb)) throw std::runtime_error("h264: first_mb_in_slice out of range");
+  h.first_mb = int(first_mb_u);
+  h.slice_type = int(br.ue() % 5);
+  if (h.slice_type != 2 && h.slice_type != 0)
+    throw std::runtime_error("h264: only I and P slices are supported (no B/SP/SI)");
+  if (nal_type == 5 && h.slice_type != 2) throw std::runtime_error("h264: IDR picture with a P slice");
+  br.ue();  // pps id (checked == 0 by the PPS parser's single-PPS rule)
+  h.frame_num = int(br.u(sps.log2_max_frame_num));
   if (nal_type == 5) br.ue();  // idr_pic_id
   if (sps.poc_type == 0) {
     br.u(sps.log2_max_poc_lsb);
@@ -1054,219 +2147,417 @@ void decode_slice(BitReader& br, int nal_type, int nal_ref_idc, const Sps& sps, 
     br.se();
     if (pps.bottom_field_pic_order) br.se();
   }
-  if (pps.redundant_pic_cnt) br.ue();
+  if (pps.redundant_pic_cnt && br.ue() != 0) throw std::runtime_error("h264: redundant pictures are not supported");
+  h.num_ref_active = pps.num_ref_default;
+  if (h.slice_type == 0) {
+    if (br.u(1)) {                                  // num_ref_idx_active_override_flag
+      const uint32_t n = br.ue();
+      if (n > 15) throw std::runtime_error("h264: num_ref_idx_l0_active out of range");
+      h.num_ref_active = int(n) + 1;
+    }
+    if (br.u(1)) {                                  // ref_pic_list_modification_flag_l0
+      for (int guard = 0;; ++guard) {
+        if (guard > 32) throw std::runtime_error("h264: too many reference list modifications");
+        const uint32_t idc = br.ue();
+        if (idc == 3) break;
+        if (idc > 2) throw std::runtime_error("h264: bad modification_of_pic_nums_idc");
+        if (idc == 2) throw std::runtime_error("h264: long-term references are not supported");
+        const uint32_t v = br.ue();
+        if (v > (1u << 16)) throw std::runtime_error("h264: abs_diff_pic_num out of range");
+        h.list_mods.emplace_back(int(idc), int(v));
+      }
+    }
+    if (pps.weighted_pred) throw std::runtime_error("h264: weighted prediction is not supported");
+  }
   if (nal_ref_idc) {
     if (nal_type == 5) {
-      br.u(1);
-      br.u(1);
+      br.u(1);                                      // no_output_of_prior_pics_flag
+      if (br.u(1)) throw std::runtime_error("h264: long-term references are not supported");
     } else if (br.u(1)) {
-      for (;;) {
+      h.adaptive_marking = true;
+      for (int guard = 0;; ++guard) {
+        if (guard > 64) throw std::runtime_error("h264: too many memory management operations");
         const uint32_t op = br.ue();
         if (op == 0) break;
-        if (op == 1 || op == 3) br.ue();
-        if (op == 2) br.ue();
-        if (op == 3 || op == 6) br.ue();
-        if (op == 4) br.ue();
+        if (op != 1 && op != 5) throw std::runtime_error("h264: long-term memory management is not supported");
+        int v = 0;
+        if (op == 1) {
+          const uint32_t d = br.ue();
+          if (d > (1u << 16)) throw std::runtime_error("h264: difference_of_pic_nums out of range");
+          v = int(d);
+        }
+        h.mmco.emplace_back(int(op), v);
       }
     }
   }
   const int64_t qp0 = pps.init_qp + int64_t(br.se());
   if (qp0 < 0 || qp0 > 51) throw std::runtime_error("h264: slice QP out of range");
-  int qp = int(qp0);
-  auto qp_delta = [&](int q) {
-    const int d = br.se();
-    if (d < -26 || d > 25) throw std::runtime_error("h264: mb_qp_delta out of range");
-    return (q + d + 52) % 52;
-  };
+  h.qp = int(qp0);
+  h.db = SliceDb{0, 0, 0};
   if (pps.deblocking_control) {
     const uint32_t idc = br.ue();
-    if (idc != 1)
-      throw std::runtime_error("h264: in-loop deblocking is not supported (disable_deblocking_filter_idc != 1)");
-  } else {
-    throw std::runtime_error("h264: in-loop deblocking is not supported (no deblocking control in the PPS)");
-  }
-  const int nmb = f.mbw * f.mbh;
-  const int Wc = f.W / 2;
-  for (int mb = first_mb; mb < nmb; ++mb) {
-    const int mx = mb % f.mbw, my = mb / f.mbw;
-    if (f.slice[mb] != -1) throw std::runtime_error("h264: macroblock decoded twice");
-    f.slice[mb] = slice_id;
-    const Nb nb = f.nb(mx, my, slice_id);
-    const uint32_t mb_type = br.ue();
-    if (mb_type == 25) {  // I_PCM
-      while (!br.byte_aligned()) br.u(1);
-      for (int y = 0; y < 16; ++y)
-        for (int x = 0; x < 16; ++x) f.y[size_t(my * 16 + y) * f.W + mx * 16 + x] = uint8_t(br.u(8));
-      for (auto* pl : {&f.cb, &f.cr})
-        for (int y = 0; y < 8; ++y)
-          for (int x = 0; x < 8; ++x) (*pl)[size_t(my * 8 + y) * Wc + mx * 8 + x] = uint8_t(br.u(8));
-      for (int b = 0; b < 16; ++b) {
-        const size_t i = size_t(4 * my + b / 4) * 4 * f.mbw + 4 * mx + b % 4;
-        f.tc_y[i] = 16;
-        f.i4mode[i] = -1;
-      }
-      for (int b = 0; b < 4; ++b) {
-        const size_t i = size_t(2 * my + b / 2) * 2 * f.mbw + 2 * mx + b % 2;
-        f.tc_cb[i] = f.tc_cr[i] = 16;
-      }
-    } else if (mb_type >= 1 && mb_type <= 24) {  // I_16x16
-      const int mode = int(mb_type - 1) % 4, cbp_chroma = (int(mb_type - 1) / 4) % 3;
-      const int cbp_luma = mb_type >= 13 ? 15 : 0;
-      const uint32_t cmode_u = br.ue();
-      if (cmode_u > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
-      const int cmode = int(cmode_u);
-      qp = qp_delta(qp);
-      if ((mode == 0 && !nb.top) || (mode == 1 && !nb.left) || (mode == 3 && !(nb.top && nb.left && nb.topleft)))
-        throw std::runtime_error("h264: Intra_16x16 mode uses unavailable samples");
-      int dc[16], ac[16][15];
-      std::memset(ac, 0, sizeof(ac));
-      read_block(br, dc, 16, f.nc(f.tc_y, 4 * mx, 4 * my, 4, slice_id));
-      for (int blk = 0; blk < 16; ++blk) {
-        const int bx = 4 * mx + kBlkX[blk], by = 4 * my + kBlkY[blk];
-        int tc = 0;
-        if (cbp_luma) tc = read_block(br, ac[blk], 15, f.nc(f.tc_y, bx, by, 4, slice_id));
-        f.tc_y[size_t(by) * 4 * f.mbw + bx] = uint8_t(tc);
-        f.i4mode[size_t(by) * 4 * f.mbw + bx] = -1;
-      }
-      uint8_t pred[256];
-      pred16(f.y.data(), f.W, mx * 16, my * 16, nb, mode, pred);
-      recon_luma16(f, mx, my, pred, dc, ac, qp);
-      // chroma
-      int cdc[2][4] = {{0}}, cac[2][4][15];
-      std::memset(cac, 0, sizeof(cac));
-      if (cbp_chroma)
-        for (int c = 0; c < 2; ++c) read_block(br, cdc[c], 4, -1);
-      for (int c = 0; c < 2; ++c) {
-        std::vector<uint8_t>& tcs = c ? f.tc_cr : f.tc_cb;
-        for (int blk = 0; blk < 4; ++blk) {
-          const int bx = 2 * mx + (blk & 1), by = 2 * my + (blk >> 1);
-          int tc = 0;
-          if (cbp_chroma == 2) tc = read_block(br, cac[c][blk], 15, f.nc(tcs, bx, by, 2, slice_id));
-          tcs[size_t(by) * 2 * f.mbw + bx] = uint8_t(tc);
-        }
-      }
-      if ((cmode == 1 && !nb.left) || (cmode == 2 && !nb.top) || (cmode == 3 && !(nb.top && nb.left && nb.topleft)))
-        throw std::runtime_error("h264: chroma mode uses unavailable samples");
-      const int qpc = kChromaQp[std::clamp(qp + pps.chroma_qp_offset, 0, 51)];
-      for (int c = 0; c < 2; ++c) {
-        std::vector<uint8_t>& pl = c ? f.cr : f.cb;
-        uint8_t cp[64];
-        pred_chroma(pl.data(), Wc, mx * 8, my * 8, nb, cmode, cp);
-        recon_chroma(pl, Wc, mx, my, cp, cdc[c], cac[c], qpc);
-      }
-    } else if (mb_type == 0) {  // I_NxN (intra 4x4)
-      int modes[16];
-      for (int blk = 0; blk < 16; ++blk) {
-        const int bx = 4 * mx + kBlkX[blk], by = 4 * my + kBlkY[blk];
-        const bool ia = kBlkX[blk] ? true : nb.left, ib = kBlkY[blk] ? true : nb.top;
-        int pred_mode = 2;
-        if (ia && ib) {
-          const int ma = f.i4mode[size_t(by) * 4 * f.mbw + bx - 1], mb_ = f.i4mode[size_t(by - 1) * 4 * f.mbw + bx];
-          pred_mode = std::min(ma < 0 ? 2 : ma, mb_ < 0 ? 2 : mb_);
-        }
-        int m = pred_mode;
-        if (!br.u(1)) {
-          const int rem = int(br.u(3));
-          m = rem < pred_mode ? rem : rem + 1;
-        }
-        modes[blk] = m;
-        f.i4mode[size_t(by) * 4 * f.mbw + bx] = int8_t(m);
-      }
-      const uint32_t cmode_u = br.ue();
-      if (cmode_u > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
-      const int cmode = int(cmode_u);
-      const uint32_t cbp_code = br.ue();
-      if (cbp_code > 47) throw std::runtime_error("h264: bad coded_block_pattern");
-      const int cbp = kIntraCbp[cbp_code], cbp_luma = cbp & 15, cbp_chroma = cbp >> 4;
-      if (cbp) qp = qp_delta(qp);
-      int coef[16][16];
-      std::memset(coef, 0, sizeof(coef));
-      for (int blk = 0; blk < 16; ++blk) {
-        const int bx = 4 * mx + kBlkX[blk], by = 4 * my + kBlkY[blk];
-        int tc = 0;
-        if (cbp_luma & (1 << (blk / 4))) tc = read_block(br, coef[blk], 16, f.nc(f.tc_y, bx, by, 4, slice_id));
-        f.tc_y[size_t(by) * 4 * f.mbw + bx] = uint8_t(tc);
-      }
-      // luma reconstruction block by block (later blocks predict from earlier ones)
-      for (int blk = 0; blk < 16; ++blk) {
-        const int lx = 4 * kBlkX[blk], ly = 4 * kBlkY[blk];
-        const int x0 = mx * 16 + lx, y0 = my * 16 + ly;
-        const bool has_left = lx ? true : nb.left, has_top = ly ? true : nb.top;
-        bool has_tl = (lx && ly) ? true : (lx ? nb.top : (ly ? nb.left : nb.topleft));
-        bool has_tr;
-        if (ly == 0) has_tr = lx < 12 ? nb.top : nb.topright;
-        else if (lx == 12) has_tr = false;
-        else {
-          const int bxr = kBlkX[blk] + 1, byr = kBlkY[blk] - 1;
-          int idx = 0;
-          for (int k = 0; k < 16; ++k)
-            if (kBlkX[k] == bxr && kBlkY[k] == byr) idx = k;
-          has_tr = idx < blk;
-        }
-        const int m = modes[blk];
-        if (((m == 0 || m == 3 || m == 7) && !has_top) || ((m == 1 || m == 8) && !has_left) ||
-            ((m == 4 || m == 5 || m == 6) && !(has_top && has_left && has_tl)))
-          throw std::runtime_error("h264: Intra_4x4 mode uses unavailable samples");
-        int t[9] = {0}, l[4] = {0};
-        if (has_tl) t[0] = f.y[size_t(y0 - 1) * f.W + x0 - 1];
-        if (has_top) {
-          for (int i = 0; i < 4; ++i) t[1 + i] = f.y[size_t(y0 - 1) * f.W + x0 + i];
-          for (int i = 4; i < 8; ++i) t[1 + i] = has_tr ? f.y[size_t(y0 - 1) * f.W + x0 + i] : t[4];
-        }
-        if (has_left)
-          for (int i = 0; i < 4; ++i) l[i] = f.y[size_t(y0 + i) * f.W + x0 - 1];
-        int p[16], d[16], r[16];
-        pred4(t, l, m, has_top, has_left, p);
-        for (int k = 0; k < 16; ++k) {
-          const int rp = kZigzag[k];
-          d[rp] = coef[blk][k] ? dequant(coef[blk][k], qp, rp) : 0;
-        }
-        inv4x4(d, r);
-        for (int y = 0; y < 4; ++y)
-          for (int x = 0; x < 4; ++x) f.y[size_t(y0 + y) * f.W + x0 + x] = clip255(p[4 * y + x] + r[4 * y + x]);
-      }
-      int cdc[2][4] = {{0}}, cac[2][4][15];
-      std::memset(cac, 0, sizeof(cac));
-      if (cbp_chroma)
-        for (int c = 0; c < 2; ++c) read_block(br, cdc[c], 4, -1);
-      for (int c = 0; c < 2; ++c) {
-        std::vector<uint8_t>& tcs = c ? f.tc_cr : f.tc_cb;
-        for (int blk = 0; blk < 4; ++blk) {
-          const int bx = 2 * mx + (blk & 1), by = 2 * my + (blk >> 1);
-          int tc = 0;
-          if (cbp_chroma == 2) tc = read_block(br, cac[c][blk], 15, f.nc(tcs, bx, by, 2, slice_id));
-          tcs[size_t(by) * 2 * f.mbw + bx] = uint8_t(tc);
-        }
-      }
-      if ((cmode == 1 && !nb.left) || (cmode == 2 && !nb.top) || (cmode == 3 && !(nb.top && nb.left && nb.topleft)))
-        throw std::runtime_error("h264: chroma mode uses unavailable samples");
-      const int qpc = kChromaQp[std::clamp(qp + pps.chroma_qp_offset, 0, 51)];
-      for (int c = 0; c < 2; ++c) {
-        std::vector<uint8_t>& pl = c ? f.cr : f.cb;
-        uint8_t cp[64];
-        pred_chroma(pl.data(), Wc, mx * 8, my * 8, nb, cmode, cp);
-        recon_chroma(pl, Wc, mx, my, cp, cdc[c], cac[c], qpc);
-      }
-    } else {
-      throw std::runtime_error("h264: macroblock type not allowed in an I slice");
+    if (idc > 2) throw std::runtime_error("h264: bad disable_deblocking_filter_idc");
+    h.db.idc = int(idc);
+    if (idc != 1) {
+      const int64_t a = br.se(), b = br.se();
+      if (a < -6 || a > 6 || b < -6 || b > 6) throw std::runtime_error("h264: deblocking offsets out of range");
+      h.db.offa = int(a) * 2;
+      h.db.offb = int(b) * 2;
     }
-    if (!br.more_rbsp_data()) break;
+  }
+  return h;
+}
+
+struct SliceCtx {
+  const Pps& pps;
+  const SliceHdr& hdr;
+  const std::vector<RefPic>& list;   // RefPicList0 (P slices)
+  int slice_id;
+};
+
+int read_te(BitReader& br, int range) {    // te(v), range = num_ref_idx_active - 1 >= 1
+  if (range == 1) return br.u(1) ? 0 : 1;
+  const uint32_t v = br.ue();
+  if (v > uint32_t(range)) throw std::runtime_error("h264: ref_idx out of range");
+  return int(v);
+}
+
+// luma / chroma residual of a non-Intra_16x16 macroblock (cbp-driven), TotalCoeff tables updated
+void read_residual(BitReader& br, Frame& f, int mx, int my, int cbp, int (*coef)[16], int (*cdc)[4],
+                   int (*cac)[4][15], int slice_id) {
+  const int cbp_luma = cbp & 15, cbp_chroma = cbp >> 4;
+  std::memset(coef, 0, sizeof(int) * 256);
+  for (int blk = 0; blk < 16; ++blk) {
+    const int bx = 4 * mx + kBlkX[blk], by = 4 * my + kBlkY[blk];
+    int tc = 0;
+    if (cbp_luma & (1 << (blk / 4))) tc = read_block(br, coef[blk], 16, f.nc(f.tc_y, bx, by, 4, slice_id));
+    f.tc_y[size_t(by) * 4 * f.mbw + bx] = uint8_t(tc);
+  }
+  std::memset(cdc, 0, sizeof(int) * 8);
+  std::memset(cac, 0, sizeof(int) * 120);
+  if (cbp_chroma)
+    for (int c = 0; c < 2; ++c) read_block(br, cdc[c], 4, -1);
+  for (int c = 0; c < 2; ++c) {
+    std::vector<uint8_t>& tcs = c ? f.tc_cr : f.tc_cb;
+    for (int blk = 0; blk < 4; ++blk) {
+      const int bx = 2 * mx + (blk & 1), by = 2 * my + (blk >> 1);
+      int tc = 0;
+      if (cbp_chroma == 2) tc = read_block(br, cac[c][blk], 15, f.nc(tcs, bx, by, 2, slice_id));
+      tcs[size_t(by) * 2 * f.mbw + bx] = uint8_t(tc);
+    }
+  }
+}
+
+// Intra macroblock (mb_type in I-slice numbering 0..25) at (mx, my)
+void decode_intra_mb(BitReader& br, Frame& f, int mx, int my, uint32_t mb_type, int& qp, const Pps& pps,
+                     int slice_id) {
+  const Nb nb = f.nb(mx, my, slice_id);
+  const int Wc = f.W / 2;
+  auto qp_delta = [&](int q) {
+    const int64_t d = br.se();
+    if (d < -26 || d > 25) throw std::runtime_error("h264: mb_qp_delta out of range");
+    return (q + int(d) + 52) % 52;
+  };
+  mark_intra(f, mx, my);
+  if (mb_type == 25) {  // I_PCM
+    while (!br.byte_aligned()) br.u(1);
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x) f.y[size_t(my * 16 + y) * f.W + mx * 16 + x] = uint8_t(br.u(8));
+    for (auto* pl : {&f.cb, &f.cr})
+      for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) (*pl)[size_t(my * 8 + y) * Wc + mx * 8 + x] = uint8_t(br.u(8));
+    for (int b = 0; b < 16; ++b) {
+      const size_t i = size_t(4 * my + b / 4) * 4 * f.mbw + 4 * mx + b % 4;
+      f.tc_y[i] = 16;
+      f.i4mode[i] = -1;
+    }
+    for (int b = 0; b < 4; ++b) {
+      const size_t i = size_t(2 * my + b / 2) * 2 * f.mbw + 2 * mx + b % 2;
+      f.tc_cb[i] = f.tc_cr[i] = 16;
+    }
+    f.mbqp[size_t(my) * f.mbw + mx] = 0;     // deblocking treats I_PCM as QP 0
+    return;
+  }
+  if (mb_type >= 1 && mb_type <= 24) {  // I_16x16
+    const int mode = int(mb_type - 1) % 4, cbp_chroma = (int(mb_type - 1) / 4) % 3;
+    const int cbp_luma = mb_type >= 13 ? 15 : 0;
+    const uint32_t cmode_u = br.ue();
+    if (cmode_u > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
+    const int cmode = int(cmode_u);
+    qp = qp_delta(qp);
+    if ((mode == 0 && !nb.top) || (mode == 1 && !nb.left) || (mode == 3 && !(nb.top && nb.left && nb.topleft)))
+      throw std::runtime_error("h264: Intra_16x16 mode uses unavailable samples");
+    int dc[16], ac[16][15];
+    std::memset(ac, 0, sizeof(ac));
+    read_block(br, dc, 16, f.nc(f.tc_y, 4 * mx, 4 * my, 4, slice_id));
+    for (int blk = 0; blk < 16; ++blk) {
+      const int bx = 4 * mx + kBlkX[blk], by = 4 * my + kBlkY[blk];
+      int tc = 0;
+      if (cbp_luma) tc = read_block(br, ac[blk], 15, f.nc(f.tc_y, bx, by, 4, slice_id));
+      f.tc_y[size_t(by) * 4 * f.mbw + bx] = uint8_t(tc);
+      f.i4mode[size_t(by) * 4 * f.mbw + bx] = -1;
+    }
+    uint8_t pred[256];
+    pred16(f.y.data(), f.W, mx * 16, my * 16, nb, mode, pred);
+    recon_luma16(f, mx, my, pred, dc, ac, qp);
+    int cdc[2][4] = {{0}}, cac[2][4][15];
+    std::memset(cac, 0, sizeof(cac));
+    if (cbp_chroma)
+      for (int c = 0; c < 2; ++c) read_block(br, cdc[c], 4, -1);
+    for (int c = 0; c < 2; ++c) {
+      std::vector<uint8_t>& tcs = c ? f.tc_cr : f.tc_cb;
+      for (int blk = 0; blk < 4; ++blk) {
+        const int bx = 2 * mx + (blk & 1), by = 2 * my + (blk >> 1);
+        int tc = 0;
+        if (cbp_chroma == 2) tc = read_block(br, cac[c][blk], 15, f.nc(tcs, bx, by, 2, slice_id));
+        tcs[size_t(by) * 2 * f.mbw + bx] = uint8_t(tc);
+      }
+    }
+    if ((cmode == 1 && !nb.left) || (cmode == 2 && !nb.top) || (cmode == 3 && !(nb.top && nb.left && nb.topleft)))
+      throw std::runtime_error("h264: chroma mode uses unavailable samples");
+    const int qpc = kChromaQp[std::clamp(qp + pps.chroma_qp_offset, 0, 51)];
+    for (int c = 0; c < 2; ++c) {
+      std::vector<uint8_t>& pl = c ? f.cr : f.cb;
+      uint8_t cp[64];
+      pred_chroma(pl.data(), Wc, mx * 8, my * 8, nb, cmode, cp);
+      recon_chroma(pl, Wc, mx, my, cp, cdc[c], cac[c], qpc);
+    }
+    f.mbqp[size_t(my) * f.mbw + mx] = uint8_t(qp);
+    return;
+  }
+  if (mb_type != 0) throw std::runtime_error("h264: macroblock type out of range");
+  // I_NxN (intra 4x4)
+  int modes[16];
+  for (int blk = 0; blk < 16; ++blk) {
+    const int bx = 4 * mx + kBlkX[blk], by = 4 * my + kBlkY[blk];
+    const bool ia = kBlkX[blk] ? true : nb.left, ib = kBlkY[blk] ? true : nb.top;
+    int pred_mode = 2;
+    if (ia && ib) {
+      const int ma = f.i4mode[size_t(by) * 4 * f.mbw + bx - 1], mb_ = f.i4mode[size_t(by - 1) * 4 * f.mbw + bx];
+      pred_mode = std::min(ma < 0 ? 2 : ma, mb_ < 0 ? 2 : mb_);
+    }
+    int m = pred_mode;
+    if (!br.u(1)) {
+      const int rem = int(br.u(3));
+      m = rem < pred_mode ? rem : rem + 1;
+    }
+    modes[blk] = m;
+    f.i4mode[size_t(by) * 4 * f.mbw + bx] = int8_t(m);
+  }
+  const uint32_t cmode_u = br.ue();
+  if (cmode_u > 3) throw std::runtime_error("h264: bad intra_chroma_pred_mode");
+  const int cmode = int(cmode_u);
+  const uint32_t cbp_code = br.ue();
+  if (cbp_code > 47) throw std::runtime_error("h264: bad coded_block_pattern");
+  const int cbp = kIntraCbp[cbp_code];
+  if (cbp) qp = qp_delta(qp);
+  int coef[16][16], cdc[2][4], cac[2][4][15];
+  read_residual(br, f, mx, my, cbp, coef, cdc, cac, slice_id);
+  // luma reconstruction block by block (later blocks predict from earlier ones)
+  for (int blk = 0; blk < 16; ++blk) {
+    const int lx = 4 * kBlkX[blk], ly = 4 * kBlkY[blk];
+    const int x0 = mx * 16 + lx, y0 = my * 16 + ly;
+    const bool has_left = lx ? true : nb.left, has_top = ly ? true : nb.top;
+    bool has_tl = (lx && ly) ? true : (lx ? nb.top : (ly ? nb.left : nb.topleft));
+    bool has_tr;
+    if (ly == 0) has_tr = lx < 12 ? nb.top : nb.topright;
+    else if (lx == 12) has_tr = false;
+    else {
+      const int bxr = kBlkX[blk] + 1, byr = kBlkY[blk] - 1;
+      int idx = 0;
+      for (int k = 0; k < 16; ++k)
+        if (kBlkX[k] == bxr && kBlkY[k] == byr) idx = k;
+      has_tr = idx < blk;
+    }
+    const int m = modes[blk];
+    if (((m == 0 || m == 3 || m == 7) && !has_top) || ((m == 1 || m == 8) && !has_left) ||
+        ((m == 4 || m == 5 || m == 6) && !(has_top && has_left && has_tl)))
+      throw std::runtime_error("h264: Intra_4x4 mode uses unavailable samples");
+    int t[9] = {0}, l[4] = {0};
+    if (has_tl) t[0] = f.y[size_t(y0 - 1) * f.W + x0 - 1];
+    if (has_top) {
+      for (int i = 0; i < 4; ++i) t[1 + i] = f.y[size_t(y0 - 1) * f.W + x0 + i];
+      for (int i = 4; i < 8; ++i) t[1 + i] = has_tr ? f.y[size_t(y0 - 1) * f.W + x0 + i] : t[4];
+    }
+    if (has_left)
+      for (int i = 0; i < 4; ++i) l[i] = f.y[size_t(y0 + i) * f.W + x0 - 1];
+    int p[16], d[16], r[16];
+    pred4(t, l, m, has_top, has_left, p);
+    for (int k = 0; k < 16; ++k) {
+      const int rp = kZigzag[k];
+      d[rp] = coef[blk][k] ? dequant(coef[blk][k], qp, rp) : 0;
+    }
+    inv4x4(d, r);
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) f.y[size_t(y0 + y) * f.W + x0 + x] = clip255(p[4 * y + x] + r[4 * y + x]);
+  }
+  if ((cmode == 1 && !nb.left) || (cmode == 2 && !nb.top) || (cmode == 3 && !(nb.top && nb.left && nb.topleft)))
+    throw std::runtime_error("h264: chroma mode uses unavailable samples");
+  const int qpc = kChromaQp[std::clamp(qp + pps.chroma_qp_offset, 0, 51)];
+  for (int c = 0; c < 2; ++c) {
+    std::vector<uint8_t>& pl = c ? f.cr : f.cb;
+    uint8_t cp[64];
+    pred_chroma(pl.data(), Wc, mx * 8, my * 8, nb, cmode, cp);
+    recon_chroma(pl, Wc, mx, my, cp, cdc[c], cac[c], qpc);
+  }
+  f.mbqp[size_t(my) * f.mbw + mx] = uint8_t(qp);
+}
+
+void recon_inter(Frame& f, const SliceCtx& sc, int mx, int my, const int (*coef)[16], const int (*cdc)[4],
+                 const int (*cac)[4][15], int qp) {
+  uint8_t py[256], pc[2][64];
+  predict_inter(f, sc.list, mx, my, py, pc[0], pc[1]);
+  recon_luma4x4(f, mx, my, py, coef, qp);
+  const int qpc = kChromaQp[std::clamp(qp + sc.pps.chroma_qp_offset, 0, 51)];
+  for (int c = 0; c < 2; ++c) recon_chroma(c ? f.cr : f.cb, f.W / 2, mx, my, pc[c], cdc[c], cac[c], qpc);
+  f.intra[size_t(my) * f.mbw + mx] = 0;
+  f.mbqp[size_t(my) * f.mbw + mx] = uint8_t(qp);
+}
+
+void decode_skip(Frame& f, const SliceCtx& sc, int mx, int my, int qp) {
+  MvPred mp{f, mx, my, sc.slice_id};
+  int px, py;
+  mp.skip(px, py);
+  if (sc.list.empty() || !sc.list[0].f) throw std::runtime_error("h264: P_Skip without a reference picture");
+  set_motion(f, mp, mx, my, 0, 0, 4, 4, 0, sc.list[0].id, px, py);
+  int coef[16][16] = {{0}}, cdc[2][4] = {{0}}, cac[2][4][15];
+  std::memset(cac, 0, sizeof(cac));
+  for (int y = 0; y < 4; ++y)
+    for (int x = 0; x < 4; ++x) f.tc_y[size_t(4 * my + y) * 4 * f.mbw + 4 * mx + x] = 0;
+  for (int y = 0; y < 2; ++y)
+    for (int x = 0; x < 2; ++x) f.tc_cb[size_t(2 * my + y) * 2 * f.mbw + 2 * mx + x] =
+        f.tc_cr[size_t(2 * my + y) * 2 * f.mbw + 2 * mx + x] = 0;
+  for (int b = 0; b < 16; ++b) f.i4mode[size_t(4 * my + b / 4) * 4 * f.mbw + 4 * mx + b % 4] = -1;
+  recon_inter(f, sc, mx, my, coef, cdc, cac, qp);
+}
+
+// P macroblock types 0..4 (Table 7-13): partitions, sub-partitions, ref_idx, mvd, cbp, residual
+void decode_inter_mb(BitReader& br, Frame& f, const SliceCtx& sc, int mx, int my, uint32_t mb_type, int& qp) {
+  const int nref = sc.hdr.num_ref_active;
+  MvPred mp{f, mx, my, sc.slice_id};
+  auto need_ref = [&](int r) {
+    if (size_t(r) >= sc.list.size() || !sc.list[size_t(r)].f)
+      throw std::runtime_error("h264: ref_idx names no reference picture");
+    return sc.list[size_t(r)].id;
+  };
+  auto mvd = [&]() {
+    const int64_t x = br.se(), y = br.se();
+    if (x < -8192 || x > 8191 || y < -2048 || y > 2047) throw std::runtime_error("h264: mvd out of range");
+    return std::make_pair(int(x), int(y));
+  };
+  auto add_mv = [](int p, int d, int lo, int hi) {
+    const int v = p + d;
+    if (v < lo || v > hi) throw std::runtime_error("h264: motion vector out of range");
+    return v;
+  };
+  if (mb_type <= 2) {
+    const int nparts = mb_type == 0 ? 1 : 2;
+    int refs[2] = {0, 0};
+    for (int p = 0; p < nparts; ++p) refs[p] = nref > 1 ? read_te(br, nref - 1) : 0;
+    for (int p = 0; p < nparts; ++p) {
+      const auto d = mvd();
+      int bx = 0, by = 0, bw = 4, bh = 4, shape = 0;
+      if (mb_type == 1) { by = 2 * p; bh = 2; shape = 1 + p; }
+      if (mb_type == 2) { bx = 2 * p; bw = 2; shape = 3 + p; }
+      int px, py;
+      mp.pred(bx, by, bw, refs[p], shape, px, py);
+      set_motion(f, mp, mx, my, bx, by, bw, bh, refs[p], need_ref(refs[p]), add_mv(px, d.first, -8192, 8191),
+                 add_mv(py, d.second, -2048, 2047));
+    }
+  } else if (mb_type <= 4) {
+    int sub[4], refs[4] = {0, 0, 0, 0};
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t t = br.ue();
+      if (t > 3) throw std::runtime_error("h264: bad sub_mb_type");
+      sub[s] = int(t);
+    }
+    if (mb_type == 3 && nref > 1)
+      for (int s = 0; s < 4; ++s) refs[s] = read_te(br, nref - 1);
+    for (int s = 0; s < 4; ++s) {
+      const int sx = 2 * (s & 1), sy = 2 * (s >> 1);
+      const int n = sub[s] == 0 ? 1 : sub[s] == 3 ? 4 : 2;
+      const int pw = sub[s] == 0 || sub[s] == 1 ? 2 : 1, ph = sub[s] == 0 || sub[s] == 2 ? 2 : 1;
+      for (int k = 0; k < n; ++k) {
+        const auto d = mvd();
+        const int bx = sx + (sub[s] == 2 || sub[s] == 3 ? (k & 1) : 0);
+        const int by = sy + (sub[s] == 1 ? k : sub[s] == 3 ? (k >> 1) : 0);
+        int px, py;
+        mp.pred(bx, by, pw, refs[s], 0, px, py);
+        set_motion(f, mp, mx, my, bx, by, pw, ph, refs[s], need_ref(refs[s]), add_mv(px, d.first, -8192, 8191),
+                   add_mv(py, d.second, -2048, 2047));
+      }
+    }
+  } else {
+    throw std::runtime_error("h264: P macroblock type out of range");
+  }
+  const uint32_t cbp_code = br.ue();
+  if (cbp_code > 47) throw std::runtime_error("h264: bad coded_block_pattern");
+  const int cbp = kInterCbp[cbp_code];
+  if (cbp) {
+    const int64_t d = br.se();
+    if (d < -26 || d > 25) throw std::runtime_error("h264: mb_qp_delta out of range");
+    qp = (qp + int(d) + 52) % 52;
+  }
+  int coef[16][16], cdc[2][4], cac[2][4][15];
+  read_residual(br, f, mx, my, cbp, coef, cdc, cac, sc.slice_id);
+  for (int b = 0; b < 16; ++b) f.i4mode[size_t(4 * my + b / 4) * 4 * f.mbw + 4 * mx + b % 4] = -1;
+  recon_inter(f, sc, mx, my, coef, cdc, cac, qp);
+}
+
+// Macroblocks of one slice: [first_mb, end_mb), f.slice already holds the slice id over that range
+// (slices of a picture decode concurrently; neighbours in other slices are never read).
+void decode_slice_data(BitReader& br, Frame& f, const SliceCtx& sc, int end_mb, std::vector<uint8_t>& done) {
+  const int nmb = f.mbw * f.mbh;
+  const bool p_slice = sc.hdr.slice_type == 0;
+  int qp = sc.hdr.qp;
+  int mb = sc.hdr.first_mb;
+  auto claim = [&](int m) {
+    if (m >= nmb) throw std::runtime_error("h264: slice data past the last macroblock");
+    if (m >= end_mb) throw std::runtime_error("h264: slice overlaps the next slice");
+    done[size_t(m)] = 1;
+  };
+  bool more = true;
+  while (more) {
+    if (p_slice) {
+      const uint32_t run = br.ue();
+      if (run > uint32_t(nmb - mb)) throw std::runtime_error("h264: mb_skip_run out of range");
+      for (uint32_t i = 0; i < run; ++i, ++mb) {
+        claim(mb);
+        decode_skip(f, sc, mb % f.mbw, mb / f.mbw, qp);
+      }
+      if (run > 0 && !br.more_rbsp_data()) break;
+    }
+    claim(mb);
+    const int mx = mb % f.mbw, my = mb / f.mbw;
+    const uint32_t mb_type = br.ue();
+    if (p_slice && mb_type < 5) {
+      decode_inter_mb(br, f, sc, mx, my, mb_type, qp);
+    } else {
+      const uint32_t it = p_slice ? mb_type - 5 : mb_type;
+      if (it > 25) throw std::runtime_error("h264: macroblock type not allowed in this slice");
+      decode_intra_mb(br, f, mx, my, it, qp, sc.pps, sc.slice_id);
+    }
+    ++mb;
+    more = br.more_rbsp_data();
   }
 }
 
 }  // namespace
 
-std::vector<Picture> decode(const std::vector<std::string>& nals, int threads) {
-  // Pass 1 (sequential): parameter sets and the split into pictures (a picture starts at a slice
-  // with first_mb_in_slice == 0).  Pass 2: pictures are intra-only and independent -> parallel.
-  struct Job {
+void decode(const std::vector<std::string>& nals, int threads, const LayoutFn& on_layout, const PictureSink& sink,
+            std::vector<SideInfo>* side) {
+  // Pass 1 (sequential): parameter sets and the split into pictures (a picture starts at a slice with
+  // first_mb_in_slice == 0), grouped into coded video sequences from IDR to IDR.  Pass 2: every
+  // sequence decodes in order (P pictures reference earlier ones); sequences run in parallel.
+  struct Pic {
     Sps sps;
     Pps pps;
     std::vector<std::pair<int, std::string>> slices;  // (nal header byte, rbsp)
   };
   Sps sps;
   Pps pps;
-  std::vector<Job> jobs;
+  std::vector<std::vector<Pic>> seqs;
+  size_t npics = 0;
   for (const std::string& nal : nals) {
     if (nal.empty()) continue;
     const uint8_t h = uint8_t(nal[0]);
@@ -1282,9 +2573,14 @@ std::vector<Picture> decode(const std::vector<std::string>& nals, int threads) {
     } else if (type == 5 || type == 1) {
       if (!sps.ok || !pps.ok) throw std::runtime_error("h264: slice before SPS/PPS");
       BitReader peek(rbsp);
-      if (peek.ue() == 0) jobs.push_back(Job{sps, pps, {}});
-      if (jobs.empty()) throw std::runtime_error("h264: slice of a picture without its first macroblock");
-      jobs.back().slices.emplace_back(h, std::move(rbsp));
+      if (peek.ue() == 0) {
+        if (type == 5 || seqs.empty()) seqs.emplace_back();
+        seqs.back().push_back(Pic{sps, pps, {}});
+        ++npics;
+      }
+      if (seqs.empty() || seqs.back().empty())
+        throw std::runtime_error("h264: slice of a picture without its first macroblock");
+      seqs.back().back().slices.emplace_back(h, std::move(rbsp));
     } else if (type == 9 || type == 6 || type == 10 || type == 11 || type == 12) {
       // access unit delimiter, SEI, end of sequence / stream, filler: ignored
     } else {
@@ -1294,43 +2590,129 @@ std::vector<Picture> decode(const std::vector<std::string>& nals, int threads) {
   // untrusted input: a few bits per macroblock can declare huge pictures, so bound what decoding
   // may allocate (4K per picture via the SPS limits, 2^31 luma samples - ~3.2 GB of 4:2:0 - in total)
   uint64_t samples = 0;
-  for (const Job& j : jobs) samples += uint64_t(j.sps.mbw) * j.sps.mbh * 256;
+  for (const auto& sq : seqs)
+    for (const Pic& j : sq) samples += uint64_t(j.sps.mbw) * j.sps.mbh * 256;
   if (samples > (uint64_t(1) << 31)) throw std::runtime_error("h264: video too large to decode");
-  std::vector<Picture> out(jobs.size());
-  std::vector<std::string> errors(jobs.size());
+  std::vector<size_t> base(seqs.size(), 0);
+  for (size_t s = 1; s < seqs.size(); ++s) base[s] = base[s - 1] + seqs[s - 1].size();
+  std::vector<std::pair<int, int>> crops;
+  for (const auto& sq : seqs)
+    for (const Pic& j : sq) {
+      const int cw = 16 * j.sps.mbw - 2 * (j.sps.crop_l + j.sps.crop_r);
+      const int ch = 16 * j.sps.mbh - 2 * (j.sps.crop_t + j.sps.crop_b);
+      if (cw <= 0 || ch <= 0) throw std::runtime_error("h264: bad cropping window");
+      crops.emplace_back(cw, ch);
+    }
+  if (on_layout) on_layout(crops);
+  if (side) side->assign(npics, SideInfo{});
+  std::vector<std::string> errors(seqs.size());
+  int inner_threads = 1;                  // slices of one picture in parallel when sequences are few
+  auto run_seq = [&](size_t s) {
+    std::vector<RefPic> dpb;              // short-term reference pictures
+    int prev_ref_frame_num = 0, next_id = 1;
+    for (size_t k = 0; k < seqs[s].size(); ++k) {
+      const Pic& j = seqs[s][k];
+      auto f = std::make_shared<Frame>(j.sps.mbw, j.sps.mbh);
+      f->constrained_intra = j.pps.constrained_intra;
+      const int nmb = f->mbw * f->mbh, max_fn = 1 << j.sps.log2_max_frame_num;
+      // slice headers first (picture-level state, ranges), then the slices' macroblocks in parallel
+      const size_t ns = j.slices.size();
+      std::vector<SliceHdr> hdrs;
+      std::vector<BitReader> readers;
+      hdrs.reserve(ns);
+      readers.reserve(ns);
+      for (size_t si = 0; si < ns; ++si) {
+        const auto& sl = j.slices[si];
+        readers.emplace_back(sl.second);
+        hdrs.push_back(parse_slice_header(readers.back(), sl.first & 0x1F, (sl.first >> 5) & 3, j.sps, j.pps, nmb));
+        if (si > 0 && hdrs[si].first_mb <= hdrs[si - 1].first_mb)
+          throw std::runtime_error("h264: slices out of order (arbitrary slice order is not supported)");
+        if (si > 0 && (hdrs[si].nal_type != hdrs[0].nal_type || hdrs[si].frame_num != hdrs[0].frame_num ||
+                       (hdrs[si].nal_ref_idc != 0) != (hdrs[0].nal_ref_idc != 0)))
+          throw std::runtime_error("h264: slices of one picture disagree");
+      }
+      const SliceHdr& first = hdrs[0];
+      if (first.nal_type == 5) {
+        dpb.clear();
+        prev_ref_frame_num = 0;
+      } else if (first.frame_num != prev_ref_frame_num && first.frame_num != (prev_ref_frame_num + 1) % max_fn &&
+                 !j.sps.gaps_allowed) {
+        throw std::runtime_error("h264: gap in frame_num (lost reference pictures)");
+      }
+      std::vector<SliceDb> dbs;
+      std::vector<std::vector<RefPic>> lists(ns);
+      for (size_t si = 0; si < ns; ++si) {
+        dbs.push_back(hdrs[si].db);
+        if (hdrs[si].slice_type == 0)
+          lists[si] = ref_list0(dpb, hdrs[si].frame_num, max_fn, hdrs[si].list_mods, hdrs[si].num_ref_active);
+        const int end = si + 1 < ns ? hdrs[si + 1].first_mb : nmb;
+        for (int m = hdrs[si].first_mb; m < end; ++m) f->slice[size_t(m)] = int(si);
+      }
+      std::vector<uint8_t> done(size_t(nmb), 0);
+      parallel_for(int(ns), inner_threads, [&](int si) {
+        const SliceCtx sc{j.pps, hdrs[size_t(si)], lists[size_t(si)], si};
+        const int end = size_t(si) + 1 < ns ? hdrs[size_t(si) + 1].first_mb : nmb;
+        decode_slice_data(readers[size_t(si)], *f, sc, end, done);
+      });
+      for (uint8_t d : done)
+        if (!d) throw std::runtime_error("h264: picture has undecoded macroblocks");
+      const size_t idx = base[s] + k;
+      if (side) {                                   // test hook: the unfiltered picture + filter inputs
+        SideInfo& si = (*side)[idx];
+        si.y = f->y;
+        si.cb = f->cb;
+        si.cr = f->cr;
+        si.mvx.assign(f->mvx.begin(), f->mvx.end());
+        si.mvy.assign(f->mvy.begin(), f->mvy.end());
+        si.refpic = f->refpic;
+        si.nonzero.assign(f->tc_y.begin(), f->tc_y.end());
+        si.intra = f->intra;
+        si.qp = f->mbqp;
+        si.slice = f->slice;
+        for (const SliceDb& d : dbs) si.deblock.push_back({d.idc, d.offa, d.offb});
+        si.chroma_qp_offset = j.pps.chroma_qp_offset;
+      }
+      deblock(*f, dbs, j.pps.chroma_qp_offset, inner_threads);
+      {
+        Picture p;
+        p.w16 = f->W;
+        p.h16 = f->H;
+        p.crop_w = crops[idx].first;
+        p.crop_h = crops[idx].second;
+        p.y = f->y;
+        p.cb = f->cb;
+        p.cr = f->cr;
+        sink(idx, std::move(p), inner_threads);
+      }
+      if (first.nal_ref_idc)
+        prev_ref_frame_num = mark_reference(dpb, RefPic{f, next_id++, first.frame_num}, max_fn, j.sps.max_refs,
+                                            first.adaptive_marking, first.mmco);
+    }
+  };
   auto work = [&](int t, int nt) {
-    for (size_t i = t; i < jobs.size(); i += nt) {
+    for (size_t s = size_t(t); s < seqs.size(); s += size_t(nt)) {
       try {
-        const Job& j = jobs[i];
-        Frame f(j.sps.mbw, j.sps.mbh);
-        int slice_id = 0;
-        for (const auto& sl : j.slices) {
-          BitReader br(sl.second);
-          decode_slice(br, sl.first & 0x1F, (sl.first >> 5) & 3, j.sps, j.pps, f, slice_id++);
-        }
-        for (int s : f.slice)
-          if (s < 0) throw std::runtime_error("h264: picture has undecoded macroblocks");
-        Picture& p = out[i];
-        p.w16 = f.W;
-        p.h16 = f.H;
-        p.crop_w = f.W - 2 * (j.sps.crop_l + j.sps.crop_r);
-        p.crop_h = f.H - 2 * (j.sps.crop_t + j.sps.crop_b);
-        if (p.crop_w <= 0 || p.crop_h <= 0) throw std::runtime_error("h264: bad cropping window");
-        p.y = std::move(f.y);
-        p.cb = std::move(f.cb);
-        p.cr = std::move(f.cr);
+        run_seq(s);
       } catch (const std::exception& e) {
-        errors[i] = e.what();
+        errors[s] = e.what();
       }
     }
   };
-  const int nt = std::max(1, std::min<int>(threads, (int)jobs.size()));
+  const int nt = std::max(1, std::min<int>(threads, (int)seqs.size()));
+  inner_threads = std::max(1, threads / nt);
   std::vector<std::thread> pool;
   for (int t = 1; t < nt; ++t) pool.emplace_back(work, t, nt);
   work(0, nt);
   for (auto& th : pool) th.join();
   for (auto& e : errors)
     if (!e.empty()) throw std::runtime_error(e);
+}
+
+std::vector<Picture> decode(const std::vector<std::string>& nals, int threads) {
+  std::vector<Picture> out;
+  decode(
+      nals, threads, [&](const std::vector<std::pair<int, int>>& crops) { out.resize(crops.size()); },
+      [&](size_t i, Picture&& p, int) { out[i] = std::move(p); }, nullptr);
   return out;
 }
 

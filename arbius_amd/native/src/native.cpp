@@ -295,73 +295,188 @@ static py::tuple h264_encode_yuv(u8arr y, u8arr cb, u8arr cr, int qp, int idr_pi
   return py::make_tuple(py::bytes(nal), ry, rcb, rcr);
 }
 
-static py::tuple h264_parameter_sets(int width, int height, int qp) {
+static py::tuple h264_parameter_sets(int width, int height, int qp, int max_refs) {
   std::string sps, pps;
-  h264::parameter_sets(width, height, qp, sps, pps);
+  h264::parameter_sets(width, height, qp, sps, pps, max_refs);
   return py::make_tuple(py::bytes(sps), py::bytes(pps));
 }
 
-// NAL units (no start codes) -> [(Y, Cb, Cr, (crop_w, crop_h))]; raises ValueError outside the subset
-static py::list h264_decode(const std::vector<std::string>& nals, int threads) {
+static py::list nal_lists(const std::vector<h264::EncodedPicture>& pics) {
+  py::list out;
+  for (const auto& p : pics) {
+    py::list n;
+    for (const auto& s : p.nals) n.append(py::bytes(s));
+    out.append(n);
+  }
+  return out;
+}
+
+// frames uint8 [F, H, W, 3] -> (sps, pps, [[slice NALs] per picture]): IPPP stream (IDR every
+// `gop` pictures), each picture's row-band slices encoded in parallel.  The colour conversion
+// runs per picture inside the encoder's loader (no whole-clip YUV copy).
+static py::tuple h264_encode_rgb_stream(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> frames,
+                                        int qp, int gop, int threads, int rows_per_slice) {
+  auto b = frames.request();
+  if (b.ndim != 4 || b.shape[3] != 3 || b.shape[0] < 1 || b.shape[1] < 1 || b.shape[2] < 1)
+    throw std::invalid_argument("h264_encode_rgb_stream: frames [F, H, W, 3]");
+  const int F = (int)b.shape[0], H = (int)b.shape[1], W = (int)b.shape[2];
+  const int H16 = (H + 15) / 16 * 16, W16 = (W + 15) / 16 * 16;
+  const uint8_t* src = static_cast<const uint8_t*>(b.ptr);
+  std::string sps, pps;
+  h264::parameter_sets(W, H, qp, sps, pps, 1);
+  h264::StreamOptions o;
+  o.qp = qp;
+  o.gop = gop;
+  o.threads = threads;
+  o.rows_per_slice = rows_per_slice;
+  std::vector<h264::EncodedPicture> pics;
+  {
+    py::gil_scoped_release nogil;
+    pics = h264::encode_stream(F, W16, H16, o, [&](int i, uint8_t* y, uint8_t* cb, uint8_t* cr) {
+      rgb_to_420(src + (size_t)i * H * W * 3, H, W, H16, W16, y, cb, cr);
+    });
+  }
+  return py::make_tuple(py::bytes(sps), py::bytes(pps), nal_lists(pics));
+}
+
+// 4:2:0 planes [F, H, W] / [F, H/2, W/2] -> ([[NAL]], recon Y, Cb, Cr) (tests: recon == decoder
+// output; seed != 0 = the randomised decoder-coverage mode)
+static py::tuple h264_encode_yuv_stream(u8arr y, u8arr cb, u8arr cr, int qp, int gop, uint32_t seed, int max_refs,
+                                        int threads, int rows_per_slice) {
+  auto by = y.request(), bcb = cb.request(), bcr = cr.request();
+  if (by.ndim != 3 || bcb.ndim != 3 || bcr.ndim != 3) throw std::invalid_argument("h264_encode_yuv_stream: [F, H, W]");
+  const int F = (int)by.shape[0], H = (int)by.shape[1], W = (int)by.shape[2];
+  if (bcb.shape[0] != F || bcr.shape[0] != F || bcb.shape[1] != H / 2 || bcb.shape[2] != W / 2 ||
+      bcr.shape[1] != H / 2 || bcr.shape[2] != W / 2)
+    throw std::invalid_argument("h264_encode_yuv_stream: chroma planes must be [F, H/2, W/2]");
+  h264::StreamOptions o;
+  o.qp = qp;
+  o.gop = gop;
+  o.seed = seed;
+  o.max_refs = max_refs;
+  o.threads = threads;
+  o.rows_per_slice = rows_per_slice;
+  o.keep_recon = true;
+  const uint8_t *py_ = static_cast<const uint8_t*>(by.ptr), *pcb = static_cast<const uint8_t*>(bcb.ptr),
+                *pcr = static_cast<const uint8_t*>(bcr.ptr);
+  const size_t ny = (size_t)H * W, nc = ny / 4;
+  std::vector<h264::EncodedPicture> pics;
+  {
+    py::gil_scoped_release nogil;
+    pics = h264::encode_stream(F, W, H, o, [&](int i, uint8_t* yy, uint8_t* cbb, uint8_t* crr) {
+      std::memcpy(yy, py_ + i * ny, ny);
+      std::memcpy(cbb, pcb + i * nc, nc);
+      std::memcpy(crr, pcr + i * nc, nc);
+    });
+  }
+  u8arr ry({F, H, W}), rcb({F, H / 2, W / 2}), rcr({F, H / 2, W / 2});
+  for (int i = 0; i < F; ++i) {
+    std::memcpy(ry.mutable_data() + i * ny, pics[i].y.data(), ny);
+    std::memcpy(rcb.mutable_data() + i * nc, pics[i].cb.data(), nc);
+    std::memcpy(rcr.mutable_data() + i * nc, pics[i].cr.data(), nc);
+  }
+  return py::make_tuple(nal_lists(pics), ry, rcb, rcr);
+}
+
+template <class T>
+static py::array_t<T> vec_array(const std::vector<T>& v) {
+  py::array_t<T> a((py::ssize_t)v.size());
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+// NAL units (no start codes) -> [(Y, Cb, Cr, (crop_w, crop_h))]; raises ValueError outside the subset.
+// with_side=True (tests) appends a dict of the deblocking filter's inputs per picture.
+static py::list h264_decode(const std::vector<std::string>& nals, int threads, bool with_side) {
   std::vector<h264::Picture> pics;
+  std::vector<h264::SideInfo> side;
   {
     py::gil_scoped_release nogil;
     try {
-      pics = h264::decode(nals, threads);
+      h264::decode(
+          nals, threads, [&](const std::vector<std::pair<int, int>>& crops) { pics.resize(crops.size()); },
+          [&](size_t i, h264::Picture&& p, int) { pics[i] = std::move(p); }, with_side ? &side : nullptr);
     } catch (const std::runtime_error& e) {
       py::gil_scoped_acquire gil;
       throw py::value_error(e.what());
     }
   }
   py::list out;
-  for (auto& p : pics) {
+  for (size_t k = 0; k < pics.size(); ++k) {
+    const auto& p = pics[k];
     u8arr y({p.h16, p.w16}), cb({p.h16 / 2, p.w16 / 2}), cr({p.h16 / 2, p.w16 / 2});
     std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
     std::memcpy(cb.mutable_data(), p.cb.data(), p.cb.size());
     std::memcpy(cr.mutable_data(), p.cr.data(), p.cr.size());
-    out.append(py::make_tuple(y, cb, cr, py::make_tuple(p.crop_w, p.crop_h)));
+    if (!with_side) {
+      out.append(py::make_tuple(y, cb, cr, py::make_tuple(p.crop_w, p.crop_h)));
+      continue;
+    }
+    const auto& s = side[k];
+    py::dict d;
+    d["y"] = vec_array(s.y);
+    d["cb"] = vec_array(s.cb);
+    d["cr"] = vec_array(s.cr);
+    d["mvx"] = vec_array(s.mvx);
+    d["mvy"] = vec_array(s.mvy);
+    d["refpic"] = vec_array(s.refpic);
+    d["nonzero"] = vec_array(s.nonzero);
+    d["intra"] = vec_array(s.intra);
+    d["qp"] = vec_array(s.qp);
+    d["slice"] = vec_array(s.slice);
+    d["deblock"] = s.deblock;
+    d["chroma_qp_offset"] = s.chroma_qp_offset;
+    out.append(py::make_tuple(y, cb, cr, py::make_tuple(p.crop_w, p.crop_h), d));
   }
   return out;
 }
 
 // NAL units -> uint8 RGB [F, crop_h, crop_w, 3]: the integer BT.601 inverse of rgb_to_420 (the
-// reference is video_io.yuv420_to_rgb: nearest chroma upsampling, clipped).
+// reference is video_io.yuv420_to_rgb: nearest chroma upsampling, clipped).  The output is
+// allocated once from the stream's layout and every picture is converted as soon as it is decoded,
+// so no plane copy of the whole clip is ever held.
 static u8arr h264_decode_rgb(const std::vector<std::string>& nals, int threads) {
-  std::vector<h264::Picture> pics;
+  uint8_t* dst = nullptr;
+  int F = 0, H = 0, W = 0;
+  std::string layout_err;
   {
     py::gil_scoped_release nogil;
     try {
-      pics = h264::decode(nals, threads);
+      h264::decode(
+          nals, threads,
+          [&](const std::vector<std::pair<int, int>>& crops) {
+            if (crops.empty()) throw std::runtime_error("no pictures in the H.264 stream");
+            W = crops[0].first;
+            H = crops[0].second;
+            for (auto& c : crops)
+              if (c.first != W || c.second != H) throw std::runtime_error("pictures of different sizes");
+            F = (int)crops.size();
+            dst = new uint8_t[(size_t)F * H * W * 3];
+          },
+          [&](size_t i, h264::Picture&& p, int free_threads) {
+            uint8_t* o = dst + i * (size_t)H * W * 3;
+            const int bands = std::max(1, std::min(free_threads, H / 16));
+            run_parallel(bands, bands, [&](int band) {
+             for (int r = band * H / bands; r < (band + 1) * H / bands; ++r)
+              for (int x = 0; x < W; ++x) {
+                const int c = int(p.y[(size_t)r * p.w16 + x]) - 16;
+                const int d = int(p.cb[(size_t)(r / 2) * (p.w16 / 2) + x / 2]) - 128;
+                const int e = int(p.cr[(size_t)(r / 2) * (p.w16 / 2) + x / 2]) - 128;
+                uint8_t* q = o + ((size_t)r * W + x) * 3;
+                q[0] = (uint8_t)std::min(255, std::max(0, (298 * c + 409 * e + 128) >> 8));
+                q[1] = (uint8_t)std::min(255, std::max(0, (298 * c - 100 * d - 208 * e + 128) >> 8));
+                q[2] = (uint8_t)std::min(255, std::max(0, (298 * c + 516 * d + 128) >> 8));
+              }
+            });
+          });
     } catch (const std::runtime_error& e) {
+      delete[] dst;
       py::gil_scoped_acquire gil;
       throw py::value_error(e.what());
     }
   }
-  if (pics.empty()) throw py::value_error("no pictures in the H.264 stream");
-  const int H = pics[0].crop_h, W = pics[0].crop_w;
-  for (auto& p : pics)
-    if (p.crop_h != H || p.crop_w != W) throw py::value_error("pictures of different sizes");
-  const int F = (int)pics.size();
-  u8arr out({F, H, W, 3});
-  uint8_t* dst = out.mutable_data();
-  {
-    py::gil_scoped_release nogil;
-    run_parallel(F, threads, [&](int i) {
-      const h264::Picture& p = pics[i];
-      uint8_t* o = dst + (size_t)i * H * W * 3;
-      for (int r = 0; r < H; ++r)
-        for (int x = 0; x < W; ++x) {
-          const int c = int(p.y[(size_t)r * p.w16 + x]) - 16;
-          const int d = int(p.cb[(size_t)(r / 2) * (p.w16 / 2) + x / 2]) - 128;
-          const int e = int(p.cr[(size_t)(r / 2) * (p.w16 / 2) + x / 2]) - 128;
-          uint8_t* q = o + ((size_t)r * W + x) * 3;
-          q[0] = (uint8_t)std::min(255, std::max(0, (298 * c + 409 * e + 128) >> 8));
-          q[1] = (uint8_t)std::min(255, std::max(0, (298 * c - 100 * d - 208 * e + 128) >> 8));
-          q[2] = (uint8_t)std::min(255, std::max(0, (298 * c + 516 * d + 128) >> 8));
-        }
-    });
-  }
-  return out;
+  py::capsule owner(dst, [](void* ptr) { delete[] static_cast<uint8_t*>(ptr); });
+  return u8arr({F, H, W, 3}, dst, owner);
 }
 
 static py::bytes as_bytes32(const py::bytes& b, const char* what) {
@@ -412,7 +527,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("secp256k1_pubkey", &py_secp_pubkey, "uncompressed public key X||Y");
   m.def("secp256k1_recover", &py_secp_recover, "ecrecover -> X||Y or None");
   m.def("sha256", &py_sha256, "SHA-256 (the RFC 6979 HMAC's hash; checked against hashlib)");
-  m.doc() = "arbius_amd native CPU runtime (keccak256, PNG, H.264 intra codec, secp256k1)";
+  m.doc() = "arbius_amd native CPU runtime (keccak256, PNG, H.264 CAVLC codec, secp256k1)";
   m.def("keccak256", &keccak256, "Ethereum keccak-256");
   m.def("png_encode", &png_encode, py::arg("img"), py::arg("level") = 6, "deterministic filter-0 PNG");
   m.def("pcm_slice_body", &pcm_slice_body, py::arg("frame"), py::arg("threads") = 8,
@@ -421,10 +536,17 @@ PYBIND11_MODULE(_native, m) {
         "H.264 CAVLC intra: RGB frames [F, H, W, 3] -> (sps, pps, [IDR NAL])");
   m.def("h264_encode_yuv", &h264_encode_yuv, py::arg("y"), py::arg("cb"), py::arg("cr"), py::arg("qp"),
         py::arg("idr_pic_id") = 0, "one 4:2:0 picture -> (IDR NAL, recon Y, Cb, Cr)");
-  m.def("h264_parameter_sets", &h264_parameter_sets, "(sps, pps) NALs for the CAVLC intra stream");
-  m.def("h264_decode", &h264_decode, py::arg("nals"), py::arg("threads") = 8,
-        "decode intra CAVLC / I_PCM NAL units -> [(Y, Cb, Cr, (w, h))]");
+  m.def("h264_parameter_sets", &h264_parameter_sets, py::arg("width"), py::arg("height"), py::arg("qp"),
+        py::arg("max_refs") = 1, "(sps, pps) NALs of the CAVLC streams");
+  m.def("h264_encode_rgb_stream", &h264_encode_rgb_stream, py::arg("frames"), py::arg("qp"), py::arg("gop"),
+        py::arg("threads") = 8, py::arg("rows_per_slice") = 4,
+        "H.264 CAVLC IPPP: RGB frames [F, H, W, 3] -> (sps, pps, [[slice NALs] per picture])");
+  m.def("h264_encode_yuv_stream", &h264_encode_yuv_stream, py::arg("y"), py::arg("cb"), py::arg("cr"), py::arg("qp"),
+        py::arg("gop"), py::arg("seed") = 0, py::arg("max_refs") = 1, py::arg("threads") = 4,
+        py::arg("rows_per_slice") = 4, "4:2:0 pictures -> ([[NAL]], recon Y, Cb, Cr)");
+  m.def("h264_decode", &h264_decode, py::arg("nals"), py::arg("threads") = 8, py::arg("with_side") = false,
+        "decode Constrained Baseline CAVLC NAL units -> [(Y, Cb, Cr, (w, h)[, side info])]");
   m.def("h264_decode_rgb", &h264_decode_rgb, py::arg("nals"), py::arg("threads") = 8,
-        "decode intra CAVLC / I_PCM NAL units -> uint8 RGB [F, H, W, 3] (cropped)");
+        "decode Constrained Baseline CAVLC NAL units -> uint8 RGB [F, H, W, 3] (cropped)");
   m.def("h264_tables_ok", &h264::tables_prefix_free, "every CAVLC VLC table is prefix-free");
 }

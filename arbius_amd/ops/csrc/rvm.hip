@@ -397,7 +397,8 @@ ARB_API int arb_rvm_pool3(const void* s0, void* s1, void* s2, void* s3, int T, i
   return (int)hipGetLastError();
 }
 
-ARB_API int arb_rvm_upcat(const void* x, int hx, int wx, int cx, const void* f, int cf, const void* sp, int cs, void* dst,
+ARB_API int arb_rvm_upcat(const void* x, int hx, int wx, int cx, const void* f, int cf, const void* sp, int cs,
+                          void* dst,
                           int T, int H, int W, int Cd, hipStream_t s) {
   if (cx + cf + cs > Cd || 2 * hx < H || 2 * wx < W) return -1;
   rvm_upcat<<<rgrid((long)T * H * W * Cd), 256, 0, s>>>((const h16*)x, hx, wx, cx, (const h16*)f, cf, (const h16*)sp,

@@ -7,12 +7,13 @@ function of the frames, so the codec is self-contained and bit-exact:
 
 * colour: RGB -> BT.601 limited-range YCbCr 4:2:0 in integer arithmetic
   (chroma = rounded 2x2 mean of the RGB samples, then the integer matrix);
-* bitstream (default, ``codec="avc-intra"``): H.264 Constrained Baseline, every picture one
-  IDR slice of Intra_16x16 macroblocks coded with CAVLC at a fixed QP, deblocking disabled
-  (``native/src/h264.cpp``: the encoder's reconstruction IS every decoder's output).  Round 1
-  wrote raw I_PCM macroblocks (``codec="pcm"``, still available and still decodable): a
-  48-frame 1080p clip was ~149 MB per task pinned to IPFS; the CAVLC intra stream is 10-40x
-  smaller;
+* bitstream: H.264 Constrained Baseline CAVLC at a fixed QP (``native/src/h264.cpp``; the
+  encoder's reconstruction IS every conforming decoder's output):
+  - ``codec="avc"`` (default): IPPP - an IDR every ``GOP`` pictures, P pictures of P_Skip /
+    P_L0_16x16 (quarter-sample motion search) / Intra_16x16 macroblocks, in-loop deblocking on,
+    slices of ``ROWS_PER_SLICE`` macroblock rows encoded in parallel;
+  - ``codec="avc-intra"``: every picture one IDR slice of Intra_16x16 macroblocks, deblocking off;
+  - ``codec="pcm"``: raw I_PCM macroblocks (round 1; a 48-frame 1080p clip was ~149 MB);
 * container: ftyp + moov (faststart) + mdat, fixed zero timestamps, AVCC
   4-byte NAL lengths, avcC with the SPS/PPS.
 
@@ -28,7 +29,8 @@ import numpy as np
 PROFILE_IDC, CONSTRAINT_FLAGS, LEVEL_IDC = 66, 0xC0, 51
 # fixed quantiser of the CAVLC intra stream (part of NUMERICS_VERSION: changing it changes CIDs)
 INTRA_QP = 20
-CODECS = ("avc-intra", "pcm")
+GOP, ROWS_PER_SLICE = 30, 4
+CODECS = ("avc", "avc-intra", "pcm")
 
 
 class _Bits:
@@ -83,14 +85,14 @@ def _nal(ref_idc: int, typ: int, payload: bytes) -> bytes:
     return bytes([(ref_idc << 5) | typ]) + payload
 
 
-def sps_pps(width: int, height: int, qp: int = 26) -> Tuple[bytes, bytes]:
+def sps_pps(width: int, height: int, qp: int = 26, max_refs: int = 1) -> Tuple[bytes, bytes]:
     mbw, mbh = (width + 15) // 16, (height + 15) // 16
     s = _Bits()
     s.u(8, PROFILE_IDC); s.u(8, CONSTRAINT_FLAGS); s.u(8, LEVEL_IDC)
     s.ue(0)               # seq_parameter_set_id
     s.ue(0)               # log2_max_frame_num_minus4
     s.ue(2)               # pic_order_cnt_type
-    s.ue(1)               # max_num_ref_frames
+    s.ue(max_refs)        # max_num_ref_frames
     s.u(1, 0)             # gaps_in_frame_num_value_allowed_flag
     s.ue(mbw - 1); s.ue(mbh - 1)
     s.u(1, 1)             # frame_mbs_only_flag
@@ -185,7 +187,7 @@ def _full(typ: bytes, version: int, flags: int, *parts: bytes) -> bytes:
 _MATRIX = struct.pack(">9I", 0x10000, 0, 0, 0, 0x10000, 0, 0, 0, 0x40000000)
 
 
-def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False) -> bytes:
+def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False, sync=None) -> bytes:
     F = len(sizes)
     dur_ms = int(round(F * 1000 / fps))
     mvhd = _full(b"mvhd", 0, 0, struct.pack(">IIII", 0, 0, 1000, dur_ms), struct.pack(">IH", 0x10000, 0x100),
@@ -198,7 +200,8 @@ def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False) -> bytes:
     dinf = _box(b"dinf", _full(b"dref", 0, 0, struct.pack(">I", 1), _full(b"url ", 0, 1)))
     avcc = _box(b"avcC", bytes([1, PROFILE_IDC, CONSTRAINT_FLAGS, LEVEL_IDC, 0xFF, 0xE1]),
                 struct.pack(">H", len(sps)), sps, b"\x01", struct.pack(">H", len(pps)), pps)
-    name = (b"\x0bI_PCM H.264" if pcm else b"\x0fAVC intra CAVLC").ljust(32, b"\0")
+    name = (b"\x0bI_PCM H.264" if pcm else b"\x0fAVC intra CAVLC" if sync is None else
+            b"\x0eAVC IPPP CAVLC").ljust(32, b"\0")
     avc1 = _box(b"avc1", b"\0" * 6, struct.pack(">H", 1), b"\0" * 16, struct.pack(">HH", width, height),
                 struct.pack(">III", 0x480000, 0x480000, 0), struct.pack(">H", 1), name,
                 struct.pack(">Hh", 0x18, -1), avcc)
@@ -207,13 +210,16 @@ def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False) -> bytes:
     stsc = _full(b"stsc", 0, 0, struct.pack(">IIII", 1, 1, F, 1))
     stsz = _full(b"stsz", 0, 0, struct.pack(">II", 0, F), struct.pack(">%dI" % F, *sizes))
     stco = _full(b"stco", 0, 0, struct.pack(">II", 1, mdat_offset))
-    stbl = _box(b"stbl", stsd, stts, stsc, stsz, stco)
+    # stss: the sync (IDR) samples; absent = every sample is a sync sample (intra streams)
+    stss = [] if sync is None else [_full(b"stss", 0, 0, struct.pack(">I", len(sync)),
+                                          struct.pack(">%dI" % len(sync), *[k + 1 for k in sync]))]
+    stbl = _box(b"stbl", stsd, stts, *stss, stsc, stsz, stco)
     minf = _box(b"minf", vmhd, dinf, stbl)
     mdia = _box(b"mdia", mdhd, hdlr, minf)
     return _box(b"moov", mvhd, _box(b"trak", tkhd, mdia))
 
 
-def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra", threads: int = 16) -> bytes:
+def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc", threads: int = 16) -> bytes:
     """uint8 RGB frames [H, W, 3] (all the same size) -> MP4 bytes (deterministic)."""
     frames = list(frames)
     if not frames:
@@ -226,23 +232,29 @@ def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra",
         if f.shape != (H, W, 3) or f.dtype != np.uint8:
             raise ValueError("encode_mp4: frames must be uint8 [H, W, 3] of one size")
     pcm = codec == "pcm"
+    sync = None
     if pcm:
         sps, pps = sps_pps(W, H)
-        nals = [encode_idr_pcm(f, i) for i, f in enumerate(frames)]
+        pics = [[encode_idr_pcm(f, i)] for i, f in enumerate(frames)]
     else:
         from .. import native
         if not native.loaded:
-            raise RuntimeError("encode_mp4: the native runtime (H.264 intra encoder) is not built; "
+            raise RuntimeError("encode_mp4: the native runtime (H.264 encoder) is not built; "
                                "run python -m arbius_amd.native.build")
         sps, pps = sps_pps(W, H, INTRA_QP)
-        _, _, nals = native.h264_encode_rgb(np.stack(frames), INTRA_QP, threads)
-    samples = [struct.pack(">I", len(n)) + n for n in nals]
+        if codec == "avc":
+            _, _, pics = native.h264_encode_rgb_stream(np.stack(frames), INTRA_QP, GOP, threads, ROWS_PER_SLICE)
+            sync = list(range(0, len(frames), GOP))
+        else:
+            _, _, nals = native.h264_encode_rgb(np.stack(frames), INTRA_QP, threads)
+            pics = [[n] for n in nals]
+    samples = [b"".join(struct.pack(">I", len(n)) + n for n in p) for p in pics]
     sizes = [len(s) for s in samples]
     ftyp = _box(b"ftyp", b"isom", struct.pack(">I", 512), b"isomiso2avc1mp41")
-    moov_len = len(_moov(W, H, fps, sizes, sps, pps, 0, pcm))
+    moov_len = len(_moov(W, H, fps, sizes, sps, pps, 0, pcm, sync))
     mdat_payload = sum(sizes)
     offset = len(ftyp) + moov_len + 8
-    moov = _moov(W, H, fps, sizes, sps, pps, offset, pcm)
+    moov = _moov(W, H, fps, sizes, sps, pps, offset, pcm, sync)
     if 8 + mdat_payload > 0xFFFFFFFF:
         raise ValueError("encode_mp4: output above 4 GiB")
     return ftyp + moov + struct.pack(">I", 8 + mdat_payload) + b"mdat" + b"".join(samples)

@@ -14,9 +14,10 @@ Local paths, ``file://`` and plain ``http://`` are refused (``VideoSourceError``
 download is capped at ``MAX_VIDEO_BYTES``.
 
 Containers: MP4 (any single avc1 track) or a raw Annex-B H.264 stream, decoded by the native
-intra decoder (``native/src/h264.cpp``: CAVLC I slices - I_PCM / Intra_16x16 / Intra_4x4,
-deblocking off; exactly what ``utils/mp4.py`` writes), and ``.npy`` uint8 [T, H, W, 3]
-(``allow_pickle=False``).  Anything else (P/B frames, CABAC, in-loop deblocking) is decoded
+decoder (``native/src/h264.cpp``: Constrained Baseline CAVLC - I and P slices, I_PCM /
+Intra_16x16 / Intra_4x4, P_Skip and every P partition, multiple reference pictures, in-loop
+deblocking; a superset of what ``utils/mp4.py`` writes), and ``.npy`` uint8 [T, H, W, 3]
+(``allow_pickle=False``).  Anything else (B slices, CABAC / High profile, interlace) is decoded
 by an ``ffmpeg`` binary when one is on PATH; the image ships none, so ``probe`` rejects such
 inputs at hydration (``UndecodableVideo``: the node skips the task, it does not mark it
 invalid - a miner with a full decoder may solve it).
@@ -213,7 +214,7 @@ def yuv420_to_rgb(y, cb, cr, H, W) -> np.ndarray:
 
 
 class UndecodableVideo(ValueError):
-    """The input is not a video this node can decode (outside the native H.264 intra subset and
+    """The input is not a video this node can decode (outside the native H.264 I/P subset and
     no ffmpeg): the task is skipped, never marked invalid - other miners may decode it."""
 
 
@@ -242,30 +243,32 @@ def _demux(data: bytes) -> Tuple[List[bytes], int]:
 
 def probe(data: bytes) -> None:
     """Cheap decodability check (hydration): container, then every slice header's slice_type
-    must be I, and the first picture must decode through the native intra decoder."""
+    must be I or P (no B / SP / SI), and the first two pictures must decode through the native
+    decoder (which refuses CABAC, interlace, weighted prediction, ... in their parameter sets and
+    slice headers)."""
     if data[:6] == b"\x93NUMPY":
         return
     if shutil.which("ffmpeg"):
         return
     nals, _ = _demux(data)
-    first_pic, started, done = [], False, False
+    head_pics, pictures = [], 0
     for n in nals:
         typ = n[0] & 0x1F
         if typ in (1, 5):
             head = "".join(f"{b:08b}" for b in n[1:9].replace(b"\x00\x00\x03", b"\x00\x00"))
             first_mb, i = _ue(head, 0)
             slice_type, _ = _ue(head, i)
-            if slice_type % 5 != 2:
-                raise UndecodableVideo("input video has inter (P/B) slices: only intra H.264 decodes natively")
-            done = done or (started and first_mb == 0)
-            if not done:
-                first_pic.append(n)
-                started = True
-        elif not started:
-            first_pic.append(n)
+            if slice_type % 5 not in (0, 2):
+                raise UndecodableVideo("input video has B / SP / SI slices: only I and P slices decode natively")
+            if first_mb == 0:
+                pictures += 1
+            if pictures <= 2:
+                head_pics.append(n)
+        elif pictures == 0:
+            head_pics.append(n)
     from .mp4 import decode_h264
     try:
-        decode_h264(first_pic)
+        decode_h264(head_pics)
     except ValueError as e:
         raise UndecodableVideo(str(e)) from None
 
@@ -282,7 +285,7 @@ def decode(data: bytes) -> Tuple[np.ndarray, int]:
         native_err = e
     ff = shutil.which("ffmpeg")
     if ff is None:
-        raise UndecodableVideo(f"native H.264 intra decoder: {native_err}; no ffmpeg binary for other streams")
+        raise UndecodableVideo(f"native H.264 decoder: {native_err}; no ffmpeg binary for other streams")
     with tempfile.NamedTemporaryFile(suffix=".mp4") as f:
         f.write(data)
         f.flush()

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Build the native C++ runtime (native/src/*.cpp: keccak, PNG, H.264 I_PCM, secp256k1) with
-AddressSanitizer + UndefinedBehaviorSanitizer on the CPU and exercise every entry point against
-its Python reference under the sanitizer runtime.  Host code only - no GPU.
+"""Build the native C++ runtime (native/src/*.cpp: keccak, PNG, H.264 codec, secp256k1) with
+AddressSanitizer + UndefinedBehaviorSanitizer (or ThreadSanitizer) on the CPU and exercise every
+entry point against its Python reference under the sanitizer runtime, plus corrupted H.264
+input.  Host code only - no GPU.
 
-    python scripts/sanitize_native.py [OUT_DIR]      # exit 0 = clean
+    python scripts/sanitize_native.py [OUT_DIR]          # exit 0 = clean
+    python scripts/sanitize_native.py --tsan [OUT_DIR]   # data races in the threaded codec
 """
 import os
 import subprocess
@@ -93,27 +95,66 @@ for h in hostile:
 frames = rng.integers(0, 256, (3, 40, 72, 3), dtype=np.uint8)
 _, _, nals = N.h264_encode_rgb(frames, 24, 3)
 assert N.h264_decode_rgb([sps_ for sps_ in N.h264_parameter_sets(72, 40, 24)] + list(nals), 2).shape == (3, 40, 72, 3)
+# IPPP / coverage-mode streams (P slices, several references, slice-parallel decode, wavefront
+# deblocking): round trip, then corrupted P slices
+F = 6
+ys = rng.integers(0, 256, (F, 48, 64), dtype=np.uint8)
+cbs = rng.integers(0, 256, (F, 24, 32), dtype=np.uint8)
+crs = rng.integers(0, 256, (F, 24, 32), dtype=np.uint8)
+for seed, refs in ((0, 1), (3, 3)):
+    pics, ry, rcb, rcr = N.h264_encode_yuv_stream(ys, cbs, crs, 26, 4, seed, refs, 4, 1)
+    ps = list(N.h264_parameter_sets(64, 48, 26, refs))
+    flat = [n for p in pics for n in p]
+    dec = N.h264_decode(ps + flat, 4)
+    assert all((d[0] == ry[i]).all() for i, d in enumerate(dec))
+    N.h264_decode(ps + flat, 4, True)
+    for trial in range(300):
+        bad = list(flat)
+        k = int(rng.integers(0, len(bad)))
+        b = bytearray(bad[k])
+        if trial % 3 == 0:
+            b = b[:rng.integers(1, len(b))]
+        else:
+            for _ in range(1 + trial % 4):
+                b[rng.integers(1, len(b))] ^= 1 << int(rng.integers(0, 8))
+        bad[k] = bytes(b)
+        try:
+            N.h264_decode(ps + bad, 4)
+        except ValueError:
+            pass
+        try:
+            N.h264_decode_rgb(ps + bad, 3)
+        except ValueError:
+            pass
+frames = rng.integers(0, 256, (5, 40, 72, 3), dtype=np.uint8)
+s_, p_, pics = N.h264_encode_rgb_stream(frames, 24, 3, 4, 1)
+assert N.h264_decode_rgb([s_, p_] + [n for p in pics for n in p], 4).shape == (5, 40, 72, 3)
 print("sanitized native runtime: all entry points clean")
 '''
 
 
 def main():
-    out_dir = sys.argv[1] if len(sys.argv) > 1 else tempfile.mkdtemp(prefix="arb_asan_")
+    args = [a for a in sys.argv[1:] if a != "--tsan"]
+    tsan = "--tsan" in sys.argv        # ThreadSanitizer build (slice-parallel decode, wavefront deblocking)
+    out_dir = args[0] if args else tempfile.mkdtemp(prefix="arb_asan_")
     import pybind11
     so = os.path.join(out_dir, "_native" + sysconfig.get_config_var("EXT_SUFFIX"))
-    flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer"] + (
+        ["-fsanitize=thread"] if tsan else ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
     cmd = ["g++", *flags, "-shared", "-fPIC", "-std=c++17", "-pthread", "-I", pybind11.get_include(),
            "-I", sysconfig.get_paths()["include"], os.path.join(SRC, "native.cpp"), os.path.join(SRC, "secp256k1.cpp"),
            os.path.join(SRC, "h264.cpp"),
            "-lz", "-o", so]
     subprocess.run(cmd, check=True)
-    asan = subprocess.check_output(["g++", "-print-file-name=libasan.so"], text=True).strip()
-    ubsan = subprocess.check_output(["g++", "-print-file-name=libubsan.so"], text=True).strip()
-    env = dict(os.environ, LD_PRELOAD=f"{asan}:{ubsan}", ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
-               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", PYTHONPATH=out_dir, ARB_ROOT=ROOT)
+    lib = lambda n: subprocess.check_output(["g++", f"-print-file-name={n}"], text=True).strip()
+    preload = lib("libtsan.so") if tsan else f"{lib('libasan.so')}:{lib('libubsan.so')}"
+    env = dict(os.environ, LD_PRELOAD=preload, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               TSAN_OPTIONS="halt_on_error=1:report_signal_unsafe=0",
+               PYTHONPATH=out_dir, ARB_ROOT=ROOT)
     r = subprocess.run([sys.executable, "-c", EXERCISE], env=env, capture_output=True, text=True)
     sys.stdout.write(r.stdout)
-    sys.stderr.write(r.stderr[-4000:])
+    sys.stderr.write(r.stderr[:6000] + ("\n...\n" + r.stderr[-2000:] if len(r.stderr) > 8000 else r.stderr[6000:]))
     return r.returncode
 
 

@@ -157,13 +157,35 @@ def test_h264_multi_slice_and_pcm_decode():
         assert (y == ey).all() and (cb == ecb).all() and (cr == ecr).all()
 
 
+def test_mp4_avc_ippp_default_roundtrip():
+    """The default output codec (IPPP, deblocked, row-band slices) through the MP4 container: sync
+    samples listed in stss, probe + decode accept it, and the picture is close to the intra one."""
+    from arbius_amd.utils.mp4 import GOP, read_mp4_nals
+    from arbius_amd.utils.video_io import decode, probe
+    yy, xx = np.mgrid[0:90, 0:160]
+    frames = [np.stack([(xx + 3 * t) % 256, (yy * 2 + t) % 256, ((xx + yy) // 2) % 256], -1).astype(np.uint8)
+              for t in range(GOP + 5)]
+    a = encode_mp4(frames, 12)
+    assert a == encode_mp4(frames, 12, threads=1)
+    assert b"stss" in a and b"AVC IPPP" in a
+    intra = encode_mp4(frames, 12, codec="avc-intra")
+    assert len(a) < 0.6 * len(intra)
+    _, nals, _ = read_mp4_nals(a)
+    assert {n[0] & 0x1F for n in nals[2:]} == {1, 5}
+    probe(a)
+    dec, fps = decode(a)
+    ref, _ = decode(encode_mp4(frames, 12, codec="pcm"))
+    assert fps == 12 and dec.shape == (GOP + 5, 90, 160, 3)
+    assert 10 * np.log10(255 ** 2 / np.mean((dec.astype(float) - ref) ** 2)) > 36
+
+
 def test_mp4_avc_intra_roundtrip_small_and_deterministic():
     from arbius_amd.utils.video_io import decode, probe
     yy, xx = np.mgrid[0:90, 0:160]
     frames = [np.stack([(xx + 3 * t) % 256, (yy * 2 + t) % 256, ((xx + yy) // 2) % 256], -1).astype(np.uint8)
               for t in range(6)]
-    a = encode_mp4(frames, 12)
-    assert a == encode_mp4(frames, 12, threads=1)          # thread count never changes bytes
+    a = encode_mp4(frames, 12, codec="avc-intra")
+    assert a == encode_mp4(frames, 12, codec="avc-intra", threads=1)   # thread count never changes bytes
     pcm = encode_mp4(frames, 12, codec="pcm")
     assert len(pcm) > 10 * len(a)
     probe(a)
@@ -175,17 +197,17 @@ def test_mp4_avc_intra_roundtrip_small_and_deterministic():
     assert 10 * np.log10(255 ** 2 / mse) > 38
 
 
-def test_probe_rejects_streams_outside_the_intra_subset():
+def test_probe_rejects_streams_outside_the_decoder_subset():
     import pytest
     from arbius_amd.utils.mp4 import _Bits, _ep
     from arbius_amd.utils.video_io import UndecodableVideo, decode, probe
     sps, pps = sps_pps(64, 64)
     hdr = _Bits()
-    hdr.ue(0); hdr.ue(5); hdr.ue(0); hdr.u(4, 1)          # first_mb 0, slice_type P
+    hdr.ue(0); hdr.ue(6); hdr.ue(0); hdr.u(4, 1)          # first_mb 0, slice_type B
     hdr.trailing()
-    p_slice = b"\x41" + _ep(hdr.bytes())
-    stream = b"".join(b"\x00\x00\x00\x01" + n for n in (sps, pps, p_slice))
-    with pytest.raises(UndecodableVideo, match="inter"):
+    b_slice = b"\x41" + _ep(hdr.bytes())
+    stream = b"".join(b"\x00\x00\x00\x01" + n for n in (sps, pps, b_slice))
+    with pytest.raises(UndecodableVideo, match="B / SP / SI"):
         probe(stream)
     with pytest.raises(UndecodableVideo):
         decode(stream)
