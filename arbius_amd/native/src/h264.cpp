@@ -2545,7 +2545,7 @@ void decode_slice_data(BitReader& br, Frame& f, const SliceCtx& sc, int end_mb, 
 }  // namespace
 
 void decode(const std::vector<std::string>& nals, int threads, const LayoutFn& on_layout, const PictureSink& sink,
-            std::vector<SideInfo>* side) {
+            std::vector<SideInfo>* side, uint64_t max_samples) {
   // Pass 1 (sequential): parameter sets and the split into pictures (a picture starts at a slice with
   // first_mb_in_slice == 0), grouped into coded video sequences from IDR to IDR.  Pass 2: every
   // sequence decodes in order (P pictures reference earlier ones); sequences run in parallel.
@@ -2588,11 +2588,12 @@ void decode(const std::vector<std::string>& nals, int threads, const LayoutFn& o
     }
   }
   // untrusted input: a few bits per macroblock can declare huge pictures, so bound what decoding
-  // may allocate (4K per picture via the SPS limits, 2^31 luma samples - ~3.2 GB of 4:2:0 - in total)
+  // may allocate: 4K per picture via the SPS limits, max_samples luma samples in total (default
+  // 2^30: ~1.6 GB of 4:2:0 planes or ~3.2 GB of RGB, about 17 s of 1080p at 30 fps)
   uint64_t samples = 0;
   for (const auto& sq : seqs)
     for (const Pic& j : sq) samples += uint64_t(j.sps.mbw) * j.sps.mbh * 256;
-  if (samples > (uint64_t(1) << 31)) throw std::runtime_error("h264: video too large to decode");
+  if (samples > max_samples) throw std::runtime_error("h264: video too large to decode");
   std::vector<size_t> base(seqs.size(), 0);
   for (size_t s = 1; s < seqs.size(); ++s) base[s] = base[s - 1] + seqs[s - 1].size();
   std::vector<std::pair<int, int>> crops;
@@ -2712,7 +2713,7 @@ std::vector<Picture> decode(const std::vector<std::string>& nals, int threads) {
   std::vector<Picture> out;
   decode(
       nals, threads, [&](const std::vector<std::pair<int, int>>& crops) { out.resize(crops.size()); },
-      [&](size_t i, Picture&& p, int) { out[i] = std::move(p); }, nullptr);
+      [&](size_t i, Picture&& p, int) { out[i] = std::move(p); }, nullptr, kDefaultMaxSamples);
   return out;
 }
 

@@ -65,8 +65,9 @@ struct SideInfo {
 };
 using LayoutFn = std::function<void(const std::vector<std::pair<int, int>>& crops)>;
 using PictureSink = std::function<void(size_t index, Picture&& picture, int threads_free)>;
+constexpr uint64_t kDefaultMaxSamples = uint64_t(1) << 30;   // total luma samples a stream may decode to
 void decode(const std::vector<std::string>& nals, int threads, const LayoutFn& on_layout, const PictureSink& sink,
-            std::vector<SideInfo>* side = nullptr);
+            std::vector<SideInfo>* side = nullptr, uint64_t max_samples = kDefaultMaxSamples);
 
 // Table sanity: every VLC table is prefix-free (checked by tests/test_video.py).
 bool tables_prefix_free();

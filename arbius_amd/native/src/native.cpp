@@ -387,7 +387,7 @@ static py::array_t<T> vec_array(const std::vector<T>& v) {
 
 // NAL units (no start codes) -> [(Y, Cb, Cr, (crop_w, crop_h))]; raises ValueError outside the subset.
 // with_side=True (tests) appends a dict of the deblocking filter's inputs per picture.
-static py::list h264_decode(const std::vector<std::string>& nals, int threads, bool with_side) {
+static py::list h264_decode(const std::vector<std::string>& nals, int threads, bool with_side, uint64_t max_samples) {
   std::vector<h264::Picture> pics;
   std::vector<h264::SideInfo> side;
   {
@@ -395,7 +395,8 @@ static py::list h264_decode(const std::vector<std::string>& nals, int threads, b
     try {
       h264::decode(
           nals, threads, [&](const std::vector<std::pair<int, int>>& crops) { pics.resize(crops.size()); },
-          [&](size_t i, h264::Picture&& p, int) { pics[i] = std::move(p); }, with_side ? &side : nullptr);
+          [&](size_t i, h264::Picture&& p, int) { pics[i] = std::move(p); }, with_side ? &side : nullptr,
+          max_samples);
     } catch (const std::runtime_error& e) {
       py::gil_scoped_acquire gil;
       throw py::value_error(e.what());
@@ -435,7 +436,7 @@ static py::list h264_decode(const std::vector<std::string>& nals, int threads, b
 // reference is video_io.yuv420_to_rgb: nearest chroma upsampling, clipped).  The output is
 // allocated once from the stream's layout and every picture is converted as soon as it is decoded,
 // so no plane copy of the whole clip is ever held.
-static u8arr h264_decode_rgb(const std::vector<std::string>& nals, int threads) {
+static u8arr h264_decode_rgb(const std::vector<std::string>& nals, int threads, uint64_t max_samples) {
   uint8_t* dst = nullptr;
   int F = 0, H = 0, W = 0;
   std::string layout_err;
@@ -468,7 +469,8 @@ static u8arr h264_decode_rgb(const std::vector<std::string>& nals, int threads) 
                 q[2] = (uint8_t)std::min(255, std::max(0, (298 * c + 516 * d + 128) >> 8));
               }
             });
-          });
+          },
+          nullptr, max_samples);
     } catch (const std::runtime_error& e) {
       delete[] dst;
       py::gil_scoped_acquire gil;
@@ -545,8 +547,10 @@ PYBIND11_MODULE(_native, m) {
         py::arg("gop"), py::arg("seed") = 0, py::arg("max_refs") = 1, py::arg("threads") = 4,
         py::arg("rows_per_slice") = 4, "4:2:0 pictures -> ([[NAL]], recon Y, Cb, Cr)");
   m.def("h264_decode", &h264_decode, py::arg("nals"), py::arg("threads") = 8, py::arg("with_side") = false,
+        py::arg("max_samples") = h264::kDefaultMaxSamples,
         "decode Constrained Baseline CAVLC NAL units -> [(Y, Cb, Cr, (w, h)[, side info])]");
   m.def("h264_decode_rgb", &h264_decode_rgb, py::arg("nals"), py::arg("threads") = 8,
+        py::arg("max_samples") = h264::kDefaultMaxSamples,
         "decode Constrained Baseline CAVLC NAL units -> uint8 RGB [F, H, W, 3] (cropped)");
   m.def("h264_tables_ok", &h264::tables_prefix_free, "every CAVLC VLC table is prefix-free");
 }

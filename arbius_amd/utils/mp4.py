@@ -411,12 +411,20 @@ def _threads() -> int:
     return max(1, min(16, os.cpu_count() or 1))
 
 
+def max_video_samples() -> int:
+    """Total luma samples one input video may decode to (untrusted input: a few bits per macroblock
+    can declare huge videos).  Default 2^30 (~17 s of 1080p30, ~3.2 GB of RGB); operators with
+    more host memory raise it with ``$ARBIUS_MAX_VIDEO_SAMPLES``."""
+    import os
+    return int(os.environ.get("ARBIUS_MAX_VIDEO_SAMPLES", 1 << 30))
+
+
 def decode_h264_rgb(nals: Sequence[bytes]) -> np.ndarray:
     """NAL units -> uint8 RGB [F, H, W, 3] (cropped), native decoder + integer BT.601 inverse."""
     from .. import native
     if not native.loaded:
         raise RuntimeError("the native runtime (H.264 decoder) is not built")
-    return native.h264_decode_rgb(list(nals), _threads())
+    return native.h264_decode_rgb(list(nals), _threads(), max_video_samples())
 
 
 def decode_h264(nals: Sequence[bytes]):
@@ -425,7 +433,7 @@ def decode_h264(nals: Sequence[bytes]):
     from .. import native
     if not native.loaded:
         raise RuntimeError("the native runtime (H.264 decoder) is not built")
-    pics = native.h264_decode(list(nals), _threads())
+    pics = native.h264_decode(list(nals), _threads(), False, max_video_samples())
     if not pics:
         raise ValueError("no pictures in the H.264 stream")
     return [(y, cb, cr) for y, cb, cr, _ in pics], pics[0][3]

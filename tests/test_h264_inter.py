@@ -242,3 +242,17 @@ def test_decoder_refuses_inter_streams_outside_the_subset():
     with pytest.raises(ValueError, match="P slice"):           # P slice inside an IDR picture
         b = _Bits(); b.ue(0); b.ue(5); b.ue(0); b.u(4, 0); b.trailing()
         native.h264_decode([sps, pps, bytes([0x65]) + _ep(b.bytes())])
+
+
+def test_decode_budget_bounds_total_samples(monkeypatch):
+    """The total decoded size is capped before any picture is allocated (untrusted
+    input_video), and the cap is an operator knob."""
+    from arbius_amd.utils.mp4 import decode_h264_rgb
+    (Y, CB, CR), _ = _clip(4, 48, 80)
+    nals, _, _ = _encode(Y, CB, CR, 30, 2)
+    assert native.h264_decode_rgb(nals, 2).shape == (4, 48, 80, 3)
+    with pytest.raises(ValueError, match="too large"):
+        native.h264_decode_rgb(nals, 2, 4 * 48 * 80 - 1)
+    monkeypatch.setenv("ARBIUS_MAX_VIDEO_SAMPLES", str(3 * 48 * 80))
+    with pytest.raises(ValueError, match="too large"):
+        decode_h264_rgb(nals)
