@@ -7,10 +7,14 @@ by one rank and RCCL-broadcast").  This module maps the PUBLIC checkpoint layout
 template's model family onto this engine's module tree:
 
 * ``anythingv3`` (SD1.5, diffusers): ``unet/``, ``vae/``, ``text_encoder/``.
-* ``kandinsky2`` (Kandinsky 2.1, diffusers ``kandinsky-community/kandinsky-2-1`` checked out at
-  the root and ``kandinsky-2-1-prior`` under ``prior/``): ``unet/``, ``movq/``, ``text_encoder/``
-  (M-CLIP XLM-R), ``prior/prior/``, ``prior/text_encoder/`` (CLIP ViT-L/14 + projection),
-  ``prior/image_encoder/`` (only to compute the decoder's zero-image embedding once).
+* ``kandinsky2`` (Kandinsky 2.1), either layout:
+  - the ORIGINAL release the mainnet container ships (``decoder_fp16.ckpt``, ``prior_fp16.ckpt``,
+    ``movq_final.ckpt``, ``ViT-L-14_stats.th``, ``text_encoder/``, OpenAI CLIP ViT-L/14 state dict;
+    optionally under ``2_1/``) - used whenever ``decoder_fp16.ckpt`` is present;
+  - diffusers ``kandinsky-community/kandinsky-2-1`` at the root and ``kandinsky-2-1-prior`` under
+    ``prior/``: ``unet/``, ``movq/``, ``text_encoder/`` (M-CLIP XLM-R), ``prior/prior/``,
+    ``prior/text_encoder/`` (CLIP ViT-L/14 + projection), ``prior/image_encoder/`` (only to
+    compute the decoder's zero-image embedding once).
 * ``zeroscopev2xl`` / ``damo`` (diffusers ``UNet3DConditionModel`` text-to-video): ``unet/``,
   ``vae/``, ``text_encoder/`` (OpenCLIP ViT-H as ``CLIPTextModel``; its 23-layer export drops the
   unused last layer, which stays optional here).
@@ -364,6 +368,203 @@ def _prior_rules(m) -> List[Rule]:
     return R
 
 
+# ---- Kandinsky 2.1 ORIGINAL layout: the ai-forever ``Kandinsky_2.1`` release the kasumi-1 container
+# bakes in (templates/kandinsky2.json:1): ``decoder_fp16.ckpt`` (guided-diffusion ``Text2ImUNet``),
+# ``prior_fp16.ckpt`` (DALL-E 2 style prior under ``model.``), ``movq_final.ckpt`` (taming-style MoVQ),
+# ``ViT-L-14_stats.th`` (CLIP image-embedding mean / std), ``text_encoder/`` (M-CLIP, HF names) and
+# the OpenAI CLIP ViT-L/14 state dict (``ViT-L-14.pt`` / ``.safetensors``; a TorchScript archive is
+# refused by the weights-only loader - save its ``state_dict()`` once).  The names follow the
+# original module trees; the head interleaving of the fused QKV projections is undone at load.
+def _k2_orig_unet_rules(m) -> List[Rule]:
+    """guided-diffusion ``Text2ImUNet`` (input_blocks / middle_block / output_blocks; ResBlock
+    in_layers / emb_layers / out_layers / skip_connection; AttentionBlock norm / qkv / encoder_kv /
+    proj_out as conv1d with per-head [q|k|v] rows) -> ``GlideUNet``."""
+    R: List[Rule] = []
+    hd = m.cfg.head_channels
+
+    def res(dst, src, blk):
+        _wb(R, f"{dst}.norm1", f"{src}.in_layers.0")
+        _wb(R, f"{dst}.conv1", f"{src}.in_layers.2", "conv")
+        _wb(R, f"{dst}.emb", f"{src}.emb_layers.1")
+        _wb(R, f"{dst}.norm2", f"{src}.out_layers.0")
+        _wb(R, f"{dst}.conv2", f"{src}.out_layers.3", "conv")
+        if blk.skip is not None:
+            _wb(R, f"{dst}.skip", f"{src}.skip_connection", "conv")
+
+    def attn(dst, src):
+        _wb(R, f"{dst}.norm", f"{src}.norm")
+        R.append((f"{dst}.qkv.weight", f"heads1d@3@{hd}", (f"{src}.qkv.weight",)))
+        R.append((f"{dst}.qkv.bias", f"headsb@3@{hd}", (f"{src}.qkv.bias",)))
+        R.append((f"{dst}.ctx_kv.weight", f"heads1d@2@{hd}", (f"{src}.encoder_kv.weight",)))
+        R.append((f"{dst}.ctx_kv.bias", f"headsb@2@{hd}", (f"{src}.encoder_kv.bias",)))
+        R.append((f"{dst}.out.weight", "lin1d", (f"{src}.proj_out.weight",)))
+        R.append((f"{dst}.out.bias", "copy", (f"{src}.proj_out.bias",)))
+
+    _wb(R, "time1", "time_embed.0")
+    _wb(R, "time2", "time_embed.2")
+    _wb(R, "img_emb", "img_layer")
+    _wb(R, "text_pool", "proj_n")
+    _wb(R, "text_norm", "ln_model_n")
+    _wb(R, "img_tokens", "clip_to_seq")
+    _wb(R, "text_proj", "to_model_dim_n")
+    _wb(R, "conv_in", "input_blocks.0.0", "conv")
+    _wb(R, "norm_out", "out.0")
+    _wb(R, "conv_out", "out.2", "conv")
+    for i, blk in enumerate(m.down):                     # input_blocks[i + 1] = [ResBlock, (Attention)]
+        res(f"down.{i}.res", f"input_blocks.{i + 1}.0", blk.res)
+        if getattr(blk, "attn", None) is not None:
+            attn(f"down.{i}.attn", f"input_blocks.{i + 1}.1")
+    res("mid1", "middle_block.0", m.mid1)
+    attn("mid_attn", "middle_block.1")
+    res("mid2", "middle_block.2", m.mid2)
+    for i, blk in enumerate(m.up):                       # output_blocks[i] = [ResBlock, (Attention), (up ResBlock)]
+        res(f"up.{i}.res", f"output_blocks.{i}.0", blk.res)
+        k = 1
+        if blk.attn is not None:
+            attn(f"up.{i}.attn", f"output_blocks.{i}.1")
+            k = 2
+        if blk.upsample is not None:
+            res(f"up.{i}.upsample", f"output_blocks.{i}.{k}", blk.upsample)
+    return R
+
+
+def _k2_orig_movq_rules(m) -> List[Rule]:
+    """taming / MoVQ ``decoder`` (up.{level} in resolution order, highest first; mid.block_1 /
+    attn_1 / block_2; 1x1-conv q / k / v / proj_out; SpatialNorm norm_layer / conv_y / conv_b;
+    nin_shortcut) -> ``MoVQDecoder`` (whose up[0] is the first, lowest-resolution stage)."""
+    R: List[Rule] = []
+    d = "decoder"
+
+    def sn(dst, src):
+        R.append((f"{dst}.weight", "copy", (f"{src}.norm_layer.weight",)))
+        R.append((f"{dst}.bias", "copy", (f"{src}.norm_layer.bias",)))
+        R.append((f"{dst}.yb.weight", "convcat", (f"{src}.conv_y.weight", f"{src}.conv_b.weight")))
+        R.append((f"{dst}.yb.bias", "cat", (f"{src}.conv_y.bias", f"{src}.conv_b.bias")))
+
+    def res(dst, src, blk):
+        sn(f"{dst}.norm1", f"{src}.norm1")
+        _wb(R, f"{dst}.conv1", f"{src}.conv1", "conv")
+        sn(f"{dst}.norm2", f"{src}.norm2")
+        _wb(R, f"{dst}.conv2", f"{src}.conv2", "conv")
+        if blk.skip is not None:
+            _wb(R, f"{dst}.skip", f"{src}.nin_shortcut", "conv")
+
+    def attn(dst, src):
+        sn(f"{dst}.norm", f"{src}.norm")
+        R.append((f"{dst}.qkv.weight", "catlin1x1", (f"{src}.q.weight", f"{src}.k.weight", f"{src}.v.weight")))
+        R.append((f"{dst}.qkv.bias", "cat", (f"{src}.q.bias", f"{src}.k.bias", f"{src}.v.bias")))
+        R.append((f"{dst}.out.weight", "lin1x1", (f"{src}.proj_out.weight",)))
+        R.append((f"{dst}.out.bias", "copy", (f"{src}.proj_out.bias",)))
+
+    _wb(R, "post_quant", "post_quant_conv", "conv")
+    _wb(R, "conv_in", f"{d}.conv_in", "conv")
+    res("mid1", f"{d}.mid.block_1", m.mid1)
+    attn("mid_attn", f"{d}.mid.attn_1")
+    res("mid2", f"{d}.mid.block_2", m.mid2)
+    n = len(m.up)
+    for i, blk in enumerate(m.up):
+        lvl = n - 1 - i
+        for j, rb in enumerate(blk.res):
+            res(f"up.{i}.res.{j}", f"{d}.up.{lvl}.block.{j}", rb)
+        for j in range(len(blk.attn)):
+            attn(f"up.{i}.attn.{j}", f"{d}.up.{lvl}.attn.{j}")
+        if blk.upsample is not None:
+            _wb(R, f"up.{i}.upsample", f"{d}.up.{lvl}.upsample.conv", "conv")
+    sn("norm_out", f"{d}.norm_out")
+    _wb(R, "conv_out", f"{d}.conv_out", "conv")
+    return R
+
+
+def _k2_orig_prior_rules(m) -> List[Rule]:
+    """DALL-E 2 style ``PriorTransformer`` under ``model.`` (glide-text2im ``Transformer``:
+    resblocks.N.attn.c_qkv with per-head [q|k|v] rows, c_proj, ln_1, mlp.c_fc / c_proj, ln_2) +
+    the CLIP image-embedding statistics -> ``PriorTransformer``."""
+    hd = m.cfg.width // m.cfg.heads
+    p = "model"
+    R: List[Rule] = [("pos", "unsq1", (f"{p}.positional_embedding",)), ("query", "unsq2", (f"{p}.prd_emb",)),
+                     ("clip_mean", "unsq1", ("clip_mean",)), ("clip_std", "unsq1", ("clip_std",))]
+    _wb(R, "text_enc_proj", f"{p}.text_enc_proj")
+    _wb(R, "text_emb_proj", f"{p}.text_emb_proj")
+    _wb(R, "img_proj", f"{p}.clip_img_proj")
+    _wb(R, "time1", f"{p}.time_embed.0")
+    _wb(R, "time2", f"{p}.time_embed.2")
+    _wb(R, "final_ln", f"{p}.final_ln")
+    _wb(R, "out_proj", f"{p}.out_proj")
+    t = f"{p}.transformer.resblocks.#"
+    _wb(R, "blocks.#.ln1", f"{t}.ln_1")
+    R.append(("blocks.#.qkv.weight", f"heads@3@{hd}", (f"{t}.attn.c_qkv.weight",)))
+    R.append(("blocks.#.qkv.bias", f"headsb@3@{hd}", (f"{t}.attn.c_qkv.bias",)))
+    _wb(R, "blocks.#.out", f"{t}.attn.c_proj")
+    _wb(R, "blocks.#.ln2", f"{t}.ln_2")
+    _wb(R, "blocks.#.fc1", f"{t}.mlp.c_fc")
+    _wb(R, "blocks.#.fc2", f"{t}.mlp.c_proj")
+    return R
+
+
+def _openai_clip_text_rules() -> List[Rule]:
+    """OpenAI CLIP (``clip`` package) text tower names -> ``CLIPTextEncoder``."""
+    L = "transformer.resblocks.#"
+    R: List[Rule] = [("tok.weight", "copy", ("token_embedding.weight",)),
+                     ("pos.weight", "copy", ("positional_embedding",)),
+                     ("final_ln.weight", "copy", ("ln_final.weight",)), ("final_ln.bias", "copy", ("ln_final.bias",)),
+                     ("layers.#.qkv.weight", "copy", (f"{L}.attn.in_proj_weight",)),
+                     ("layers.#.qkv.bias", "copy", (f"{L}.attn.in_proj_bias",))]
+    for p in ("weight", "bias"):
+        R.extend([(f"layers.#.out.{p}", "copy", (f"{L}.attn.out_proj.{p}",)),
+                  (f"layers.#.ln1.{p}", "copy", (f"{L}.ln_1.{p}",)),
+                  (f"layers.#.ln2.{p}", "copy", (f"{L}.ln_2.{p}",)),
+                  (f"layers.#.fc1.{p}", "copy", (f"{L}.mlp.c_fc.{p}",)),
+                  (f"layers.#.fc2.{p}", "copy", (f"{L}.mlp.c_proj.{p}",))])
+    return R
+
+
+def openai_visual_to_hf(src: Dict[str, Tensor]) -> Dict[str, Tensor]:
+    """OpenAI CLIP ``visual.*`` names -> transformers ``CLIPVisionModelWithProjection`` names (the
+    decoder's zero-image embedding is computed through transformers)."""
+    out: Dict[str, Tensor] = {}
+    V, H = "visual.", "vision_model."
+    direct = {"class_embedding": "embeddings.class_embedding", "conv1.weight": "embeddings.patch_embedding.weight",
+              "positional_embedding": "embeddings.position_embedding.weight", "ln_pre.weight": "pre_layrnorm.weight",
+              "ln_pre.bias": "pre_layrnorm.bias", "ln_post.weight": "post_layernorm.weight",
+              "ln_post.bias": "post_layernorm.bias"}
+    for k, v in src.items():
+        if not k.startswith(V):
+            continue
+        r = k[len(V):]
+        if r in direct:
+            out[H + direct[r]] = v
+        elif r == "proj":
+            out["visual_projection.weight"] = v.t().contiguous()
+        elif r.startswith("transformer.resblocks."):
+            i, rest = r[len("transformer.resblocks."):].split(".", 1)
+            L = f"{H}encoder.layers.{i}."
+            if rest in ("attn.in_proj_weight", "attn.in_proj_bias"):
+                kind = "weight" if rest.endswith("weight") else "bias"
+                for name, part in zip(("q_proj", "k_proj", "v_proj"), v.chunk(3, 0)):
+                    out[f"{L}self_attn.{name}.{kind}"] = part.contiguous()
+            else:
+                ren = {"attn.out_proj.": "self_attn.out_proj.", "ln_1.": "layer_norm1.", "ln_2.": "layer_norm2.",
+                       "mlp.c_fc.": "mlp.fc1.", "mlp.c_proj.": "mlp.fc2."}
+                for a, b in ren.items():
+                    if rest.startswith(a):
+                        out[L + b + rest[len(a):]] = v
+    return out
+
+
+def _k2_stats(weights_dir: str) -> Dict[str, Tensor]:
+    """``ViT-L-14_stats.th``: (mean, std) of the CLIP image embeddings (tuple, list or dict)."""
+    for rel in ("ViT-L-14_stats.th", "2_1/ViT-L-14_stats.th"):
+        path = os.path.join(weights_dir, rel)
+        if os.path.isfile(path):
+            obj = torch.load(path, map_location="cpu", weights_only=True)
+            if isinstance(obj, dict):
+                return {"clip_mean": obj["clip_mean"] if "clip_mean" in obj else obj["mean"],
+                        "clip_std": obj["clip_std"] if "clip_std" in obj else obj["std"]}
+            mean, std = obj
+            return {"clip_mean": mean, "clip_std": std}
+    return {}
+
+
 # ---- text-to-video UNet3D (diffusers UNet3DConditionModel: zeroscope_v2_XL, text-to-video-ms-1.7b)
 def _temporal_transformer_rules(dst: str, src: str) -> List[Rule]:
     """diffusers ``TransformerTemporalModel`` (double self-attention over frames, GEGLU FF)."""
@@ -497,7 +698,25 @@ def _bn_scale(gamma: Tensor, var: Tensor, eps: float) -> Tensor:
     return gamma.double() / torch.sqrt(var.double() + eps)
 
 
+def _heads_split(kind: str):
+    """"heads@N@HD" / "heads1d@N@HD" / "headsb@N@HD" -> (N, HD): a fused projection whose output rows
+    are interleaved PER HEAD ([head][q|k|v][HD], guided-diffusion / GLIDE / DALL-E 2 QKV attention),
+    against the engine's [q | k | v] concatenation of whole projections."""
+    _, n, hd = kind.split("@")
+    return int(n), int(hd)
+
+
 def _to_target(kind: str, srcs: List[Tensor], like: Tensor) -> Tensor:
+    if kind.startswith(("heads@", "heads1d@", "headsb@")):
+        n, hd = _heads_split(kind)
+        t = srcs[0]
+        t = t.reshape(t.shape[0], -1) if t.dim() > 1 else t           # conv1d [O, I, 1] -> [O, I]
+        rest = tuple(t.shape[1:])
+        return t.reshape(-1, n, hd, *rest).transpose(0, 1).reshape(t.shape)
+    if kind == "T":
+        return srcs[0].t()
+    if kind == "catlin1x1":
+        return torch.cat([s.reshape(s.shape[0], s.shape[1]) for s in srcs], 0)
     if kind == "conv":
         t = srcs[0]
         t = t.permute(0, 2, 3, 1) if t.dim() == 4 else t      # OIHW -> OHWI
@@ -505,7 +724,7 @@ def _to_target(kind: str, srcs: List[Tensor], like: Tensor) -> Tensor:
             t = t[:, None, None, :]
     elif kind == "lin1x1":
         t = srcs[0]
-        t = t.reshape(t.shape[0], t.shape[1]) if t.dim() == 4 else t
+        t = t.reshape(t.shape[0], t.shape[1]) if t.dim() > 2 else t    # 1x1 conv2d / conv1d -> linear
     elif kind == "cat":
         t = torch.cat(srcs, 0)
     elif kind == "convcat":
@@ -515,6 +734,8 @@ def _to_target(kind: str, srcs: List[Tensor], like: Tensor) -> Tensor:
         t = t.reshape(t.shape[0], t.shape[1], t.shape[2]).permute(0, 2, 1)[:, :, None, :]
     elif kind in ("unsq1", "unsq2"):
         t = srcs[0].reshape(like.shape)
+    elif kind == "lin1d":                                       # conv1d [O, I, 1] -> linear
+        t = srcs[0].reshape(srcs[0].shape[0], -1)
     elif kind.startswith("bnw@"):
         w, g, var = srcs
         s = _bn_scale(g, var, float(kind[4:]))
@@ -581,6 +802,10 @@ def _clip_optional(m):
     return tuple(rf"^layers\.{len(m.layers) - 1 - i}\." for i in range(n))
 
 
+def _no_extra(weights_dir):
+    return {}
+
+
 @dataclass
 class Source:
     """Where one engine module's tensors live in a public checkpoint directory."""
@@ -588,6 +813,7 @@ class Source:
     rules: Callable[[torch.nn.Module], List[Rule]]
     rename: Callable[[Dict[str, Tensor]], Dict[str, Tensor]] = _ident
     optional: Callable[[torch.nn.Module], Tuple[str, ...]] = _no_optional
+    extra: Callable[[str], Dict[str, Tensor]] = _no_extra     # side files merged into the source tensors
 
 
 _DIFF = "diffusion_pytorch_model.safetensors"
@@ -607,6 +833,19 @@ LAYOUTS: Dict[str, Dict[str, Source]] = {
         "clip_proj": Source(("prior/text_encoder/model.safetensors",),
                             lambda m: [("weight", "copy", ("text_projection.weight",))]),
         "xlmr": Source(("text_encoder/model.safetensors",), lambda m: _xlmr_rules()),
+    },
+    # the original release (see _k2_orig_unet_rules); used when its decoder checkpoint is present
+    "kandinsky2_original": {
+        "unet": Source(("decoder_fp16.ckpt", "2_1/decoder_fp16.ckpt"), _k2_orig_unet_rules),
+        "movq": Source(("movq_final.ckpt", "2_1/movq_final.ckpt"), _k2_orig_movq_rules),
+        "prior": Source(("prior_fp16.ckpt", "2_1/prior_fp16.ckpt"), _k2_orig_prior_rules, extra=_k2_stats),
+        "clip": Source(("ViT-L-14.safetensors", "ViT-L-14.pt", "2_1/ViT-L-14.safetensors", "2_1/ViT-L-14.pt"),
+                       lambda m: _openai_clip_text_rules()),
+        "clip_proj": Source(("ViT-L-14.safetensors", "ViT-L-14.pt", "2_1/ViT-L-14.safetensors", "2_1/ViT-L-14.pt"),
+                            lambda m: [("weight", "T", ("text_projection",))]),
+        "xlmr": Source(("text_encoder/model.safetensors", "text_encoder/pytorch_model.bin",
+                        "2_1/text_encoder/model.safetensors", "2_1/text_encoder/pytorch_model.bin"),
+                       lambda m: _xlmr_rules()),
     },
     "zeroscopev2xl": _VIDEO,
     "damo": _VIDEO,
@@ -637,6 +876,42 @@ def _k2_zero_image_embed(weights_dir: str, like: Tensor) -> Tensor:
     if tuple(emb.shape) != tuple(like.shape):
         raise ValueError(f"zero-image embedding {tuple(emb.shape)} != engine {tuple(like.shape)}")
     return emb
+
+
+def _k2_zero_image_embed_openai(path: str, like: Tensor) -> Tensor:
+    """The zero-image embedding from an OpenAI-layout CLIP state dict (original Kandinsky 2.1
+    release): ``visual.*`` mapped onto transformers' CLIP vision tower, config read off the shapes."""
+    from transformers import CLIPVisionConfig, CLIPVisionModelWithProjection
+    src = read_checkpoint(path)
+    if "visual.conv1.weight" not in src:
+        raise KeyError(f"{path}: no visual.* tensors (CLIP vision tower for the zero-image embedding)")
+    width, patch = src["visual.conv1.weight"].shape[0], src["visual.conv1.weight"].shape[-1]
+    grid = int(round((src["visual.positional_embedding"].shape[0] - 1) ** 0.5))
+    layers = len({k.split(".")[3] for k in src if k.startswith("visual.transformer.resblocks.")})
+    inter = src["visual.transformer.resblocks.0.mlp.c_fc.weight"].shape[0]
+    cfg = CLIPVisionConfig(hidden_size=width, intermediate_size=inter, num_hidden_layers=layers,
+                           num_attention_heads=max(1, width // 64), image_size=grid * patch, patch_size=patch,
+                           projection_dim=src["visual.proj"].shape[1], hidden_act="quick_gelu", layer_norm_eps=1e-5)
+    model = CLIPVisionModelWithProjection(cfg).eval()
+    missing, _ = model.load_state_dict(openai_visual_to_hf(src), strict=False)
+    missing = [k for k in missing if not k.endswith("position_ids")]
+    if missing:
+        raise KeyError(f"{path}: CLIP vision tower lacks {missing[:5]}")
+    with torch.no_grad():
+        emb = model(pixel_values=torch.zeros(1, 3, cfg.image_size, cfg.image_size)).image_embeds[0]
+    if tuple(emb.shape) != tuple(like.shape):
+        raise ValueError(f"zero-image embedding {tuple(emb.shape)} != engine {tuple(like.shape)}")
+    return emb
+
+
+def _layout(weights_dir: str, model: str) -> Tuple[Dict[str, Source], str]:
+    """The public layout present in ``weights_dir`` (Kandinsky: the original release when its
+    decoder checkpoint is there, else the diffusers conversion)."""
+    if model == "kandinsky2":
+        orig = LAYOUTS["kandinsky2_original"]
+        if _first_file(weights_dir, orig["unet"].files) is not None:
+            return orig, "kandinsky2_original"
+    return LAYOUTS.get(model, {}), model
 
 
 def _native_path(weights_dir: str, name: str) -> str:
@@ -677,7 +952,7 @@ def _first_file(weights_dir: str, files: Tuple[str, ...]) -> Optional[str]:
 def load_pipeline(pipe, weights_dir: str, model: str):
     """Fill every module of ``pipe`` from ``weights_dir``: per module the native file if present,
     else the family's public layout (``LAYOUTS``).  Missing files / tensors are errors."""
-    layout = LAYOUTS.get(model, {})
+    layout, variant = _layout(weights_dir, model)
     cache: Dict[str, Dict[str, Tensor]] = {}
     problems = []
     for name, mod in pipe.modules().items():
@@ -685,11 +960,16 @@ def load_pipeline(pipe, weights_dir: str, model: str):
             load_native_module(name, mod, weights_dir)
             continue
         if model == "kandinsky2" and name == "buffers":
-            if os.path.isdir(os.path.join(weights_dir, "prior")):
+            clip_file = _first_file(weights_dir, LAYOUTS["kandinsky2_original"]["clip"].files)
+            if variant == "kandinsky2" and os.path.isdir(os.path.join(weights_dir, "prior")):
                 with torch.no_grad():
                     mod.zero_img_emb.copy_(_k2_zero_image_embed(weights_dir, mod.zero_img_emb))
                 continue
-            problems.append(f"{name}.safetensors or prior/image_encoder/")
+            if variant == "kandinsky2_original" and clip_file is not None:
+                with torch.no_grad():
+                    mod.zero_img_emb.copy_(_k2_zero_image_embed_openai(clip_file, mod.zero_img_emb))
+                continue
+            problems.append(f"{name}.safetensors, prior/image_encoder/ or an OpenAI CLIP ViT-L/14 state dict")
             continue
         src = layout.get(name)
         path = _first_file(weights_dir, src.files) if src is not None else None
@@ -699,6 +979,9 @@ def load_pipeline(pipe, weights_dir: str, model: str):
         if path not in cache:
             cache[path] = read_checkpoint(path)
         state = src.rename(cache[path])
+        extra = src.extra(weights_dir)
+        if extra:
+            state = {**state, **extra}
         target = dict(mod.named_parameters())
         load_state(mod, convert(src.rules(mod), target, state, src.optional(mod)))
     if problems:
@@ -715,6 +998,22 @@ def load_sd15(pipe, weights_dir: str):
 # --------------------------------------------------------------------------- export (tests, tools)
 def _from_target(kind: str, t: Tensor, keys: List[str], out: Dict[str, Tensor]):
     """Inverse of ``_to_target``: engine tensor -> the public tensors it was built from."""
+    if kind.startswith(("heads@", "heads1d@", "headsb@")):
+        n, hd = _heads_split(kind)
+        rest = tuple(t.shape[1:])
+        r = t.reshape(n, -1, hd, *rest).transpose(0, 1).reshape(t.shape)
+        out[keys[0]] = (r[..., None] if kind.startswith("heads1d@") else r).contiguous()
+        return
+    if kind == "T":
+        out[keys[0]] = t.t().contiguous()
+        return
+    if kind == "catlin1x1":
+        for k, part in zip(keys, t.chunk(len(keys), 0)):
+            out[k] = part[:, :, None, None].contiguous()
+        return
+    if kind == "lin1d":
+        out[keys[0]] = t[:, :, None].contiguous()
+        return
     if kind == "conv":
         out[keys[0]] = t.permute(0, 3, 1, 2).contiguous()
     elif kind == "lin1x1":
@@ -773,8 +1072,15 @@ def export_diffusers(pipe) -> Dict[str, Dict[str, Tensor]]:
 
 
 def write_public(pipe, model: str, weights_dir: str):
+    """Write ``export_public`` files: safetensors, or a plain tensor dict (``torch.save``) for the
+    ``.ckpt`` / ``.pt`` / ``.bin`` names of layouts that use them."""
     for rel, state in export_public(pipe, model).items():
-        write_safetensors(state, os.path.join(weights_dir, rel))
+        path = os.path.join(weights_dir, rel)
+        if path.endswith(".safetensors"):
+            write_safetensors(state, path)
+        else:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+            torch.save({k: v.detach().contiguous().cpu() for k, v in state.items()}, path)
 
 
 def main(argv: Optional[List[str]] = None):

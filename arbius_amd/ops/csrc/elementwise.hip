@@ -3,6 +3,8 @@
 // (cdna_hip_programming.md Guideline 11/13).
 #include "common.h"
 
+#include <cstdlib>
+
 // h: [M, 2F] (value | gate) -> out [M, F] = value * gelu(gate)
 __global__ void __launch_bounds__(256) geglu_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ out,
                                                     long M, int F) {
@@ -57,6 +59,85 @@ __global__ void __launch_bounds__(256) norm_table_apply_kernel(const bf16_t* __r
     }
     st16(y + i * 8, pack8(f));
   }
+}
+
+// The same transform in a 2-D geometry (grid: row slabs x images): thread (v, rl) owns channel
+// vector v (8 channels) for RP rows of the slab, keeps its 8 (scale, shift) pairs in registers and
+// issues all RP 16-byte loads before the first store - no 64-bit index division, table read once
+// per thread instead of per element.  Bitwise identical to norm_table_apply_kernel.
+template <int VPT, int RP>
+__global__ void __launch_bounds__(256) norm_table_apply2_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                                const float2* __restrict__ table, int HW, int C,
+                                                                int silu, const bf16_t* __restrict__ x2, int C1) {
+  const int b = blockIdx.y, t = threadIdx.x;
+  const int CV = C >> 3;
+  const int k = CV >= 256 ? 1 : 256 / CV;
+  const int v0 = CV >= 256 ? t : t % CV, rl = CV >= 256 ? 0 : t / CV;
+  if (rl >= k) return;
+  const int r0 = blockIdx.x * k * RP + rl;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int v = v0 + 256 * j;
+    if (v >= CV) break;
+    const int c = 8 * v;
+    float sc[8], sh[8];
+    const float4* tp = reinterpret_cast<const float4*>(table + (size_t)b * C + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float4 q = tp[e];
+      sc[2 * e] = q.x; sh[2 * e] = q.y; sc[2 * e + 1] = q.z; sh[2 * e + 1] = q.w;
+    }
+    const bf16_t* src;
+    int sstride;
+    if (x2 == nullptr) { src = x + (size_t)b * HW * C + c; sstride = C; }
+    else if (c < C1) { src = x + (size_t)b * HW * C1 + c; sstride = C1; }
+    else { src = x2 + (size_t)b * HW * (C - C1) + (c - C1); sstride = C - C1; }
+    bf16_t* dst = y + (size_t)b * HW * C + c;
+    uint4 raw[RP];
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const int r = r0 + i * k;
+      raw[i] = r < HW ? ld16(src + (size_t)r * sstride) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const int r = r0 + i * k;
+      if (r >= HW) break;
+      float f[8];
+      unpack8(raw[i], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float o = fmaf(f[e], sc[e], sh[e]);
+        f[e] = silu ? silu_f(o) : o;
+      }
+      st16(dst + (size_t)r * C, pack8(f));
+    }
+  }
+}
+
+static int launch_apply2(const void* x, const void* x2, int C1, void* y, const void* table, int B, long HW, int C,
+                         int silu, hipStream_t stream) {
+  if (HW > (1L << 30)) return -1;
+  const int CV = C / 8;
+  const int k = CV >= 256 ? 1 : 256 / CV;
+  constexpr int RP = 8;
+  dim3 grid((unsigned)((HW + (long)k * RP - 1) / ((long)k * RP)), B);
+  if (CV > 512) return -1;
+  if (CV > 256)
+    norm_table_apply2_kernel<2, RP><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
+                                                              (int)HW, C, silu, (const bf16_t*)x2, C1);
+  else
+    norm_table_apply2_kernel<1, RP><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
+                                                              (int)HW, C, silu, (const bf16_t*)x2, C1);
+  return (int)hipGetLastError();
+}
+
+static bool apply2_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("ARB_GN_APPLY2");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
 }
 
 // Row softmax of a score matrix: P = softmax(scale * S) per row, S / P [R, N] bf16 (N % 8 == 0), fp32
@@ -122,6 +203,7 @@ ARB_API int arb_silu(const void* x, void* y, long n, hipStream_t stream) {
 ARB_API int arb_norm_table_apply(const void* x, void* y, const void* table, int B, long HW, int C, int silu,
                                  hipStream_t stream) {
   if (C % 8 != 0) return -1;
+  if (apply2_on() && C / 8 <= 512) return launch_apply2(x, nullptr, 0, y, table, B, HW, C, silu, stream);
   const long total8 = (long)B * HW * (C / 8);
   norm_table_apply_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
                                                                 HW, C, total8, silu, nullptr, 0);
@@ -131,6 +213,7 @@ ARB_API int arb_norm_table_apply(const void* x, void* y, const void* table, int 
 ARB_API int arb_norm_table_apply_cat(const void* x, const void* x2, int C1, void* y, const void* table, int B, long HW,
                                      int C, int silu, hipStream_t stream) {
   if (C % 8 != 0 || C1 <= 0 || C1 >= C || C1 % 8 != 0 || x2 == nullptr) return -1;
+  if (apply2_on() && C / 8 <= 512) return launch_apply2(x, x2, C1, y, table, B, HW, C, silu, stream);
   const long total8 = (long)B * HW * (C / 8);
   norm_table_apply_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
                                                                 HW, C, total8, silu, (const bf16_t*)x2, C1);

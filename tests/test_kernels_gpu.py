@@ -32,13 +32,22 @@ def test_group_norm(cuda, B, H, W, C, G, silu):
     assert torch.equal(y, y2), "group norm must be bitwise deterministic"
 
 
-@pytest.mark.parametrize("M,C", [(8192, 320), (2048, 640), (154, 768), (512, 1280), (77, 1024)])
+@pytest.mark.parametrize("M,C", [(8192, 320), (2048, 640), (154, 768), (512, 1280), (77, 1024), (4099, 320),
+                                 (77, 384), (33, 2048), (65, 256), (19, 960)])
 def test_layer_norm(cuda, M, C):
-    x = torch.randn(M, C, device=cuda).bfloat16()
+    """Packed-row LayerNorm (every (lanes/row, vectors/lane) geometry the UNets and text towers use,
+    ragged row counts) and the fallback wave-per-row kernel (C = 960) against fp32; row_stats is the
+    same per-row arithmetic."""
+    x = (torch.randn(M, C, device=cuda) * 3 + 1).bfloat16()
     g = torch.randn(C, device=cuda).bfloat16()
     b = torch.randn(C, device=cuda).bfloat16()
     y = _lib.layer_norm(x, g, b, 1e-5)
     assert _rel(y, ref.layer_norm(x.float(), g.float(), b.float(), 1e-5)) < 1e-2
+    assert torch.equal(y, _lib.layer_norm(x, g, b, 1e-5))
+    rs = _lib.row_stats(x, 1e-5)
+    xf = x.float()
+    assert torch.allclose(rs[:, 0], xf.mean(1), atol=1e-3, rtol=1e-3)
+    assert torch.allclose(rs[:, 1], torch.rsqrt(xf.var(1, unbiased=False) + 1e-5), rtol=2e-3)
 
 
 @pytest.mark.parametrize("B,Nq,Nk,H,D,causal", [
@@ -453,7 +462,8 @@ def test_splitk_inlaunch_reduce_bitwise_equals_reduce_kernel(cuda, cfg):
     assert torch.equal(a, _lib.conv2d_nhwc(x, w, b, 1, False, r, None, 1, cfg + 10, 4))
 
 
-@pytest.mark.parametrize("B,H,W,C,silu", [(2, 16, 16, 320, True), (1, 8, 24, 1280, False), (3, 5, 7, 64, True)])
+@pytest.mark.parametrize("B,H,W,C,silu", [(2, 16, 16, 320, True), (1, 8, 24, 1280, False), (3, 5, 7, 64, True),
+                                          (2, 9, 13, 2560, True), (1, 64, 64, 4096, False)])
 def test_norm_table_apply(cuda, B, H, W, C, silu):
     """Unfused GroupNorm-table prologue kernel == fp32 x*scale+shift(+SiLU)."""
     from arbius_amd import ops

@@ -172,3 +172,154 @@ def test_read_checkpoint_refuses_non_tensor_pickles(tmp_path):
     torch.save({"a": torch.zeros(2), "meta": {"lr": 0.1}}, p)
     with pytest.raises(ValueError):
         W.read_checkpoint(str(p))
+
+
+# ---- Kandinsky 2.1 ORIGINAL release layout (decoder_fp16.ckpt / prior_fp16.ckpt / movq_final.ckpt /
+# ViT-L-14_stats.th / text_encoder / OpenAI CLIP state dict): round trip through the original names,
+# plus the semantics of the per-head fused QKV rows against the original attention arithmetic
+def test_kandinsky2_original_layout_round_trip(tmp_path):
+    a = build_pipeline("kandinsky2", tiny=True, weight_seed=0)
+    W.write_public(a, "kandinsky2_original", str(tmp_path))
+    dec = torch.load(os.path.join(tmp_path, "decoder_fp16.ckpt"), weights_only=True)
+    for k in ("input_blocks.0.0.weight", "input_blocks.1.0.in_layers.2.weight", "middle_block.1.qkv.weight",
+              "middle_block.1.encoder_kv.weight", "output_blocks.0.0.emb_layers.1.weight", "out.2.weight",
+              "clip_to_seq.weight", "to_model_dim_n.weight", "proj_n.weight", "ln_model_n.weight",
+              "img_layer.weight", "time_embed.0.weight"):
+        assert k in dec, k
+    assert dec["middle_block.1.qkv.weight"].dim() == 3                      # conv1d on disk
+    prior = torch.load(os.path.join(tmp_path, "prior_fp16.ckpt"), weights_only=True)
+    assert "model.transformer.resblocks.0.attn.c_qkv.weight" in prior and "model.prd_emb" in prior
+    movq = torch.load(os.path.join(tmp_path, "movq_final.ckpt"), weights_only=True)
+    assert "decoder.mid.attn_1.q.weight" in movq and "decoder.up.0.block.0.conv1.weight" in movq
+    # stats in their own file, as released: drop them from the prior checkpoint
+    torch.save((prior.pop("clip_mean"), prior.pop("clip_std")), os.path.join(tmp_path, "ViT-L-14_stats.th"))
+    torch.save(prior, os.path.join(tmp_path, "prior_fp16.ckpt"))
+    b = build_pipeline("kandinsky2", tiny=True, weight_seed=11, weights_dir=str(tmp_path))
+    pa, pb = _params(a), _params(b)
+    diff = [k for k in pa if not torch.equal(pa[k], pb[k])]
+    assert not diff, diff[:5]
+
+
+def test_original_unet_attention_rows_are_per_head_interleaved():
+    """guided-diffusion QKVAttentionLegacy with encoder_kv (fused rows [head][q|k|v], context K/V
+    prepended) computed from the ORIGINAL tensors == JointAttention loaded through the rules."""
+    from arbius_amd.models.glide_unet import JointAttention
+    torch.manual_seed(3)
+    C, Cctx, hd, groups, B, Hs, Ws, S = 32, 24, 16, 8, 2, 3, 5, 4
+    heads = C // hd
+    att = JointAttention(C, Cctx, hd, groups).eval()
+    orig = {"norm.weight": torch.randn(C), "norm.bias": torch.randn(C),
+            "qkv.weight": torch.randn(3 * C, C, 1) / 6, "qkv.bias": torch.randn(3 * C) / 6,
+            "encoder_kv.weight": torch.randn(2 * C, Cctx, 1) / 5, "encoder_kv.bias": torch.randn(2 * C) / 5,
+            "proj_out.weight": torch.randn(C, C, 1) / 6, "proj_out.bias": torch.randn(C)}
+    rules = [(dst.replace("mid_attn.", ""), kind, tuple(s.replace("middle_block.1.", "") for s in srcs))
+             for dst, kind, srcs in W._k2_orig_unet_rules(_TinyGlide(hd)) if dst.startswith("mid_attn.")]
+    W.load_state(att, W.convert(rules, dict(att.named_parameters()), orig))
+    x = torch.randn(B, Hs, Ws, C)
+    ctx = torch.randn(B, S, Cctx)
+    with torch.no_grad():
+        got = att(x, ctx)
+        xc = x.permute(0, 3, 1, 2).reshape(B, C, -1)
+        h = torch.nn.functional.group_norm(xc, groups, orig["norm.weight"], orig["norm.bias"], 1e-5)
+        qkv = torch.nn.functional.conv1d(h, orig["qkv.weight"], orig["qkv.bias"])
+        q, k, v = qkv.reshape(B * heads, 3 * hd, -1).split(hd, dim=1)
+        ekv = torch.nn.functional.conv1d(ctx.transpose(1, 2), orig["encoder_kv.weight"], orig["encoder_kv.bias"])
+        ek, ev = ekv.reshape(B * heads, 2 * hd, -1).split(hd, dim=1)
+        k, v = torch.cat([ek, k], -1), torch.cat([ev, v], -1)
+        sc = 1 / hd ** 0.25
+        w = torch.softmax(torch.einsum("bct,bcs->bts", q * sc, k * sc), -1)
+        a = torch.einsum("bts,bcs->bct", w, v).reshape(B, C, -1)
+        ref = xc + torch.nn.functional.conv1d(a, orig["proj_out.weight"], orig["proj_out.bias"])
+        ref = ref.reshape(B, C, Hs, Ws).permute(0, 2, 3, 1)
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4), (got - ref).abs().max()
+
+
+class _TinyGlide(torch.nn.Module):
+    """Just enough of a GlideUNet for _k2_orig_unet_rules to emit the mid-block attention rules."""
+
+    def __init__(self, hd):
+        super().__init__()
+        from types import SimpleNamespace
+        self.cfg = SimpleNamespace(head_channels=hd)
+        blk = SimpleNamespace(skip=None)
+        self.down, self.up = [], []
+        self.mid1 = self.mid2 = blk
+
+
+def test_original_prior_attention_rows_are_per_head_interleaved():
+    """DALL-E 2 / glide-text2im QKVMultiheadAttention (c_qkv viewed [bs, n, heads, 3*hd], split
+    q|k|v, causal) + MLP from the ORIGINAL tensors == PriorBlock loaded through the rules."""
+    from arbius_amd.models.prior import PriorBlock, PriorConfig
+    torch.manual_seed(4)
+    cfg = PriorConfig(width=32, layers=1, heads=2, clip_dim=16)
+    blk = PriorBlock(cfg).eval()
+    w, H = cfg.width, cfg.heads
+    hd = w // H
+    p = "model.transformer.resblocks.0"
+    orig = {f"{p}.ln_1.weight": torch.randn(w), f"{p}.ln_1.bias": torch.randn(w),
+            f"{p}.attn.c_qkv.weight": torch.randn(3 * w, w) / 6, f"{p}.attn.c_qkv.bias": torch.randn(3 * w) / 6,
+            f"{p}.attn.c_proj.weight": torch.randn(w, w) / 6, f"{p}.attn.c_proj.bias": torch.randn(w),
+            f"{p}.ln_2.weight": torch.randn(w), f"{p}.ln_2.bias": torch.randn(w),
+            f"{p}.mlp.c_fc.weight": torch.randn(4 * w, w) / 6, f"{p}.mlp.c_fc.bias": torch.randn(4 * w),
+            f"{p}.mlp.c_proj.weight": torch.randn(w, 4 * w) / 12, f"{p}.mlp.c_proj.bias": torch.randn(w)}
+
+    class _M:
+        pass
+    m = _M()
+    m.cfg = cfg
+    rules = [(dst.replace("blocks.#.", ""), kind, tuple(s.replace("#", "0") for s in srcs))
+             for dst, kind, srcs in W._k2_orig_prior_rules(m) if dst.startswith("blocks.#.")]
+    W.load_state(blk, W.convert(rules, dict(blk.named_parameters()), orig))
+    x = torch.randn(2, 7, w)
+    F = torch.nn.functional
+    with torch.no_grad():
+        got = blk(x)
+        h = F.layer_norm(x, (w,), orig[f"{p}.ln_1.weight"], orig[f"{p}.ln_1.bias"])
+        qkv = F.linear(h, orig[f"{p}.attn.c_qkv.weight"], orig[f"{p}.attn.c_qkv.bias"]).view(2, 7, H, -1)
+        q, k, v = torch.split(qkv, hd, dim=-1)
+        sc = 1 / hd ** 0.25
+        s = torch.einsum("bthc,bshc->bhts", q * sc, k * sc)
+        s = s + torch.triu(torch.full((7, 7), float("-inf")), 1)
+        a = torch.einsum("bhts,bshc->bthc", torch.softmax(s, -1), v).reshape(2, 7, w)
+        x1 = x + F.linear(a, orig[f"{p}.attn.c_proj.weight"], orig[f"{p}.attn.c_proj.bias"])
+        h2 = F.layer_norm(x1, (w,), orig[f"{p}.ln_2.weight"], orig[f"{p}.ln_2.bias"])
+        ref = x1 + F.linear(F.gelu(F.linear(h2, orig[f"{p}.mlp.c_fc.weight"], orig[f"{p}.mlp.c_fc.bias"])),
+                            orig[f"{p}.mlp.c_proj.weight"], orig[f"{p}.mlp.c_proj.bias"])
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4), (got - ref).abs().max()
+
+
+def test_kandinsky2_original_zero_image_embedding_from_openai_clip(tmp_path):
+    """No native buffers file and no diffusers prior/: the zero-image embedding comes from the
+    OpenAI-layout CLIP state dict's visual.* tensors (mapped onto transformers' vision tower)."""
+    transformers = pytest.importorskip("transformers")
+    a = build_pipeline("kandinsky2", tiny=True, weight_seed=0)
+    W.write_public(a, "kandinsky2_original", str(tmp_path))
+    os.remove(os.path.join(tmp_path, "buffers.safetensors"))
+    d = a.cfg.prior.clip_dim
+    torch.manual_seed(0)
+    vcfg = transformers.CLIPVisionConfig(hidden_size=64, intermediate_size=96, num_hidden_layers=2,
+                                         num_attention_heads=1, image_size=32, patch_size=8, projection_dim=d,
+                                         hidden_act="quick_gelu", layer_norm_eps=1e-5)
+    vis = transformers.CLIPVisionModelWithProjection(vcfg).eval()
+    with torch.no_grad():
+        ref = vis(pixel_values=torch.zeros(1, 3, 32, 32)).image_embeds[0]
+    # the same tower under OpenAI names (inverse of openai_visual_to_hf)
+    hf = vis.state_dict()
+    V, P = "visual.", "vision_model."
+    ov = {V + "class_embedding": hf[P + "embeddings.class_embedding"],
+          V + "conv1.weight": hf[P + "embeddings.patch_embedding.weight"],
+          V + "positional_embedding": hf[P + "embeddings.position_embedding.weight"],
+          V + "ln_pre.weight": hf[P + "pre_layrnorm.weight"], V + "ln_pre.bias": hf[P + "pre_layrnorm.bias"],
+          V + "ln_post.weight": hf[P + "post_layernorm.weight"], V + "ln_post.bias": hf[P + "post_layernorm.bias"],
+          V + "proj": hf["visual_projection.weight"].t().contiguous()}
+    for i in range(2):
+        L, O = f"{P}encoder.layers.{i}.", f"{V}transformer.resblocks.{i}."
+        for kind in ("weight", "bias"):
+            ov[O + f"attn.in_proj_{kind}"] = torch.cat([hf[L + f"self_attn.{n}_proj.{kind}"] for n in "qkv"])
+            for a_, b_ in (("attn.out_proj.", "self_attn.out_proj."), ("ln_1.", "layer_norm1."),
+                           ("ln_2.", "layer_norm2."), ("mlp.c_fc.", "mlp.fc1."), ("mlp.c_proj.", "mlp.fc2.")):
+                ov[O + a_ + kind] = hf[L + b_ + kind]
+    clip_path = os.path.join(tmp_path, "ViT-L-14.safetensors")
+    W.write_safetensors({**W.read_safetensors(clip_path), **ov}, clip_path)
+    b = build_pipeline("kandinsky2", tiny=True, weight_seed=3, weights_dir=str(tmp_path))
+    assert torch.allclose(b.buffers.zero_img_emb.float(), ref, atol=1e-5)
