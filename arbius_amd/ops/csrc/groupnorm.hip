@@ -520,6 +520,135 @@ static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma
                         float one_plus, void* workspace, void* table, int B, int HW, int C, int G, float eps,
                         hipStream_t stream);
 
+// ---------------------------------------------------------------------------------------------
+// Small images (HW * C <= GN_FUSED_MAX, the deep UNet levels): statistics AND table in ONE launch.
+// Grid (G / GB, B): a block owns GB consecutive groups (CB = GB * Cg channels, a multiple of 8) of
+// one image and walks every row of them - thread (v, rl) takes channel vector v of the slice and
+// rows rl, rl + k, ... (k = 256 / (CB / 8) row lanes), 4 rows' 16-byte loads in flight, exact
+// per-channel (n, mean, M2) per 4-row batch Chan-combined; then a fixed LDS / xor-butterfly combine
+// per group and the (scale, shift) table of the slice.  Two launches (stats partials + table) and
+// the partials round trip become one; the partition depends on (HW, C, G) only, never on the batch.
+#define GN_FUSED_MAX (1 << 20)
+__host__ __device__ inline int gn_fused_gb(int C, int G) {
+  const int Cg = C / G;
+  for (int gb = 1; gb <= G && gb <= 8; ++gb)
+    if (G % gb == 0 && (gb * Cg) % 8 == 0 && (gb * Cg) / 8 <= 128) return gb;
+  return 0;
+}
+
+__global__ void __launch_bounds__(256) gn_fused_table_kernel(
+    const bf16_t* __restrict__ x, float2* __restrict__ table, const bf16_t* __restrict__ gamma,
+    const bf16_t* __restrict__ beta, const bf16_t* __restrict__ mod, float one_plus, int HW, int C, int G, int GB,
+    float eps, const bf16_t* __restrict__ x2, int C1) {
+  const int gs = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int Cg = C / G, CB = GB * Cg, NVB = CB >> 3;
+  const int k = 256 / NVB;
+  const int v = t % NVB, rl = t / NVB;
+  const int c0 = gs * CB, ch = c0 + 8 * v;
+  const bool active = rl < k;
+  __shared__ float sh_n[256];
+  __shared__ float sh_mean[256 * 8];
+  __shared__ float sh_m2[256 * 8];
+  __shared__ float2 sh_g[8];
+  const bool second = x2 != nullptr && ch >= C1;
+  const int cs = x2 == nullptr ? C : (second ? C - C1 : C1);
+  const bf16_t* base = (second ? x2 : x) + (size_t)b * HW * cs + (second ? ch - C1 : ch);
+  Stat acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = Stat{0.f, 0.f, 0.f, 0.f};
+  float nt = 0.f;
+  if (active) {
+    for (int r0 = rl; r0 < HW; r0 += 4 * k) {
+      uint4 raw[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + i * k;
+        raw[i] = r < HW ? ld16(base + (size_t)r * cs) : make_uint4(0, 0, 0, 0);
+      }
+      float n = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) n += (r0 + i * k < HW) ? 1.f : 0.f;
+      nt += n;
+      const float inv_n = 1.f / n;
+      float f[4][8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) unpack8(raw[i], f[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sm += f[i][e];
+        const float mean = sm * inv_n;
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float d = f[i][e] - mean;
+          m2 += (r0 + i * k < HW) ? d * d : 0.f;
+        }
+        acc[e] = chan_combine(acc[e], Stat{n, mean, m2, 0.f});
+      }
+    }
+  }
+  sh_n[t] = nt;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sh_mean[t * 8 + e] = acc[e].mean;
+    sh_m2[t * 8 + e] = acc[e].m2;
+  }
+  __syncthreads();
+  // per group of the slice: L lanes (one wave at most) take every L-th (channel, row lane) item
+  int L = 1;
+  while (L < 64 && 2 * L * GB <= 256) L *= 2;
+  const int g = t / L, sl = t % L;
+  const int items = Cg * k;
+  float N = 0.f, sum = 0.f;
+  if (g < GB) {
+    for (int it = sl; it < items; it += L) {
+      const int c = g * Cg + it / k, j = it % k;           // channel within the slice, row lane
+      const int tt = j * NVB + (c >> 3), o = tt * 8 + (c & 7);
+      N += sh_n[tt];
+      sum += sh_n[tt] * sh_mean[o];
+    }
+  }
+  for (int o = 1; o < L; o <<= 1) {
+    N += __shfl_xor(N, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+  }
+  const float mu = N > 0.f ? sum / N : 0.f;
+  float m2 = 0.f;
+  if (g < GB) {
+    for (int it = sl; it < items; it += L) {
+      const int c = g * Cg + it / k, j = it % k;
+      const int tt = j * NVB + (c >> 3), o = tt * 8 + (c & 7);
+      const float d = sh_mean[o] - mu;
+      m2 += sh_m2[o] + sh_n[tt] * d * d;
+    }
+  }
+  for (int o = 1; o < L; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+  if (g < GB && sl == 0) sh_g[g] = make_float2(mu, rsqrtf(m2 / fmaxf(N, 1.f) + eps));
+  __syncthreads();
+  for (int i = t; i < CB; i += 256) {
+    const int c = c0 + i;
+    const float2 st = sh_g[i / Cg];
+    float sc = st.y * bf2f(gamma[c]);
+    float sf = bf2f(beta[c]) - st.x * sc;
+    if (mod) {
+      const float m = bf2f(mod[(size_t)b * 2 * C + c]) + one_plus, a = bf2f(mod[(size_t)b * 2 * C + C + c]);
+      sc *= m;
+      sf = fmaf(sf, m, a);
+    }
+    table[(size_t)b * C + c] = make_float2(sc, sf);
+  }
+}
+
+static bool gn_fused_path(int HW, int C, int G) {
+  static const bool on = [] {
+    const char* e = std::getenv("ARB_GN_FUSED");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on && (long)HW * C <= GN_FUSED_MAX && gn_fused_gb(C, G) > 0;
+}
+
 ARB_API int arb_group_norm_table(const void* x, const void* gamma, const void* beta, const void* mod, float one_plus,
                                  void* workspace, void* table, int B, int HW, int C, int G, float eps,
                                  hipStream_t stream) {
@@ -540,6 +669,13 @@ static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma
   if (C % 8 != 0 || C / 8 > 512 || C % G != 0 || G > 256) return -1;
   if (gn_group_path(HW, C, G)) {   // same path (and bits) with or without the concat read in place
     launch_gn_group(x, (float2*)table, nullptr, gamma, beta, mod, one_plus, B, HW, C, G, eps, stream, x2, C1);
+    return (int)hipGetLastError();
+  }
+  if (gn_fused_path(HW, C, G)) {   // small images: stats + table in one launch (concat read in place)
+    const int gb = gn_fused_gb(C, G);
+    gn_fused_table_kernel<<<dim3(G / gb, B), 256, 0, stream>>>(
+        (const bf16_t*)x, (float2*)table, (const bf16_t*)gamma, (const bf16_t*)beta, (const bf16_t*)mod, one_plus,
+        HW, C, G, gb, eps, (const bf16_t*)x2, x2 ? C1 : C);
     return (int)hipGetLastError();
   }
   const int chunks = gn_stat_chunks(HW, C);

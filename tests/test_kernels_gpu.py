@@ -404,6 +404,23 @@ def test_small_channel_conv_padded_onto_mfma(cuda, B, H, W, Cin, Cout, k):
     assert y.shape == r.shape and y.is_contiguous() and _rel(y, r) < 1e-2
 
 
+@pytest.mark.parametrize("H,W,C,G", [(8, 8, 1280, 32), (16, 16, 1280, 32), (32, 32, 640, 32), (5, 7, 320, 32),
+                                     (8, 8, 2560, 32), (64, 64, 320, 32), (3, 3, 96, 8), (24, 24, 1152, 32)])
+def test_group_norm_table_paths_accurate_and_batch_invariant(cuda, H, W, C, G):
+    """Every GN-table path (single-launch small-image kernel, stats + table slabs) against fp32,
+    and image 0 of a batch of 8 bitwise equal to the same image alone (lock-step groups)."""
+    torch.manual_seed(13)
+    x = (torch.randn(8, H, W, C, device=cuda) * 3 + 1).bfloat16()
+    g = (torch.rand(C, device=cuda) + 0.5).bfloat16()
+    bt = torch.randn(C, device=cuda).bfloat16()
+    t8 = _lib.group_norm_table(x, g, bt, G, 1e-5)
+    rt = ref.group_norm_table(x.float(), g.float(), bt.float(), G, 1e-5)
+    assert _rel(t8, rt) < 1e-4
+    t1 = _lib.group_norm_table(x[:1].contiguous(), g, bt, G, 1e-5)
+    assert torch.equal(t8[:1], t1)
+    assert torch.equal(t8, _lib.group_norm_table(x, g, bt, G, 1e-5))
+
+
 @pytest.mark.parametrize("B,H,W,C,Co,k,silu,up,mod", [
     (2, 64, 64, 320, 320, 3, True, False, False), (2, 32, 32, 640, 1280, 3, True, False, False),
     (2, 16, 16, 2560, 1280, 3, True, False, False), (1, 48, 48, 384, 384, 3, True, True, False),
