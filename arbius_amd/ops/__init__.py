@@ -30,7 +30,14 @@ _FORCE_REF = os.environ.get("ARBIUS_REFERENCE_OPS", "0") == "1"
 # elementwise kernel in front of the LDS-DMA conv variant (0, default: measured 9098 vs 7925
 # tasks/h on SD1.5 512^2 - the register-staged kernel that can take the prologue is slower than
 # the LDS-DMA one by more than the extra elementwise pass costs).
-_NORM_PROLOGUE = os.environ.get("ARBIUS_NORM_PROLOGUE", "0") == "1"
+# "1": every GN consumer takes the table as an operand prologue; "1x1": only 1x1 convs / linears
+# (no tap re-reads of the same activation, so the prologue costs no more VALU than the separate pass)
+_NORM_PROLOGUE_MODE = os.environ.get("ARBIUS_NORM_PROLOGUE", "0")
+_NORM_PROLOGUE = _NORM_PROLOGUE_MODE == "1"
+
+
+def _norm_prologue(w) -> bool:
+    return _NORM_PROLOGUE or (_NORM_PROLOGUE_MODE == "1x1" and w.shape[1] == 1 and w.shape[2] == 1)
 
 # Library convolutions (MIOpen: depthwise / 3-4 channel / fp16 RVM convs) must pick the
 # same deterministic solver on every call and every GPU: a solution CID is consensus.
@@ -266,7 +273,7 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
     GroupNorm(+SiLU) prologue from ``group_norm_table`` inside the conv's operand load."""
     kern_ok = (w.shape[1] in (1, 3) and w.shape[1] == w.shape[2]) or tuple(w.shape[1:3]) == (3, 1)
     if isinstance(x, CatPair):
-        if (norm is not None and _hip(x.a) and not _NORM_PROLOGUE and kern_ok and x.shape[-1] % 64 == 0
+        if (norm is not None and _hip(x.a) and not _norm_prologue(w) and kern_ok and x.shape[-1] % 64 == 0
                 and w.shape[0] % 8 == 0 and "gnapply" not in _EXP_SKIP):
             table, nsilu = norm
             x, norm = _lib.norm_table_apply(x.a, table, nsilu, x2=x.b), None     # reads both parts in place
@@ -277,7 +284,7 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
             x = x.materialize()
     if _hip(x) and kern_ok:
         table, nsilu = norm if norm is not None else (None, False)
-        if table is not None and not _NORM_PROLOGUE and x.shape[-1] % 8 == 0:
+        if table is not None and not _norm_prologue(w) and x.shape[-1] % 8 == 0:
             if "gnapply" in _EXP_SKIP:
                 table, nsilu = None, False
             else:

@@ -1320,15 +1320,38 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
     const int m = (int)(i / (p.N / 8));
     const int n = (int)(i - (long)m * (p.N / 8)) * 8;
     float v[8];
-    {
-      const float4* src = reinterpret_cast<const float4*>(p.ws + (size_t)m * p.N + n);
-      const float4 a = src[0], b = src[1];
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    }
-    for (int s = 1; s < S; ++s) {
-      const float4* src = reinterpret_cast<const float4*>(p.ws + ((size_t)s * p.M + m) * p.N + n);
-      const float4 a = src[0], b = src[1];
-      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    if (S <= 8) {
+      // every slab's loads issued before the first add (the per-slab dependent loop exposed one
+      // load latency per slab); the adds then run in slab order - bitwise the same sum
+      float4 a[8], b[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        if (s < S) {
+          const float4* src = reinterpret_cast<const float4*>(p.ws + ((size_t)s * p.M + m) * p.N + n);
+          a[s] = src[0];
+          b[s] = src[1];
+        }
+      }
+      v[0] = a[0].x; v[1] = a[0].y; v[2] = a[0].z; v[3] = a[0].w;
+      v[4] = b[0].x; v[5] = b[0].y; v[6] = b[0].z; v[7] = b[0].w;
+#pragma unroll
+      for (int s = 1; s < 8; ++s) {
+        if (s < S) {
+          v[0] += a[s].x; v[1] += a[s].y; v[2] += a[s].z; v[3] += a[s].w;
+          v[4] += b[s].x; v[5] += b[s].y; v[6] += b[s].z; v[7] += b[s].w;
+        }
+      }
+    } else {
+      {
+        const float4* src = reinterpret_cast<const float4*>(p.ws + (size_t)m * p.N + n);
+        const float4 a = src[0], b = src[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+      for (int s = 1; s < S; ++s) {
+        const float4* src = reinterpret_cast<const float4*>(p.ws + ((size_t)s * p.M + m) * p.N + n);
+        const float4 a = src[0], b = src[1];
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
     }
     float t[8];
     if (p.rowstat) ln_fold8(p, m, n, v);
