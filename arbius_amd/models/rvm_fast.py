@@ -93,9 +93,8 @@ class FastMatting:
 
     # ------------------------------------------------------------------ encoder
     def _se(self, se, x):
-        w = x.float().mean(dim=(1, 2), keepdim=True).to(x.dtype)             # [T, 1, 1, C]
-        w = self.conv(self.conv(w, se.fc1, "relu"), se.fc2)
-        return x * F.hardsigmoid(w)
+        w = self.conv(self.conv(_lib.rvm_chan_mean(x), se.fc1, "relu"), se.fc2)   # [T, 1, 1, C]
+        return _lib.rvm_gate(x, w.contiguous(), 0)                                 # x * hardsigmoid(w), in place
 
     def _block(self, blk, x):
         h = self.convact(x, blk.expand) if blk.expand is not None else x
@@ -165,8 +164,8 @@ class FastMatting:
         f1, f2, f3, f4 = self.encoder(small)
         asp = self.net.aspp
         a1 = self.convact(f4, asp.aspp1)
-        g = torch.sigmoid(self.conv(f4.float().mean(dim=(1, 2), keepdim=True).to(f4.dtype), asp.aspp2))
-        f4 = (a1 * g).contiguous()
+        g = self.conv(_lib.rvm_chan_mean(f4), asp.aspp2)
+        f4 = _lib.rvm_gate(a1.contiguous(), g.contiguous(), 1)                     # a1 * sigmoid(g), in place
         hid, rec = self.decoder(small, f1, f2, f3, f4, rec)
         out = _lib.rvm_dgf(hid.contiguous(), small, self.dgf_args, frames_u8, _MODE.get(output_type, 0), green)
         return out, rec

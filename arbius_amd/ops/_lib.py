@@ -63,6 +63,8 @@ _SIGS = {
                                 c_void_p, c_long, c_int, c_long, c_int, c_void_p]),
     "arb_rvm_dgf": (c_int, [c_void_p] * 7 + [c_int] * 6 + [c_float] * 3 + [c_void_p]),
     "arb_rvm_args_sizes": (c_size_t, [c_int]),
+    "arb_rvm_chan_mean": (c_int, [c_void_p, c_void_p, c_int, c_long, c_int, c_void_p]),
+    "arb_rvm_gate": (c_int, [c_void_p, c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "arb_gemm_ln": (c_int, [c_void_p] * 8 + [c_int] * 6 + [c_void_p]),
 }
 
@@ -731,6 +733,27 @@ def rvm_dgf(hid, small, args_dev, frames, mode, green):
     _check(_fn("arb_rvm_dgf")(_p(hid), _p(small), _p(args_dev), _p(xy), _p(ab), _p(frames), _p(out), T, H, W, h, w,
                               int(mode), float(green[0]), float(green[1]), float(green[2]), _stream()), "rvm_dgf")
     return out
+
+
+def rvm_chan_mean(x):
+    """fp16 [T, H, W, C] -> fp16 [T, 1, 1, C] spatial mean (fp32 accumulation, fixed order)."""
+    _f16(x)
+    if not x.is_contiguous() or x.shape[-1] % 8:
+        raise ValueError("rvm_chan_mean: contiguous [T, H, W, C], C % 8 == 0")
+    T, C = x.shape[0], x.shape[-1]
+    out = torch.empty(T, 1, 1, C, dtype=torch.float16, device=x.device)
+    _check(_fn("arb_rvm_chan_mean")(_p(x), _p(out), T, x.numel() // (T * C), C, _stream()), "rvm_chan_mean")
+    return out
+
+
+def rvm_gate(x, w, mode):
+    """x [T, H, W, C] *= (hardsigmoid if mode == 0 else sigmoid)(w [T, 1, 1, C]) in place; returns x."""
+    _f16(x, w)
+    if not (x.is_contiguous() and w.is_contiguous()) or x.shape[-1] % 8 or w.numel() != x.shape[0] * x.shape[-1]:
+        raise ValueError("rvm_gate: contiguous x [T, H, W, C] and w [T, 1, 1, C], C % 8 == 0")
+    T, C = x.shape[0], x.shape[-1]
+    _check(_fn("arb_rvm_gate")(_p(x), _p(w), T, x.numel() // (T * C), C, int(mode), _stream()), "rvm_gate")
+    return x
 
 
 def rvm_args_size(which: int) -> int:

@@ -17,6 +17,8 @@
 //   rvm_dgf_ab      3x3 box means / covariance / variance + the 3 1x1 convs (24 -> 16 -> 16 -> 4) -> A, b
 //   rvm_dgf_out     full resolution: bilinear A, b; out = A [src, mean(src)] + b; fgr / alpha clamp;
 //                   green-screen / alpha / foreground composite -> uint8 [T,H,W,3]
+//   rvm_chan_mean   per-(t, channel) spatial mean (squeeze-excite / LR-ASPP pooling), fixed-order tree
+//   rvm_gate        x *= hardsigmoid(w) / sigmoid(w) per (t, channel), in place
 // Every pass is elementwise or a fixed-order local reduction: bitwise deterministic.
 #include "common.h"
 
@@ -371,6 +373,62 @@ __global__ void __launch_bounds__(256) rvm_dgf_out(const uint8_t* __restrict__ s
   }
 }
 
+// Per-(t, channel) spatial mean (squeeze-excite / LR-ASPP global pool): x fp16 [T, P, C] -> fp16
+// [T, C], fp32 accumulation.  Block (t, 64-channel slab): thread (vector v of 8 channels, row lane
+// rl) sums rows rl, rl + k, ...; the k row-lane partials are added in a fixed LDS tree order.
+__global__ void __launch_bounds__(256) rvm_chan_mean(const h16* __restrict__ x, h16* __restrict__ out, long P, int C) {
+  const int t = blockIdx.y, tid = threadIdx.x;
+  const int v = tid & 7, rl = tid >> 3;                 // 8 vectors (64 channels) x 32 row lanes
+  const int c = blockIdx.x * 64 + 8 * v;
+  __shared__ float sh[32][65];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const h16* base = x + (size_t)t * P * C + c;
+    for (long r = rl; r < P; r += 32) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(base + (size_t)r * C);
+      const h16* hv = reinterpret_cast<const h16*>(&raw);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += (float)hv[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sh[rl][8 * v + e] = acc[e];
+  __syncthreads();
+  for (int st = 16; st > 0; st >>= 1) {
+    if (rl < st) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sh[rl][8 * v + e] += sh[rl + st][8 * v + e];
+    }
+    __syncthreads();
+  }
+  if (rl == 0 && c < C) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[(size_t)t * C + c + e] = (h16)(sh[0][8 * v + e] / (float)P);
+  }
+}
+
+// x[t, p, c] *= gate(w[t, c]) in place: mode 0 hardsigmoid (squeeze-excite), 1 sigmoid (LR-ASPP)
+__global__ void __launch_bounds__(256) rvm_gate(h16* __restrict__ x, const h16* __restrict__ w, long P, int C,
+                                                int mode, long total8) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
+    const long e0 = i * 8;
+    const long row = e0 / C;
+    const int c = (int)(e0 - row * C);
+    const long t = row / P;
+    uint4 raw = *reinterpret_cast<const uint4*>(x + e0);
+    const uint4 wr = *reinterpret_cast<const uint4*>(w + t * C + c);
+    h16* hv = reinterpret_cast<h16*>(&raw);
+    const h16* gv = reinterpret_cast<const h16*>(&wr);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = (float)gv[e];
+      const float a = mode == 0 ? fminf(fmaxf(g * (1.f / 6.f) + 0.5f, 0.f), 1.f) : 1.f / (1.f + __expf(-g));
+      hv[e] = (h16)((float)hv[e] * (float)(h16)a);
+    }
+    *reinterpret_cast<uint4*>(x + e0) = raw;
+  }
+}
+
 static int rgrid(long work) {
   long b = (work + 255) / 256;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -431,6 +489,19 @@ ARB_API int arb_rvm_dgf(const void* hid, const void* small, const void* dgf_args
                                        h, w);
   rvm_dgf_out<<<rgrid((long)T * H * W), 256, 0, s>>>((const uint8_t*)src, (const float*)ab, (uint8_t*)dst, T, H, W, h,
                                                       w, (float)h / (float)H, (float)w / (float)W, mode, g0, g1, g2);
+  return (int)hipGetLastError();
+}
+
+ARB_API int arb_rvm_chan_mean(const void* x, void* out, int T, long P, int C, hipStream_t s) {
+  if (T < 1 || P < 1 || C % 8 != 0) return -1;
+  rvm_chan_mean<<<dim3((C + 63) / 64, T), 256, 0, s>>>((const h16*)x, (h16*)out, P, C);
+  return (int)hipGetLastError();
+}
+
+ARB_API int arb_rvm_gate(void* x, const void* w, int T, long P, int C, int mode, hipStream_t s) {
+  if (T < 1 || P < 1 || C % 8 != 0 || mode < 0 || mode > 1) return -1;
+  const long total8 = (long)T * P * C / 8;
+  rvm_gate<<<rgrid(total8), 256, 0, s>>>((h16*)x, (const h16*)w, P, C, mode, total8);
   return (int)hipGetLastError();
 }
 

@@ -9,10 +9,13 @@ function of the frames, so the codec is self-contained and bit-exact:
   (chroma = rounded 2x2 mean of the RGB samples, then the integer matrix);
 * bitstream: H.264 Constrained Baseline CAVLC at a fixed QP (``native/src/h264.cpp``; the
   encoder's reconstruction IS every conforming decoder's output):
-  - ``codec="avc"`` (default): IPPP - an IDR every ``GOP`` pictures, P pictures of P_Skip /
-    P_L0_16x16 (quarter-sample motion search) / Intra_16x16 macroblocks, in-loop deblocking on,
-    slices of ``ROWS_PER_SLICE`` macroblock rows encoded in parallel;
-  - ``codec="avc-intra"``: every picture one IDR slice of Intra_16x16 macroblocks, deblocking off;
+  - ``codec="avc-intra"`` (default, the output codec of every video template): every picture one
+    IDR slice of Intra_16x16 macroblocks, deblocking off, pictures encoded in parallel;
+  - ``codec="avc"``: IPPP - an IDR every ``GOP`` pictures, P pictures of P_Skip / P_L0_16x16
+    (quarter-sample motion search) / Intra_16x16 macroblocks, in-loop deblocking on, slices of
+    ``ROWS_PER_SLICE`` macroblock rows encoded in parallel.  1.7-2x smaller files, but its motion
+    search made the RVM task host-bound (1.12 s vs ~0.2 s encode per 1080p 48-frame clip on the
+    MI355X box: 6.4k vs 16k clips/h, ``profiles/bench_r3_rvm_ippp.json``), so it is opt-in;
   - ``codec="pcm"``: raw I_PCM macroblocks (round 1; a 48-frame 1080p clip was ~149 MB);
 * container: ftyp + moov (faststart) + mdat, fixed zero timestamps, AVCC
   4-byte NAL lengths, avcC with the SPS/PPS.
@@ -219,7 +222,7 @@ def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False, sync=None
     return _box(b"moov", mvhd, _box(b"trak", tkhd, mdia))
 
 
-def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc", threads: int = 16) -> bytes:
+def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra", threads: int = 16) -> bytes:
     """uint8 RGB frames [H, W, 3] (all the same size) -> MP4 bytes (deterministic)."""
     frames = list(frames)
     if not frames:

@@ -12,12 +12,15 @@ timeout -k 10 420 python -u -m pytest tests/test_kernels_gpu.py tests/test_rvm_g
 rc=$?; tail -3 $O/tests.log
 if [ $rc -ne 0 ]; then grep -B5 -A30 "^E " $O/tests.log | head -80; exit $rc; fi
 step normbench
-ARB_GN_APPLY2=0 ARB_LN_PACKED=0 TAG=old timeout -k 10 120 python scripts/norm_bench.py > $O/norm_old.jsonl 2>&1 || { tail $O/norm_old.jsonl; exit 1; }
-TAG=new timeout -k 10 120 python scripts/norm_bench.py > $O/norm_new.jsonl 2>&1 || { tail $O/norm_new.jsonl; exit 1; }
-paste -d' ' <(cut -c1-80 $O/norm_old.jsonl) <(grep -o '"us": [0-9.]*' $O/norm_new.jsonl)
+ARB_GN_APPLY2=0 ARB_LN_PACKED=0 ARB_GN_FUSED=0 TAG=old timeout -k 10 120 python scripts/norm_bench.py > $O/norm_old.jsonl 2>$O/norm.err || { tail $O/norm.err; exit 1; }
+TAG=new timeout -k 10 120 python scripts/norm_bench.py > $O/norm_new.jsonl 2>>$O/norm.err || { tail $O/norm.err; exit 1; }
+paste -d' ' <(cut -c1-70 $O/norm_old.jsonl) <(grep -o '"us": [0-9.]*' $O/norm_new.jsonl)
 step rvm_bench
 timeout -k 10 400 python bench.py --model robust_video_matting > $O/rvm.log 2>$O/rvm.err || { tail -20 $O/rvm.err; exit 1; }
 tail -1 $O/rvm.log | cut -c1-600
+step rvm_bench_sdma
+HSA_ENABLE_SDMA=1 timeout -k 10 400 python bench.py --model robust_video_matting > $O/rvm_sdma.log 2>$O/rvm_sdma.err || { tail -20 $O/rvm_sdma.err; exit 1; }
+tail -1 $O/rvm_sdma.log | cut -c1-300
 step sd_bench
 timeout -k 10 400 python bench.py > $O/sd.log 2>$O/sd.err || { tail -20 $O/sd.err; exit 1; }
 tail -1 $O/sd.log | cut -c1-400

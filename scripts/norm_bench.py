@@ -10,7 +10,34 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from arbius_amd.ops import _lib  # noqa: E402
-from microbench import timeit  # noqa: E402
+
+
+def timeit(fn, iters=50, reps=5):
+    """GPU time per call: `iters` calls captured in one hipGraph, replayed (the eager loop is
+    launch-bound at ~10 us per call for these small kernels)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1000 / iters)
+    ts.sort()
+    return ts[len(ts) // 2]
 
 
 def main():

@@ -47,6 +47,22 @@ def test_pool3_and_upcat_match_torch(cuda):
     assert (y.float() - ref).abs().max().item() < 1e-2
 
 
+@pytest.mark.parametrize("T,H,W,C", [(3, 17, 29, 96), (2, 68, 120, 16), (4, 9, 16, 960), (1, 1, 1, 40)])
+def test_chan_mean_and_gates_match_torch(cuda, T, H, W, C):
+    """Squeeze-excite / LR-ASPP pooling and gating kernels against fp32 torch."""
+    torch.manual_seed(4)
+    x = torch.randn(T, H, W, C, device=cuda).half()
+    m = _lib.rvm_chan_mean(x)
+    ref = x.float().mean(dim=(1, 2), keepdim=True)
+    assert (m.float() - ref).abs().max().item() < 2e-3
+    assert torch.equal(m, _lib.rvm_chan_mean(x))
+    w = torch.randn(T, 1, 1, C, device=cuda).half() * 4
+    for mode, fn in ((0, F.hardsigmoid), (1, torch.sigmoid)):
+        y = _lib.rvm_gate(x.clone(), w, mode)
+        r = x.float() * fn(w.float()).half().float()
+        assert (y.float() - r).abs().max().item() < 1e-2
+
+
 @pytest.mark.parametrize("cx,co,k,stride,act,res", [(24, 72, 1, 1, 2, False), (40, 40, 1, 1, 0, True),
                                                      (176, 80, 3, 1, 1, False), (16, 16, 3, 1, 1, False),
                                                      (960, 128, 1, 1, 1, False), (72, 24, 1, 1, 0, True),

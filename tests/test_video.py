@@ -157,18 +157,18 @@ def test_h264_multi_slice_and_pcm_decode():
         assert (y == ey).all() and (cb == ecb).all() and (cr == ecr).all()
 
 
-def test_mp4_avc_ippp_default_roundtrip():
-    """The default output codec (IPPP, deblocked, row-band slices) through the MP4 container: sync
-    samples listed in stss, probe + decode accept it, and the picture is close to the intra one."""
+def test_mp4_avc_ippp_roundtrip():
+    """The IPPP codec (deblocked, row-band slices) through the MP4 container: sync samples listed in
+    stss, probe + decode accept it, and the picture is close to the intra one."""
     from arbius_amd.utils.mp4 import GOP, read_mp4_nals
     from arbius_amd.utils.video_io import decode, probe
     yy, xx = np.mgrid[0:90, 0:160]
     frames = [np.stack([(xx + 3 * t) % 256, (yy * 2 + t) % 256, ((xx + yy) // 2) % 256], -1).astype(np.uint8)
               for t in range(GOP + 5)]
-    a = encode_mp4(frames, 12)
-    assert a == encode_mp4(frames, 12, threads=1)
+    a = encode_mp4(frames, 12, codec="avc")
+    assert a == encode_mp4(frames, 12, codec="avc", threads=1)
     assert b"stss" in a and b"AVC IPPP" in a
-    intra = encode_mp4(frames, 12, codec="avc-intra")
+    intra = encode_mp4(frames, 12)
     assert len(a) < 0.6 * len(intra)
     _, nals, _ = read_mp4_nals(a)
     assert {n[0] & 0x1F for n in nals[2:]} == {1, 5}
