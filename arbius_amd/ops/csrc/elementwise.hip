@@ -203,7 +203,11 @@ ARB_API int arb_silu(const void* x, void* y, long n, hipStream_t stream) {
 ARB_API int arb_norm_table_apply(const void* x, void* y, const void* table, int B, long HW, int C, int silu,
                                  hipStream_t stream) {
   if (C % 8 != 0) return -1;
-  if (apply2_on() && C / 8 <= 512) return launch_apply2(x, nullptr, 0, y, table, B, HW, C, silu, stream);
+  // 2-D kernel for large tensors only (graph replay: 9.4 vs 10.6 us at [8, 64, 64, 320], 15.4 vs 17.6 at
+  // [8, 64, 64, 640], 21.3 vs 24.9 at [1, 512, 512, 128]; slower below ~8M elements: 3.7 vs 2.6 us at
+  // [8, 8, 8, 1280] - profiles/norm_kernels_ab_r3.jsonl)
+  if (apply2_on() && C / 8 <= 512 && (long)B * HW * C >= (8L << 20))
+    return launch_apply2(x, nullptr, 0, y, table, B, HW, C, silu, stream);
   const long total8 = (long)B * HW * (C / 8);
   norm_table_apply_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
                                                                 HW, C, total8, silu, nullptr, 0);
@@ -213,7 +217,8 @@ ARB_API int arb_norm_table_apply(const void* x, void* y, const void* table, int 
 ARB_API int arb_norm_table_apply_cat(const void* x, const void* x2, int C1, void* y, const void* table, int B, long HW,
                                      int C, int silu, hipStream_t stream) {
   if (C % 8 != 0 || C1 <= 0 || C1 >= C || C1 % 8 != 0 || x2 == nullptr) return -1;
-  if (apply2_on() && C / 8 <= 512) return launch_apply2(x, x2, C1, y, table, B, HW, C, silu, stream);
+  if (apply2_on() && C / 8 <= 512 && (long)B * HW * C >= (8L << 20))
+    return launch_apply2(x, x2, C1, y, table, B, HW, C, silu, stream);
   const long total8 = (long)B * HW * (C / 8);
   norm_table_apply_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, (const float2*)table,
                                                                 HW, C, total8, silu, (const bf16_t*)x2, C1);

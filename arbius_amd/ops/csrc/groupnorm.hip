@@ -641,10 +641,14 @@ __global__ void __launch_bounds__(256) gn_fused_table_kernel(
   }
 }
 
+// Opt-in (ARB_GN_FUSED=1): measured slower than stats + table on the SD1.5 batch-8 shapes under
+// graph replay (10.6 vs 7.8 us at [8, 8, 8, 1280], 11.9 vs 8.7 at [8, 16, 16, 1280], 15.1 vs 11.0
+// at [8, 32, 32, 640]: profiles/norm_kernels_ab_r3.jsonl) - 256 small blocks spend their time in
+// the per-group (channel x row-lane) LDS combine, while the two-kernel path spreads it.
 static bool gn_fused_path(int HW, int C, int G) {
   static const bool on = [] {
     const char* e = std::getenv("ARB_GN_FUSED");
-    return e == nullptr || e[0] != '0';
+    return e != nullptr && e[0] == '1';
   }();
   return on && (long)HW * C <= GN_FUSED_MAX && gn_fused_gb(C, G) > 0;
 }

@@ -162,8 +162,11 @@ static bool ln_packed_launch(const void* x, void* y, const void* gamma, const vo
     const char* e = std::getenv("ARB_LN_PACKED");
     return e == nullptr || e[0] != '0';
   }();
+  // Measured (graph replay, profiles/norm_kernels_ab_r3.jsonl): faster only for short inputs
+  // (154 x 768 text-tower rows: 2.9 vs 4.1 us); at the UNet token counts the wave-per-row kernel
+  // wins (32768 x 320: 13.2 vs 13.7 us, 8192 x 640: 6.6 vs 8.0 us).
   int lpr = 0, vpl = 0;
-  if (!on || !ln_packed_geom(C, lpr, vpl)) return false;
+  if (!on || (long)M * C > (1L << 18) || !ln_packed_geom(C, lpr, vpl)) return false;
   const int rows_per_block = 4 * (64 / lpr);
   const dim3 grid((M + rows_per_block - 1) / rows_per_block);
 #define LNP(L, V)                                                                                   \
