@@ -87,12 +87,13 @@ def read_table(path):
 def candidates(M, N, K, mode):
     """(cfg, split) pairs worth timing: split-K only when the grid is short of 2 waves."""
     deep = list(range(28, 28 + len(KDEEP)))
-    big = list(range(20, 20 + len(KBIG))) + list(range(24, 24 + len(KPERSIST))) + deep
+    xreg = list(range(32, 32 + len(KXREG)))
+    big = list(range(20, 20 + len(KBIG))) + list(range(24, 24 + len(KPERSIST))) + deep + xreg
     cfgs = {"legacy": range(10, NCFG), "big": big, "glds": list(range(10)) + big, "deep": deep}.get(
         mode, list(range(NCFG)) + big)
     for cfg in cfgs:
-        bn, bm = (KDEEP[cfg - 28] if cfg >= 28 else KPERSIST[cfg - 24] if cfg >= 24 else KBIG[cfg - 20]
-                  if cfg >= 20 else KCFG[cfg % 10])
+        bn, bm = (KXREG[cfg - 32] if cfg >= 32 else KDEEP[cfg - 28] if cfg >= 28 else KPERSIST[cfg - 24]
+                  if cfg >= 24 else KBIG[cfg - 20] if cfg >= 20 else KCFG[cfg % 10])
         if cfg >= 20 and bn > N + N // 2:
             continue
         if 24 <= cfg < 28:      # persistent short-K kernel: no split-K
@@ -110,6 +111,7 @@ KCFG = [(128, 128), (64, 128), (128, 64), (64, 64), (160, 64), (160, 128), (320,
 KBIG = [(256, 256), (320, 128), (256, 128), (320, 192)]
 KPERSIST = [(128, 128), (256, 128), (160, 128), (128, 64)]
 KDEEP = [(128, 256), (256, 128), (192, 192), (320, 64)]     # 8-wave, 3-stage ring
+KXREG = [(160, 256), (128, 256), (160, 128), (256, 128)]     # 8-wave, activation operand in VGPRs
 
 
 def _agrees(y, ref):
@@ -171,6 +173,7 @@ def main():
     ap.add_argument("--merge", default=None, help="existing conv_plans.inc to keep entries from")
     ap.add_argument("--batch", type=int, default=2, help="SD UNet batch for shape collection (8 = groups of 4)")
     ap.add_argument("--gemms-only", action="store_true", help="tune the linear (GEMM) shapes only")
+    ap.add_argument("--convs-only", action="store_true", help="tune the conv shapes only")
     args = ap.parse_args()
     out_dir = args.out_dir
     os.makedirs(out_dir, exist_ok=True)
@@ -178,6 +181,8 @@ def main():
     convs, gemms = collect_shapes(tuple(args.models.split(",")), batch=args.batch)
     if args.gemms_only:
         convs = []
+    if args.convs_only:
+        gemms = []
     mode = "big" if args.big_only else "legacy" if args.legacy_only else args.mode
     global CONC
     CONC = args.conc
