@@ -101,7 +101,9 @@ def golden_cases(device) -> List[Tuple[str, Callable[[], object]]]:
         """anythingv3's template defaults (templates/anythingv3.json: 768^2, 20 steps, guidance 12,
         DPMSolverMultistep) with the template's default negative prompt."""
         from .node.models import hydrate_input, load_template
-        inp, err, msg = hydrate_input({"prompt": "arbius test cat"}, load_template("anythingv3"))
+        tpl = load_template("anythingv3")
+        neg = next(f["default"] for f in tpl["input"] if f["variable"] == "negative_prompt")   # required field
+        inp, err, msg = hydrate_input({"prompt": "arbius test cat", "negative_prompt": neg}, tpl)
         if err:
             raise AssertionError(msg)
         inp["seed"] = 1337

@@ -92,6 +92,15 @@ def _canon_batch(batch: int):
     return max(PLAN_CANON, pb) // pb * pb
 
 
+def _plan_rows(x) -> int:
+    """Rows of x [batch, ..., C] at the canonical batch (the actual rows outside ``plan_batch``):
+    every size-dependent kernel choice (LayerNorm variant, LN fold) is made on this, so a lock-step
+    group makes each of its tasks' solo choices."""
+    rows = x.numel() // x.shape[-1]
+    canon = _canon_batch(x.shape[0])
+    return rows // x.shape[0] * canon if canon else rows
+
+
 def _hip(t: torch.Tensor) -> bool:
     return t.is_cuda and not _FORCE_REF
 
@@ -180,7 +189,7 @@ LN_FOLD_MAX_ROWS = 2048
 
 def _ln_fold_ok(x, w, geglu):
     return (_hip(x) and x.dtype == torch.bfloat16 and _gemm_ok(x.shape[-1], w.shape[0]) and x.shape[-1] <= 2048
-            and x.numel() // x.shape[-1] <= LN_FOLD_MAX_ROWS
+            and _plan_rows(x) <= LN_FOLD_MAX_ROWS
             and (not geglu or w.shape[0] % 16 == 0) and "lnfold" not in _EXP_SKIP)
 
 
@@ -189,7 +198,7 @@ def ln_linear(x, gamma, beta, eps, w, b=None, residual=None):
     row-stats pass over x, no normalised tensor in HBM)."""
     if _ln_fold_ok(x, w, False):
         wf, bf, wsum = ln_fold(gamma, beta, w, b)
-        rs = _lib.row_stats(x, eps)
+        rs = _lib.row_stats(x, eps, _plan_rows(x))
         return _lib.gemm_ln(x, wf, bf, wsum, rs, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
     return linear(layer_norm(x, gamma, beta, eps), w, b, residual)
 
@@ -198,7 +207,7 @@ def ln_linear_geglu(x, gamma, beta, eps, w, b=None):
     """linear_geglu(LayerNorm(x)) with the LayerNorm folded in (see ``ln_linear``)."""
     if _GEGLU_FUSED and _ln_fold_ok(x, w, True):
         wf, bf, wsum = ln_fold(gamma, beta, w, b, geglu=True)
-        rs = _lib.row_stats(x, eps)
+        rs = _lib.row_stats(x, eps, _plan_rows(x))
         return _lib.gemm_ln(x, wf, bf, wsum, rs, geglu=True, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
     return linear_geglu(layer_norm(x, gamma, beta, eps), w, b)
 
@@ -448,7 +457,7 @@ def scale_shift_norm(x, ss, gamma, beta, groups, eps, silu=True):
 
 def layer_norm(x, gamma, beta, eps):
     if _hip(x):
-        return _lib.layer_norm(x, gamma, beta, eps)
+        return _lib.layer_norm(x, gamma, beta, eps, _plan_rows(x))
     return ref.layer_norm(x, gamma, beta, eps)
 
 

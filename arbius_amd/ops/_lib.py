@@ -27,7 +27,7 @@ _SIGS = {
     "arb_group_norm_nhwc": (c_int, [c_void_p] * 5 + [c_int] * 4 + [c_float, c_int, c_void_p]),
     "arb_group_norm_mod_nhwc": (c_int, [c_void_p] * 6 + [c_int] * 5 + [c_float, c_int, c_int, c_int, c_float,
                                                                         c_void_p]),
-    "arb_layer_norm": (c_int, [c_void_p] * 4 + [c_int, c_int, c_float, c_void_p]),
+    "arb_layer_norm": (c_int, [c_void_p] * 4 + [c_int, c_int, c_float, c_long, c_void_p]),
     "arb_flash_attention": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float, c_int] + [c_void_p] * 3
                             + [c_int, c_void_p]),
     "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
@@ -51,7 +51,7 @@ _SIGS = {
     "arb_norm_table_apply_cat": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_long, c_int, c_int,
                                          c_void_p]),
     "arb_conv2d_nhwc_cat": (c_int, [c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_int] * 11 + [c_void_p]),
-    "arb_row_stats": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "arb_row_stats": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_long, c_void_p]),
     "arb_conv2d_ex": (c_int, [c_void_p] * 7 + [c_int] * 13 + [c_void_p]),
     "arb_rvm_resize_u8": (c_int, [c_void_p, c_void_p] + [c_int] * 5 + [c_void_p]),
     "arb_rvm_stem": (c_int, [c_void_p] * 3 + [c_int] * 3 + [c_void_p]),
@@ -168,7 +168,9 @@ def group_norm_mod_nhwc(x, gamma, beta, groups, eps, silu, mod, one_plus):
     return y
 
 
-def layer_norm(x, gamma, beta, eps):
+def layer_norm(x, gamma, beta, eps, plan_rows=None):
+    """plan_rows: the row count the kernel variant is chosen for (the canonical batch's rows under
+    ops.plan_batch, so a lock-step group picks its solo tasks' variant); default: the actual rows."""
     _bf16(x, gamma, beta)
     x = x.contiguous()
     C = x.shape[-1]
@@ -176,7 +178,8 @@ def layer_norm(x, gamma, beta, eps):
         raise ValueError(f"layer_norm: unsupported C={C}")
     M = x.numel() // C
     y = torch.empty_like(x)
-    _check(_fn("arb_layer_norm")(_p(x), _p(y), _p(gamma), _p(beta), M, C, float(eps), _stream()), "layer_norm")
+    _check(_fn("arb_layer_norm")(_p(x), _p(y), _p(gamma), _p(beta), M, C, float(eps),
+                                 int(M if plan_rows is None else plan_rows), _stream()), "layer_norm")
     return y
 
 
@@ -525,7 +528,7 @@ def gemm_geglu(x, w_il, b_il=None, cfg=-1, split=-1, plan_batch=None):
     return y.reshape(*x.shape[:-1], N // 2)
 
 
-def row_stats(x, eps):
+def row_stats(x, eps, plan_rows=None):
     """(mean, rstd) per row of x [..., C] (csrc/norm.hip, the LayerNorm kernel's arithmetic) -> fp32
     [M, 2] - the statistics of a LayerNorm folded into the following GEMM."""
     _bf16(x)
@@ -535,7 +538,8 @@ def row_stats(x, eps):
         raise ValueError(f"row_stats: unsupported C={C}")
     M = x.numel() // C
     rs = torch.empty(M, 2, dtype=torch.float32, device=x.device)
-    _check(_fn("arb_row_stats")(_p(x), _p(rs), M, C, float(eps), _stream()), "row_stats")
+    _check(_fn("arb_row_stats")(_p(x), _p(rs), M, C, float(eps), int(M if plan_rows is None else plan_rows),
+                                _stream()), "row_stats")
     return rs
 
 

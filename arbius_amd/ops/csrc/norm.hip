@@ -155,9 +155,13 @@ static bool ln_packed_geom(int C, int& lpr, int& vpl) {
   return false;
 }
 
+// plan_rows: the row count the kernel choice is made for - the CANONICAL batch's rows under
+// batch-invariant planning (ops.plan_batch), never the launch's own M: the packed and wave-per-row
+// kernels reduce a row in different orders, so a choice by M would make a lock-step group's bytes
+// differ from its solo tasks'.
 template <bool STATS>
 static bool ln_packed_launch(const void* x, void* y, const void* gamma, const void* beta, void* rs, int M, int C,
-                             float eps, hipStream_t stream) {
+                             float eps, long plan_rows, hipStream_t stream) {
   static const bool on = [] {
     const char* e = std::getenv("ARB_LN_PACKED");
     return e == nullptr || e[0] != '0';
@@ -166,7 +170,7 @@ static bool ln_packed_launch(const void* x, void* y, const void* gamma, const vo
   // (154 x 768 text-tower rows: 2.9 vs 4.1 us); at the UNet token counts the wave-per-row kernel
   // wins (32768 x 320: 13.2 vs 13.7 us, 8192 x 640: 6.6 vs 8.0 us).
   int lpr = 0, vpl = 0;
-  if (!on || (long)M * C > (1L << 18) || !ln_packed_geom(C, lpr, vpl)) return false;
+  if (!on || plan_rows * C > (1L << 18) || !ln_packed_geom(C, lpr, vpl)) return false;
   const int rows_per_block = 4 * (64 / lpr);
   const dim3 grid((M + rows_per_block - 1) / rows_per_block);
 #define LNP(L, V)                                                                                   \
@@ -183,9 +187,9 @@ static bool ln_packed_launch(const void* x, void* y, const void* gamma, const vo
 }
 
 ARB_API int arb_layer_norm(const void* x, void* y, const void* gamma, const void* beta, int M, int C, float eps,
-                           hipStream_t stream) {
+                           long plan_rows, hipStream_t stream) {
   if (C % 8 != 0) return -1;
-  if (ln_packed_launch<false>(x, y, gamma, beta, nullptr, M, C, eps, stream)) return (int)hipGetLastError();
+  if (ln_packed_launch<false>(x, y, gamma, beta, nullptr, M, C, eps, plan_rows, stream)) return (int)hipGetLastError();
   const int NV = C / 8;
 #define LN_LAUNCH(NVM, R)                                                                                   \
   layer_norm_kernel<NVM, R><<<dim3((M + 4 * R - 1) / (4 * R)), 256, 0, stream>>>(                                \
@@ -208,9 +212,9 @@ ARB_API int arb_layer_norm(const void* x, void* y, const void* gamma, const void
 }
 
 // Per-row (mean, rstd) of x [M, C] - the statistics of a LayerNorm folded into the next GEMM.
-ARB_API int arb_row_stats(const void* x, void* rs, int M, int C, float eps, hipStream_t stream) {
+ARB_API int arb_row_stats(const void* x, void* rs, int M, int C, float eps, long plan_rows, hipStream_t stream) {
   if (C % 8 != 0) return -1;
-  if (ln_packed_launch<true>(x, nullptr, nullptr, nullptr, rs, M, C, eps, stream)) return (int)hipGetLastError();
+  if (ln_packed_launch<true>(x, nullptr, nullptr, nullptr, rs, M, C, eps, plan_rows, stream)) return (int)hipGetLastError();
   const int NV = C / 8;
 #define RS_LAUNCH(NVM, R)                                                                                   \
   layer_norm_kernel<NVM, R, true><<<dim3((M + 4 * R - 1) / (4 * R)), 256, 0, stream>>>(                          \

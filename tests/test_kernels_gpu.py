@@ -580,3 +580,27 @@ def test_gemm_with_folded_layer_norm(cuda, M, K, N, geglu, res, cfg, split):
         h = h + r.float()
     assert _rel(y, h) < 1.5e-2, _rel(y, h)
     assert torch.equal(y, _lib.gemm_ln(x, wf, bf, wsum, rs, r, geglu=geglu, cfg=cfg, split=split))   # bitwise rerun
+
+
+@pytest.mark.parametrize("C,T,heads", [(320, 1024, 5), (640, 256, 10), (1280, 64, 20), (768, 77, 12)])
+def test_transformer_block_batch_invariant(cuda, C, T, heads):
+    """A lock-step group (batch 8) reproduces each CFG pair's solo (batch 2) bytes through a whole
+    transformer block under ops.plan_batch(2): every size-dependent kernel choice (LayerNorm variant,
+    LN fold into the GEMM, GEMM plan, attention tiling) is made for the canonical batch, never the
+    launch's own row count (a choice by rows made a group's LN differ from solo)."""
+    from arbius_amd.models.layers import init_weights
+    from arbius_amd.models.unet2d import BasicTransformerBlock
+    torch.manual_seed(12)
+    blk = init_weights(BasicTransformerBlock(C, 768, heads), 5).to(cuda, torch.bfloat16)
+    h = (torch.randn(8, T, C, device=cuda) * 2 + 0.5).bfloat16()
+    ctx = torch.randn(8, 77, 768, device=cuda).bfloat16()
+    xs = (torch.randn(8, T, C, device=cuda) + 1).bfloat16()
+    g = (torch.rand(C, device=cuda) + 0.5).bfloat16()
+    be = torch.randn(C, device=cuda).bfloat16()
+    with torch.no_grad(), ops.plan_batch(2):
+        full = blk(h, ctx)
+        ln_full = ops.layer_norm(xs, g, be, 1e-5)
+        for j in range(4):
+            sl = slice(2 * j, 2 * j + 2)
+            assert torch.equal(blk(h[sl].contiguous(), ctx[sl].contiguous()), full[sl]), f"pair {j}"
+            assert torch.equal(ops.layer_norm(xs[sl].contiguous(), g, be, 1e-5), ln_full[sl])

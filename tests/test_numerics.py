@@ -61,3 +61,14 @@ def test_family_table_well_formed():
     for M, N, K, split, ratio, cfg in rows:
         assert ratio in (1, 2, 4) and split >= 1 and K % 64 == 0
         assert 0 <= cfg < 36 and not (24 <= cfg < 28 and split > 1)
+
+
+def test_plan_rows_is_batch_invariant():
+    """Size-dependent kernel choices use the canonical batch's rows under ops.plan_batch, so a
+    lock-step group (batch 2k) makes the same choice as each solo CFG pair (batch 2)."""
+    import torch
+    from arbius_amd import ops
+    solo, group = torch.empty(2, 1024, 320), torch.empty(8, 1024, 320)
+    with ops.plan_batch(2):
+        assert ops._plan_rows(solo) == ops._plan_rows(group) == ops.PLAN_CANON * 1024
+    assert ops._plan_rows(solo) == 2 * 1024 and ops._plan_rows(group) == 8 * 1024
