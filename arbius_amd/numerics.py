@@ -16,7 +16,7 @@ import os
 from typing import Callable, Dict, List, Tuple
 
 # bump on ANY change of output bytes (kernels, conv plans, sampler arithmetic, PNG/MP4 encoders)
-NUMERICS_VERSION = "r2.6-avc-intra-cavlc-qp20"
+NUMERICS_VERSION = "r3.0-bs8-2stream-plans-lnfold"
 
 # Environment knobs that select a different kernel library, plan table, tiling or reference ops.
 # They exist for A/B measurement only; ``start`` refuses to mine with any of them set.
@@ -126,7 +126,7 @@ def golden_cases(device) -> List[Tuple[str, Callable[[], object]]]:
     def k2_sampler(name):
         def f():
             return pipe("kandinsky2").solve({"prompt": "arbius test cat", "width": 768, "height": 768, "seed": 1337,
-                                             "num_inference_steps": 3, "prior_steps": "2",
+                                             "num_inference_steps": 4, "prior_steps": "2",
                                              "scheduler": name}).cid
         return f
 
@@ -169,7 +169,7 @@ def golden_cases(device) -> List[Tuple[str, Callable[[], object]]]:
     cases += [("sd15_512_dpm4_group2", sd_group(2)), ("sd15_512_dpm4_group3", sd_group(3)),
               ("sd15_768_dpm20_template_default", sd_template_default)]
     cases += [("kandinsky2_768_group2", k2_group2)]
-    cases += [(f"kandinsky2_768_{n}_3", k2_sampler(n)) for n in ("ddim_sampler", "pims_sampler")]
+    cases += [(f"kandinsky2_768_{n}_4", k2_sampler(n)) for n in ("ddim_sampler", "pims_sampler")]
     cases += [("kandinsky2_768_2+2", k2), ("zeroscopev2xl_256x256x8_2", video("zeroscopev2xl")),
               ("damo_256x256x8_2", video("damo")), ("rvm_320x180x8", rvm)]
     return cases

@@ -214,7 +214,8 @@ ARB_API int arb_layer_norm(const void* x, void* y, const void* gamma, const void
 // Per-row (mean, rstd) of x [M, C] - the statistics of a LayerNorm folded into the next GEMM.
 ARB_API int arb_row_stats(const void* x, void* rs, int M, int C, float eps, long plan_rows, hipStream_t stream) {
   if (C % 8 != 0) return -1;
-  if (ln_packed_launch<true>(x, nullptr, nullptr, nullptr, rs, M, C, eps, plan_rows, stream)) return (int)hipGetLastError();
+  if (ln_packed_launch<true>(x, nullptr, nullptr, nullptr, rs, M, C, eps, plan_rows, stream))
+    return (int)hipGetLastError();
   const int NV = C / 8;
 #define RS_LAUNCH(NVM, R)                                                                                   \
   layer_norm_kernel<NVM, R, true><<<dim3((M + 4 * R - 1) / (4 * R)), 256, 0, stream>>>(                          \
