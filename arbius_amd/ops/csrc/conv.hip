@@ -820,17 +820,16 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
     // only after every wave has arrived there, i.e. finished this tile's MFMAs (whose
     // operands - these ds_reads - had to complete first).
   };
+  // block-uniform guards instead of early exits: with breaks, hipcc gave every exit its own
+  // accumulator copy (320x128: 256 VGPRs + scratch spills whose reloads drained the DMA ring)
   for (int i = 0; i < nk; i += NS) {
     step(IC<0>(), i);
-    if (i + 1 >= nk) break;
-    step(IC<1>(), i + 1);
+    if (i + 1 < nk) step(IC<1>(), i + 1);
     if constexpr (NS > 2) {
-      if (i + 2 >= nk) break;
-      step(IC<2 % NS>(), i + 2);
+      if (i + 2 < nk) step(IC<2 % NS>(), i + 2);
     }
     if constexpr (NS > 3) {
-      if (i + 3 >= nk) break;
-      step(IC<3 % NS>(), i + 3);
+      if (i + 3 < nk) step(IC<3 % NS>(), i + 3);
     }
   }
 
@@ -873,6 +872,200 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
       o.x = enc16<EL>(v0) | (enc16<EL>(v1) << 16);
       o.y = enc16<EL>(v2) | (enc16<EL>(v3) << 16);
       *reinterpret_cast<uint2*>(p.out + (size_t)m * p.N + n) = o;
+    }
+  }
+}
+
+// Staggered two-group variant (cfg 36 + i).  Same LDS-DMA ring, tiling, fragments and epilogue as
+// conv_glds_kernel, but the 8 waves form two groups (waves 0-3 and 4-7: one wave of each per SIMD,
+// the hardware places waves w and w+4 on one SIMD) that run ONE BARRIER APART
+// (cdna_hip_programming.md §5 "The 256^2 8-phase template": staggered wave groups, per-phase
+// interleave).  Each K tile is two phases (its two k32 halves); a phase is
+//     LOAD:    this k-half's A/B fragments from LDS (+ at odd phases the next-but-one tile's DMA
+//              and the counted wait for the next tile), then s_barrier
+//     COMPUTE: the k-half's MFMAs at raised priority, then s_barrier
+// and group 1 starts with one extra barrier (group 0 ends with one), so every barrier interval
+// pairs one group's MFMAs with the other group's LDS reads / DMA issue on each SIMD - in the
+// one-barrier-per-K-tile kernel both waves of a SIMD read, then both multiply.
+// Ordering (barrier events numbered in group 0's count; group 1 passes event e at its own e-1):
+//   RAW: tile j is waited (vmcnt, own DMA) in phase 2j-1 before its first barrier and first read
+//        in phase 2j: group 0's wait precedes event 4j-2, group 1's event 4j-1, and the earliest
+//        read (group 0, phase 2j) follows event 4j-1.
+//   WAR: tile j+2 is issued in phase 2j+1 into the stage of tile j-1, whose last reads (phase
+//        2j-1) retire before that phase's MFMAs (lgkmcnt); group 1 finishes those MFMAs at
+//        event 4j and group 0 issues only after event 4j+1.  Three stages (NS = 3).
+// Per output the MFMA sequence (k-tiles ascending, k-halves ascending) is that of every other
+// family, so the results are bitwise those of conv_glds_kernel / conv_igemm_kernel at every split.
+template <int BN, int BM, int WN, int WM, bool SPLIT>
+__global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
+  constexpr int EL = 0, BK = 64, NT = 512, NS = 3;
+  constexpr int RPI = NT / 8;
+  static_assert(WN * WM == 8, "8 waves");
+  static_assert((BN * 8) % NT == 0 && (BM * 8) % NT == 0, "whole DMA rounds per tile");
+  constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
+  constexpr int WCH = BN * 8 / NT, XCH = BM * 8 / NT;
+  constexpr int LPT = WCH + XCH;
+  constexpr int STAGE = (BN + BM) * BK;
+  static_assert((size_t)NS * STAGE * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16_t lds0[STAGE];
+  __shared__ __attribute__((aligned(16))) bf16_t lds1[STAGE];
+  __shared__ __attribute__((aligned(16))) bf16_t lds2[STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WM, wm = wave % WM;
+  const int g = lane >> 4, l16 = lane & 15;
+  const bool grp1 = wave >= 4;
+  int split_idx, n0, m0;
+  tile_coords(p, BN, BM, split_idx, n0, m0);
+  const int kt0 = SPLIT ? split_idx * p.kt_per_split : 0;
+  const int kt1 = SPLIT ? min(p.ktiles, kt0 + p.kt_per_split) : p.ktiles;
+  const int nk = kt1 - kt0;
+
+  const int pos = tid & 7;
+  int woff[WCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) {
+    const int row = (tid >> 3) + RPI * i;
+    woff[i] = n0 + row < p.N ? (n0 + row) * p.K + ((pos ^ (row & 7)) << 3) : -1;
+  }
+  int xb[XCH], xho[XCH], xwo[XCH], xcc[XCH];
+  bool xok[XCH];
+  const int hw = p.Ho * p.Wo;
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int row = (tid >> 3) + RPI * i;
+    xcc[i] = pos ^ (row & 7);
+    const int m = m0 + row;
+    xok[i] = m < p.M;
+    const int mm = xok[i] ? m : 0;
+    xb[i] = mm / hw;
+    const int rem = mm - xb[i] * hw;
+    xho[i] = (rem / p.Wo) * p.stride - p.pad;
+    xwo[i] = (rem % p.Wo) * p.stride - p.padw;
+  }
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  int wk = kt0 * BK, wc = wk % p.Cin, wrs = wk / p.Cin;
+  int wr = wrs / p.kw, ws = wrs - wr * p.kw;
+  int xoff[XCH];
+  auto set_tap = [&]() {
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      int hi = xho[i] + wr, wi = xwo[i] + ws;
+      const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
+      if (p.upsample) { hi >>= 1; wi >>= 1; }
+      xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + xcc[i] * 8 : -1;
+    }
+  };
+  set_tap();
+  auto issue = [&](auto stage_c) {
+    bf16_t* sW = ring_stage<decltype(stage_c)::value>(lds0, lds1, lds2, lds2);
+    bf16_t* sX = sW + BN * BK;
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sW + ((wave * 8) + RPI * i) * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sX + ((wave * 8) + RPI * i) * BK), 16, 0, 0);
+    }
+    wk += BK;
+    wc += BK;
+    if (wc == p.Cin) {
+      wc = 0;
+      if (++ws == p.kw) { ws = 0; ++wr; }
+      set_tap();
+    }
+  };
+  auto bar = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed for every wave before the first read
+  if (0 < nk) issue(IC<0>());
+  if (1 < nk) {
+    issue(IC<1>());
+    wait_vmcnt<LPT>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  bar();
+  if (grp1) bar();   // group 1 runs one barrier behind group 0
+
+  // one phase: k-half KK of the tile in stage S; at KK = 1 also the DMA of tile i+2 (into stage
+  // S+2 mod 3 = the stage of tile i-1) and the wait for tile i+1
+  auto phase = [&](auto stage_c, auto kk_c, int i) __attribute__((always_inline)) {
+    constexpr int S = decltype(stage_c)::value, KK = decltype(kk_c)::value;
+    const bf16_t* sW = ring_stage<S>(lds0, lds1, lds2, lds2);
+    const bf16_t* sX = sW + BN * BK;
+    uint4 af[TN], bfr[TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a) {
+      const int row = wn * (BN / WN) + a * 16 + l16;
+      af[a] = ld16(&sW[row * BK + (((KK * 4 + g) ^ (row & 7)) << 3)]);
+    }
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int row = wm * (BM / WM) + b * 16 + l16;
+      bfr[b] = ld16(&sX[row * BK + (((KK * 4 + g) ^ (row & 7)) << 3)]);
+    }
+    if constexpr (KK == 1) {
+      if (i + 2 < nk) {
+        issue(IC<(S + 2) % NS>());
+        wait_vmcnt<LPT>();          // tile i+1 landed (tile i+2 may still be in flight)
+      } else {
+        wait_vmcnt<0>();
+      }
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+      for (int b = 0; b < TM; ++b) acc[a][b] = mma16<EL>(af[a], bfr[b], acc[a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+  // unrolled by the ring depth (compile-time stages); a tile past the end is skipped by a
+  // block-uniform branch - no early exits, so the accumulators keep one register home
+  for (int i = 0; i < nk; i += NS) {
+    phase(IC<0>(), IC<0>(), i);
+    phase(IC<0>(), IC<1>(), i);
+    if (i + 1 < nk) {
+      phase(IC<1>(), IC<0>(), i + 1);
+      phase(IC<1>(), IC<1>(), i + 1);
+    }
+    if (i + 2 < nk) {
+      phase(IC<2>(), IC<0>(), i + 2);
+      phase(IC<2>(), IC<1>(), i + 2);
+    }
+  }
+  if (!grp1) bar();  // equal barrier counts: group 0 makes up group 1's head start
+
+  if constexpr (!SPLIT) {
+    epilogue_lds<BN, BM, WN, WM, NT, STAGE / 2, EL>(p, acc, reinterpret_cast<float*>(lds0), m0, n0);
+  } else {
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int m = m0 + wm * (BM / WM) + b * 16 + l16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
+        if (n < p.N)
+          *reinterpret_cast<float4*>(p.ws + ((size_t)split_idx * p.M + m) * p.N + n) =
+              make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+      }
     }
   }
 }
@@ -1016,13 +1209,11 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_xreg_kernel(ConvArgs p) {
     }
     if constexpr (NT == 512) __builtin_amdgcn_s_setprio(0);
   };
-  for (int i = 0; i < nk; i += NS) {
+  for (int i = 0; i < nk; i += NS) {   // guards, not early exits (see conv_glds_kernel)
     step(IC<0>(), i);
-    if (i + 1 >= nk) break;
-    step(IC<1>(), i + 1);
+    if (i + 1 < nk) step(IC<1>(), i + 1);
     if constexpr (NS > 2) {
-      if (i + 2 >= nk) break;
-      step(IC<2 % NS>(), i + 2);
+      if (i + 2 < nk) step(IC<2 % NS>(), i + 2);
     }
   }
   if (split) {
@@ -1253,17 +1444,14 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_persist_kernel(ConvArgs 
       }
     }
   };
-  for (int j = 0; j < J; j += NS) {
+  for (int j = 0; j < J; j += NS) {   // guards, not early exits (see conv_glds_kernel)
     step(IC<0>(), j);
-    if (j + 1 >= J) break;
-    step(IC<1>(), j + 1);
+    if (j + 1 < J) step(IC<1>(), j + 1);
     if constexpr (NS > 2) {
-      if (j + 2 >= J) break;
-      step(IC<2 % NS>(), j + 2);
+      if (j + 2 < J) step(IC<2 % NS>(), j + 2);
     }
     if constexpr (NS > 3) {
-      if (j + 3 >= J) break;
-      step(IC<3 % NS>(), j + 3);
+      if (j + 3 < J) step(IC<3 % NS>(), j + 3);
     }
   }
 }
@@ -1424,14 +1612,14 @@ static const std::vector<PinnedPlan>& env_plans() {
 
 // cfg ids: 0..9 LDS-DMA 4-wave, 10..19 register-staged 4-wave, 20..23 8-wave LDS-DMA 2-stage,
 // 24..27 persistent short-K, 28..31 8-wave LDS-DMA 3-stage ring (two K-tiles in flight),
-// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring)
+// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring), 36..39 8-wave staggered two-group ring
 static inline bool is_persist(int cfg) { return cfg >= 24 && cfg < 28; }
 // 32..35 X-in-registers 8-wave tiles (weights through an LDS-DMA ring, activations straight to VGPRs)
 static inline bool is_xreg(int cfg) { return cfg >= 32 && cfg < 36; }
 
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
-  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 36))) {
+  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 40))) {
     if (is_persist(want_cfg)) return {want_cfg, 1, ktiles};   // persistent: no split-K
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
@@ -1607,6 +1795,27 @@ static void launch_xreg(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   }
 }
 
+// Staggered two-group tiles (cfg 36 + i): 8 waves, three-stage LDS-DMA ring.
+template <int BN, int BM, int WN, int WM>
+static void launch_stag(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
+  ConvArgs p = a;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
+  p.nsplit = pl.split > 1 ? pl.split : 1;
+  p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;
+  p.norm = nullptr;
+  p.counters = nullptr;
+  if (pl.split > 1) {
+    p.kt_per_split = pl.kt_per_split;
+    conv_stag_kernel<BN, BM, WN, WM, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
+    long blocks = ((long)p.M * (p.N / 8) + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<0><<<(int)blocks, 256, 0, s>>>(p, pl.split);
+  } else {
+    conv_stag_kernel<BN, BM, WN, WM, false><<<p.tiles_total, 512, 0, s>>>(p);
+  }
+}
+
 // 8-wave LDS-DMA tiles (cfg 20 + i): two full K-tile stages, per-wave 128x64 / 160x64 outputs.
 struct BigCfg {
   int bn, bm;
@@ -1736,6 +1945,16 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
     else if (pl.cfg < kNumCfgs) pl.cfg += kNumCfgs;
   }
   if (pl.split > 1 && ws == nullptr) return -3;
+  if (pl.cfg >= 36) {   // staggered two-group 8-wave tiles (bf16, no norm prologue / dual source)
+    if (EL != 0 || a.norm != nullptr) return -4;
+    switch (pl.cfg - 36) {
+      case 0: launch_stag<256, 128, 4, 2>(a, pl, stream); break;
+      case 1: launch_stag<128, 256, 2, 4>(a, pl, stream); break;
+      case 2: launch_stag<192, 192, 2, 4>(a, pl, stream); break;
+      default: launch_stag<320, 64, 4, 2>(a, pl, stream); break;
+    }
+    return (int)hipGetLastError();
+  }
   if (is_xreg(pl.cfg)) {   // X-in-registers 8-wave tiles (bf16, no norm prologue / dual source)
     if (EL != 0 || a.norm != nullptr) return -4;
     switch (pl.cfg - 32) {

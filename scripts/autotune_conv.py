@@ -88,12 +88,14 @@ def candidates(M, N, K, mode):
     """(cfg, split) pairs worth timing: split-K only when the grid is short of 2 waves."""
     deep = list(range(28, 28 + len(KDEEP)))
     xreg = list(range(32, 32 + len(KXREG)))
-    big = list(range(20, 20 + len(KBIG))) + list(range(24, 24 + len(KPERSIST))) + deep + xreg
+    stag = list(range(36, 36 + len(KSTAG)))
+    big = list(range(20, 20 + len(KBIG))) + list(range(24, 24 + len(KPERSIST))) + deep + xreg + stag
     cfgs = {"legacy": range(10, NCFG), "big": big, "glds": list(range(10)) + big, "deep": deep}.get(
         mode, list(range(NCFG)) + big)
     for cfg in cfgs:
-        bn, bm = (KXREG[cfg - 32] if cfg >= 32 else KDEEP[cfg - 28] if cfg >= 28 else KPERSIST[cfg - 24]
-                  if cfg >= 24 else KBIG[cfg - 20] if cfg >= 20 else KCFG[cfg % 10])
+        bn, bm = (KSTAG[cfg - 36] if cfg >= 36 else KXREG[cfg - 32] if cfg >= 32 else KDEEP[cfg - 28]
+                  if cfg >= 28 else KPERSIST[cfg - 24] if cfg >= 24 else KBIG[cfg - 20] if cfg >= 20
+                  else KCFG[cfg % 10])
         if cfg >= 20 and bn > N + N // 2:
             continue
         if 24 <= cfg < 28:      # persistent short-K kernel: no split-K
@@ -112,6 +114,7 @@ KBIG = [(256, 256), (320, 128), (256, 128), (320, 192)]
 KPERSIST = [(128, 128), (256, 128), (160, 128), (128, 64)]
 KDEEP = [(128, 256), (256, 128), (192, 192), (320, 64)]     # 8-wave, 3-stage ring
 KXREG = [(160, 256), (128, 256), (160, 128), (256, 128)]     # 8-wave, activation operand in VGPRs
+KSTAG = [(256, 128), (128, 256), (192, 192), (320, 64)]     # 8-wave, two groups a barrier apart, 3-stage ring
 
 
 def _agrees(y, ref):
