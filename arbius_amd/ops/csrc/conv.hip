@@ -896,20 +896,25 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
 //        event 4j and group 0 issues only after event 4j+1.  Three stages (NS = 3).
 // Per output the MFMA sequence (k-tiles ascending, k-halves ascending) is that of every other
 // family, so the results are bitwise those of conv_glds_kernel / conv_igemm_kernel at every split.
+// A tile operand of R rows is R/8 DMA wave-instructions (8 rows of 128 B each); wave w issues
+// instructions w, w+8, ... - when R/8 is not a multiple of 8 (BN = 160) the surplus ones of a round
+// write a 1 KiB dummy buffer nobody reads, so every wave keeps the same vmcnt count per tile.
 template <int BN, int BM, int WN, int WM, bool SPLIT>
 __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
   constexpr int EL = 0, BK = 64, NT = 512, NS = 3;
-  constexpr int RPI = NT / 8;
   static_assert(WN * WM == 8, "8 waves");
-  static_assert((BN * 8) % NT == 0 && (BM * 8) % NT == 0, "whole DMA rounds per tile");
+  static_assert(BN % 8 == 0 && BM % 8 == 0, "whole DMA wave-instructions per operand");
   constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
-  constexpr int WCH = BN * 8 / NT, XCH = BM * 8 / NT;
+  constexpr int WINS = BN / 8, XINS = BM / 8;
+  constexpr int WCH = (WINS + 7) / 8, XCH = (XINS + 7) / 8;
+  constexpr bool DUMMY = (WINS % 8) != 0 || (XINS % 8) != 0;
   constexpr int LPT = WCH + XCH;
   constexpr int STAGE = (BN + BM) * BK;
-  static_assert((size_t)NS * STAGE * 2 <= 160 * 1024, "LDS");
+  static_assert((size_t)NS * STAGE * 2 + (DUMMY ? 1024 : 0) <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) bf16_t lds0[STAGE];
   __shared__ __attribute__((aligned(16))) bf16_t lds1[STAGE];
   __shared__ __attribute__((aligned(16))) bf16_t lds2[STAGE];
+  __shared__ __attribute__((aligned(16))) bf16_t ldsd[DUMMY ? 512 : 8];   // surplus DMA target
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
@@ -925,18 +930,18 @@ __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
   int woff[WCH];
 #pragma unroll
   for (int i = 0; i < WCH; ++i) {
-    const int row = (tid >> 3) + RPI * i;
-    woff[i] = n0 + row < p.N ? (n0 + row) * p.K + ((pos ^ (row & 7)) << 3) : -1;
+    const int j = wave + 8 * i, row = 8 * j + (lane >> 3);
+    woff[i] = (j < WINS && n0 + row < p.N) ? (n0 + row) * p.K + ((pos ^ (row & 7)) << 3) : -1;
   }
   int xb[XCH], xho[XCH], xwo[XCH], xcc[XCH];
   bool xok[XCH];
   const int hw = p.Ho * p.Wo;
 #pragma unroll
   for (int i = 0; i < XCH; ++i) {
-    const int row = (tid >> 3) + RPI * i;
+    const int j = wave + 8 * i, row = 8 * j + (lane >> 3);
     xcc[i] = pos ^ (row & 7);
     const int m = m0 + row;
-    xok[i] = m < p.M;
+    xok[i] = j < XINS && m < p.M;
     const int mm = xok[i] ? m : 0;
     xb[i] = mm / hw;
     const int rem = mm - xb[i] * hw;
@@ -963,13 +968,17 @@ __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
     bf16_t* sX = sW + BN * BK;
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
+      const int j = wave + 8 * i;
       const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sW + ((wave * 8) + RPI * i) * BK), 16, 0, 0);
+      bf16_t* dst = (!DUMMY || j < WINS) ? sW + 8 * j * BK : ldsd;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
+      const int j = wave + 8 * i;
       const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sX + ((wave * 8) + RPI * i) * BK), 16, 0, 0);
+      bf16_t* dst = (!DUMMY || j < XINS) ? sX + 8 * j * BK : ldsd;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
     }
     wk += BK;
     wc += BK;
@@ -1612,14 +1621,14 @@ static const std::vector<PinnedPlan>& env_plans() {
 
 // cfg ids: 0..9 LDS-DMA 4-wave, 10..19 register-staged 4-wave, 20..23 8-wave LDS-DMA 2-stage,
 // 24..27 persistent short-K, 28..31 8-wave LDS-DMA 3-stage ring (two K-tiles in flight),
-// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring), 36..39 8-wave staggered two-group ring
+// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring), 36..41 8-wave staggered two-group ring
 static inline bool is_persist(int cfg) { return cfg >= 24 && cfg < 28; }
 // 32..35 X-in-registers 8-wave tiles (weights through an LDS-DMA ring, activations straight to VGPRs)
 static inline bool is_xreg(int cfg) { return cfg >= 32 && cfg < 36; }
 
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
-  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 40))) {
+  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 42))) {
     if (is_persist(want_cfg)) return {want_cfg, 1, ktiles};   // persistent: no split-K
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
@@ -1795,7 +1804,7 @@ static void launch_xreg(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   }
 }
 
-// Staggered two-group tiles (cfg 36 + i): 8 waves, three-stage LDS-DMA ring.
+// Staggered two-group tiles (cfg 36 + i, i < 6): 8 waves, three-stage LDS-DMA ring.
 template <int BN, int BM, int WN, int WM>
 static void launch_stag(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   ConvArgs p = a;
@@ -1951,7 +1960,9 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
       case 0: launch_stag<256, 128, 4, 2>(a, pl, stream); break;
       case 1: launch_stag<128, 256, 2, 4>(a, pl, stream); break;
       case 2: launch_stag<192, 192, 2, 4>(a, pl, stream); break;
-      default: launch_stag<320, 64, 4, 2>(a, pl, stream); break;
+      case 3: launch_stag<320, 64, 4, 2>(a, pl, stream); break;
+      case 4: launch_stag<160, 256, 2, 4>(a, pl, stream); break;
+      default: launch_stag<160, 128, 2, 4>(a, pl, stream); break;
     }
     return (int)hipGetLastError();
   }
