@@ -59,6 +59,8 @@ def parse_args(argv=None):
     ap.add_argument("--node", action="store_true",
                     help="whole-node mode: tasks flow through the node's own stack (MockEngine events -> "
                          "orchestrator -> solver pool -> commit/submit); one process, N GPU worker processes")
+    ap.add_argument("--node-outstanding", type=int, default=0,
+                    help="--node: tasks kept in flight (default 2 x pool capacity: a saturated node)")
     args = ap.parse_args(argv)
     k2 = args.model == "kandinsky2"
     vid = args.model in ("zeroscopev2xl", "damo")
@@ -329,6 +331,7 @@ def run_node(args):
         "p90_task_latency_ms": round(r["p90_s"] * 1000.0, 2),
         "tasks_timed": r["tasks"],
         "pool_capacity": r["capacity"],
+        "tasks_outstanding": r["outstanding"],
         "pins_ok": r["pins_ok"],
         "jobs": r["jobs"],
         "stage_p50_s": r["stage_p50_s"],

@@ -16,6 +16,12 @@ candidate bitwise against the canonical plan's own output, and writes the winner
 With ``--batch 8 --conc 2`` the same search runs on the lock-step group shapes (canonical plan =
 their own plan) with two concurrent copies, i.e. the family that keeps the most throughput while
 the other task stream shares the GPU - again without moving a bit.
+
+``--plans`` (video models: no lock-step groups, planned by their own shape): the winners replace
+the tile config of the shapes' ``conv_plans.inc`` entries at the SAME split-K (the output file is
+a full plan table), so the plans get faster without any output byte changing.
+
+    python scripts/tune_family.py OUT_FILE --plans --models video --conc 2
 """
 import argparse
 import math
@@ -28,7 +34,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from arbius_amd.ops import _lib  # noqa: E402
 from scripts.autotune_conv import collect_shapes, graph_time  # noqa: E402
 
-FAMILIES = list(range(20)) + [20, 21, 22, 23, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39]
+FAMILIES = list(range(20)) + [20, 21, 22, 23, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41]
 NOSPLIT = [24, 25, 26, 27]   # persistent: split 1 only
 
 
@@ -41,7 +47,10 @@ def main():
     ap.add_argument("--merge", default=None, help="existing conv_family.inc whose entries are kept")
     ap.add_argument("--models", default="sd15", help="comma list: sd15,kandinsky2")
     ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--plans", action="store_true", help="rewrite conv_plans.inc cfgs (any batch, own plans)")
     a = ap.parse_args()
+    if a.plans:
+        return tune_plans(a)
     import scripts.autotune_conv as at
     at.CONC = a.conc
     dev = torch.device("cuda")
@@ -123,6 +132,71 @@ def main():
                 "static const FamilyPlan kFamilyPlans[] = {\n")
         for (M, N, K, sp, r), cfg in sorted(rows.items()):
             f.write(f"    {{{M}, {N}, {K}, {sp}, {r}, {cfg}}},\n")
+        f.write("};\n")
+
+
+def tune_plans(a):
+    """Every conv / GEMM of the models at its OWN plan: the fastest bitwise-equal family at the
+    planned split replaces the cfg in a copy of conv_plans.inc (entries added for shapes the cost
+    model planned, with the cost model's split)."""
+    import scripts.autotune_conv as at
+    at.CONC = a.conc
+    dev = torch.device("cuda")
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "arbius_amd", "ops", "csrc")
+    table = at.read_table(os.path.join(here, "conv_plans.inc"))
+    convs, gemms = collect_shapes(tuple(a.models.split(",")), a.res, a.batch)
+    torch.manual_seed(0)
+    jobs = []
+    for (B, H, W, C, Co, kh, kw, pad, up, stride) in convs:
+        if kh != kw:
+            continue
+        cfg0, sp = _lib.conv_plan(B, H, W, C, Co, kh, pad, up, stride)
+        Hl, Wl = (2 * H, 2 * W) if up else (H, W)
+        M = B * ((Hl + 2 * pad - kh) // stride + 1) * ((Wl + 2 * pad - kw) // stride + 1)
+        x = torch.randn(B, H, W, C, device=dev).bfloat16()
+        w = (torch.randn(Co, kh, kw, C, device=dev) / math.sqrt(kh * kw * C)).bfloat16()
+        b = torch.randn(Co, device=dev).bfloat16()
+        jobs.append(((M, Co, kh * kw * C), cfg0, sp,
+                     lambda cfg, sp, x=x, w=w, b=b, pad=pad, up=up, st=stride:
+                     _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st, cfg, sp)))
+    for (M, K, N, res) in gemms:
+        cfg0, sp = _lib.conv_plan(1, 1, M, K, N, 1, 0, 0, 1)
+        x = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
+        b = torch.randn(N, device=dev).bfloat16()
+        r = torch.randn(M, N, device=dev).bfloat16() if res else None
+        jobs.append(((M, N, K), cfg0, sp, lambda cfg, sp, x=x, w=w, b=b, r=r: _lib.gemm(x, w, b, r, cfg, sp)))
+    done = set()
+    for key, cfg0, sp, run in jobs:
+        if key in done:
+            continue
+        done.add(key)
+        ref = run(cfg0, sp)
+        best = (graph_time(lambda: run(cfg0, sp)), cfg0)
+        base = best[0]
+        for cfg in FAMILIES + (NOSPLIT if sp == 1 else []):
+            if cfg == cfg0:
+                continue
+            try:
+                y = run(cfg, sp)
+            except Exception:  # noqa: BLE001 - family not available for this shape
+                continue
+            if not torch.equal(y, ref):
+                print(f"# NOT bitwise: {key} cfg {cfg} vs {cfg0}", flush=True)
+                continue
+            best = min(best, (graph_time(lambda: run(cfg, sp)), cfg))
+        if key in table and table[key][1] != sp:
+            print(f"# {key}: planned split {sp} differs from the table's {table[key][1]}; kept", flush=True)
+            continue
+        table[key] = (best[1], sp)
+        print(f"plan M={key[0]} N={key[1]} K={key[2]} split={sp}: cfg {cfg0} {base:.1f} us -> cfg {best[1]} "
+              f"{best[0]:.1f} us", flush=True)
+    head = [ln for ln in open(os.path.join(here, "conv_plans.inc")) if ln.startswith("//")]
+    with open(a.out, "w") as f:
+        f.writelines(head)
+        f.write("static const PinnedPlan kPinnedPlans[] = {\n")
+        for (M, N, K), (c, sp) in sorted(table.items()):
+            f.write(f"    {{{M}, {N}, {K}, {c}, {sp}}},\n")
         f.write("};\n")
 
 
