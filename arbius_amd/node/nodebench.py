@@ -19,8 +19,8 @@ the timed region exactly as in production.  The loop keeps ``2 x capacity`` task
 default (``--node-outstanding``): a node measured for throughput is a SATURATED node, whose queue
 holds the next lock-step group while the current one runs; with exactly ``capacity`` outstanding
 every solution's replacement is still in hydration when a slot frees up and the slots run partial
-groups (measured: 3.0 tasks per group of 4, 20.2k vs 25.0k tasks/h on SD1.5).  Latency is per task, from ``submitTask`` (the event's
-block) to the accepted ``submitSolution``.
+groups (measured: 3.0 tasks per group of 4, 20.2k vs 25.0k tasks/h on SD1.5).  Latency is per
+task, from ``submitTask`` (the event's block) to the accepted ``submitSolution``.
 """
 from __future__ import annotations
 

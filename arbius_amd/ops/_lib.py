@@ -34,6 +34,7 @@ _SIGS = {
     "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
     "arb_norm_table_apply": (c_int, [c_void_p] * 3 + [c_int, c_long, c_int, c_int, c_void_p]),
     "arb_conv2d_nhwc": (c_int, [c_void_p] * 8 + [c_int] * 12 + [c_void_p]),
+    "arb_conv2d_nhwc_tld": (c_int, [c_void_p] * 4 + [c_int] + [c_void_p] * 4 + [c_int] * 12 + [c_void_p]),
     "arb_conv2d_nhwc_f16": (c_int, [c_void_p] * 7 + [c_int] * 11 + [c_void_p]),
     "arb_group_norm_table": (c_int, [c_void_p] * 4 + [c_float] + [c_void_p] * 2 + [c_int] * 4 + [c_float, c_void_p]),
     "arb_conv2d_workspace": (c_size_t, [c_int] * 11),
@@ -453,10 +454,16 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
         residual = residual.contiguous()
         if tuple(residual.shape) != tuple(y.shape):
             raise ValueError(f"conv2d residual {tuple(residual.shape)} != out {tuple(y.shape)}")
+    temb_ld = 0
     if temb is not None:
-        temb = temb.contiguous()
         if tuple(temb.shape) != (B, Cout):
             raise ValueError("conv2d temb must be [B, Cout]")
+        # a column slice of the batched ResBlock time projection is read in place at its row stride
+        if (not f16 and x1 is None and temb.stride(-1) == 1 and temb.stride(0) % 8 == 0
+                and temb.stride(0) >= Cout and temb.data_ptr() % 16 == 0):
+            temb_ld = temb.stride(0) if B > 1 else Cout
+        else:
+            temb = temb.contiguous()
     if b is not None and b.numel() != Cout:
         raise ValueError("conv2d bias size")
     if norm is not None:
@@ -478,6 +485,10 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     if x1 is not None:
         _check(_fn("arb_conv2d_nhwc_cat")(_p(x1), _p(x2), x1.shape[-1], _p(w), _p(b), _p(temb), _p(residual), _p(y),
                                           _p(ws), *args, _stream()), "conv2d_cat")
+        return y
+    if temb_ld:
+        _check(_fn("arb_conv2d_nhwc_tld")(_p(x), _p(w), _p(b), _p(temb), temb_ld, _p(residual), _p(y), _p(ws), _p(norm),
+                                          *args, int(bool(norm_silu)), _stream()), "conv2d")
         return y
     _check(_fn("arb_conv2d_nhwc")(_p(x), _p(w), _p(b), _p(temb), _p(residual), _p(y), _p(ws), _p(norm), *args,
                                   int(bool(norm_silu)), _stream()), "conv2d")

@@ -33,7 +33,7 @@ struct ConvArgs {
   const bf16_t* x;      // [B, H, W, Cin]
   const bf16_t* w;      // [N, K]
   const bf16_t* bias;   // [N] or null
-  const bf16_t* temb;   // [B, N] or null (per-batch bias, e.g. ResBlock time embedding)
+  const bf16_t* temb;   // [B, N] (row stride temb_ld) or null (per-batch bias, e.g. ResBlock time embedding)
   const bf16_t* res;    // [M, N] or null
   bf16_t* out;          // [M, N]
   float* ws;            // split-K slabs [S, M, N]
@@ -64,6 +64,7 @@ struct ConvArgs {
   // Register-staged kernel only.
   const bf16_t* x2 = nullptr;
   int C1 = 0;
+  int temb_ld = 0;      // temb row stride in elements (a column slice of the batched projection: no copy)
 };
 
 // ---- element type: EL = 0 bf16 (the diffusion models), EL = 1 fp16 (robust video matting).
@@ -247,7 +248,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&ac
         for (int e = 0; e < 8; ++e) v[e] += t[e];
       }
       if (p.temb) {
-        unpack8e<EL>(ld16(p.temb + (size_t)(m / hw) * p.N + n), t);
+        unpack8e<EL>(ld16(p.temb + (size_t)(m / hw) * p.temb_ld + n), t);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += t[e];
       }
@@ -555,7 +556,7 @@ __global__ void __launch_bounds__(256, MINW) conv_igemm_kernel(ConvArgs p) {
       v2 += lo16<EL>(bv.y); v3 += hi16<EL>(bv.y);
     }
     if (p.temb) {
-      const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)(m / hw) * p.N + n);
+      const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)(m / hw) * p.temb_ld + n);
       v0 += lo16<EL>(tv.x); v1 += hi16<EL>(tv.x);
       v2 += lo16<EL>(tv.y); v3 += hi16<EL>(tv.y);
     }
@@ -859,7 +860,7 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
         v2 += lo16<EL>(bv.y); v3 += hi16<EL>(bv.y);
       }
       if (p.temb) {
-        const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)bb * p.N + n);
+        const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)bb * p.temb_ld + n);
         v0 += lo16<EL>(tv.x); v1 += hi16<EL>(tv.x);
         v2 += lo16<EL>(tv.y); v3 += hi16<EL>(tv.y);
       }
@@ -1436,7 +1437,7 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_persist_kernel(ConvArgs 
         v0 += lo16<EL>(bv.x); v1 += hi16<EL>(bv.x);
         v2 += lo16<EL>(bv.y); v3 += hi16<EL>(bv.y);
         if (p.temb) {
-          const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)(m / hw) * p.N + n);
+          const uint2 tv = *reinterpret_cast<const uint2*>(p.temb + (size_t)(m / hw) * p.temb_ld + n);
           v0 += lo16<EL>(tv.x); v1 += hi16<EL>(tv.x);
           v2 += lo16<EL>(tv.y); v3 += hi16<EL>(tv.y);
         }
@@ -1558,7 +1559,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(ConvArgs p, int S) {
       for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
     if (p.temb) {
-      unpack8e<EL>(ld16(p.temb + (size_t)(m / hw) * p.N + n), t);
+      unpack8e<EL>(ld16(p.temb + (size_t)(m / hw) * p.temb_ld + n), t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
@@ -1917,7 +1918,7 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
                     void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
                     int stride, int cfg, int split, int norm_silu, hipStream_t stream, int geglu = 0,
                     const void* x2 = nullptr, int C1 = 0, const void* rowstat = nullptr,
-                    const void* wsum = nullptr, int cx = 0, int act = 0) {
+                    const void* wsum = nullptr, int cx = 0, int act = 0, int temb_ld = 0) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
   if (cx == 0) cx = Cin;
   if (cx % 8 != 0 || cx > Cin || Cin - cx >= 64 || act < 0 || act > 2) return -1;
@@ -1927,6 +1928,8 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
   a.x2 = (const bf16_t*)x2;
   a.C1 = C1;
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = (const bf16_t*)bias; a.temb = (const bf16_t*)temb;
+  a.temb_ld = temb_ld > 0 ? temb_ld : Cout;
+  if (temb_ld > 0 && (temb_ld < Cout || temb_ld % 8 != 0)) return -1;
   a.res = (const bf16_t*)res; a.out = (bf16_t*)out; a.ws = (float*)ws;
   a.norm = (const float*)norm; a.norm_silu = norm_silu;
   conv_geom(a, B, H, W, Cin, Cout, k, pad, upsample, stride);
@@ -2028,6 +2031,16 @@ ARB_API int arb_conv2d_nhwc(const void* x, const void* w, const void* bias, cons
                             hipStream_t stream) {
   return conv_run<0>(x, w, bias, temb, res, out, ws, norm, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg, split,
                      norm_silu, stream);
+}
+
+// As arb_conv2d_nhwc with the time embedding read at row stride temb_ld (a column slice of the batched
+// [B, sum(Cout)] ResBlock projection, no contiguous copy); temb_ld % 8 == 0 (16-byte rows).
+ARB_API int arb_conv2d_nhwc_tld(const void* x, const void* w, const void* bias, const void* temb, int temb_ld,
+                                const void* res, void* out, void* ws, const void* norm, int B, int H, int W, int Cin,
+                                int Cout, int k, int pad, int upsample, int stride, int cfg, int split, int norm_silu,
+                                hipStream_t stream) {
+  return conv_run<0>(x, w, bias, temb, res, out, ws, norm, B, H, W, Cin, Cout, k, pad, upsample, stride, cfg, split,
+                     norm_silu, stream, 0, nullptr, 0, nullptr, nullptr, 0, 0, temb_ld);
 }
 
 // Conv over the channel concat [x | x2] without materialising it (UNet up-path skip connections):

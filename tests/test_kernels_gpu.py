@@ -604,3 +604,22 @@ def test_transformer_block_batch_invariant(cuda, C, T, heads):
             sl = slice(2 * j, 2 * j + 2)
             assert torch.equal(blk(h[sl].contiguous(), ctx[sl].contiguous()), full[sl]), f"pair {j}"
             assert torch.equal(ops.layer_norm(xs[sl].contiguous(), g, be, 1e-5), ln_full[sl])
+
+
+@pytest.mark.parametrize("cfg,split", [(-1, -1), (10, 1), (21, 1), (34, 1), (36, 2), (24, 1), (15, 3)])
+def test_conv_temb_column_slice_read_in_place(cuda, cfg, split):
+    """The ResBlock time embedding is a column slice of ONE batched projection [B, sum(Cout)]; the
+    conv epilogue reads it at its row stride (no contiguous copy) with bytes equal to the copied
+    operand, on every epilogue path (LDS-staged, split-K reduce, persistent)."""
+    torch.manual_seed(14)
+    B, H, W, C, Co = 4, 16, 16, 128, 192
+    x = torch.randn(B, H, W, C, device=cuda).bfloat16()
+    w = (torch.randn(Co, 3, 3, C, device=cuda) / math.sqrt(9 * C)).bfloat16()
+    b = torch.randn(Co, device=cuda).bfloat16()
+    allp = torch.randn(B, 64 + Co + 320, device=cuda).bfloat16()
+    temb = allp[:, 64:64 + Co]
+    assert not temb.is_contiguous()
+    y = _lib.conv2d_nhwc(x, w, b, 1, False, None, temb, 1, cfg, split)
+    assert torch.equal(y, _lib.conv2d_nhwc(x, w, b, 1, False, None, temb.contiguous(), 1, cfg, split))
+    ref_y = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, 1, False) + temb.float()[:, None, None, :]
+    assert _rel(y, ref_y) < 1e-2
