@@ -32,6 +32,7 @@ import time
 from typing import Dict, List
 
 E18 = 10 ** 18
+POLL_S = 0.05          # event poll / top-up period of the bench loop
 DEPLOYER, USER, MINER = ("0x" + f"{i:040x}" for i in (1, 2, 3))
 
 
@@ -119,20 +120,28 @@ async def _run(args, device: str) -> dict:
         mine: List[str] = []
         while len(mine) < min(n, outstanding):
             mine.append(submit_one())
+        # The node's own loop polls chain events on a timer (Miner.run); here every POLL_S.  The
+        # bookkeeping (top-up, invalid-task check) runs at that rate too: the event loop shares the
+        # GIL with the task streams' launch threads, and a 2 ms poll + a DB query per task per pass
+        # starved them (the two streams ran mostly one after the other).
+        last = -1.0
         while True:
-            finished = sum(1 for t in mine if t in done)
-            if finished >= n:
-                return mine
-            while len(mine) - finished < outstanding and len(mine) < n:
-                mine.append(submit_one())
-            await miner.poll_events()
+            now = time.perf_counter()
+            if now - last >= POLL_S:
+                last = now
+                finished = sum(1 for t in mine if t in done)
+                if finished >= n:
+                    return mine
+                while len(mine) - finished < outstanding and len(mine) < n:
+                    mine.append(submit_one())
+                await miner.poll_events()
+                if miner.metrics.counters.get("jobs_failed_solve"):
+                    raise RuntimeError("a solve job failed during the node bench")
+                bad = [t for t in mine if t not in done and miner.db.get_invalid_task(t)]
+                if bad:
+                    raise RuntimeError(f"the node judged bench task {bad[0]} invalid (input outside the template?)")
             if await miner.process_jobs() == 0:
-                await asyncio.sleep(0.002)
-            if miner.metrics.counters.get("jobs_failed_solve"):
-                raise RuntimeError("a solve job failed during the node bench")
-            bad = [t for t in mine if miner.db.get_invalid_task(t)]
-            if bad:
-                raise RuntimeError(f"the node judged bench task {bad[0]} invalid (input outside the template?)")
+                await asyncio.sleep(0.005)
 
     per_step = capacity                              # one bench step = one task per pool slot
     if args.warmup:

@@ -8,6 +8,12 @@ O=$R/gpurun_out/${1:-prof3}
 mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)"; }
+step node_bench
+timeout -k 10 400 python bench.py --node --steps 8 --warmup 2 > $O/node.log 2>$O/node.err || { tail -20 $O/node.err; exit 1; }
+tail -1 $O/node.log | cut -c1-300
+step k2_bench
+timeout -k 10 500 python bench.py --model kandinsky2 --steps 4 > $O/k2.log 2>$O/k2.err || { tail -20 $O/k2.err; exit 1; }
+tail -1 $O/k2.log | cut -c1-300
 step zs_bench
 timeout -k 10 600 python bench.py --model zeroscopev2xl --steps 3 > $O/zs.log 2>$O/zs.err || { tail -20 $O/zs.err; exit 1; }
 tail -1 $O/zs.log | cut -c1-400
