@@ -74,8 +74,13 @@ class LocalSolverPool:
         # lock-step groups only where launches are batch-invariant (the HIP kernels); the CPU
         # reference path's library GEMMs are not, so grouping there would change CIDs
         self.lockstep = max(1, int(lockstep)) if str(device).startswith("cuda") else 1
-        # concurrent solves the orchestrator may hand us: every stream takes lock-step groups
-        self.capacity = self.streams * self.lockstep
+        # concurrent solves the orchestrator may hand us: every stream takes lock-step groups, and
+        # with lock-step grouping one more group per stream waits in the pool - a stream that frees
+        # up must find its next FULL group already pending (a group forms from whatever is queued at
+        # that instant; at depth 1 the replacements were still being leased: 3.0 tasks per group of 4)
+        self.depth = 2 if self.lockstep > 1 else 1
+        self.capacity = self.streams * self.lockstep * self.depth
+        self._exec = None
         self.factory = pipeline_factory or build_pipeline
         self.factory_kw = factory_kw
         self.pipes: Dict[str, object] = {}
@@ -157,8 +162,13 @@ class LocalSolverPool:
             pending = self._pending.setdefault(model.name, queue.Queue())
         fut: cf.Future = cf.Future()
         pending.put((model, inp, fut))
-        loop.run_in_executor(None, self._solve_waiting, model, pending)
+        with self._lock:
+            if self._exec is None:   # own threads: waiting turns must not exhaust the loop's default pool
+                self._exec = cf.ThreadPoolExecutor(max_workers=self.capacity, thread_name_prefix="solve")
+        loop.run_in_executor(self._exec, self._solve_waiting, model, pending)
         return await asyncio.wrap_future(fut)
 
     async def close(self):
+        if self._exec is not None:
+            self._exec.shutdown(wait=False)
         self.pipes.clear()

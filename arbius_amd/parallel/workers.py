@@ -172,6 +172,9 @@ class MultiGPUSolverPool:
         self.beats = self.ctx.Array("d", n * self.streams, lock=False)
         # tasks per lock-step group on one stream (HIP kernels only: batch-invariant launches)
         self.lockstep = max(1, int(lockstep)) if device_type == "cuda" else 1
+        # one more lock-step group per stream queued in the worker (node/pool.py LocalSolverPool.depth)
+        self.depth = 2 if self.lockstep > 1 else 1
+        self.slots_per_rank = self.streams * self.lockstep * self.depth
         self.busy: Dict[int, int] = {}           # job id -> rank
         self._started: Dict[int, float] = {}     # job id -> dispatch time
         self._gpu: Dict[int, dict] = {}          # rank -> {"task_s", "tasks"} (/metrics)
@@ -218,7 +221,7 @@ class MultiGPUSolverPool:
                     continue
                 if kind == "ready":
                     pending.discard(rank)
-                    self.idle.extend([rank] * self.streams * self.lockstep)
+                    self.idle.extend([rank] * self.slots_per_rank)
                     self.broadcast_stats[rank] = payload
                     self.world = payload.get("world")
 
@@ -233,7 +236,7 @@ class MultiGPUSolverPool:
 
     @property
     def capacity(self) -> int:
-        return self.streams * self.lockstep * sum(1 for p in self.procs if p is not None and p.is_alive())
+        return self.slots_per_rank * sum(1 for p in self.procs if p is not None and p.is_alive())
 
     def _spawn(self, rank, port, group):
         for k in range(self.streams):
@@ -253,7 +256,7 @@ class MultiGPUSolverPool:
         kind = msg[0]
         if kind == "ready":
             rank = msg[1]
-            self.idle = [r for r in self.idle if r != rank] + [rank] * self.streams * self.lockstep
+            self.idle = [r for r in self.idle if r != rank] + [rank] * self.slots_per_rank
             return
         _, jid, rank, payload = msg
         if self.busy.pop(jid, None) is not None:

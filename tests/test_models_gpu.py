@@ -178,7 +178,7 @@ def test_local_pool_lockstep_groups_match_solo(cuda):
     sols = asyncio.run(go())
     pipe = pool.pipes["anythingv3"]
     assert [s.cid for s in sols] == [solve_image(pipe, inp).cid for inp in inps]
-    assert pool.capacity == 3
+    assert pool.capacity == 6       # 1 stream x group of 3 running + one group queued (pool depth 2)
 
 
 def test_kandinsky2_lockstep_group_bitwise_equals_solo(cuda):
