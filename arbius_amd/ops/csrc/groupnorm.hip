@@ -516,6 +516,66 @@ __global__ void __launch_bounds__(256) gn_table_kernel(const Stat* __restrict__ 
   }
 }
 
+// gn_table as ONE WAVE per (group, image): the same combine tree as the 256-thread LDS version, bit for
+// bit - lane l holds tree leaves l, l+64, l+128, l+192 (leaf t = the sequential Chan combine of chunks
+// t, t+256, ...); levels 128 and 64 combine in-lane, levels 32..1 through __shfl_down (node t takes node
+// t+s) - with no LDS round trips and no block barriers (the 256-thread version was launch/latency bound:
+// 6 us per call, 2 % of the SD1.5 bench's kernel time).
+__global__ void __launch_bounds__(64) gn_table_wave_kernel(const Stat* __restrict__ part, float2* __restrict__ table,
+                                                           const bf16_t* __restrict__ gamma,
+                                                           const bf16_t* __restrict__ beta,
+                                                           const bf16_t* __restrict__ mod, float one_plus,
+                                                           int chunks, int C, int G, float eps) {
+  const int g = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
+  Stat leaf[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    Stat acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c = l + 64 * q; c < chunks; c += 256) acc = chan_combine(acc, part[((size_t)b * chunks + c) * G + g]);
+    leaf[q] = acc;
+  }
+  // level 128: t <- (t, t + 128) for t < 128  (t = l: leaf 0 with leaf 2; t = l + 64: leaf 1 with leaf 3)
+  Stat n0 = chan_combine(leaf[0], leaf[2]);
+  const Stat n1 = chan_combine(leaf[1], leaf[3]);
+  // level 64: t <- (t, t + 64) for t < 64
+  n0 = chan_combine(n0, n1);
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    Stat o;
+    o.n = __shfl_down(n0.n, s, 64);
+    o.mean = __shfl_down(n0.mean, s, 64);
+    o.m2 = __shfl_down(n0.m2, s, 64);
+    o.pad = 0.f;
+    n0 = chan_combine(n0, o);
+  }
+  const float mean = __shfl(n0.mean, 0, 64), m2 = __shfl(n0.m2, 0, 64), n = __shfl(n0.n, 0, 64);
+  const float rstd = rsqrtf(m2 / fmaxf(n, 1.f) + eps);
+  const int Cg = C / G;
+  for (int i = l; i < Cg; i += 64) {
+    const int c = g * Cg + i;
+    float sc = rstd * bf2f(gamma[c]);
+    float sf = bf2f(beta[c]) - mean * sc;
+    if (mod) {
+      const float m = bf2f(mod[(size_t)b * 2 * C + c]) + one_plus, a = bf2f(mod[(size_t)b * 2 * C + C + c]);
+      sc *= m;
+      sf = fmaf(sf, m, a);
+    }
+    table[(size_t)b * C + c] = make_float2(sc, sf);
+  }
+}
+
+// A/B switch (bitwise-equal variants): ARB_GN_TABLE_LDS=1 or arb_set_gn_table_lds(1) -> the 256-thread
+// LDS-tree table kernel instead of the one-wave one (tests/test_kernels_gpu.py compares the two).
+static int g_gn_table_lds = -1;
+static bool gn_table_lds() {
+  if (g_gn_table_lds < 0) {
+    const char* e = std::getenv("ARB_GN_TABLE_LDS");
+    g_gn_table_lds = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return g_gn_table_lds == 1;
+}
+ARB_API void arb_set_gn_table_lds(int on) { g_gn_table_lds = on ? 1 : 0; }
+
 static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma, const void* beta, const void* mod,
                         float one_plus, void* workspace, void* table, int B, int HW, int C, int G, float eps,
                         hipStream_t stream);
@@ -685,7 +745,12 @@ static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma
   const int chunks = gn_stat_chunks(HW, C);
   Stat* part = (Stat*)workspace;
   launch_gn_stats(x, part, B, HW, C, G, stream, x2, C1);
-  gn_table_kernel<<<dim3(G, B), 256, 0, stream>>>(part, (float2*)table, (const bf16_t*)gamma, (const bf16_t*)beta,
-                                                  (const bf16_t*)mod, one_plus, chunks, C, G, eps);
+  if (gn_table_lds())
+    gn_table_kernel<<<dim3(G, B), 256, 0, stream>>>(part, (float2*)table, (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                    (const bf16_t*)mod, one_plus, chunks, C, G, eps);
+  else
+    gn_table_wave_kernel<<<dim3(G, B), 64, 0, stream>>>(part, (float2*)table, (const bf16_t*)gamma,
+                                                        (const bf16_t*)beta, (const bf16_t*)mod, one_plus, chunks, C,
+                                                        G, eps);
   return (int)hipGetLastError();
 }

@@ -623,3 +623,29 @@ def test_conv_temb_column_slice_read_in_place(cuda, cfg, split):
     assert torch.equal(y, _lib.conv2d_nhwc(x, w, b, 1, False, None, temb.contiguous(), 1, cfg, split))
     ref_y = ref.conv2d_nhwc(x.float(), w.float(), b.float(), 1, 1, False) + temb.float()[:, None, None, :]
     assert _rel(y, ref_y) < 1e-2
+
+
+@pytest.mark.parametrize("B,HW,C,G,mod", [(8, 4096, 320, 32, False), (8, 1024, 640, 32, False),
+                                          (8, 256, 1280, 32, True), (2, 64, 2560, 32, False),
+                                          (16, 9216, 384, 32, True), (1, 16384, 128, 32, False),
+                                          (4, 2880, 960, 32, False), (2, 144, 1536, 32, True)])
+def test_group_norm_table_wave_kernel_bitwise_equals_lds_tree(cuda, B, HW, C, G, mod):
+    """The one-wave GroupNorm table kernel reproduces the 256-thread LDS tree's Chan combine exactly
+    (same leaves, same pairings): tables bitwise equal, so the faster kernel moves no output byte."""
+    torch.manual_seed(15)
+    x = (torch.randn(B, HW, C, device=cuda) * 2 + 0.7).bfloat16()
+    g = (torch.rand(C, device=cuda) + 0.5).bfloat16()
+    bt = torch.randn(C, device=cuda).bfloat16()
+    m = torch.randn(B, 2 * C, device=cuda).bfloat16() if mod else None
+    fn = _lib._fn("arb_set_gn_table_lds")
+    try:
+        fn(1)
+        t_lds = _lib.group_norm_table(x, g, bt, G, 1e-5, m, 1.0 if mod else 0.0)
+        fn(0)
+        t_wave = _lib.group_norm_table(x, g, bt, G, 1e-5, m, 1.0 if mod else 0.0)
+    finally:
+        fn(0)
+    assert torch.equal(t_lds, t_wave)
+    r = ref.group_norm_table(x.float(), g.float(), bt.float(), G, 1e-5, m.float() if mod else None,
+                             1.0 if mod else 0.0)
+    assert _rel(t_wave, r) < 1e-4
