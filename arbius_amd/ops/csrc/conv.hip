@@ -1080,6 +1080,225 @@ __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
   }
 }
 
+// Half-slot staggered variant (cfg 42 + i): conv_stag_kernel's two wave groups one barrier apart, but
+// the LDS-DMA ring is kept in K-HALF slots (32 channels x all rows of both operands per slot): a phase
+// reads exactly one slot, the DMA of half u is issued three phases before its first read and waited one
+// phase before it, so HS = 5 half slots (2.5 K tiles) carry the same two-phase latency cover as the
+// three-stage ring - and a 320 x 128 tile fits in 140 KiB (three full stages would take 168 KiB).
+// Slot rows are 64 B (4 x 16-B chunks); the chunk of row r sits at position chunk ^ f(r) with
+// f(r) = 2 * ((r >> 3) & 1), which spreads the 16-lane groups of every ds_read_b128 fragment read
+// over 16 distinct 16-B slots of the 256-B bank row (checked against the ds_read_b128 lane groups of
+// MI355X_MICROARCH.md §LDS).  DMA stays lane-linear: the permutation lives on the source address.
+// Ordering, with half u read in phase u (phase = one k-half of one K tile):
+//   RAW: half u is waited (vmcnt) in phase u-1 before its first barrier - the conv_stag_kernel
+//        argument with half slots for stages.
+//   WAR: half u is issued in phase u-3 into the slot of half u-HS, last read in phase u-HS <= u-5:
+//        its readers' MFMAs are done by group 1's barrier ending phase u-5 < the event before
+//        group 0's load part of phase u-3.
+// MFMA order per output (K tiles ascending, k-halves ascending) = every other family: bitwise equal.
+__device__ __forceinline__ int half_swz(int r) { return ((r >> 3) & 1) << 1; }
+
+template <int S, typename T>
+__device__ __forceinline__ T* half_slot(T* s0, T* s1, T* s2, T* s3, T* s4, T* s5) {
+  if constexpr (S == 0) return s0;
+  else if constexpr (S == 1) return s1;
+  else if constexpr (S == 2) return s2;
+  else if constexpr (S == 3) return s3;
+  else if constexpr (S == 4) return s4;
+  else return s5;
+}
+
+template <int BN, int BM, int WN, int WM, int HS, bool SPLIT>
+__global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
+  constexpr int EL = 0, BK = 64, HK = 32, NT = 512;
+  static_assert(WN * WM == 8, "8 waves");
+  static_assert(HS == 5 || HS == 6, "half-slot ring depth");
+  static_assert(BN % 16 == 0 && BM % 16 == 0, "16-row DMA wave-instructions");
+  constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
+  constexpr int WINS = BN / 16, XINS = BM / 16;      // DMA wave-instructions per operand and half
+  constexpr int WCH = (WINS + 7) / 8, XCH = (XINS + 7) / 8;
+  constexpr bool DUMMY = (WINS % 8) != 0 || (XINS % 8) != 0;
+  constexpr int LPH = WCH + XCH;                      // vmcnt units per half per wave
+  constexpr int SLOT = (BN + BM) * HK;                // bf16 per half slot
+  constexpr int U = HS == 5 ? 10 : 6;                 // phases per unrolled round (slot and parity static)
+  static_assert((size_t)HS * SLOT * 2 + (DUMMY ? 1024 : 0) <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16_t hs0[SLOT];
+  __shared__ __attribute__((aligned(16))) bf16_t hs1[SLOT];
+  __shared__ __attribute__((aligned(16))) bf16_t hs2[SLOT];
+  __shared__ __attribute__((aligned(16))) bf16_t hs3[SLOT];
+  __shared__ __attribute__((aligned(16))) bf16_t hs4[SLOT];
+  __shared__ __attribute__((aligned(16))) bf16_t hs5[HS > 5 ? SLOT : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t ldsd[DUMMY ? 512 : 8];   // surplus DMA target
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WM, wm = wave % WM;
+  const int g = lane >> 4, l16 = lane & 15;
+  const bool grp1 = wave >= 4;
+  int split_idx, n0, m0;
+  tile_coords(p, BN, BM, split_idx, n0, m0);
+  const int kt0 = SPLIT ? split_idx * p.kt_per_split : 0;
+  const int kt1 = SPLIT ? min(p.ktiles, kt0 + p.kt_per_split) : p.ktiles;
+  const int H = 2 * (kt1 - kt0);                      // halves of this block's K range
+
+  // DMA lane geometry: wave-instruction jj = wave + 8 i fills slot rows 16 jj .. 16 jj + 15, lane l
+  // writes row 16 jj + l / 4 at chunk position l % 4 (logical chunk = position ^ f(row))
+  const int pos = lane & 3;
+  int woff[WCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) {
+    const int jj = wave + 8 * i, row = 16 * jj + (lane >> 2);
+    woff[i] = (jj < WINS && n0 + row < p.N) ? (n0 + row) * p.K + ((pos ^ half_swz(row)) << 3) : -1;
+  }
+  int xb[XCH], xho[XCH], xwo[XCH], xcc[XCH];
+  bool xok[XCH];
+  const int hw = p.Ho * p.Wo;
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int jj = wave + 8 * i, row = 16 * jj + (lane >> 2);
+    xcc[i] = pos ^ half_swz(row);
+    const int m = m0 + row;
+    xok[i] = jj < XINS && m < p.M;
+    const int mm = xok[i] ? m : 0;
+    xb[i] = mm / hw;
+    const int rem = mm - xb[i] * hw;
+    xho[i] = (rem / p.Wo) * p.stride - p.pad;
+    xwo[i] = (rem % p.Wo) * p.stride - p.padw;
+  }
+  typedef __attribute__((address_space(1))) const void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  int wk = kt0 * BK, wc = wk % p.Cin, wrs = wk / p.Cin;
+  int wr = wrs / p.kw, ws = wrs - wr * p.kw;
+  int xoff[XCH];
+  auto set_tap = [&]() {
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      int hi = xho[i] + wr, wi = xwo[i] + ws;
+      const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
+      if (p.upsample) { hi >>= 1; wi >>= 1; }
+      xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + xcc[i] * 8 : -1;
+    }
+  };
+  set_tap();
+  // DMA of the next half (halves are issued in order; parity PAR = which k-half of the current tile)
+  auto issue = [&](auto slot_c, auto par_c) {
+    constexpr int S = decltype(slot_c)::value, PAR = decltype(par_c)::value;
+    bf16_t* sW = half_slot<S>(hs0, hs1, hs2, hs3, hs4, hs5);
+    bf16_t* sX = sW + BN * HK;
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int jj = wave + 8 * i;
+      const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk + PAR * HK) : (const void*)g_conv_zero_page;
+      bf16_t* dst = (!DUMMY || jj < WINS) ? sW + 16 * jj * HK : ldsd;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int jj = wave + 8 * i;
+      const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc + PAR * HK) : (const void*)g_conv_zero_page;
+      bf16_t* dst = (!DUMMY || jj < XINS) ? sX + 16 * jj * HK : ldsd;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+    }
+    if constexpr (PAR == 1) {       // both halves of this K tile issued: next tile
+      wk += BK;
+      wc += BK;
+      if (wc == p.Cin) {
+        wc = 0;
+        if (++ws == p.kw) { ws = 0; ++wr; }
+        set_tap();
+      }
+    }
+  };
+  auto bar = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue: halves 0..2 in flight (H >= 2 always), half 0 landed for every wave before any read
+  issue(IC<0>(), IC<0>());
+  issue(IC<1>(), IC<1>());
+  if (2 < H) {
+    issue(IC<2>(), IC<0>());
+    wait_vmcnt<2 * LPH>();
+  } else {
+    wait_vmcnt<LPH>();
+  }
+  bar();
+  if (grp1) bar();   // group 1 runs one barrier behind group 0
+
+  // phase P (K = P % U static): reads slot K % HS, issues half P + 3 into slot (K + 3) % HS
+  auto phase = [&](auto k_c, int P) __attribute__((always_inline)) {
+    constexpr int K = decltype(k_c)::value;
+    const bf16_t* sW = half_slot<K % HS>(hs0, hs1, hs2, hs3, hs4, hs5);
+    const bf16_t* sX = sW + BN * HK;
+    uint4 af[TN], bfr[TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a) {
+      const int row = wn * (BN / WN) + a * 16 + l16;
+      af[a] = ld16(&sW[row * HK + ((g ^ half_swz(row)) << 3)]);
+    }
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int row = wm * (BM / WM) + b * 16 + l16;
+      bfr[b] = ld16(&sX[row * HK + ((g ^ half_swz(row)) << 3)]);
+    }
+    if (P + 3 < H) {
+      issue(IC<(K + 3) % HS>(), IC<(K + 3) & 1>());
+      wait_vmcnt<2 * LPH>();      // half P+1 landed (P+2, P+3 may be in flight)
+    } else if (P + 2 < H) {
+      wait_vmcnt<LPH>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+      for (int b = 0; b < TM; ++b) acc[a][b] = mma16<EL>(af[a], bfr[b], acc[a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+  for (int P = 0; P < H; P += U) {   // block-uniform guards, no early exits (see conv_glds_kernel)
+    phase(IC<0>(), P);
+    phase(IC<1>(), P + 1);           // H is even: a round always has its first two phases
+    if (P + 2 < H) phase(IC<2>(), P + 2);
+    if (P + 3 < H) phase(IC<3>(), P + 3);
+    if (P + 4 < H) phase(IC<4>(), P + 4);
+    if (P + 5 < H) phase(IC<5>(), P + 5);
+    if constexpr (U > 6) {
+      if (P + 6 < H) phase(IC<6>(), P + 6);
+      if (P + 7 < H) phase(IC<7>(), P + 7);
+      if (P + 8 < H) phase(IC<8>(), P + 8);
+      if (P + 9 < H) phase(IC<9>(), P + 9);
+    }
+  }
+  if (!grp1) bar();
+
+  if constexpr (!SPLIT) {
+    epilogue_lds<BN, BM, WN, WM, NT, SLOT / 2, EL>(p, acc, reinterpret_cast<float*>(hs0), m0, n0);
+  } else {
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int m = m0 + wm * (BM / WM) + b * 16 + l16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int a = 0; a < TN; ++a) {
+        const int n = n0 + wn * (BN / WN) + a * 16 + 4 * g;
+        if (n < p.N)
+          *reinterpret_cast<float4*>(p.ws + ((size_t)split_idx * p.M + m) * p.N + n) =
+              make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+      }
+    }
+  }
+}
+
 // X-in-registers variant (cfg 32 + i), for the big-M SD level-0 convs (M = 32768 pixels at
 // lock-step batch 8).  The register-staged 160x128 tile is LDS-bound (profiles/pmc_r2_conv.md:
 // per K tile a CU moves 8 waves x (18 ds_read_b128 + 9 ds_write_b128) through LDS against 2 x 640
@@ -1622,14 +1841,14 @@ static const std::vector<PinnedPlan>& env_plans() {
 
 // cfg ids: 0..9 LDS-DMA 4-wave, 10..19 register-staged 4-wave, 20..23 8-wave LDS-DMA 2-stage,
 // 24..27 persistent short-K, 28..31 8-wave LDS-DMA 3-stage ring (two K-tiles in flight),
-// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring), 36..41 8-wave staggered two-group ring
+// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring), 36..41 8-wave staggered two-group ring, 42..44 the same on K-half slots
 static inline bool is_persist(int cfg) { return cfg >= 24 && cfg < 28; }
 // 32..35 X-in-registers 8-wave tiles (weights through an LDS-DMA ring, activations straight to VGPRs)
 static inline bool is_xreg(int cfg) { return cfg >= 32 && cfg < 36; }
 
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
-  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 42))) {
+  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 45))) {
     if (is_persist(want_cfg)) return {want_cfg, 1, ktiles};   // persistent: no split-K
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
@@ -1826,6 +2045,27 @@ static void launch_stag(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   }
 }
 
+// Half-slot staggered tiles (cfg 42 + i): 8 waves, HS-deep ring of K-half slots.
+template <int BN, int BM, int WN, int WM, int HS>
+static void launch_stag2(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
+  ConvArgs p = a;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.tiles_total = p.tiles_n * ((p.M + BM - 1) / BM);
+  p.nsplit = pl.split > 1 ? pl.split : 1;
+  p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;
+  p.norm = nullptr;
+  p.counters = nullptr;
+  if (pl.split > 1) {
+    p.kt_per_split = pl.kt_per_split;
+    conv_stag2_kernel<BN, BM, WN, WM, HS, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
+    long blocks = ((long)p.M * (p.N / 8) + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_kernel<0><<<(int)blocks, 256, 0, s>>>(p, pl.split);
+  } else {
+    conv_stag2_kernel<BN, BM, WN, WM, HS, false><<<p.tiles_total, 512, 0, s>>>(p);
+  }
+}
+
 // 8-wave LDS-DMA tiles (cfg 20 + i): two full K-tile stages, per-wave 128x64 / 160x64 outputs.
 struct BigCfg {
   int bn, bm;
@@ -1957,6 +2197,15 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
     else if (pl.cfg < kNumCfgs) pl.cfg += kNumCfgs;
   }
   if (pl.split > 1 && ws == nullptr) return -3;
+  if (pl.cfg >= 42) {   // half-slot staggered 8-wave tiles (bf16, no norm prologue / dual source)
+    if (EL != 0 || a.norm != nullptr) return -4;
+    switch (pl.cfg - 42) {
+      case 0: launch_stag2<320, 128, 4, 2, 5>(a, pl, stream); break;
+      case 1: launch_stag2<256, 256, 2, 4, 5>(a, pl, stream); break;
+      default: launch_stag2<256, 192, 4, 2, 5>(a, pl, stream); break;
+    }
+    return (int)hipGetLastError();
+  }
   if (pl.cfg >= 36) {   // staggered two-group 8-wave tiles (bf16, no norm prologue / dual source)
     if (EL != 0 || a.norm != nullptr) return -4;
     switch (pl.cfg - 36) {

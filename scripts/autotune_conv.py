@@ -115,7 +115,8 @@ KPERSIST = [(128, 128), (256, 128), (160, 128), (128, 64)]
 KDEEP = [(128, 256), (256, 128), (192, 192), (320, 64)]     # 8-wave, 3-stage ring
 KXREG = [(160, 256), (128, 256), (160, 128), (256, 128)]     # 8-wave, activation operand in VGPRs
 # 8-wave, two groups a barrier apart, 3-stage ring
-KSTAG = [(256, 128), (128, 256), (192, 192), (320, 64), (160, 256), (160, 128)]
+KSTAG = [(256, 128), (128, 256), (192, 192), (320, 64), (160, 256), (160, 128),
+         (320, 128), (256, 256), (256, 192)]   # 42-44: K-half slot ring
 
 
 def _agrees(y, ref):

@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from arbius_amd.ops import _lib  # noqa: E402
 from scripts.autotune_conv import collect_shapes, graph_time  # noqa: E402
 
-FAMILIES = list(range(20)) + [20, 21, 22, 23, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41]
+FAMILIES = list(range(20)) + [20, 21, 22, 23] + list(range(28, 45))
 NOSPLIT = [24, 25, 26, 27]   # persistent: split 1 only
 
 

@@ -133,7 +133,7 @@ def test_gemm(cuda, M, K, N):
     assert _rel(y, x.float() @ w.float().t() + b.float() + r.float()) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(20)) + list(range(20, 28)) + list(range(32, 42)))
+@pytest.mark.parametrize("cfg", list(range(20)) + list(range(20, 28)) + list(range(32, 45)))
 @pytest.mark.parametrize("split", [1, 3])
 def test_conv2d_all_tile_configs(cuda, cfg, split):
     """Every tile config of both kernel variants (LDS-DMA ring / register staged) and split-K."""
@@ -159,7 +159,7 @@ def test_conv_tile_families_bitwise_equal(cuda, B, H, W, C, Co, k):
     b = torch.randn(Co, device=cuda).bfloat16()
     pad = k // 2
     ref_y = _lib.conv2d_nhwc(x, w, b, pad, False, None, None, 1, 10, 1)
-    for cfg in (0, 3, 5, 6, 13, 15, 16, 20, 21, 22, 28, 29, 31, 36, 37, 38, 39, 40, 41):
+    for cfg in (0, 3, 5, 6, 13, 15, 16, 20, 21, 22, 28, 29, 31, 36, 37, 38, 39, 40, 41, 42, 43, 44):
         y = _lib.conv2d_nhwc(x, w, b, pad, False, None, None, 1, cfg, 1)
         assert torch.equal(y, ref_y), cfg
 
@@ -179,7 +179,8 @@ def test_conv_tile_families_bitwise_equal_at_split(cuda, split, B, H, W, C, Co, 
     r = torch.randn(B, H, W, Co, device=cuda).bfloat16()
     pad = k // 2
     ref_y = _lib.conv2d_nhwc(x, w, b, pad, False, r, None, 1, 15, split)
-    for cfg in (0, 3, 4, 5, 10, 13, 14, 16, 20, 21, 22, 28, 29, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41):
+    for cfg in (0, 3, 4, 5, 10, 13, 14, 16, 20, 21, 22, 28, 29, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42,
+                43, 44):
         y = _lib.conv2d_nhwc(x, w, b, pad, False, r, None, 1, cfg, split)
         assert torch.equal(y, ref_y), cfg
 
