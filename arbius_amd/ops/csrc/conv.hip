@@ -1841,7 +1841,8 @@ static const std::vector<PinnedPlan>& env_plans() {
 
 // cfg ids: 0..9 LDS-DMA 4-wave, 10..19 register-staged 4-wave, 20..23 8-wave LDS-DMA 2-stage,
 // 24..27 persistent short-K, 28..31 8-wave LDS-DMA 3-stage ring (two K-tiles in flight),
-// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring), 36..41 8-wave staggered two-group ring, 42..44 the same on K-half slots
+// 32..35 8-wave X-in-registers (weights-only LDS-DMA ring), 36..41 8-wave staggered two-group ring,
+// 42..44 the same on K-half slots
 static inline bool is_persist(int cfg) { return cfg >= 24 && cfg < 28; }
 // 32..35 X-in-registers 8-wave tiles (weights through an LDS-DMA ring, activations straight to VGPRs)
 static inline bool is_xreg(int cfg) { return cfg >= 32 && cfg < 36; }
