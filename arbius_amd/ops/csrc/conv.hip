@@ -158,12 +158,14 @@ __device__ __forceinline__ void ln_fold4(const ConvArgs& p, int m, int n, float&
   v3 = rs.y * (v3 - rs.x * w.w);
 }
 
-// Largest row block (a power-of-two fraction of BM, >= 16) whose fp32 staging fits LDSF floats.
-template <int BM, int OROW, int LDSF>
+// Largest row block whose fp32 staging fits LDSF floats: a multiple of 16 (an MFMA fragment block
+// never straddles two row blocks) dividing BM, aligned with the wave rows.  (Halving BM = 192 gave
+// 24-row blocks that cut fragments in two: rows 24..31 were staged past the block and never stored.)
+template <int BM, int WMR, int OROW, int LDSF>
 constexpr int epi_rows() {
-  int r = BM;
-  while (r > 16 && r * OROW > LDSF) r /= 2;
-  return r;
+  for (int r = BM; r >= 16; r -= 16)
+    if (BM % r == 0 && r * OROW <= LDSF && (r % WMR == 0 || WMR % r == 0)) return r;
+  return 16;
 }
 
 // Non-split epilogue through LDS.  The MFMA layout leaves each lane 4 channels of ONE pixel, so
@@ -177,8 +179,9 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&ac
                                              float* stage, int m0, int n0) {
   constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
   constexpr int OROW = BN + 4;           // floats per staged row (16-B pad: spreads the rows' banks)
-  constexpr int PR = epi_rows<BM, OROW, LDSF>();
+  constexpr int PR = epi_rows<BM, BM / WM, OROW, LDSF>();
   static_assert(PR * OROW <= LDSF, "epilogue staging exceeds LDS");
+  static_assert(PR % 16 == 0 && BM % PR == 0, "row blocks hold whole MFMA fragment blocks");
   static_assert(PR % (BM / WM) == 0 || (BM / WM) % PR == 0, "row blocks align with wave rows");
   constexpr int CPR = BN / 8;            // 8-channel chunks per row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
