@@ -117,10 +117,13 @@ class LocalSolverPool:
             free.put(pipe)
 
     def _solve_waiting(self, model, pending: "queue.Queue"):
-        """A stream's turn: this request plus any queued compatible ones, solved lock-step."""
-        from .solver import solve_images, take_group
+        """A stream's turn: this request plus any queued compatible ones, solved lock-step.  A group's
+        pipeline goes back to the pool as soon as its GPU work is done; the PNG + CID tail runs on
+        this thread while the next group already uses the stream."""
+        from .solver import encode_images, infer_images, take_group
         free = self._pipe(model)
         pipe = free.get()
+        batch, imgs, tm = [], None, None
         try:
             try:
                 first = pending.get_nowait()
@@ -128,17 +131,28 @@ class LocalSolverPool:
                 return                      # an earlier turn already took this request in its group
             batch = take_group(pending, first, self.lockstep, lambda r: r[0].kind, lambda r: r[1],
                                lambda r: r[0].name)
-            try:
-                sols = (solve_images(pipe, [r[1] for r in batch]) if len(batch) > 1
-                        else [solve_task(batch[0][0], pipe, batch[0][1])])
+            if len(batch) > 1 and hasattr(pipe, "run_group"):
+                imgs, tm = infer_images(pipe, [r[1] for r in batch])
+            else:
+                sols = [solve_task(r[0], pipe, r[1]) for r in batch]
                 for r, sol in zip(batch, sols):
                     r[2].set_result(sol)
-            except BaseException as e:  # noqa: BLE001
-                for r in batch:
-                    if not r[2].done():
-                        r[2].set_exception(e)
+        except BaseException as e:  # noqa: BLE001
+            for r in batch:
+                if not r[2].done():
+                    r[2].set_exception(e)
+            return
         finally:
             free.put(pipe)
+        if imgs is None:
+            return
+        try:
+            for r, sol in zip(batch, encode_images(imgs, tm)):
+                r[2].set_result(sol)
+        except BaseException as e:  # noqa: BLE001
+            for r in batch:
+                if not r[2].done():
+                    r[2].set_exception(e)
 
     async def solve(self, model, taskid, inp) -> Solution:
         import time

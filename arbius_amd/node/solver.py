@@ -47,24 +47,57 @@ def solve_image(pipe, inp: dict, png_level: int = 6) -> Solution:
     return Solution([("out-1.png", png)], dag.cid_hex, dag, tm)
 
 
+_ENCODE_POOL = None
+
+
+def _encode_pool():
+    """Threads for the per-image PNG + CID work of a group (the native PNG encoder and hashlib
+    release the GIL, so a group's images encode in parallel)."""
+    global _ENCODE_POOL
+    if _ENCODE_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _ENCODE_POOL = ThreadPoolExecutor(max_workers=8, thread_name_prefix="png")
+    return _ENCODE_POOL
+
+
+def infer_images(pipe, inps: List[dict]):
+    """The GPU part of ``solve_images``: k compatible SD-family tasks lock-step (``run_group``) ->
+    (uint8 images, timings).  Returning here lets a task slot hand its pipeline to the next group
+    while ``encode_images`` runs on the CPU."""
+    t0 = time.perf_counter()
+    imgs = pipe.run_group(list(inps))
+    tm = dict(getattr(pipe, "timings", {}))
+    tm.update({"infer_s": time.perf_counter() - t0, "group": len(inps)})
+    return imgs, tm
+
+
+def _one_png(img, png_level):
+    png = encode_png(img, png_level)
+    dag = wrap_directory([("out-1.png", png)])
+    return Solution([("out-1.png", png)], dag.cid_hex, dag, {})
+
+
+def encode_images(imgs, tm: dict, png_level: int = 6) -> List[Solution]:
+    """PNG + wrapped-directory CID of every image of a group, the images in parallel (bytes are
+    independent of the thread that encodes them)."""
+    t1 = time.perf_counter()
+    if len(imgs) > 1:
+        out = list(_encode_pool().map(lambda im: _one_png(im, png_level), imgs))
+    else:
+        out = [_one_png(im, png_level) for im in imgs]
+    tm = dict(tm)
+    tm["encode_cid_s"] = time.perf_counter() - t1
+    for s in out:
+        s.timings = dict(tm)
+    return out
+
+
 def solve_images(pipe, inps: List[dict], png_level: int = 6) -> List[Solution]:
     """k compatible SD-family tasks solved lock-step (``run_group``): same bytes as k solo solves."""
     if len(inps) == 1 or not hasattr(pipe, "run_group"):     # e.g. Kandinsky 2: one at a time
         return [pipe.solve(i) if hasattr(pipe, "solve") else solve_image(pipe, i, png_level) for i in inps]
-    t0 = time.perf_counter()
-    imgs = pipe.run_group(list(inps))
-    t1 = time.perf_counter()
-    out = []
-    for img in imgs:
-        png = encode_png(img, png_level)
-        dag = wrap_directory([("out-1.png", png)])
-        out.append(Solution([("out-1.png", png)], dag.cid_hex, dag, {}))
-    t2 = time.perf_counter()
-    tm = dict(getattr(pipe, "timings", {}))
-    tm.update({"infer_s": t1 - t0, "encode_cid_s": t2 - t1, "group": len(inps)})
-    for s in out:
-        s.timings = dict(tm)
-    return out
+    imgs, tm = infer_images(pipe, inps)
+    return encode_images(imgs, tm, png_level)
 
 
 def group_key(inp: dict):

@@ -60,7 +60,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
 
     from ..models.registry import build_pipeline
     from ..node.models import Model
-    from ..node.solver import solve_images, solve_task, take_group
+    from ..node.solver import encode_images, infer_images, solve_task, take_group
     from . import dist as D
 
     try:
@@ -97,6 +97,20 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
         # `streams` task slots: slot k solves on its own pipeline forks (private HIP stream + graphs)
         slots = [{n: (p if streams == 1 else p.fork()) for n, p in pipes.items()} for _ in range(streams)]
         jobs: "_queue.Queue" = _queue.Queue()
+        from concurrent.futures import ThreadPoolExecutor
+        # per slot: one thread for a lock-step group's PNG + CID tail, so the slot's stream starts
+        # its next group while the previous one encodes
+        tails = [ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"tail{k}") for k in range(streams)]
+
+        def finish(batch, imgs, tm, t0):
+            try:
+                for m, sol in zip(batch, encode_images(imgs, tm)):
+                    sol.dag = None
+                    sol.timings["worker_s"] = time.perf_counter() - t0
+                    out_q.put(("ok", m[0], rank, sol))
+            except Exception:  # noqa: BLE001
+                for m in batch:
+                    out_q.put(("err", m[0], rank, traceback.format_exc()))
 
         def slot_loop(k):
             progress.set_slot(k)
@@ -113,10 +127,11 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                         while True:                 # test hook: a hung kernel - no beats, no result
                             time.sleep(1.0)
                     t0 = time.perf_counter()
-                    if len(batch) == 1:
-                        sols = [solve_task(Model(mid, mname, {}, True, [], kind), slots[k][mname], inp)]
-                    else:
-                        sols = solve_images(slots[k][mname], [m[5] for m in batch])
+                    if len(batch) > 1 and hasattr(slots[k][mname], "run_group"):
+                        imgs, tm = infer_images(slots[k][mname], [m[5] for m in batch])
+                        tails[k].submit(finish, batch, imgs, tm, t0)
+                        continue
+                    sols = [solve_task(Model(m[3], m[1], {}, True, [], m[2]), slots[k][m[1]], m[5]) for m in batch]
                     for m, sol in zip(batch, sols):
                         sol.dag = None  # blocks are recomputed by the pinner; keep the message small
                         sol.timings["worker_s"] = time.perf_counter() - t0
@@ -143,6 +158,8 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
             jobs.put(None)
         for t in threads:
             t.join()
+        for tp in tails:
+            tp.shutdown(wait=True)
     finally:
         # bounded: with a dead peer destroy_process_group can block forever, and a worker that never
         # exits would stall the pool's shutdown (close() joins it)

@@ -141,8 +141,19 @@ def run(args):
     def tid_of(i, j=None):
         return "0x" + keccak256((f"bench-task-{rank}-{i}" + ("" if j is None else f"-{j}")).encode()).hex()
 
-    def one_task(i, pipe=pipe):
-        """Solve this slot's task(s) of step i; every solution gets its own task id's commitment."""
+    def finish_group(t0, tids, imgs, tm):
+        """CPU tail of a lock-step group (PNG + CID of every image, commitments): runs on the slot's
+        tail thread while the slot's stream already solves its next group, as the node's pools do."""
+        from arbius_amd.node.solver import encode_images
+        sols = encode_images(imgs, tm)
+        for tid, sol in zip(tids, sols):
+            generate_commitment(wallet, tid, sol.cid)
+        lat.extend([time.perf_counter() - t0] * len(sols))
+        return sols[-1]
+
+    def one_task(i, pipe=pipe, tail=None):
+        """Solve this slot's task(s) of step i; every solution gets its own task id's commitment.
+        ``tail``: executor for a lock-step group's CPU tail (returns its future)."""
         t0 = time.perf_counter()
         if rvm:
             from arbius_amd.node.solver import solve_files
@@ -165,6 +176,9 @@ def run(args):
             tids = [tid_of(i, j) for j in range(max(1, args.group))]
             inps = [{"prompt": f"a red cat sitting on a castle wall, oil painting, task {i}.{j}",
                      "width": args.res, "height": args.res, "seed": taskid2seed(t)} for j, t in enumerate(tids)]
+            if tail is not None and len(inps) > 1:
+                from arbius_amd.node.solver import infer_images
+                return tail.submit(finish_group, t0, tids, *infer_images(pipe, inps))
             done = list(zip(tids, solve_images(pipe, inps) if len(inps) > 1 else [pipe.solve(inps[0])]))
         else:
             from arbius_amd.node.solver import solve_images
@@ -174,6 +188,9 @@ def run(args):
                      "width": args.res, "height": args.res, "num_inference_steps": args.denoise_steps,
                      "guidance_scale": args.guidance, "scheduler": args.scheduler,
                      "seed": taskid2seed(t)} for j, t in enumerate(tids)]
+            if tail is not None and len(inps) > 1:
+                from arbius_amd.node.solver import infer_images
+                return tail.submit(finish_group, t0, tids, *infer_images(pipe, inps))
             sols = solve_images(pipe, inps) if len(inps) > 1 else [solve_image(pipe, inps[0])]
             done = list(zip(tids, sols))
         for tid, sol in done:
@@ -218,14 +235,21 @@ def run(args):
         # C free-running task slots (as the node's scheduler runs them): each fork solves its K
         # tasks back to back, so one slot's CPU tail (PNG / MP4 encode + CID) overlaps the other
         # slots' GPU work instead of every slot idling the GPU at a per-step join.  Same K x C tasks.
+        # A lock-step group's CPU tail (PNG + CID) runs on the slot's tail thread while the slot's
+        # stream solves its next group; the clock stops only after every tail finished.
+        from concurrent.futures import Future, ThreadPoolExecutor as _TPE
+        tails = [_TPE(max_workers=1) for _ in range(C)]
+
         def run_slot(j):
             r = None
             for i in range(args.steps):
-                r = one_task(i * C + j, forks[j])
+                r = one_task(i * C + j, forks[j], tails[j])
                 progress(f"slot {j} task {i} done")
-            return r
+            return r.result() if isinstance(r, Future) else r
         futs = [ex.submit(run_slot, j) for j in range(C)]
         last = [f.result() for f in futs][-1]
+        for tp in tails:
+            tp.shutdown(wait=True)
     sync()
     D.barrier(dev)
     elapsed = time.perf_counter() - t0
