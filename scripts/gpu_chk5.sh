@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU tests + smoke + SD1.5 bench (driver steps) + node / K2 benches + zeroscope at 1 / 2 task streams.
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-chk5}
+mkdir -p $O
+step() { echo "== $1 $(date +%T)"; }
+SKIP_PROF=1 BENCH_ARGS="--steps 20 --warmup 5" bash scripts/gpu_check.sh ${1:-chk5} || exit 1
+step node
+timeout -k 10 400 python bench.py --node --steps 8 --warmup 2 > $O/node.log 2>$O/node.err || { tail -20 $O/node.err; exit 1; }
+tail -1 $O/node.log | cut -c1-200
+step k2
+timeout -k 10 500 python bench.py --model kandinsky2 --steps 4 > $O/k2.log 2>$O/k2.err || { tail -20 $O/k2.err; exit 1; }
+tail -1 $O/k2.log | cut -c1-200
+for c in 2 1; do
+  step zs_c$c
+  timeout -k 10 500 python bench.py --model zeroscopev2xl --steps 3 --concurrent $c > $O/zs_c$c.log 2>$O/zs_c$c.err || { tail -20 $O/zs_c$c.err; exit 1; }
+  tail -1 $O/zs_c$c.log | cut -c1-200
+done
+step done
