@@ -25,7 +25,7 @@ from .. import ops
 from ..utils.trace import span
 from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
-from .graphs import CAPTURE_LOCK, PipelineBase
+from .graphs import CAPTURE_LOCK, GraphCache, PipelineBase
 from .layers import init_weights
 from .schedulers import GroupSampler, TaskSampler, make_scheduler
 from .tokenizer import CLIPTokenizer
@@ -126,6 +126,9 @@ class SD15Pipeline(PipelineBase):
         self.tokenizer = CLIPTokenizer(tokenizer_dir, self.cfg.text.max_len, self.cfg.text.vocab)
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
         self._graphs: Dict[tuple, _GraphedUNet] = {}
+        # the CLIP text tower as one graph replay per task (~150 small launches eager; same kernels,
+        # same bytes); the graph's output buffer is static, so encode_prompt copies it out
+        self._text_graph = GraphCache(self._text_hidden, self.use_graphs)
         self.timings: Dict[str, float] = {}
 
     def modules(self):
@@ -133,12 +136,18 @@ class SD15Pipeline(PipelineBase):
 
     def _reset_graphs(self):
         self._graphs = {}
+        self._text_graph = GraphCache(self._text_hidden, self.use_graphs)
+
+    def _text_hidden(self, ids):
+        return self.text(ids)[0]
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
     def encode_prompt(self, prompt: str, negative_prompt: str = ""):
         ids = torch.tensor([self.tokenizer(negative_prompt), self.tokenizer(prompt)], dtype=torch.long,
                            device=self.device)
+        if self.use_graphs:
+            return self._text_graph(ids).clone()   # [2, 77, C]: (uncond, cond)
         hidden, _ = self.text(ids)
         return hidden  # [2, 77, C]: (uncond, cond)
 
