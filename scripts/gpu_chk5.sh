@@ -16,4 +16,10 @@ for c in 2 1; do
   timeout -k 10 500 python bench.py --model zeroscopev2xl --steps 3 --concurrent $c > $O/zs_c$c.log 2>$O/zs_c$c.err || { tail -20 $O/zs_c$c.err; exit 1; }
   tail -1 $O/zs_c$c.log | cut -c1-200
 done
+if [ "${PROF:-0}" = "1" ]; then
+  step sd_prof_c2
+  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/p_sd -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 > $O/prof_sd.log 2>&1) || { tail -20 $O/prof_sd.log; exit 1; }
+  python scripts/prof_summary.py $O/p_sd/run_results.db --top 50 --md $O/rocprof_sd15_default.md > /dev/null 2>&1; rm -rf $O/p_sd
+  head -12 $O/rocprof_sd15_default.md | cut -c1-160
+fi
 step done
