@@ -22,4 +22,8 @@ if [ "${PROF:-0}" = "1" ]; then
   python scripts/prof_summary.py $O/p_sd/run_results.db --top 50 --md $O/rocprof_sd15_default.md > /dev/null 2>&1; rm -rf $O/p_sd
   head -12 $O/rocprof_sd15_default.md | cut -c1-160
 fi
+if [ "${PMC:-0}" = "1" ]; then
+  step pmc_eager20
+  STEPS=20 bash scripts/gpu_pmc_bench.sh ${1:-chk5}/pmc || exit 1
+fi
 step done
