@@ -95,12 +95,10 @@ class Kandinsky2Pipeline(PipelineBase):
         self.xlmr_tok = XLMRTokenizer(cfg.xlmr.vocab, cfg.xlmr.max_len, tokenizer_dir)
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
         self._unet = GraphCache(self.unet, self.use_graphs)
-        self._movq_graph = GraphCache(lambda z: self.movq(z)[0], self.use_graphs)   # one image per replay
         self.timings: Dict[str, float] = {}
 
     def _reset_graphs(self):
         self._unet = GraphCache(self.unet, self.use_graphs)
-        self._movq_graph = GraphCache(lambda z: self.movq(z)[0], self.use_graphs)   # one image per replay
 
     def modules(self) -> Dict[str, nn.Module]:
         return {"unet": self.unet, "movq": self.movq, "prior": self.prior, "clip": self.clip,
@@ -256,8 +254,7 @@ class Kandinsky2Pipeline(PipelineBase):
 
     @torch.no_grad()
     def decode(self, latent):
-        lat = latent.to(self.dtype)
-        img = (self._movq_graph(lat) if self.use_graphs else self.movq(lat)[0]).float()
+        img = self.movq(latent.to(self.dtype))[0].float()
         img = ((img + 1.0) * 127.5).clamp(0, 255).round().to(torch.uint8)
         return img.cpu().numpy()
 

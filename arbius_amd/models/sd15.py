@@ -129,7 +129,6 @@ class SD15Pipeline(PipelineBase):
         # the CLIP text tower as one graph replay per task (~150 small launches eager; same kernels,
         # same bytes); the graph's output buffer is static, so encode_prompt copies it out
         self._text_graph = GraphCache(self._text_hidden, self.use_graphs)
-        self._vae_graph = GraphCache(self._vae_image, self.use_graphs)    # one image per replay, as eager
         self.timings: Dict[str, float] = {}
 
     def modules(self):
@@ -138,13 +137,9 @@ class SD15Pipeline(PipelineBase):
     def _reset_graphs(self):
         self._graphs = {}
         self._text_graph = GraphCache(self._text_hidden, self.use_graphs)
-        self._vae_graph = GraphCache(self._vae_image, self.use_graphs)
 
     def _text_hidden(self, ids):
         return self.text(ids)[0]
-
-    def _vae_image(self, z):
-        return self.vae(z)[0]
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -256,6 +251,6 @@ class SD15Pipeline(PipelineBase):
     @torch.no_grad()
     def decode(self, latent):
         z = (latent / self.cfg.vae.scaling_factor).to(self.dtype)
-        img = (self._vae_graph(z) if self.use_graphs else self.vae(z)[0]).float()   # .float(): a copy of the static out
+        img = self.vae(z)[0].float()
         img = ((img / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
         return img.cpu().numpy()  # [H, W, 3]
