@@ -1,10 +1,10 @@
 #!/bin/bash
 # GPU tests + smoke + SD1.5 bench (driver steps) + node / K2 benches + zeroscope at 1 / 2 task streams.
 set -o pipefail
-O=$GRAFT_REPO_ROOT/gpurun_out/${1:-chk5}
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-benches}
 mkdir -p $O
 step() { echo "== $1 $(date +%T)"; }
-SKIP_PROF=1 BENCH_ARGS="--steps 20 --warmup 5" bash scripts/gpu_check.sh ${1:-chk5} || exit 1
+SKIP_PROF=1 BENCH_ARGS="--steps 20 --warmup 5" bash scripts/gpu_check.sh ${1:-benches} || exit 1
 step node
 timeout -k 10 400 python bench.py --node --steps 8 --warmup 2 > $O/node.log 2>$O/node.err || { tail -20 $O/node.err; exit 1; }
 tail -1 $O/node.log | cut -c1-200
@@ -24,6 +24,6 @@ if [ "${PROF:-0}" = "1" ]; then
 fi
 if [ "${PMC:-0}" = "1" ]; then
   step pmc_eager20
-  STEPS=20 bash scripts/gpu_pmc_bench.sh ${1:-chk5}/pmc || exit 1
+  STEPS=20 bash scripts/gpu_pmc_bench.sh ${1:-benches}/pmc || exit 1
 fi
 step done

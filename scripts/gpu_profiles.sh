@@ -4,7 +4,7 @@
 # step; the first failure ends the script.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${1:-prof3}
+O=$R/gpurun_out/${1:-profiles}
 mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)"; }
@@ -26,5 +26,5 @@ step sd_prof_c2
 python scripts/prof_summary.py $O/p_sd/run_results.db --top 50 --md $O/rocprof_sd15_default.md > /dev/null 2>&1; rm -rf $O/p_sd
 head -16 $O/rocprof_sd15_default.md | cut -c1-160
 step pmc
-bash scripts/gpu_pmc_bench.sh ${1:-prof3}/pmc || exit 1
+bash scripts/gpu_pmc_bench.sh ${1:-profiles}/pmc || exit 1
 step done

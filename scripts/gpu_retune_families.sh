@@ -4,7 +4,7 @@
 # zeroscope benches and a graphed PMC pass.  First failure ends the script.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${1:-fam3}
+O=$R/gpurun_out/${1:-retune}
 mkdir -p $O/pmc
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)"; }
