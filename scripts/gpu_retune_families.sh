@@ -1,6 +1,6 @@
 #!/bin/bash
 # Tile tests of the K-half slot tiles, a short lab sweep, then the bitwise-neutral family / plan
-# re-tune with every family (scripts/gpu_fam2.sh steps), rebuild, GPU tests, SD1.5 / node / K2 /
+# re-tune with every family, rebuild, GPU tests, SD1.5 / node / K2 /
 # zeroscope benches and a graphed PMC pass.  First failure ends the script.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
