@@ -1,7 +1,7 @@
 #!/bin/bash
 # Tile tests of the K-half slot tiles, a short lab sweep, then the bitwise-neutral family / plan
 # re-tune with every family, rebuild, GPU tests, SD1.5 / node / K2 /
-# zeroscope benches and a graphed PMC pass.  First failure ends the script.
+# zeroscope benches and a 20-step eager PMC pass.  First failure ends the script.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-retune}
@@ -38,7 +38,6 @@ tail -1 $O/k2.log | cut -c1-200
 step bench_zs
 timeout -k 10 500 python bench.py --model zeroscopev2xl --steps 3 > $O/zs.log 2>$O/zs.err || { tail -20 $O/zs.err; exit 1; }
 tail -1 $O/zs.log | cut -c1-200
-step pmc_graphs
-(cd /tmp && timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmc/raw -o pmc -- python3 $R/bench.py --steps 1 --warmup 1 --denoise-steps 20 > $O/pmc/pmc.log 2>&1) || { tail -20 $O/pmc/pmc.log; exit 1; }
-python scripts/pmc_summary.py $O/pmc/raw --md $O/pmc/pmc_summary.md > /dev/null && head -3 $O/pmc/pmc_summary.md && rm -rf $O/pmc/raw
+step pmc
+STEPS=20 bash scripts/gpu_pmc_bench.sh ${1:-retune}/pmc || exit 1
 step done
