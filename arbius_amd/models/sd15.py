@@ -106,6 +106,21 @@ class _GraphedUNet:
         return self.out
 
 
+# A/B (bitwise-equal paths): ARB_VAE_GRAPH=1 replays the VAE decode as a hipGraph per image
+_VAE_GRAPH = os.environ.get("ARB_VAE_GRAPH", "0") == "1"
+
+
+def _to_host(img):
+    """Device uint8 image -> numpy through a pinned staging buffer: an async copy on the current
+    stream and a wait on that stream only (a pageable ``.cpu()`` copy is a synchronous transfer)."""
+    if not img.is_cuda:
+        return img.numpy()
+    host = torch.empty(img.shape, dtype=img.dtype, pin_memory=True)
+    host.copy_(img, non_blocking=True)
+    torch.cuda.current_stream(img.device).synchronize()
+    return host.numpy()
+
+
 class SD15Pipeline(PipelineBase):
     def __init__(self, cfg: SD15Config = None, device="cpu", dtype=None, weight_seed: int = 0,
                  use_graphs: Optional[bool] = None, tokenizer_dir: Optional[str] = None, init=True):
@@ -129,6 +144,7 @@ class SD15Pipeline(PipelineBase):
         # the CLIP text tower as one graph replay per task (~150 small launches eager; same kernels,
         # same bytes); the graph's output buffer is static, so encode_prompt copies it out
         self._text_graph = GraphCache(self._text_hidden, self.use_graphs)
+        self._vae_graph = GraphCache(self._vae_image, self.use_graphs)
         self.timings: Dict[str, float] = {}
 
     def modules(self):
@@ -137,9 +153,13 @@ class SD15Pipeline(PipelineBase):
     def _reset_graphs(self):
         self._graphs = {}
         self._text_graph = GraphCache(self._text_hidden, self.use_graphs)
+        self._vae_graph = GraphCache(self._vae_image, self.use_graphs)
 
     def _text_hidden(self, ids):
         return self.text(ids)[0]
+
+    def _vae_image(self, z):
+        return self.vae(z)[0]
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -251,6 +271,9 @@ class SD15Pipeline(PipelineBase):
     @torch.no_grad()
     def decode(self, latent):
         z = (latent / self.cfg.vae.scaling_factor).to(self.dtype)
-        img = self.vae(z)[0].float()
+        if self.use_graphs and _VAE_GRAPH:
+            img = self._vae_graph(z).float()      # .float(): a copy out of the graph's static output
+        else:
+            img = self.vae(z)[0].float()
         img = ((img / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
-        return img.cpu().numpy()  # [H, W, 3]
+        return _to_host(img)  # [H, W, 3]
