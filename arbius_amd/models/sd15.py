@@ -106,15 +106,18 @@ class _GraphedUNet:
         return self.out
 
 
-# A/B (bitwise-equal paths): ARB_VAE_GRAPH=1 replays the VAE decode as a hipGraph per image
+# A/B switches (bitwise-equal paths): ARB_VAE_GRAPH=1 replays the VAE decode as a hipGraph per
+# image (measured: the 2-stream bench fell from 26.4k to 19.0k tasks/h with it); ARB_PINNED_D2H=1
+# copies the image to the host through a pinned buffer instead of a pageable ``.cpu()``
 _VAE_GRAPH = os.environ.get("ARB_VAE_GRAPH", "0") == "1"
+_PINNED_D2H = os.environ.get("ARB_PINNED_D2H", "0") == "1"
 
 
 def _to_host(img):
-    """Device uint8 image -> numpy through a pinned staging buffer: an async copy on the current
-    stream and a wait on that stream only (a pageable ``.cpu()`` copy is a synchronous transfer)."""
-    if not img.is_cuda:
-        return img.numpy()
+    """Device uint8 image -> numpy (pinned staging buffer, async copy and a wait on the current
+    stream only, with ARB_PINNED_D2H=1)."""
+    if not img.is_cuda or not _PINNED_D2H:
+        return img.cpu().numpy()
     host = torch.empty(img.shape, dtype=img.dtype, pin_memory=True)
     host.copy_(img, non_blocking=True)
     torch.cuda.current_stream(img.device).synchronize()
