@@ -19,6 +19,7 @@ weights); byte-parity with the kasumi-1 container is "parity unpinned".
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -69,6 +70,10 @@ class _Buffers(nn.Module):
         self.zero_img_emb.data.normal_(0.0, 0.5, generator=gen)
 
 
+# A/B switch (bitwise-equal paths): ARB_PRIOR_GRAPH=1 replays each diffusion-prior step as a hipGraph
+_PRIOR_GRAPH = os.environ.get("ARB_PRIOR_GRAPH", "0") == "1"
+
+
 class Kandinsky2Pipeline(PipelineBase):
     def __init__(self, cfg: Kandinsky2Config = None, device="cpu", dtype=None, weight_seed: int = 0,
                  use_graphs: Optional[bool] = None, tokenizer_dir: Optional[str] = None, init=True):
@@ -95,10 +100,15 @@ class Kandinsky2Pipeline(PipelineBase):
         self.xlmr_tok = XLMRTokenizer(cfg.xlmr.vocab, cfg.xlmr.max_len, tokenizer_dir)
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
         self._unet = GraphCache(self.unet, self.use_graphs)
+        self._prior_graph = GraphCache(self._prior_step, self.use_graphs)
         self.timings: Dict[str, float] = {}
+
+    def _prior_step(self, xin, tt, hidden, pooled, idx, q):
+        return self.prior(xin, None, hidden, pooled, None, (idx, q), tt=tt)
 
     def _reset_graphs(self):
         self._unet = GraphCache(self.unet, self.use_graphs)
+        self._prior_graph = GraphCache(self._prior_step, self.use_graphs)
 
     def modules(self) -> Dict[str, nn.Module]:
         return {"unet": self.unet, "movq": self.movq, "prior": self.prior, "clip": self.clip,
@@ -166,7 +176,11 @@ class Kandinsky2Pipeline(PipelineBase):
         for i, t in enumerate(sched.timesteps):
             beat()
             with ops.plan_batch(2):
-                out = self.prior(xin, t, hidden, pooled, lens, layout).contiguous()
+                if self.use_graphs and _PRIOR_GRAPH:
+                    tbuf = torch.full((1,), float(t), dtype=torch.float32, device=self.device)
+                    out = self._prior_graph(xin, tbuf, hidden, pooled, layout[0], layout[1]).contiguous()
+                else:
+                    out = self.prior(xin, t, hidden, pooled, lens, layout).contiguous()
             samp.step(i, out)
         std, mean = self._prior_stats()
         return torch.stack([(ts.x.view(d) * std + mean) for ts in tasks]).to(self.dtype)

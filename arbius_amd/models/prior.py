@@ -97,13 +97,15 @@ class PriorTransformer(nn.Module):
         idx = torch.where(j < n, j, torch.where(j < n + 4, ctx + (j - n), torch.full_like(j, L)))
         return idx, (n[:, 0] + 3)
 
-    def forward(self, x_t, t, text_states, text_pooled, ns, layout=None):
+    def forward(self, x_t, t, text_states, text_pooled, ns, layout=None, tt=None):
         """x_t [B,d] (normalised), t scalar, text_states [B,77,d], text_pooled [B,d], ns[b] = real
-        text tokens of row b -> predicted x_0 [B,d].  ``layout``: a cached ``self.layout(ns)``."""
+        text tokens of row b -> predicted x_0 [B,d].  ``layout``: a cached ``self.layout(ns)``;
+        ``tt``: the timestep as a device tensor [1] fp32 instead of ``t`` (hipGraph replay)."""
         w = self.cfg.width
         B = x_t.shape[0]
         idx, q = layout if layout is not None else self.layout(ns, x_t.device)
-        tt = torch.tensor([float(t)], device=x_t.device)
+        if tt is None:
+            tt = torch.tensor([float(t)], device=x_t.device)
         temb = self.time2(ops.silu(self.time1(timestep_embedding(tt, w).to(x_t.dtype))))
         src = torch.cat([self.text_enc_proj(text_states), self.text_emb_proj(text_pooled)[:, None],
                          temb[:, None].expand(B, 1, w), self.img_proj(x_t)[:, None],

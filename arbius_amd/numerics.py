@@ -24,7 +24,7 @@ NUMERICS_ENV_KNOBS = (
     "ARBIUS_PLAN_CANON", "ARB_CONV_PLANS", "ARB_GN_GROUP", "ARBIUS_NORM_PROLOGUE", "ARBIUS_KERNEL_LIB",
     "ARBIUS_EXPERIMENT_SKIP", "ARBIUS_REFERENCE_OPS", "ARB_ATTN_GLDS", "ARB_ATTN_QT", "ARB_LN_ROWS",
     "ARB_SPLITK_INLAUNCH", "ARBIUS_GEGLU_FUSED", "ARBIUS_CROSS_KV_HOIST", "ARBIUS_FAULT_INJECTION",
-    "ARBIUS_SAMPLER_REF", "ARB_GN_TABLE_LDS", "ARB_VAE_GRAPH", "ARB_PINNED_D2H",
+    "ARBIUS_SAMPLER_REF", "ARB_GN_TABLE_LDS", "ARB_VAE_GRAPH", "ARB_PINNED_D2H", "ARB_PRIOR_GRAPH",
 )
 
 
