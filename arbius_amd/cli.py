@@ -67,12 +67,13 @@ def build_pool(cfg, models):
         return ReplicateSolverPool(cfg.ml.replicate.api_token)
     import torch
     names = sorted({m.name for m in models.values()})
+    # device_count() does not initialise HIP: the dispatcher process stays GPU-free
     n = cfg.mi355x.gpus if cfg.mi355x.gpus is not None else torch.cuda.device_count()
-    if n > 1:
+    if n > 1 or (n == 1 and cfg.mi355x.worker_processes):
         from .parallel.workers import MultiGPUSolverPool
         return MultiGPUSolverPool(n, names, "cuda", streams_per_gpu=cfg.mi355x.workers_per_gpu,
                                   lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir,
-                                  hang_timeout=cfg.mi355x.hang_timeout_s)
+                                  hang_timeout=cfg.mi355x.hang_timeout_s, force_group=n == 1)
     from .node.pool import LocalSolverPool
     return LocalSolverPool("cuda:0" if n == 1 else "cpu", capacity=cfg.mi355x.workers_per_gpu,
                            lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir)

@@ -82,6 +82,9 @@ class MI355XConfig(_Base):
     model_ids: Dict[str, str] = Field(default_factory=dict)  # template name -> on-chain model id
     weights_dir: Optional[str] = None     # safetensors (+ tokenizer files); None = random-init (benchmark only)
     hang_timeout_s: float = 300.0         # kill a GPU worker whose busy slot has not progressed this long
+    # one worker PROCESS per GPU even on a one-GPU node (the multi-GPU pool: watchdog respawn, a
+    # one-rank RCCL communicator carrying the weight broadcast); default: in-process pool at 1 GPU
+    worker_processes: bool = False
     # models.ts:185-194 quirks Q2/Q3 (decimal must be integral, max never enforced).  ON by default:
     # validity decides contestations, so this node must judge inputs as the deployed miners do
     reference_hydration_quirks: bool = True

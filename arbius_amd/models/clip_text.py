@@ -59,11 +59,7 @@ class CLIPLayer(nn.Module):
         qkv = self.ln1.linear(x, self.qkv).view(B, N, 3, H, C // H)   # LayerNorm folded into QKV
         o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
         x = self.out(o.reshape(B, N, C), residual=x)
-        h = self.ln2.linear(x, self.fc1)
-        if self.quick:
-            h = h * torch.sigmoid(1.702 * h)
-        else:
-            h = torch.nn.functional.gelu(h)
+        h = self.ln2.linear(x, self.fc1, act="quick_gelu" if self.quick else "gelu")   # LN + act in the GEMM
         return self.fc2(h, residual=x)
 
 

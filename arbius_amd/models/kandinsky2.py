@@ -101,6 +101,8 @@ class Kandinsky2Pipeline(PipelineBase):
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else use_graphs
         self._unet = GraphCache(self.unet, self.use_graphs)
         self._prior_graph = GraphCache(self._prior_step, self.use_graphs)
+        # A/B switch (bitwise-equal paths, tests/test_models_gpu.py): replay each prior step as a hipGraph
+        self.prior_graph = _PRIOR_GRAPH
         self.timings: Dict[str, float] = {}
 
     def _prior_step(self, xin, tt, hidden, pooled, idx, q):
@@ -176,7 +178,7 @@ class Kandinsky2Pipeline(PipelineBase):
         for i, t in enumerate(sched.timesteps):
             beat()
             with ops.plan_batch(2):
-                if self.use_graphs and _PRIOR_GRAPH:
+                if self.use_graphs and self.prior_graph:
                     tbuf = torch.full((1,), float(t), dtype=torch.float32, device=self.device)
                     out = self._prior_graph(xin, tbuf, hidden, pooled, layout[0], layout[1]).contiguous()
                 else:
@@ -222,8 +224,15 @@ class Kandinsky2Pipeline(PipelineBase):
             raise ValueError(f"run_group needs one resolution, got {sorted(sizes)}")
         width, height = sizes.pop()
         st = [self.settings(i) for i in inps]
-        if len({(s["steps"], s["scheduler"]) for s in st}) != 1:
-            raise ValueError("run_group needs one step count and scheduler")
+        kinds = sorted({(s["steps"], s["scheduler"]) for s in st})
+        if len(kinds) != 1:
+            # tasks that cannot share decoder launches run as separate lock-step groups (same bytes)
+            out = [None] * len(inps)
+            for kd in kinds:
+                sel = [j for j, s in enumerate(st) if (s["steps"], s["scheduler"]) == kd]
+                for j, im in zip(sel, self.run_group([inps[j] for j in sel])):
+                    out[j] = im
+            return out
         cfg = self.cfg
         with self._stream_ctx():
             sync = self._sync

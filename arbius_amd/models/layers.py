@@ -32,8 +32,8 @@ class Linear(nn.Module):
         if self.bias is not None:
             self.bias.data.uniform_(-bound, bound, generator=gen)
 
-    def forward(self, x, residual=None):
-        return ops.linear(x, self.weight, self.bias, residual=residual)
+    def forward(self, x, residual=None, act=None):
+        return ops.linear(x, self.weight, self.bias, residual=residual, act=act)
 
     def forward_norm(self, x, norm):
         """x [B, ..., Cin] with a GroupNorm(+SiLU) prologue from ``norm = (table, silu)`` (table per
@@ -102,9 +102,9 @@ class LayerNorm(nn.Module):
     def forward(self, x):
         return ops.layer_norm(x, self.weight, self.bias, self.eps)
 
-    def linear(self, x, lin: "Linear", residual=None):
-        """lin(self(x)) with this LayerNorm folded into the GEMM (ops.ln_linear)."""
-        return ops.ln_linear(x, self.weight, self.bias, self.eps, lin.weight, lin.bias, residual=residual)
+    def linear(self, x, lin: "Linear", residual=None, act=None):
+        """act(lin(self(x))) with this LayerNorm (and the activation) folded into the GEMM (ops.ln_linear)."""
+        return ops.ln_linear(x, self.weight, self.bias, self.eps, lin.weight, lin.bias, residual=residual, act=act)
 
     def linear_geglu(self, x, lin: "Linear"):
         """GEGLU projection of self(x) with this LayerNorm folded in (ops.ln_linear_geglu)."""

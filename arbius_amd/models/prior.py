@@ -60,7 +60,7 @@ class PriorBlock(nn.Module):
         qkv = self.ln1.linear(x, self.qkv).view(B, N, 3, H, C // H)   # LayerNorm folded into QKV
         o = ops.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
         x = self.out(o.reshape(B, N, C), residual=x)
-        return self.fc2(torch.nn.functional.gelu(self.ln2.linear(x, self.fc1)), residual=x)
+        return self.fc2(self.ln2.linear(x, self.fc1, act="gelu"), residual=x)     # GELU in the GEMM epilogue
 
 
 class PriorTransformer(nn.Module):

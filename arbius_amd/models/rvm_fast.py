@@ -71,6 +71,7 @@ class FastMatting:
         b = torch.zeros(cop, dtype=self.dtype, device=conv.weight.device)
         if conv.bias is not None:
             b[:co] = conv.bias.detach().to(self.dtype)
+        ops.derived_ready(w)
         self._w[id(conv)] = (conv.weight, conv.weight._version, w, b)
         return w, b
 

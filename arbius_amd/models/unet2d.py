@@ -269,6 +269,7 @@ class UNet2DCondition(nn.Module):
         if self._temb_cache is None or self._temb_cache[0] != key:
             w = torch.cat([r.temb_proj.weight for r in rbs], dim=0)
             b = torch.cat([r.temb_proj.bias for r in rbs], dim=0)
+            ops.derived_ready(w)
             self._temb_cache = (key, w, b, [r.cout for r in rbs])
         return self._temb_cache[1:]
 

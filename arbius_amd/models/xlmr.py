@@ -108,7 +108,7 @@ class XLMRLayer(nn.Module):
                     for b in rows:
                         o[b:b + 1] = ops.attention(qkv[b:b + 1, :, 0], qkv[b:b + 1, :n, 1], qkv[b:b + 1, :n, 2])
         x = self.ln1(self.out(o.reshape(B, N, C), residual=x))
-        h = torch.nn.functional.gelu(self.fc1(x))
+        h = self.fc1(x, act="gelu")                                 # GELU in the GEMM epilogue
         return self.ln2(self.fc2(h, residual=x))
 
 

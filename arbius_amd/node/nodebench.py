@@ -89,10 +89,11 @@ async def _run(args, device: str) -> dict:
     cfg = MiningConfig.from_dict({"db_path": ":memory:", "mi355x": {
         "selftest": False, "workers_per_gpu": C, "lockstep_group": G, "poll_interval_ms": 2}})
     t_init = time.perf_counter()
-    if args.gpus > 1:
+    if args.gpus > 1 or getattr(args, "rccl_group", False):
         from ..parallel.workers import MultiGPUSolverPool
         pool = MultiGPUSolverPool(args.gpus, [model], "cuda" if device.startswith("cuda") else "cpu",
-                                  tiny=args.tiny, streams_per_gpu=C, lockstep=G, weights_dir=args.weights_dir)
+                                  tiny=args.tiny, streams_per_gpu=C, lockstep=G, weights_dir=args.weights_dir,
+                                  force_group=getattr(args, "rccl_group", False))
     else:
         from .pool import LocalSolverPool
         pool = LocalSolverPool(device, capacity=C, lockstep=G, tiny=args.tiny, weights_dir=args.weights_dir)

@@ -100,10 +100,20 @@ def solve_images(pipe, inps: List[dict], png_level: int = 6) -> List[Solution]:
     return encode_images(imgs, tm, png_level)
 
 
-def group_key(inp: dict):
-    """Tasks with equal keys can share lock-step launches (SD-family image templates)."""
-    return (int(inp.get("width", 768)), int(inp.get("height", 768)), int(inp.get("num_inference_steps", 20)),
-            inp.get("scheduler", "DPMSolverMultistep"))
+# Per-family defaults of the lock-step key fields (what each pipeline's ``run_group`` fills in for a
+# missing input): SD-family templates (anythingv3) vs the Kandinsky 2 container's hidden defaults.
+_GROUP_DEFAULTS = {"kandinsky2": (768, 768, 100, "p_sampler")}
+_SD_DEFAULTS = (768, 768, 20, "DPMSolverMultistep")
+
+
+def group_key(inp: dict, model: str = None):
+    """Tasks with equal keys can share lock-step launches (image templates): resolution, step count
+    and scheduler, missing fields filled with the MODEL FAMILY's defaults - a Kandinsky2 task without
+    ``num_inference_steps`` runs 100 steps, not the SD default 20, so it must not join a group of
+    explicit 20-step tasks."""
+    w, h, n, sch = _GROUP_DEFAULTS.get(model, _SD_DEFAULTS)
+    return (int(inp.get("width", w)), int(inp.get("height", h)), int(inp.get("num_inference_steps", n)),
+            str(inp.get("scheduler", sch)))
 
 
 def take_group(jobs, first, lockstep: int, kind_of, inp_of, model_of):
@@ -114,14 +124,14 @@ def take_group(jobs, first, lockstep: int, kind_of, inp_of, model_of):
     if lockstep <= 1 or kind_of(first) != "image":
         return batch
     import queue as _q
-    key = (model_of(first), group_key(inp_of(first)))
+    key = (model_of(first), group_key(inp_of(first), model_of(first)))
     back = []
     while len(batch) < lockstep:
         try:
             m = jobs.get_nowait()
         except _q.Empty:
             break
-        if m is not None and kind_of(m) == "image" and (model_of(m), group_key(inp_of(m))) == key:
+        if m is not None and kind_of(m) == "image" and (model_of(m), group_key(inp_of(m), model_of(m))) == key:
             batch.append(m)
         else:
             back.append(m)

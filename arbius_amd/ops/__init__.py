@@ -105,9 +105,32 @@ def _hip(t: torch.Tensor) -> bool:
     return t.is_cuda and not _FORCE_REF
 
 
+# ------------------------------------------------------------------ derived-weight caches
+def derived_ready(t) -> None:
+    """Call before publishing a derived-weight cache entry (LN fold, GEGLU interleave, padded conv
+    weights, ...) computed from ``t``'s device on the calling thread's stream.  Pipeline forks share
+    these caches across threads and HIP streams; nothing would order another stream's first consumer
+    after the producing kernels, so the entry is published only once they have finished.  A miss
+    inside a hipGraph capture is refused: the tensors would be written only when the graph replays
+    (every graph warms its ops eagerly before capturing)."""
+    if t is None or not t.is_cuda:
+        return
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("derived-weight cache miss inside a hipGraph capture (warm the op eagerly first)")
+    torch.cuda.current_stream(t.device).synchronize()
+
+
 # --------------------------------------------------------------------------- GEMM / conv
-def linear(x, w, b=None, residual=None):
-    """y = x @ w^T + b (+ residual).
+def _act_ref(y, act):
+    if act == "gelu":
+        return F.gelu(y)
+    if act == "quick_gelu":
+        return y * torch.sigmoid(1.702 * y)
+    return y
+
+
+def linear(x, w, b=None, residual=None, act=None):
+    """y = act(x @ w^T + b (+ residual)), act None / "gelu" / "quick_gelu" (fused into the GPU epilogue).
 
     GPU: every linear whose K % 64 == 0 and N % 8 == 0 runs on the implicit-GEMM kernel (bias and
     residual fused into its epilogue, pinned plans - so a task's bytes never depend on which
@@ -115,7 +138,9 @@ def linear(x, w, b=None, residual=None):
     stream-K kernels spin on other workgroups of their own launch, and two of them replayed
     concurrently on the two task streams of a GPU deadlocked (zeroscope, 2 streams)."""
     if _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]):
-        return _lib.gemm(x, w, b, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
+        return _lib.gemm(x, w, b, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])), act=act)
+    if act is not None:
+        return _act_ref(linear(x, w, b, residual), act)
     if residual is not None:
         x2 = x.reshape(-1, x.shape[-1])
         r2 = residual.reshape(-1, w.shape[0])
@@ -144,6 +169,7 @@ def linear_geglu(x, w, b=None):
             wi = _lib.interleave_geglu(w.detach())
             bi = _lib.interleave_geglu(b.detach()) if b is not None else None
             ent = (weakref.ref(w), weakref.ref(b) if b is not None else (lambda: None), wi, bi, stamp)
+            derived_ready(wi)
             _GEGLU_W[id(w)] = ent
         return _lib.gemm_geglu(x, ent[2], ent[3], plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
     return geglu(linear(x, w, b))
@@ -175,6 +201,7 @@ def ln_fold(gamma, beta, w, b, geglu=False):
             wf, bf = _lib.interleave_geglu(wf), _lib.interleave_geglu(bf)
             wsum = _lib.interleave_geglu(wsum)
         out = (wf.contiguous(), bf.contiguous(), wsum.contiguous())
+    derived_ready(out[0])
     _LN_FOLD[key] = (weakref.ref(gamma), weakref.ref(w), stamp, out)
     return out
 
@@ -193,14 +220,15 @@ def _ln_fold_ok(x, w, geglu):
             and (not geglu or w.shape[0] % 16 == 0) and "lnfold" not in _EXP_SKIP)
 
 
-def ln_linear(x, gamma, beta, eps, w, b=None, residual=None):
-    """linear(LayerNorm(x)) - on the GPU the LayerNorm is folded into the GEMM's epilogue (one
-    row-stats pass over x, no normalised tensor in HBM)."""
+def ln_linear(x, gamma, beta, eps, w, b=None, residual=None, act=None):
+    """act(linear(LayerNorm(x))) - on the GPU the LayerNorm is folded into the GEMM's epilogue (one
+    row-stats pass over x, no normalised tensor in HBM), the activation too."""
     if _ln_fold_ok(x, w, False):
         wf, bf, wsum = ln_fold(gamma, beta, w, b)
         rs = _lib.row_stats(x, eps, _plan_rows(x))
-        return _lib.gemm_ln(x, wf, bf, wsum, rs, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))
-    return linear(layer_norm(x, gamma, beta, eps), w, b, residual)
+        return _lib.gemm_ln(x, wf, bf, wsum, rs, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])),
+                            act=act)
+    return linear(layer_norm(x, gamma, beta, eps), w, b, residual, act=act)
 
 
 def ln_linear_geglu(x, gamma, beta, eps, w, b=None):
@@ -355,6 +383,7 @@ def _padded_weights(w, b):
     if b is not None:
         bp = torch.zeros(co, dtype=b.dtype, device=b.device)
         bp[:cout] = b
+    derived_ready(wp)
     _PAD_W[key] = (weakref.ref(owner(w)), None if b is None else weakref.ref(owner(b)), wp, bp)
     return wp, bp
 
@@ -390,6 +419,7 @@ def depthwise_conv(x, weight, bias, stride=1, dilation=1, act=None):
         ent = _DW_W.get(id(weight))
         if ent is None or ent[0]() is not weight or ent[1] != stamp:
             ent = (weakref.ref(weight), stamp, weight.detach().reshape(C, k * k).t().contiguous())
+            derived_ready(ent[2])
             _DW_W[id(weight)] = ent
         return _lib.dwconv_f16(x, ent[2], bias, k, stride, dilation, act)
     y = F.conv2d(x, weight, bias, stride=stride, padding=dilation * (k // 2), dilation=dilation, groups=C)

@@ -67,7 +67,8 @@ _SIGS = {
     "arb_rvm_args_sizes": (c_size_t, [c_int]),
     "arb_rvm_chan_mean": (c_int, [c_void_p, c_void_p, c_int, c_long, c_int, c_void_p]),
     "arb_rvm_gate": (c_int, [c_void_p, c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
-    "arb_gemm_ln": (c_int, [c_void_p] * 8 + [c_int] * 6 + [c_void_p]),
+    "arb_gemm_ln": (c_int, [c_void_p] * 8 + [c_int] * 7 + [c_void_p]),
+    "arb_gemm_act": (c_int, [c_void_p] * 6 + [c_int] * 6 + [c_void_p]),
 }
 
 
@@ -384,6 +385,49 @@ def conv_plan(B, H, W, Cin, Cout, k, pad, upsample, stride):
     return out[0], out[1]
 
 
+def conv_choice(B, H, W, Cin, Cout, kcode, pad, upsample, stride, plan_b):
+    """(cfg, split) a planned conv launch runs: the canonical batch's plan at its split-K on the tile
+    family tuned for the actual shape (what ``conv2d_nhwc`` does; -1, -1 = the library's own plan)."""
+    if not plan_b:
+        return -1, -1
+    kh, kw = (3, 1) if kcode == 31 else (kcode, kcode)
+    Hl, Wl = (2 * H, 2 * W) if upsample else (H, W)
+    Ho = (Hl + 2 * pad - kh) // stride + 1
+    Wo = (Wl + 2 * (0 if kcode == 31 else pad) - kw) // stride + 1
+    cfg, split = conv_plan(plan_b, H, W, Cin, Cout, kcode, pad, upsample, stride)
+    ratio = plan_b // B if plan_b % B == 0 else 0
+    return _fn("arb_conv_family")(B * Ho * Wo, Cout, kh * kw * Cin, split, ratio, cfg), split
+
+
+def gemm_choice(M, N, K, plan_batch):
+    """(cfg, split) of a planned GEMM launch of M rows (see ``gemm``)."""
+    if not (plan_batch and plan_batch[1]):
+        return -1, -1
+    cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
+    return _fn("arb_conv_family")(M, N, K, split, plan_batch[1] // plan_batch[0], cfg), split
+
+
+# tile configs by id (csrc/conv.hip conv_run): kernel template the launch runs
+_CFG4 = ["128x128", "64x128", "128x64", "64x64", "160x64", "160x128", "320x32", "256x64", "128x256", "64x256"]
+_CFG_NAMES = {20: "glds<256,256>", 21: "glds<320,128>", 22: "glds<256,128>", 23: "glds<320,192>",
+              24: "persist<128,128>", 25: "persist<256,128>", 26: "persist<160,128>", 27: "persist<128,64>",
+              28: "glds3<128,256>", 29: "glds3<256,128>", 30: "glds3<192,192>", 31: "glds3<320,64>",
+              32: "xreg<160,8,2>", 33: "xreg<128,8,2>", 34: "xreg<160,8,1>", 35: "xreg<256,8,1>",
+              36: "stag<256,128>", 37: "stag<128,256>", 38: "stag<192,192>", 39: "stag<320,64>",
+              40: "stag<160,256>", 41: "stag<160,128>", 42: "stag2<320,128>", 43: "stag2<256,256>",
+              44: "stag2<256,192>"}
+
+
+def cfg_name(cfg: int) -> str:
+    if cfg < 0:
+        return "?"
+    if cfg < 10:
+        return "glds4w<%s>" % _CFG4[cfg]
+    if cfg < 20:
+        return "igemm<%s>" % _CFG4[cfg - 10]
+    return _CFG_NAMES.get(cfg, f"cfg{cfg}")
+
+
 def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0, x2=None):
     """GroupNorm of x [B, *, C] as a per-(batch, channel) affine table [B, C, 2] fp32
     (scale, shift) for a consumer prologue; ``mod`` [B, 2C] folds a scale-shift modulation.
@@ -471,11 +515,9 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
         if norm.dtype != torch.float32 or tuple(norm.shape) != (B, Cin, 2) or not norm.is_contiguous():
             raise ValueError("conv2d norm table must be contiguous fp32 [B, Cin, 2]")
     kcode = 31 if temporal else kh
-    if plan_b and cfg < 0:   # batch-invariant: the canonical batch's plan
-        cfg, split = conv_plan(plan_b, H, W, Cin, Cout, kcode, padding, upsample, stride)
-        # ... at its split-K, on the tile family tuned for the actual shape (bitwise-neutral)
-        ratio = plan_b // B if plan_b % B == 0 else 0
-        cfg = _fn("arb_conv_family")(B * Ho * Wo, Cout, kh * kw * Cin, split, ratio, cfg)
+    if plan_b and cfg < 0:   # batch-invariant: the canonical batch's plan at its split-K, on the tile
+        # family tuned for the actual shape (bitwise-neutral)
+        cfg, split = conv_choice(B, H, W, Cin, Cout, kcode, padding, upsample, stride, plan_b)
     args = (B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride, int(cfg), int(split))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
@@ -496,9 +538,13 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     return y
 
 
-def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None):
+ACTS = {None: 0, "gelu": 3, "quick_gelu": 4}
+
+
+def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None, act=None):
     """out = x @ w^T (+ b + residual) on the implicit-GEMM kernel. x [...,K], w [N,K].
-    plan_batch = (batch, canonical batch): plan for M * canonical / batch rows (batch-invariant)."""
+    plan_batch = (batch, canonical batch): plan for M * canonical / batch rows (batch-invariant).
+    ``act``: "gelu" / "quick_gelu" applied in the epilogue (conv.hip act_f)."""
     _bf16(x, w, b, residual)
     K = x.shape[-1]
     N = w.shape[0]
@@ -507,12 +553,15 @@ def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None):
     if K % 64 or N % 8 or w.shape[1] != K:
         raise ValueError(f"gemm: unsupported K={K} N={N}")
     if plan_batch and plan_batch[1] and cfg < 0:
-        cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
-        cfg = _fn("arb_conv_family")(M, N, K, split, plan_batch[1] // plan_batch[0], cfg)
+        cfg, split = gemm_choice(M, N, K, plan_batch)
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
+    if act is not None:
+        _check(_fn("arb_gemm_act")(_p(x2), _p(w.contiguous()), _p(b), _p(r2), _p(y), _p(ws), M, N, K, int(cfg),
+                                   int(split), ACTS[act], _stream()), "gemm_act")
+        return y.reshape(*x.shape[:-1], N)
     _check(_fn("arb_gemm_bias_res")(_p(x2), _p(w.contiguous()), _p(b), _p(r2), _p(y), _p(ws), M, N, K, int(cfg),
                                     int(split), _stream()), "gemm")
     return y.reshape(*x.shape[:-1], N)
@@ -530,8 +579,7 @@ def gemm_geglu(x, w_il, b_il=None, cfg=-1, split=-1, plan_batch=None):
     if K % 64 or N % 16 or w_il.shape[1] != K:
         raise ValueError(f"gemm_geglu: unsupported K={K} N={N}")
     if plan_batch and plan_batch[1] and cfg < 0:
-        cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
-        cfg = _fn("arb_conv_family")(M, N, K, split, plan_batch[1] // plan_batch[0], cfg)
+        cfg, split = gemm_choice(M, N, K, plan_batch)
     y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
@@ -555,7 +603,7 @@ def row_stats(x, eps, plan_rows=None):
     return rs
 
 
-def gemm_ln(x, w, b, wsum, rs, residual=None, geglu=False, cfg=-1, split=-1, plan_batch=None):
+def gemm_ln(x, w, b, wsum, rs, residual=None, geglu=False, cfg=-1, split=-1, plan_batch=None, act=None):
     """LayerNorm folded into a GEMM: x is the LN INPUT, ``w`` / ``b`` / ``wsum`` from ``ops.ln_fold``,
     ``rs`` = ``row_stats(x)``.  out = rstd (x w^T - mean wsum) + b (+ residual | GEGLU, out N/2)."""
     _bf16(x, w, b, residual)
@@ -568,14 +616,13 @@ def gemm_ln(x, w, b, wsum, rs, residual=None, geglu=False, cfg=-1, split=-1, pla
     if rs.dtype != torch.float32 or wsum.dtype != torch.float32 or not rs.is_contiguous() or not wsum.is_contiguous():
         raise ValueError("gemm_ln: row stats / wsum must be contiguous fp32")
     if plan_batch and plan_batch[1] and cfg < 0:
-        cfg, split = conv_plan(1, 1, M * plan_batch[1] // plan_batch[0], K, N, 1, 0, 0, 1)
-        cfg = _fn("arb_conv_family")(M, N, K, split, plan_batch[1] // plan_batch[0], cfg)
+        cfg, split = gemm_choice(M, N, K, plan_batch)
     y = torch.empty(M, N // 2 if geglu else N, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
     _check(_fn("arb_gemm_ln")(_p(x2), _p(w.contiguous()), _p(b), _p(r2), _p(y), _p(ws), _p(rs), _p(wsum), M, N, K,
-                              int(cfg), int(split), int(bool(geglu)), _stream()), "gemm_ln")
+                              int(cfg), int(split), int(bool(geglu)), ACTS[act], _stream()), "gemm_ln")
     return y.reshape(*x.shape[:-1], y.shape[-1])
 
 

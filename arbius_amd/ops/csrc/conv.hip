@@ -134,9 +134,20 @@ __device__ __forceinline__ void tile_coords(const ConvArgs& p, int BN, int BM, i
   }
 }
 
+__device__ __forceinline__ float bf16_round(float v) { return __uint_as_float((uint32_t)f2bf(v) << 16); }
+
+// Epilogue activation (after bias / temb / residual): 1 ReLU, 2 hardswish (RVM, either dtype);
+// 3 GELU(erf) and 4 quick-GELU x * sigmoid(1.702 x) (text towers / prior MLPs, bf16): the
+// pre-activation is rounded to bf16 first and quick-GELU keeps the bf16 roundings of the unfused
+// elementwise chain (h, 1.702 h, sigmoid) - the MLP hidden state never reaches HBM un-activated.
 __device__ __forceinline__ float act_f(int act, float v) {
   if (act == 1) return fmaxf(v, 0.f);
   if (act == 2) return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+  if (act == 3) return gelu_f(bf16_round(v));
+  if (act == 4) {
+    const float h = bf16_round(v), t = bf16_round(1.702f * h);
+    return h * bf16_round(1.f / (1.f + __expf(-t)));
+  }
   return v;
 }
 
@@ -2165,7 +2176,7 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
                     const void* wsum = nullptr, int cx = 0, int act = 0, int temb_ld = 0) {
   if (Cin % 64 != 0 || Cout % 8 != 0 || (k != 1 && k != 3 && k != 31) || (stride != 1 && stride != 2)) return -1;
   if (cx == 0) cx = Cin;
-  if (cx % 8 != 0 || cx > Cin || Cin - cx >= 64 || act < 0 || act > 2) return -1;
+  if (cx % 8 != 0 || cx > Cin || Cin - cx >= 64 || act < 0 || act > 4 || (act > 2 && EL != 0)) return -1;
   if (cx != Cin && (norm != nullptr || x2 != nullptr || rowstat != nullptr)) return -1;
   if (x2 != nullptr && (EL != 0 || C1 <= 0 || C1 >= Cin || C1 % 64 != 0 || geglu)) return -1;
   ConvArgs a;
@@ -2355,16 +2366,23 @@ ARB_API int arb_gemm_bias_res(const void* x, const void* w, const void* bias, co
   return arb_conv2d_nhwc(x, w, bias, nullptr, res, out, ws, nullptr, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, 0, stream);
 }
 
+// As arb_gemm_bias_res with an epilogue activation (act_f: 3 GELU, 4 quick-GELU; bf16).
+ARB_API int arb_gemm_act(const void* x, const void* w, const void* bias, const void* res, void* out, void* ws, int M,
+                         int N, int K, int cfg, int split, int act, hipStream_t stream) {
+  return conv_run<0>(x, w, bias, nullptr, res, out, ws, nullptr, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, 0, stream, 0,
+                     nullptr, 0, nullptr, nullptr, 0, act);
+}
+
 // GEMM with a LayerNorm folded in (see ConvArgs::rowstat): x is the LN's INPUT [M, K], w the
 // gamma-scaled weights, bias the beta-folded bias, rowstat[m] = (mean, rstd) of x's row m
 // (arb_row_stats), wsum[n] = sum_k w[n, k] in fp32.  geglu: w / bias / wsum interleaved as for
 // arb_gemm_geglu, out [M, N/2].  The normalised activation never exists in memory.
 ARB_API int arb_gemm_ln(const void* x, const void* w, const void* bias, const void* res, void* out, void* ws,
                         const void* rowstat, const void* wsum, int M, int N, int K, int cfg, int split, int geglu,
-                        hipStream_t stream) {
-  if (rowstat == nullptr || wsum == nullptr || (geglu && res != nullptr)) return -1;
+                        int act, hipStream_t stream) {
+  if (rowstat == nullptr || wsum == nullptr || (geglu && (res != nullptr || act != 0))) return -1;
   return conv_run<0>(x, w, bias, nullptr, res, out, ws, nullptr, 1, 1, M, K, N, 1, 0, 0, 1, cfg, split, 0, stream,
-                     geglu, nullptr, 0, rowstat, wsum);
+                     geglu, nullptr, 0, rowstat, wsum, 0, act);
 }
 
 // General entry: x has Cx channels per pixel (Cx % 8 == 0; the K walk pads to Cin = Cx rounded up to

@@ -42,16 +42,20 @@ def env_rank():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
 
 
-def init(backend: str = None, device_type: str = "cuda"):
-    """Initialise torch.distributed from torchrun env vars (no-op at world size 1)."""
+def init(backend: str = None, device_type: str = "cuda", force_group: bool = False):
+    """Initialise torch.distributed from torchrun env vars (no-op at world size 1 unless
+    ``force_group``: then a one-rank group is formed too - on a GPU a one-rank RCCL communicator, so
+    the weight broadcast runs the same RCCL code path as on an 8-GPU node)."""
     rank, local, world = env_rank()
     if device_type == "cuda" and torch.cuda.is_available():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_group) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         if backend is None:
             backend = "nccl" if dev.type == "cuda" else "gloo"
         kw = {"device_id": dev} if dev.type == "cuda" else {}
@@ -62,7 +66,7 @@ def init(backend: str = None, device_type: str = "cuda"):
 def world_info(dev) -> Dict[str, object]:
     """The world this rank actually joined (logged, and reported in the bench JSON): backend, size,
     every rank's device and host, the RCCL version, the HIP / RCCL environment that shapes it."""
-    info: Dict[str, object] = {"backend": backend_name(), "world_size": dist.get_world_size() if is_dist() else 1,
+    info: Dict[str, object] = {"backend": backend_name(), "world_size": dist.get_world_size() if in_group() else 1,
                                "torch": torch.__version__, "hip": getattr(torch.version, "hip", None)}
     try:
         v = torch.cuda.nccl.version() if torch.cuda.is_available() else None
@@ -86,9 +90,23 @@ def is_dist():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def in_group() -> bool:
+    """A process group exists (possibly of one rank: ``init(force_group=True)``)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def backend_name() -> str:
-    """'nccl' (= RCCL on ROCm), 'gloo', or 'none' at world size 1."""
-    return str(dist.get_backend()) if is_dist() else "none"
+    """'nccl' (= RCCL on ROCm) or 'gloo' when a process group exists (any size), else 'none'."""
+    return str(dist.get_backend()) if in_group() else "none"
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
 def shutdown(timeout: float = 30.0) -> bool:
@@ -153,9 +171,11 @@ def _rehome(group: List[torch.Tensor], copy: bool) -> torch.Tensor:
 
 def broadcast_tensors(tensors: List[torch.Tensor], src: int = 0, bucket_bytes: int = 1 << 30) -> Dict[str, float]:
     """Broadcast a list of same-device tensors from ``src`` in flat buckets the tensors are re-homed
-    into (views): the collective runs straight on the buckets on every rank."""
+    into (views): the collective runs straight on the buckets on every rank.  Runs whenever a
+    process group exists - also a one-rank group (``init(force_group=True)``), where the RCCL
+    collective is trivial but the whole path (re-homing, buckets, communicator) executes."""
     stats = {"bytes": 0, "buckets": 0, "seconds": 0.0}
-    if not is_dist() or not tensors:
+    if not in_group() or not tensors:
         return stats
     t0 = time.perf_counter()
     by_dtype: Dict[torch.dtype, List[torch.Tensor]] = {}

@@ -50,7 +50,7 @@ def _free_port() -> int:
 
 def _worker_main(rank: int, world: int, port: int, device_type: str, models: List[str], tiny: bool,
                  in_q, out_q, group: bool, weight_seed: int, streams: int = 1, lockstep: int = 1,
-                 weights_dir: Optional[str] = None, beats=None):
+                 weights_dir: Optional[str] = None, beats=None, force_group: bool = False):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import queue as _queue
     import threading
@@ -69,7 +69,10 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
             dev = torch.device("cuda", rank)
         else:
             dev = torch.device("cpu")
-        if group and world > 1:
+        # the weight-broadcast group: every rank of a multi-GPU start; ``force_group`` forms it at
+        # world size 1 too (a one-rank RCCL communicator: the broadcast path runs exactly as on a node)
+        grouped = group and (world > 1 or force_group)
+        if grouped:
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
             backend = "nccl" if device_type == "cuda" else "gloo"
             kw = {"device_id": dev} if device_type == "cuda" else {}
@@ -84,7 +87,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
             pipe = build_pipeline(name, device=dev, tiny=tiny, weight_seed=weight_seed,
                                   init=src and not weights_dir, weights_dir=weights_dir if src else None,
                                   tokenizer_dir=weights_dir)
-            if group and world > 1:
+            if grouped:
                 if (os.environ.get("ARBIUS_FAULT_INJECTION") == "1"
                         and os.environ.get("ARBIUS_FAULT_BCAST_DIE_RANK") == str(rank)):
                     os._exit(17)                    # test hook: a rank lost in the middle of the broadcast
@@ -146,9 +149,11 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
         threads = [threading.Thread(target=slot_loop, args=(k,), daemon=True) for k in range(streams)]
         for t in threads:
             t.start()
-        world_info = D.world_info(dev) if group and world > 1 else {"backend": "none", "world_size": 1}
+        world_info = D.world_info(dev) if grouped else {"backend": "none", "world_size": 1}
         log.info("worker %d ready: %s", rank, world_info)
-        out_q.put(("ready", rank, dict(bstats, world=world_info)))
+        from ..node.pool import hardware_id
+        # the dispatcher never touches the GPU: the worker reports its device's arch (self-test key)
+        out_q.put(("ready", rank, dict(bstats, world=world_info, arch=hardware_id(dev))))
         while True:
             msg = in_q.get()
             if msg is None:
@@ -163,15 +168,18 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
     finally:
         # bounded: with a dead peer destroy_process_group can block forever, and a worker that never
         # exits would stall the pool's shutdown (close() joins it)
-        if group and world > 1 and dist.is_initialized() and not D.shutdown(timeout=15.0):
+        if dist.is_initialized() and not D.shutdown(timeout=15.0):
             os._exit(0)
 
 
 class MultiGPUSolverPool:
     def __init__(self, n: int, models: List[str], device_type: str = "cuda", tiny: bool = False,
                  weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1,
-                 lockstep: int = 1, weights_dir: Optional[str] = None, hang_timeout: float = 300.0):
+                 lockstep: int = 1, weights_dir: Optional[str] = None, hang_timeout: float = 300.0,
+                 force_group: bool = False):
         self.n = n
+        self.force_group = bool(force_group)
+        self.arch = None                         # gcnArchName reported by the workers (no GPU call here)
         self.models = models
         self.device_type = device_type
         self.tiny = tiny
@@ -241,10 +249,12 @@ class MultiGPUSolverPool:
                     self.idle.extend([rank] * self.slots_per_rank)
                     self.broadcast_stats[rank] = payload
                     self.world = payload.get("world")
+                    self.arch = self.arch or payload.get("arch")
 
     def hardware(self) -> str:
-        from ..node.pool import hardware_id
-        return hardware_id("cuda:0" if self.device_type == "cuda" else "cpu")
+        """The workers' device arch ('gfx950'), from their ``ready`` messages: the dispatcher process
+        never initialises HIP, so every respawn is a spawned child of a GPU-free parent."""
+        return self.arch or ("cpu" if self.device_type != "cuda" else "unknown")
 
     def weights_id(self) -> str:
         base = (f"safetensors:{os.path.basename(os.path.normpath(self.weights_dir))}" if self.weights_dir
@@ -261,7 +271,7 @@ class MultiGPUSolverPool:
         p = self.ctx.Process(target=_worker_main, daemon=True,
                              args=(rank, self.n, port, self.device_type, self.models, self.tiny,
                                    self.in_qs[rank], self.out_qs[rank], group, self.weight_seed, self.streams,
-                                   self.lockstep, self.weights_dir, self.beats))
+                                   self.lockstep, self.weights_dir, self.beats, group and self.force_group))
         p.start()
         self.procs[rank] = p
 
@@ -274,6 +284,7 @@ class MultiGPUSolverPool:
         if kind == "ready":
             rank = msg[1]
             self.idle = [r for r in self.idle if r != rank] + [rank] * self.slots_per_rank
+            self.arch = self.arch or msg[2].get("arch")
             return
         _, jid, rank, payload = msg
         if self.busy.pop(jid, None) is not None:

@@ -145,9 +145,26 @@ def _get(url: str, max_redirects: int = 3) -> bytes:
 
 
 # Fetched inputs are cached on disk between hydration (``probe_video``) and the solve
-# (``load_video``, possibly in a GPU worker process): one download per task input.
-_CACHE_DIR = os.environ.get("ARBIUS_VIDEO_CACHE") or os.path.join(tempfile.gettempdir(), "arbius_video_cache")
+# (``load_video``, possibly in a GPU worker process): one download per task input.  The cache is a
+# directory private to this user (mode 0700, owner checked before every use: another local user
+# must not be able to plant or swap the bytes behind a task's input), by default per uid under the
+# temp dir; ``$ARBIUS_VIDEO_CACHE`` (e.g. under the node's data dir) overrides it.  A cached
+# ``ipfs://Qm...`` entry is also checked against its CID (kubo's default chunking) before use.
+_CACHE_DIR = os.environ.get("ARBIUS_VIDEO_CACHE") or os.path.join(tempfile.gettempdir(),
+                                                                  f"arbius_video_cache-{os.getuid()}")
 _CACHE_KEEP = 16
+
+
+def _cache_dir_ok(create: bool) -> bool:
+    """The cache dir exists (or was created) as a directory owned by us with no group/other access."""
+    import stat
+    try:
+        if create:
+            os.makedirs(_CACHE_DIR, mode=0o700, exist_ok=True)
+        st = os.lstat(_CACHE_DIR)
+    except OSError:
+        return False
+    return stat.S_ISDIR(st.st_mode) and st.st_uid == os.getuid() and not (st.st_mode & 0o077)
 
 
 def _cache_path(ref: str) -> str:
@@ -155,20 +172,38 @@ def _cache_path(ref: str) -> str:
     return os.path.join(_CACHE_DIR, hashlib.sha256(ref.encode()).hexdigest())
 
 
+def _cid_matches(ref: str, data: bytes) -> bool:
+    """For a bare CIDv0 reference (``Qm...`` without a path): the bytes' UnixFS file CID (kubo
+    defaults) equals it.  Other references (paths, CIDv1, https) are not content-addressed here."""
+    cid = ref[len("ipfs://"):] if ref.startswith("ipfs://") else ref
+    if not (cid.startswith("Qm") and "/" not in cid):
+        return True
+    from ..ipfs.unixfs import add_file
+    return add_file(data).cid_str == cid
+
+
 def _cache_get(ref: str):
+    if not _cache_dir_ok(False):
+        return None
     p = _cache_path(ref)
     try:
+        st = os.lstat(p)
+        if st.st_uid != os.getuid() or not os.path.isfile(p):
+            return None
         with open(p, "rb") as f:
             data = f.read(MAX_VIDEO_BYTES + 1)
         os.utime(p)
-        return data if len(data) <= MAX_VIDEO_BYTES else None
     except OSError:
         return None
+    if len(data) > MAX_VIDEO_BYTES or not _cid_matches(ref, data):
+        return None
+    return data
 
 
 def _cache_put(ref: str, data: bytes):
     try:
-        os.makedirs(_CACHE_DIR, exist_ok=True)
+        if not _cache_dir_ok(True):
+            return
         tmp = _cache_path(ref) + f".{os.getpid()}.tmp"
         with open(tmp, "wb") as f:
             f.write(data)
@@ -254,6 +289,10 @@ def probe(data: bytes) -> None:
     head_pics, pictures = [], 0
     for n in nals:
         typ = n[0] & 0x1F
+        if typ in (7, 8):
+            if pictures <= 2:       # parameter sets re-sent or updated between the first pictures
+                head_pics.append(n)
+            continue
         if typ in (1, 5):
             head = "".join(f"{b:08b}" for b in n[1:9].replace(b"\x00\x00\x03", b"\x00\x00"))
             first_mb, i = _ue(head, 0)

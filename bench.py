@@ -56,6 +56,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--tiny", action="store_true", help="tiny config (CPU plumbing check only)")
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is visible) or cpu (gloo ranks)")
+    ap.add_argument("--rccl-group", action="store_true",
+                    help="form the process group at N = 1 too: the weight broadcast then runs through a one-rank "
+                         "RCCL communicator (the multi-GPU code path, exercised on one GPU)")
     ap.add_argument("--node", action="store_true",
                     help="whole-node mode: tasks flow through the node's own stack (MockEngine events -> "
                          "orchestrator -> solver pool -> commit/submit); one process, N GPU worker processes")
@@ -100,7 +103,7 @@ def run(args):
     rvm = args.model == "robust_video_matting"
     if args.reference_ops:
         ops.set_reference_ops(True)
-    rank, local, world, dev = D.init(device_type=_device_type(args))
+    rank, local, world, dev = D.init(device_type=_device_type(args), force_group=args.rccl_group)
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but the process group has {world} ranks")
     if world > 1:

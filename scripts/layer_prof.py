@@ -2,9 +2,12 @@
 """Per-op / per-shape GPU time of one lock-step SD1.5 (or Kandinsky2) solve, eager (no hipGraphs):
 every HIP op entry point in ``ops._lib`` is wrapped with a pair of HIP events, so the table says
 which conv / GEMM / norm / attention shapes carry the time (rocprofv3's summary only names kernels).
+Each row carries the useful FLOPs of the call, the achieved TFLOP/s and - for conv / GEMM launches -
+the tile family and split-K the launch runs (``_lib.conv_choice`` / ``gemm_choice``: the canonical
+plan at its split, on the family tuned for the actual shape).
 
     python scripts/layer_prof.py [--model anythingv3|kandinsky2] [--group 4] [--res 512] [--steps 2]
-        [--json out.jsonl]
+        [--streams 1] [--json out.jsonl] [--md out.md]
 """
 import argparse
 import json
@@ -22,26 +25,66 @@ SLEEP_CYCLES = 400_000
 WRAPPED = ("conv2d_nhwc", "gemm", "gemm_geglu", "group_norm_table", "norm_table_apply", "layer_norm",
            "flash_attention", "group_norm_nhwc", "group_norm_mod_nhwc", "softmax_rows", "sampler_step", "silu",
            "geglu", "temporal_attention", "gemm_ln", "row_stats")
+_ORIG = {}
 
 
-def _key(name, a, k):
-    def sh(t):
-        return tuple(t.shape) if hasattr(t, "shape") else None
+def _arg(a, k, i, name, default=None):
+    if len(a) > i:
+        return a[i]
+    return k.get(name, default)
+
+
+def _sh(t):
+    return tuple(t.shape) if hasattr(t, "shape") else None
+
+
+def _info(name, a, k):
+    """(key, flops, family) of one call."""
     if name == "conv2d_nhwc":
         x, w = a[0], a[1]
-        return (sh(x), sh(w), "s%d" % k.get("stride", a[7] if len(a) > 7 else 1),
-                "up" if (a[4] if len(a) > 4 else k.get("upsample")) else "", "cat" if k.get("x2") is not None else "",
-                "norm" if k.get("norm") is not None else "")
+        pad, up = _arg(a, k, 3, "padding", 1), bool(_arg(a, k, 4, "upsample", False))
+        stride = _arg(a, k, 7, "stride", 1)
+        x2 = k.get("x2")
+        B, H, W, Cin = x.shape
+        if x2 is not None:
+            Cin += x2.shape[-1]
+        Cout, kh, kw, _ = w.shape
+        kcode = 31 if (kh, kw) == (3, 1) else kh
+        Hl, Wl = (2 * H, 2 * W) if up else (H, W)
+        Ho = (Hl + 2 * pad - kh) // stride + 1
+        Wo = (Wl + 2 * (0 if kcode == 31 else pad) - kw) // stride + 1
+        M, N, K = B * Ho * Wo, Cout, kh * kw * Cin
+        plan_b = k.get("plan_b")
+        cfg, split = _ORIG["conv_choice"](B, H, W, Cin, Cout, kcode, pad, up, stride, plan_b)
+        temb, res = _arg(a, k, 6, "temb"), _arg(a, k, 5, "residual")
+        flags = ("up" if up else "", "cat" if x2 is not None else "", "norm" if k.get("norm") is not None else "",
+                 "temb" if temb is not None else "", "res" if res is not None else "")
+        key = ("conv%dx%d" % (kh, kw), _sh(x), Cout, "s%d" % stride) + flags
+        return key, 2.0 * M * N * K, (M, N, K, _lib.cfg_name(cfg), split)
     if name in ("gemm", "gemm_geglu", "gemm_ln"):
-        return (sh(a[0]), sh(a[1]))
+        x, w = a[0], a[1]
+        K, N = x.shape[-1], w.shape[0]
+        M = x.numel() // K
+        cfg, split = _ORIG["gemm_choice"](M, N, K, k.get("plan_batch"))
+        return (_sh(x), _sh(w)), 2.0 * M * N * K, (M, N, K, _lib.cfg_name(cfg), split)
     if name == "flash_attention":
-        return (sh(a[0]), sh(a[1]), "prefix" if (a[5] if len(a) > 5 else k.get("kv_prefix")) is not None else "")
+        q, kk = a[0], a[1]
+        B, Nq, H, D = q.shape
+        kvp = _arg(a, k, 5, "kv_prefix")
+        Nk = kk.shape[1] + (kvp[0].shape[1] if kvp is not None else 0)
+        return (_sh(q), _sh(kk), "prefix" if kvp is not None else ""), 4.0 * B * H * Nq * Nk * D, None
+    if name == "temporal_attention":
+        q = a[0]
+        B, F, P, H, D = q.shape
+        return (_sh(q),), 4.0 * B * P * H * F * F * D, None
     if name == "sampler_step":
-        return (len(a[0]),)
-    return tuple(sh(t) for t in a[:2] if hasattr(t, "shape"))
+        return (len(a[0]),), 0.0, None
+    return tuple(_sh(t) for t in a[:2] if hasattr(t, "shape")), 0.0, None
 
 
 def wrap():
+    _ORIG["conv_choice"] = _lib.conv_choice
+    _ORIG["gemm_choice"] = _lib.gemm_choice
     for name in WRAPPED:
         f = getattr(_lib, name, None)
         if f is None:
@@ -55,7 +98,8 @@ def wrap():
             s.record()
             r = __f(*a, **k)
             e.record()
-            REC.append((__n, _key(__n, a, k), s, e))
+            key, flops, fam = _info(__n, a, k)
+            REC.append((__n, key, flops, fam, s, e))
             return r
         setattr(_lib, name, g)
 
@@ -67,7 +111,8 @@ def main():
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--top", type=int, default=60)
+    ap.add_argument("--md", default=None)
+    ap.add_argument("--top", type=int, default=80)
     args = ap.parse_args()
     from arbius_amd.models.registry import build_pipeline
     from arbius_amd.node.solver import solve_images
@@ -84,28 +129,43 @@ def main():
     wrap()
     solve_images(pipe, inps)
     torch.cuda.synchronize()
-    agg = defaultdict(lambda: [0.0, 0])
-    for n, key, s, e in REC:
+    agg = defaultdict(lambda: [0.0, 0, 0.0, None])
+    for n, key, flops, fam, s, e in REC:
         a = agg[(n, key)]
         a[0] += s.elapsed_time(e) * 1000.0
         a[1] += 1
+        a[2] += flops
+        a[3] = fam
     total = sum(v[0] for v in agg.values())
+    tot_fl = sum(v[2] for v in agg.values())
     by_op = defaultdict(float)
     for (n, _), v in agg.items():
         by_op[n] += v[0]
-    print(f"total op time {total / 1000:.2f} ms over {len(REC)} calls ({args.model}, group {args.group}, "
-          f"{args.steps} steps, eager)")
+    lines = [f"total op time {total / 1000:.2f} ms over {len(REC)} calls ({args.model} {res}^2, group {args.group} "
+             f"= batch {2 * args.group}, {args.steps} steps, eager, each op timed in isolation); "
+             f"{tot_fl / 1e12:.1f} TFLOP of matmul work -> {tot_fl / (total * 1e-6) / 1e12:.0f} TFLOP/s overall", ""]
+    lines += ["| op | % | ms |", "|---|---:|---:|"]
     for n, t in sorted(by_op.items(), key=lambda kv: -kv[1]):
-        print(f"  {n:20s} {100 * t / total:5.1f} %  {t / 1000:8.2f} ms")
-    print("| % | ms | calls | avg us | op | shape |")
-    print("|---:|---:|---:|---:|---|---|")
+        lines.append(f"| {n} | {100 * t / total:.1f} | {t / 1000:.2f} |")
+    lines += ["", "| % | ms | calls | avg us | TFLOP/s | op | shape | M x N x K | family | split |",
+              "|---:|---:|---:|---:|---:|---|---|---|---|---:|"]
     rows = sorted(agg.items(), key=lambda kv: -kv[1][0])
-    for (n, key), (t, c) in rows[:args.top]:
-        print(f"| {100 * t / total:.1f} | {t / 1000:.2f} | {c} | {t / c:.1f} | {n} | {key} |")
+    for (n, key), (t, c, fl, fam) in rows[:args.top]:
+        tf = f"{fl / (t * 1e-6) / 1e12:.0f}" if fl else "-"
+        mnk = f"{fam[0]}x{fam[1]}x{fam[2]}" if fam else ""
+        fname, split = (fam[3], fam[4]) if fam else ("", "")
+        lines.append(f"| {100 * t / total:.1f} | {t / 1000:.2f} | {c} | {t / c:.1f} | {tf} | {n} | {key} | {mnk} | "
+                     f"{fname} | {split} |")
+    text = "\n".join(lines)
+    print(text)
+    if args.md:
+        with open(args.md, "w") as f:
+            f.write(text + "\n")
     if args.json:
         with open(args.json, "w") as f:
-            for (n, key), (t, c) in rows:
-                f.write(json.dumps({"op": n, "key": repr(key), "us": t, "calls": c}) + "\n")
+            for (n, key), (t, c, fl, fam) in rows:
+                f.write(json.dumps({"op": n, "key": repr(key), "us": t, "calls": c, "flops": fl,
+                                    "family": fam}) + "\n")
 
 
 if __name__ == "__main__":

@@ -188,3 +188,59 @@ def test_kandinsky2_lockstep_group_bitwise_equals_solo(cuda):
     inps = [{"prompt": f"arbius test cat {i}", "width": 256, "height": 256, "seed": 1337 + i} for i in range(2)]
     solo = [pipe.solve(i).cid for i in inps]
     assert [s.cid for s in solve_images(pipe, inps)] == solo
+
+
+def _clear_derived_caches(pipe):
+    ops._LN_FOLD.clear()
+    ops._GEGLU_W.clear()
+    ops._PAD_W.clear()
+    unet = getattr(pipe, "unet", None)
+    if unet is not None and hasattr(unet, "_temb_cache"):
+        unet._temb_cache = None
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_cold_cache_concurrent_first_use_matches_solo(cuda, graphs):
+    """Derived-weight caches (LayerNorm fold, GEGLU interleave, padded conv weights, batched time
+    projection) are shared by pipeline forks on other threads and HIP streams: two forks whose FIRST
+    solve races on an empty cache still give the solo CIDs (an entry is published only after the
+    kernels that computed it finished - ``ops.derived_ready``)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from arbius_amd.node.solver import solve_image
+    pipe = build_pipeline("anythingv3", device=cuda, use_graphs=graphs)
+    inps = [{"prompt": f"lake {i}", "negative_prompt": "", "width": 128, "height": 128, "num_inference_steps": 3,
+             "guidance_scale": 7.5, "scheduler": "DPMSolverMultistep", "seed": 300 + i} for i in range(2)]
+    solo = [solve_image(pipe, inp).cid for inp in inps]
+    for _ in range(2):
+        _clear_derived_caches(pipe)
+        forks = [pipe.fork() for _ in range(2)]
+        with ThreadPoolExecutor(2) as ex:
+            conc = list(ex.map(lambda a: solve_image(a[0], a[1]).cid, zip(forks, inps)))
+        assert conc == solo
+
+
+def test_kandinsky2_prior_graph_bitwise_equals_eager(cuda):
+    """The opt-in hipGraph replay of the diffusion-prior step (``prior_graph``) gives the eager CIDs:
+    a lock-step group of 2 with different prompt lengths and a mixed prior_steps group."""
+    from arbius_amd.node.solver import solve_images
+    pipe = build_pipeline("kandinsky2", device=cuda)
+    pipe.cfg.num_steps = 2
+    inps = [{"prompt": "cat", "width": 256, "height": 256, "seed": 5},
+            {"prompt": "a very long prompt about a castle on a hill at dawn", "width": 256, "height": 256,
+             "seed": 6, "prior_steps": "3"},
+            {"prompt": "dog on a boat", "width": 256, "height": 256, "seed": 7}]
+    pipe.prior_graph = False
+    eager = [s.cid for s in solve_images(pipe, inps)]
+    pipe.prior_graph = True
+    graph = [s.cid for s in solve_images(pipe, inps)]
+    assert graph == eager
+    assert [pipe.solve(i).cid for i in inps] == eager
+
+
+def test_kandinsky2_group_with_mixed_steps_splits(cuda):
+    """A K2 group whose tasks differ in step count runs as separate lock-step groups (no failure)."""
+    from arbius_amd.node.solver import solve_images
+    pipe = build_pipeline("kandinsky2", device=cuda)
+    inps = [{"prompt": "cat", "width": 256, "height": 256, "seed": 5, "num_inference_steps": 2},
+            {"prompt": "cat", "width": 256, "height": 256, "seed": 6, "num_inference_steps": 3}]
+    assert [s.cid for s in solve_images(pipe, inps)] == [pipe.solve(i).cid for i in inps]

@@ -1,5 +1,6 @@
 """Robust video matting (BASELINE config #5) on CPU: recurrence semantics,
 time-batched chunks == frame-by-frame, output types, MP4 input/output, node run."""
+import os
 import pytest
 import asyncio
 import json
@@ -183,10 +184,20 @@ def test_gateway_fetch_is_capped_while_streaming_and_cached(monkeypatch, tmp_pat
         monkeypatch.setenv("ARBIUS_IPFS_GATEWAY", f"http://127.0.0.1:{srv.server_address[1]}")
         monkeypatch.setattr(V, "_CACHE_DIR", str(tmp_path / "cache"))
         monkeypatch.setattr(V, "MAX_VIDEO_BYTES", 64 << 10)
-        cid = "QmYwAPJzv5CZsnA625s3Xf2nemtYgPpHdWEz79ojWnPbdG"
+        from arbius_amd.ipfs.unixfs import add_file
+        cid = add_file(b"\0" * 4096).cid_str
         assert len(V.fetch(cid)) == 4096
         assert len(V.fetch("ipfs://" + cid)) == 4096 and len(V.fetch(cid)) == 4096
         assert len(hits) == 2            # "ipfs://X" and "X" are two refs; the repeat came from the cache
+        assert (os.stat(tmp_path / "cache").st_mode & 0o777) == 0o700
+        # a cache entry whose bytes do not hash to the CID is never used (re-fetched instead)
+        with open(V._cache_path(cid), "wb") as f:
+            f.write(b"planted")
+        assert V.fetch(cid) == b"\0" * 4096 and len(hits) == 3
+        # a cache dir other users can write to is not used at all
+        os.chmod(tmp_path / "cache", 0o777)
+        assert V._cache_get(cid) is None
+        os.chmod(tmp_path / "cache", 0o700)
         with pytest.raises(V.VideoSourceError):
             V.fetch(cid + "/big")
     finally:
