@@ -2,10 +2,16 @@
 
 Every op here has exactly one GPU implementation: a hand-written gfx950 HIP
 kernel in ``csrc/`` (loaded from the in-tree ``libarbius_kernels.so`` through
-``_lib``), or - for plain GEMMs / convolutions not yet covered by a kernel -
-the ROCm library call (hipBLASLt / MIOpen) that PyTorch issues.  CPU tensors
-run the PyTorch reference in ``ref.py`` (the no-GPU plumbing config and the
-numerics oracle for tests).
+``_lib``).  Shapes a kernel does not tile natively are zero-padded onto it
+(channels, K, N: zeros add nothing to a dot product, so the bytes are those of
+an exact-size kernel).  A GPU tensor never falls back to a ROCm library
+(hipBLASLt / MIOpen): such a call would pick its reduction order by shape and
+break the batch invariance of lock-step groups, so it raises
+``LibraryFallback`` instead (``ARBIUS_LIBRARY_FALLBACK=1`` only counts it, in
+``LIBRARY_CALLS`` - for experiments).  ``ops/audit.py`` runs every template's
+legal operating points on the meta device through this module to prove no
+shape reaches that path.  CPU tensors run the PyTorch reference in ``ref.py``
+(the no-GPU plumbing config and the numerics oracle for tests).
 
 On a GPU, a missing ``libarbius_kernels.so`` is a hard error (``_lib.lib()``
 raises): there is no silent eager fallback.  ``ARBIUS_REFERENCE_OPS=1`` forces
@@ -14,6 +20,7 @@ the PyTorch reference on GPU tensors too; it exists only for A/B measurement
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import threading
@@ -102,7 +109,22 @@ def _plan_rows(x) -> int:
 
 
 def _hip(t: torch.Tensor) -> bool:
-    return t.is_cuda and not _FORCE_REF
+    return (t.is_cuda or (t.device.type == "meta" and _lib.auditing())) and not _FORCE_REF
+
+
+class LibraryFallback(RuntimeError):
+    """A GPU tensor reached a shape no HIP kernel (or padded form of one) serves."""
+
+
+_ALLOW_LIBRARY = os.environ.get("ARBIUS_LIBRARY_FALLBACK", "0") == "1"
+LIBRARY_CALLS = collections.Counter()     # op -> library calls made on GPU tensors (only when allowed)
+
+
+def _library(op: str, detail: str) -> None:
+    """Gate of every library-call branch on GPU tensors (see the module docstring)."""
+    if not _ALLOW_LIBRARY:
+        raise LibraryFallback(f"{op}: no HIP kernel for {detail}; GPU tensors never take a library fallback")
+    LIBRARY_CALLS[op] += 1
 
 
 # ------------------------------------------------------------------ derived-weight caches
@@ -139,6 +161,11 @@ def linear(x, w, b=None, residual=None, act=None):
     concurrently on the two task streams of a GPU deadlocked (zeroscope, 2 streams)."""
     if _hip(x) and _gemm_ok(x.shape[-1], w.shape[0]):
         return _lib.gemm(x, w, b, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])), act=act)
+    if _hip(x):
+        if x.dtype != torch.bfloat16:
+            _library("linear", f"dtype {x.dtype} x {tuple(x.shape)} w {tuple(w.shape)}")
+        else:
+            return _padded_linear(x, w, b, residual, act)
     if act is not None:
         return _act_ref(linear(x, w, b, residual), act)
     if residual is not None:
@@ -149,6 +176,39 @@ def linear(x, w, b=None, residual=None, act=None):
             y = y.add_(b)
         return y.reshape(*x.shape[:-1], w.shape[0])
     return F.linear(x, w, b)
+
+
+_PAD_LIN = {}
+
+
+def _padded_linear(x, w, b, residual, act):
+    """A bf16 linear whose K (in) % 64 or N (out) % 8 the implicit-GEMM kernel does not tile: zero
+    columns of x / w up to K % 64 == 0 (products of zeros add nothing: the exact-K dot product),
+    zero rows of w / b up to N % 8 == 0, sliced off the output.  Padded weights are cached per live
+    weight (``derived_ready``)."""
+    N, K = w.shape
+    Kp, Np = -(-K // 64) * 64, -(-N // 8) * 8
+    key = (id(w), None if b is None else id(b))
+    stamp = (w.data_ptr(), w._version, None if b is None else (b.data_ptr(), b._version))
+    ent = _PAD_LIN.get(key)
+    if ent is None or ent[0]() is not w or ent[1] != stamp:
+        wp = torch.zeros(Np, Kp, dtype=w.dtype, device=w.device)
+        wp[:N, :K] = w
+        bp = None
+        if b is not None:
+            bp = torch.zeros(Np, dtype=b.dtype, device=b.device)
+            bp[:N] = b
+        derived_ready(wp)
+        ent = (weakref.ref(w), stamp, wp, bp)
+        _PAD_LIN[key] = ent
+    wp, bp = ent[2], ent[3]
+    xp = F.pad(x, (0, Kp - K)) if Kp != K else x
+    if Np != N:
+        y = _lib.gemm(xp, wp, bp, None, plan_batch=(x.shape[0], _canon_batch(x.shape[0])))[..., :N]
+        if residual is not None:
+            y = y + residual
+        return _act_ref(y, act).contiguous()
+    return _lib.gemm(xp, wp, bp, residual, plan_batch=(x.shape[0], _canon_batch(x.shape[0])), act=act)
 
 
 _GEGLU_FUSED = os.environ.get("ARBIUS_GEGLU_FUSED", "1") != "0"   # A/B switch (same numerics)
@@ -335,12 +395,13 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
             # FLOPs) instead of a library fallback - MIOpen's deterministic mode picks its naive
             # direct kernel for these shapes (1.1 ms per RVM conv: profiles/rocprof_r1_v11_rvm.md).
             return _padded_conv(x, w, b, padding, upsample, residual, temb, stride, table, nsilu)
+    if _hip(x):
+        _library("conv2d", f"x {tuple(x.shape)} w {tuple(w.shape)} stride {stride}")
     if norm is not None:
         x = apply_norm_table(x, *norm)
     if x.is_cuda:
-        # MIOpen NHWC path (channel counts the kernel does not tile: 3/4-channel
-        # conv_in / conv_out).  A permuted view of a contiguous NHWC tensor is an
-        # NCHW tensor in channels_last memory format (no copy).
+        # MIOpen NHWC path (only with ARBIUS_LIBRARY_FALLBACK=1).  A permuted view of a contiguous
+        # NHWC tensor is an NCHW tensor in channels_last memory format (no copy).
         xc = x.permute(0, 3, 1, 2)
         if upsample:
             xc = F.interpolate(xc, scale_factor=2.0, mode="nearest")
@@ -422,6 +483,8 @@ def depthwise_conv(x, weight, bias, stride=1, dilation=1, act=None):
             derived_ready(ent[2])
             _DW_W[id(weight)] = ent
         return _lib.dwconv_f16(x, ent[2], bias, k, stride, dilation, act)
+    if _hip(x):
+        _library("depthwise_conv", f"x {tuple(x.shape)} {x.dtype} k {k} stride {stride}")
     y = F.conv2d(x, weight, bias, stride=stride, padding=dilation * (k // 2), dilation=dilation, groups=C)
     if act == "relu":
         return F.relu(y)
@@ -511,8 +574,20 @@ def temporal_attention(q, k, v, scale=None):
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     if _hip(q):
-        return _lib.temporal_attention(q, k, v, scale)
+        B, F_, P, H, D = q.shape
+        if F_ <= TEMPORAL_MAX_FRAMES:
+            return _lib.temporal_attention(q, k, v, scale)
+        # longer clips (damo: num_frames up to 500): the frame axis no longer fits one wave's
+        # registers - gather (video, pixel) problems into the flash kernel's [batch, seq, head, d]
+        # layout (one copy each way; the UNet3D's common frame counts never take this path)
+        def gather(t):
+            return t.permute(0, 2, 1, 3, 4).reshape(B * P, F_, H, D).contiguous()
+        o = _lib.flash_attention(gather(q), gather(k), gather(v), scale, False)
+        return o.view(B, P, F_, H, D).permute(0, 2, 1, 3, 4).contiguous()
     return ref.temporal_attention(q, k, v, scale)
+
+
+TEMPORAL_MAX_FRAMES = 96     # csrc/temporal_attention.hip keeps <= 96 frames in registers
 
 
 # --------------------------------------------------------------------------- ConvGRU

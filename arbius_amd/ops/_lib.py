@@ -101,6 +101,24 @@ def loaded() -> bool:
     return _lib is not None
 
 
+# ---- shape audit (ops/audit.py): every launch symbol becomes a recording stub and HIP streams are
+# not touched, so the models run on the META device through the real host-side validation and plan
+# selection of this module (no GPU, no data).  Host-only queries still call the library.
+_AUDIT = None
+_HOST_SYMBOLS = ("arb_conv2d_plan", "arb_conv_family", "arb_conv2d_workspace", "arb_group_norm_workspace",
+                 "arb_rvm_args_sizes")
+
+
+def auditing() -> bool:
+    return _AUDIT is not None
+
+
+def audit_note(kind, **info):
+    """Record one planned launch (conv / GEMM shape, tile config, split-K) while auditing."""
+    if _AUDIT is not None:
+        _AUDIT.append(dict(kind=kind, **info))
+
+
 def has(op: str) -> bool:
     try:
         lib()
@@ -112,12 +130,17 @@ def has(op: str) -> bool:
 def _fn(name):
     lib()
     try:
-        return _SYMBOLS[name]
+        fn = _SYMBOLS[name]
     except KeyError:
         raise RuntimeError(f"kernel symbol {name} not in {_LIB_PATH} (rebuild)") from None
+    if _AUDIT is not None and name not in _HOST_SYMBOLS:
+        return lambda *a: (_AUDIT.append(dict(kind="launch", symbol=name)), 0)[1]
+    return fn
 
 
 def _stream():
+    if _AUDIT is not None:
+        return ctypes.c_void_p(0)
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
@@ -265,6 +288,8 @@ def _large_head_attention(q, k, v, scale):
                 s = gemm(q[b, :, h], k[b, :, h].contiguous())                 # [Nq, Nk] = q k^T
                 o[b, :, h] = gemm(softmax_rows(s, scale), v[b, :, h].t().contiguous())
         return o
+    from . import _library
+    _library("attention", f"head dim {D} with {Nk} keys (the GEMM path needs D % 64 == Nk % 64 == 0)")
     qf = q.transpose(1, 2)
     kf = k.transpose(1, 2)
     vf = v.transpose(1, 2)
@@ -338,7 +363,8 @@ def silu(x):
     _bf16(x)
     x = x.contiguous()
     if x.numel() % 8:
-        from . import ref
+        from . import _library, ref
+        _library("silu", f"{x.numel()} elements")
         return ref.silu(x)
     y = torch.empty_like(x)
     _check(_fn("arb_silu")(_p(x), _p(y), x.numel(), _stream()), "silu")
@@ -519,6 +545,8 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
         # family tuned for the actual shape (bitwise-neutral)
         cfg, split = conv_choice(B, H, W, Cin, Cout, kcode, padding, upsample, stride, plan_b)
     args = (B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride, int(cfg), int(split))
+    audit_note("conv", M=B * Ho * Wo, N=Cout, K=kh * kw * Cin, cfg=int(cfg), split=int(split), plan_b=plan_b,
+               batch=B, shape=(B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride), dtype=str(x.dtype))
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
     if f16:
@@ -554,6 +582,8 @@ def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None, act=Non
         raise ValueError(f"gemm: unsupported K={K} N={N}")
     if plan_batch and plan_batch[1] and cfg < 0:
         cfg, split = gemm_choice(M, N, K, plan_batch)
+    audit_note("gemm", M=M, N=N, K=K, cfg=int(cfg), split=int(split), plan_b=plan_batch and plan_batch[1],
+               batch=plan_batch and plan_batch[0], dtype=str(x.dtype))
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
@@ -580,6 +610,8 @@ def gemm_geglu(x, w_il, b_il=None, cfg=-1, split=-1, plan_batch=None):
         raise ValueError(f"gemm_geglu: unsupported K={K} N={N}")
     if plan_batch and plan_batch[1] and cfg < 0:
         cfg, split = gemm_choice(M, N, K, plan_batch)
+    audit_note("gemm", M=M, N=N, K=K, cfg=int(cfg), split=int(split), plan_b=plan_batch and plan_batch[1],
+               batch=plan_batch and plan_batch[0], dtype=str(x.dtype))
     y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
@@ -617,6 +649,8 @@ def gemm_ln(x, w, b, wsum, rs, residual=None, geglu=False, cfg=-1, split=-1, pla
         raise ValueError("gemm_ln: row stats / wsum must be contiguous fp32")
     if plan_batch and plan_batch[1] and cfg < 0:
         cfg, split = gemm_choice(M, N, K, plan_batch)
+    audit_note("gemm", M=M, N=N, K=K, cfg=int(cfg), split=int(split), plan_b=plan_batch and plan_batch[1],
+               batch=plan_batch and plan_batch[0], dtype=str(x.dtype))
     y = torch.empty(M, N // 2 if geglu else N, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))

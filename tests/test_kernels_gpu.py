@@ -650,3 +650,17 @@ def test_group_norm_table_wave_kernel_bitwise_equals_lds_tree(cuda, B, HW, C, G,
     r = ref.group_norm_table(x.float(), g.float(), bt.float(), G, 1e-5, m.float() if mod else None,
                              1.0 if mod else 0.0)
     assert _rel(t_wave, r) < 1e-4
+
+
+@pytest.mark.parametrize("F", [97, 200])
+def test_temporal_attention_long_clips_via_flash(cuda, F):
+    """damo accepts up to 500 frames: beyond the register-resident kernel's 96 the op gathers the
+    (video, pixel) problems into the flash kernel - strided views of a fused QKV activation."""
+    B, P, H, D = 2, 12, 2, 64
+    qkv = torch.randn(B * F, P, 3 * H * D, device=cuda).to(torch.bfloat16)
+    v5 = qkv.view(B, F, P, 3, H, D)
+    q, k, v = v5[:, :, :, 0], v5[:, :, :, 1], v5[:, :, :, 2]
+    o = ops.temporal_attention(q, k, v)
+    r = ref.temporal_attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D))
+    assert o.shape == (B, F, P, H, D) and _rel(o, r) < 2e-2
+    assert torch.equal(o, ops.temporal_attention(q, k, v))
