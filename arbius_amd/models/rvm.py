@@ -347,8 +347,10 @@ class RVMPipeline(PipelineBase):
             return self._matte(frames, output_type)
 
     def _fast_ok(self, ratio) -> bool:
-        return (self.device.type == "cuda" and self.dtype == torch.float16 and ratio < 1.0 and not ops.reference_ops()
-                and self.net.backbone.features[0].conv.out_channels == 16)
+        # every size: ratio < 1 runs the guided filter at full resolution, ratio 1 (inputs <= 512 px)
+        # composes the network's own full-resolution output (csrc/rvm.hip rvm_dgf_base ``direct``)
+        return (self.device.type == "cuda" and self.dtype == torch.float16 and ratio <= 1.0
+                and not ops.reference_ops() and self.net.backbone.features[0].conv.out_channels == 16)
 
     def _pinned(self, key, nbytes):
         """Reusable page-locked host staging buffers (async H2D / D2H), per pipeline fork."""

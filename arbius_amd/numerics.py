@@ -25,6 +25,7 @@ NUMERICS_ENV_KNOBS = (
     "ARBIUS_EXPERIMENT_SKIP", "ARBIUS_REFERENCE_OPS", "ARB_ATTN_GLDS", "ARB_ATTN_QT", "ARB_LN_ROWS",
     "ARB_SPLITK_INLAUNCH", "ARBIUS_GEGLU_FUSED", "ARBIUS_CROSS_KV_HOIST", "ARBIUS_FAULT_INJECTION",
     "ARBIUS_SAMPLER_REF", "ARB_GN_TABLE_LDS", "ARB_VAE_GRAPH", "ARB_PINNED_D2H", "ARB_PRIOR_GRAPH",
+    "ARB_ATTN_PP", "ARB_LN_FOLD_NARROW", "ARB_LN_FOLD_NARROW_N", "ARBIUS_LIBRARY_FALLBACK",
 )
 
 
@@ -164,6 +165,29 @@ def golden_cases(device) -> List[Tuple[str, Callable[[], object]]]:
         out = pipe("robust_video_matting")(clip, "green-screen")
         return solve_files([("out-1.mp4", encode_mp4(list(out), 24))]).cid
 
+    def sd_1024():
+        """the largest anythingv3 size (1024^2: 16,384-token spatial attention), 2 steps"""
+        inp = _sd_inp("arbius test cat", 1337, 1024, 2, "DPMSolverMultistep", 12.0)
+        return solve_image(pipe("anythingv3"), inp).cid
+
+    def k2_1024():
+        """kandinsky2 at its largest template size (1024^2), 2 decoder + 2 prior steps"""
+        return pipe("kandinsky2").solve({"prompt": "arbius test cat", "width": 1024, "height": 1024, "seed": 1337,
+                                         "num_inference_steps": 2, "prior_steps": "2"}).cid
+
+    def zeroscope_template_default():
+        """zeroscopev2xl at its template defaults (templates/zeroscopev2xl.json: 1024x576, 24 frames,
+        guidance 17.5, fps 24; spatial attention over 9,216 tokens) with 2 denoising steps"""
+        from .node.models import hydrate_input, load_template
+        tpl = load_template("zeroscopev2xl")
+        inp, err, msg = hydrate_input({"prompt": "a red cat walking on a castle wall",
+                                       "negative_prompt": "noisy, washed out, ugly, distorted, broken",
+                                       "num_inference_steps": 2}, tpl)
+        if err:
+            raise AssertionError(msg)
+        inp["seed"] = 1337
+        return pipe("zeroscopev2xl").solve(inp).cid
+
     cases = [("sd15_512_dpm4_solo", sd_solo), ("sd15_512_dpm4_2streams_group4", sd_group_streams)]
     cases += [(f"sd15_256_{s}_3", sd_sched(s)) for s in SD_SCHEDULERS]
     cases += [("sd15_512_dpm4_group2", sd_group(2)), ("sd15_512_dpm4_group3", sd_group(3)),
@@ -172,6 +196,8 @@ def golden_cases(device) -> List[Tuple[str, Callable[[], object]]]:
     cases += [(f"kandinsky2_768_{n}_4", k2_sampler(n)) for n in ("ddim_sampler", "pims_sampler")]
     cases += [("kandinsky2_768_2+2", k2), ("zeroscopev2xl_256x256x8_2", video("zeroscopev2xl")),
               ("damo_256x256x8_2", video("damo")), ("rvm_320x180x8", rvm)]
+    cases += [("sd15_1024_dpm2", sd_1024), ("kandinsky2_1024_2+2", k2_1024),
+              ("zeroscopev2xl_1024x576x24_2_template_default", zeroscope_template_default)]
     return cases
 
 

@@ -272,12 +272,16 @@ def ln_fold(gamma, beta, w, b, geglu=False):
 # (CLIP [2,77,768]: 21 vs 27 us), the 8k-32k-row level-0/1 projections lose (GEGLU [32768, 320 ->
 # 2560]: 159 + 13 vs 137 + 17 us) - the epilogue of those short-K GEMMs is already their bottleneck.
 LN_FOLD_MAX_ROWS = 2048
+# Narrow consumers (N <= LN_FOLD_NARROW_N: the attention Q / QKV projections) fold at any row count when
+# ARB_LN_FOLD_NARROW=1: their epilogues are small next to the LN pass they replace (A/B switch).
+LN_FOLD_NARROW_N = int(os.environ.get("ARB_LN_FOLD_NARROW_N", "1920"))
+_LN_FOLD_NARROW = os.environ.get("ARB_LN_FOLD_NARROW", "0") == "1"
 
 
 def _ln_fold_ok(x, w, geglu):
+    rows_ok = _plan_rows(x) <= LN_FOLD_MAX_ROWS or (_LN_FOLD_NARROW and not geglu and w.shape[0] <= LN_FOLD_NARROW_N)
     return (_hip(x) and x.dtype == torch.bfloat16 and _gemm_ok(x.shape[-1], w.shape[0]) and x.shape[-1] <= 2048
-            and _plan_rows(x) <= LN_FOLD_MAX_ROWS
-            and (not geglu or w.shape[0] % 16 == 0) and "lnfold" not in _EXP_SKIP)
+            and rows_ok and (not geglu or w.shape[0] % 16 == 0) and "lnfold" not in _EXP_SKIP)
 
 
 def ln_linear(x, gamma, beta, eps, w, b=None, residual=None, act=None):

@@ -35,6 +35,7 @@ _SIGS = {
     "arb_norm_table_apply": (c_int, [c_void_p] * 3 + [c_int, c_long, c_int, c_int, c_void_p]),
     "arb_conv2d_nhwc": (c_int, [c_void_p] * 8 + [c_int] * 12 + [c_void_p]),
     "arb_set_gn_table_lds": (None, [c_int]),
+    "arb_set_attn_pp": (None, [c_int]),
     "arb_conv2d_nhwc_tld": (c_int, [c_void_p] * 4 + [c_int] + [c_void_p] * 4 + [c_int] * 12 + [c_void_p]),
     "arb_conv2d_nhwc_f16": (c_int, [c_void_p] * 7 + [c_int] * 11 + [c_void_p]),
     "arb_group_norm_table": (c_int, [c_void_p] * 4 + [c_float] + [c_void_p] * 2 + [c_int] * 4 + [c_float, c_void_p]),

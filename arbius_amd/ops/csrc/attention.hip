@@ -61,7 +61,7 @@ __device__ __attribute__((aligned(16))) uint4 g_attn_ones[1] = {{0x3F80u, 0u, 0u
 // by (row & 7) on the SOURCE address (lane-linear LDS image, rule 21) and on the QK read; V rows
 // are VROW/8 chunks, already lane-linear; padding chunks read a zero page, V's row-sum column a
 // ones page.  One LDS array for everything (hipcc's vmcnt trap with two __shared__ objects).
-template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false>
+template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false, bool PP = false>
 __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   static_assert(!GLDS || KSTEPS == 2, "LDS-DMA staging: 8-chunk K rows only");
   constexpr int KROW = GLDS ? KSTEPS * 32 : KSTEPS * 32 + 8;   // K tile row (elements)
@@ -243,11 +243,8 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     }
   };
 
-  auto compute = [&](int kv0, const bf16_t* cK, const bf16_t* cV) __attribute__((always_inline)) {
-    const bool full = !a.causal && kv0 + KV_BLK <= a.Nk;
-
-    // ---- S^T tiles: 4 key tiles x QT query tiles
-    f32x4 st[QT][4];
+  // ---- S^T tiles of one 64-key tile: 4 key tiles x QT query tiles
+  auto qk = [&](const bf16_t* cK, f32x4 (&st)[QT][4]) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
@@ -262,72 +259,72 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
           st[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][s], st[qt][t], 0, 0, 0);
       }
     }
+  };
 
-    // ---- online softmax (per query column = lane&15)
-    bf16x8 pf[QT][2];
+  // ---- online softmax of one query tile (per query column = lane&15): P^T fragments, and the
+  // running max / sum update; returns whether O needs the rescale by alpha (any lane)
+  auto softmax = [&](int kv0, int qt, f32x4 (&st)[QT][4], bf16x8 (&pf)[QT][2],
+                     float& alpha) __attribute__((always_inline)) {
+    const bool full = !a.causal && kv0 + KV_BLK <= a.Nk;
+    if (!full) {
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-      if (!full) {
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kv0 + 16 * t + 4 * g + r;
-            const bool masked = key >= a.Nk || (a.causal && key > qidx[qt]);
-            st[qt][t][r] = masked ? -INFINITY : st[qt][t][r];
-          }
-      }
-      float mloc = fmaxf(fmaxf(st[qt][0][0], st[qt][0][1]), fmaxf(st[qt][0][2], st[qt][0][3]));
-#pragma unroll
-      for (int t = 1; t < 4; ++t)
-        mloc = fmaxf(mloc, fmaxf(fmaxf(st[qt][t][0], st[qt][t][1]), fmaxf(st[qt][t][2], st[qt][t][3])));
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      // lazy rescale (T13): keep the running max unless it grew by > 8 (log2 units), so
-      // p <= 2^8; the O/l rescale then runs only on the (rare) tiles where some lane needs it.
-      const float m_cand = mloc * a.scale_log2;
-      const bool need = m_cand > m_run[qt] + 8.f;
-      float alpha = 1.f;
-      if (need) {
-        alpha = (m_run[qt] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run[qt] - m_cand);
-        m_run[qt] = m_cand;
-      }
-      const float m_use = (m_run[qt] == -INFINITY) ? 0.f : m_run[qt];
-      if (ONES) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            st[qt][t][r] = __builtin_amdgcn_exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
-      } else {
-        float lsum = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
-            st[qt][t][r] = p;
-            lsum += p;
-          }
-        l_run[qt] = l_run[qt] * alpha + lsum;
-      }
-      if (__any(need)) {
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) o[qt][dt] *= alpha;
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 p;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          p[j] = (__bf16)st[qt][2 * ks][j];
-          p[j + 4] = (__bf16)st[qt][2 * ks + 1][j];
+        for (int r = 0; r < 4; ++r) {
+          const int key = kv0 + 16 * t + 4 * g + r;
+          const bool masked = key >= a.Nk || (a.causal && key > qidx[qt]);
+          st[qt][t][r] = masked ? -INFINITY : st[qt][t][r];
         }
-        pf[qt][ks] = p;
-      }
     }
+    float mloc = fmaxf(fmaxf(st[qt][0][0], st[qt][0][1]), fmaxf(st[qt][0][2], st[qt][0][3]));
+#pragma unroll
+    for (int t = 1; t < 4; ++t)
+      mloc = fmaxf(mloc, fmaxf(fmaxf(st[qt][t][0], st[qt][t][1]), fmaxf(st[qt][t][2], st[qt][t][3])));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    // lazy rescale (T13): keep the running max unless it grew by > 8 (log2 units), so
+    // p <= 2^8; the O/l rescale then runs only on the (rare) tiles where some lane needs it.
+    const float m_cand = mloc * a.scale_log2;
+    const bool need = m_cand > m_run[qt] + 8.f;
+    alpha = 1.f;
+    if (need) {
+      alpha = (m_run[qt] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run[qt] - m_cand);
+      m_run[qt] = m_cand;
+    }
+    const float m_use = (m_run[qt] == -INFINITY) ? 0.f : m_run[qt];
+    if (ONES) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          st[qt][t][r] = __builtin_amdgcn_exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
+    } else {
+      float lsum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[qt][t][r], a.scale_log2, -m_use));
+          st[qt][t][r] = p;
+          lsum += p;
+        }
+      l_run[qt] = l_run[qt] * alpha + lsum;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 p;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        p[j] = (__bf16)st[qt][2 * ks][j];
+        p[j + 4] = (__bf16)st[qt][2 * ks + 1][j];
+      }
+      pf[qt][ks] = p;
+    }
+    return __any(need);
+  };
 
-    // ---- O^T += V^T P^T  (A = V^T via transposing LDS reads)
+  // ---- O^T += V^T P^T  (A = V^T via transposing LDS reads)
+  auto pv = [&](const bf16_t* cV, const bf16x8 (&pf)[QT][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
@@ -346,8 +343,88 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       }
     }
   };
+  auto rescale = [&](int qt, float alpha) __attribute__((always_inline)) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[qt][dt] *= alpha;
+  };
 
-  if constexpr (GLDS) {
+  auto compute = [&](int kv0, const bf16_t* cK, const bf16_t* cV) __attribute__((always_inline)) {
+    f32x4 st[QT][4];
+    bf16x8 pf[QT][2];
+    qk(cK, st);
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      float alpha;
+      if (softmax(kv0, qt, st, pf, alpha)) rescale(qt, alpha);
+    }
+    pv(cV, pf);
+  };
+
+  if constexpr (GLDS && PP) {
+    // Software-pipelined K / V rings (bitwise the same arithmetic on O as the plain loop: O sees
+    // *alpha_j then +PV_j in the same order): iteration j runs QK(j) on K(j) while the MFMAs of
+    // PV(j-1) on V(j-1) (from the previous iteration's P) keep the matrix core busy through the
+    // softmax VALU of tile j.  V lags K by one tile: K(j+1) and V(j) are in flight during
+    // iteration j, in the stage whose previous occupant was last read in iteration j-1 (K) / j-2
+    // (V) - both retired by the barrier that opens iteration j.
+    auto issue_k = [&](int kv, bf16_t* dst) __attribute__((always_inline)) {
+      const long ko = (long)kv * a.k_sn;
+#pragma unroll
+      for (int i = 0; i < KBW; ++i) {
+        const void* src = (gkm[i] && kv + gkr[i] < a.Nk) ? (const void*)(gk[i] + ko) : (const void*)g_attn_zero;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (wave + 4 * i) * 512), 16, 0, 0);
+      }
+    };
+    auto issue_v = [&](int kv, bf16_t* dst) __attribute__((always_inline)) {
+      const long vo = (long)kv * a.v_sn;
+#pragma unroll
+      for (int i = 0; i < VBW; ++i) {
+        const void* src = gvm[i] == 2 ? (const void*)g_attn_ones
+                          : (gvm[i] == 1 && kv + gvr[i] < a.Nk) ? (const void*)(gv[i] + vo) : (const void*)g_attn_zero;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + KV_BLK * KROW + gvb[i] * 512), 16, 0, 0);
+      }
+    };
+    bf16x8 pprev[QT][2];
+    // one pipelined iteration on tile kv0 (stage roles static: CUR holds K(kv0), OTH holds V(kv0 - 64))
+    auto step = [&](int kv0, bf16_t* cur, bf16_t* oth, bool first) __attribute__((always_inline)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kv0 + KV_BLK < kv_end) issue_k(kv0 + KV_BLK, oth);
+      issue_v(kv0, cur);
+      f32x4 st[QT][4];
+      bf16x8 pf[QT][2];
+      qk(cur, st);
+      if (!first) pv(oth + KV_BLK * KROW, pprev);
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        float alpha;
+        if (softmax(kv0, qt, st, pf, alpha)) rescale(qt, alpha);
+      }
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        pprev[qt][0] = pf[qt][0];
+        pprev[qt][1] = pf[qt][1];
+      }
+    };
+    if (kv_end > 0) {
+      issue_k(0, sS0);
+      int kv0 = 0;
+      step(0, sS0, sS1, true);
+      for (kv0 = KV_BLK; kv0 + KV_BLK < kv_end; kv0 += 2 * KV_BLK) {
+        step(kv0, sS1, sS0, false);
+        step(kv0 + KV_BLK, sS0, sS1, false);
+      }
+      // tail: at most one more K tile, then the last tile's PV (its V went to the stage of its K)
+      bf16_t* vlast = sS0;
+      if (kv0 < kv_end) {
+        step(kv0, sS1, sS0, false);
+        vlast = sS1;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      pv(vlast + KV_BLK * KROW, pprev);
+    }
+  } else if constexpr (GLDS) {
     // stage roles are static (loop unrolled by 2): DMA into one stage while the other is read;
     // a stage is refilled only after the barrier that retired its last reads
     if (kv_end > 0) issue_kv(0, sS0);
@@ -426,6 +503,18 @@ static bool attn_glds_enabled() {
   return on;
 }
 
+// A/B switch (bitwise-equal paths): ARB_ATTN_PP=1 runs the software-pipelined K / V ring (PV of
+// tile j-1 overlapped with QK and softmax of tile j) on the LDS-DMA kernels
+static int g_attn_pp = -1;
+static bool attn_pp_enabled() {
+  if (g_attn_pp < 0) {
+    const char* e = std::getenv("ARB_ATTN_PP");
+    g_attn_pp = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return g_attn_pp == 1;
+}
+ARB_API void arb_set_attn_pp(int on) { g_attn_pp = on ? 1 : 0; }
+
 template <int KSTEPS, int DT, int QT>
 static void launch_fa(const AttnArgs& a, hipStream_t s) {
   constexpr int QBLK = 4 * QT * 16;
@@ -433,6 +522,15 @@ static void launch_fa(const AttnArgs& a, hipStream_t s) {
   dim3 grid(nqb * a.H * a.B);
   if constexpr (KSTEPS == 2) {
     if (a.Np == 0 && attn_glds_enabled()) {     // LDS-DMA staging (no prefix segment)
+      // pipelined variants that fit the 256-VGPR budget of two waves per SIMD without spilling
+      // (the 4-q-tile d = 48 / 64 ones carry two S tile sets + P(j-1) past it)
+      if constexpr (QT <= 2 || DT == 3) {
+        if (attn_pp_enabled() && (QT <= 2 || (a.D & 15))) {
+          if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true, true><<<grid, 256, 0, s>>>(a);
+          else if constexpr (QT <= 2) flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, true><<<grid, 256, 0, s>>>(a);
+          return;
+        }
+      }
       if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true><<<grid, 256, 0, s>>>(a);
       else flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true><<<grid, 256, 0, s>>>(a);
       return;

@@ -248,9 +248,12 @@ struct DgfArgs {
   float w3[4 * 16], b3[4];
 };
 
-// per low-res pixel: y = proj(hid) (fgr residual 3 | alpha 1), x = [small, mean(small)] -> xy [P, 8] fp32
+// per low-res pixel: y = proj(hid) (fgr residual 3 | alpha 1), x = [small, mean(small)] -> xy [P, 8] fp32.
+// direct (no downsampling, ratio 1: the network ran at full resolution, no guided filter): write the
+// affine map A = 0, b = y straight to xy, so rvm_dgf_out composes fgr = src + residual, alpha = y[3].
 __global__ void __launch_bounds__(256) rvm_dgf_base(const h16* __restrict__ hid, const h16* __restrict__ small,
-                                                    const DgfArgs* __restrict__ a, float* __restrict__ xy, long P) {
+                                                    const DgfArgs* __restrict__ a, float* __restrict__ xy, long P,
+                                                    int direct) {
   for (long p = (long)blockIdx.x * 256 + threadIdx.x; p < P; p += (long)gridDim.x * 256) {
     float hv[16];
 #pragma unroll
@@ -258,6 +261,7 @@ __global__ void __launch_bounds__(256) rvm_dgf_base(const h16* __restrict__ hid,
     float o[8];
     const float s0 = (float)small[p * 3], s1 = (float)small[p * 3 + 1], s2 = (float)small[p * 3 + 2];
     o[0] = s0; o[1] = s1; o[2] = s2; o[3] = (s0 + s1 + s2) * (1.f / 3.f);
+    if (direct) o[0] = o[1] = o[2] = o[3] = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float acc = a->bp[j];
@@ -483,12 +487,15 @@ ARB_API int arb_rvm_dgf(const void* hid, const void* small, const void* dgf_args
                         const void* src, void* dst, int T, int H, int W, int h, int w, int mode, float g0, float g1,
                         float g2, hipStream_t s) {
   const long P = (long)T * h * w;
+  const int direct = h == H && w == W;      // full-resolution network (inputs <= 512 px): no guided filter
   rvm_dgf_base<<<rgrid(P), 256, 0, s>>>((const h16*)hid, (const h16*)small, (const DgfArgs*)dgf_args_dev, (float*)xy,
-                                         P);
-  rvm_dgf_ab<<<rgrid(P), 256, 0, s>>>((const float*)xy, (const h16*)hid, (const DgfArgs*)dgf_args_dev, (float*)ab, T,
-                                       h, w);
-  rvm_dgf_out<<<rgrid((long)T * H * W), 256, 0, s>>>((const uint8_t*)src, (const float*)ab, (uint8_t*)dst, T, H, W, h,
-                                                      w, (float)h / (float)H, (float)w / (float)W, mode, g0, g1, g2);
+                                         P, direct);
+  if (!direct)
+    rvm_dgf_ab<<<rgrid(P), 256, 0, s>>>((const float*)xy, (const h16*)hid, (const DgfArgs*)dgf_args_dev, (float*)ab,
+                                         T, h, w);
+  rvm_dgf_out<<<rgrid((long)T * H * W), 256, 0, s>>>((const uint8_t*)src, (const float*)(direct ? xy : ab),
+                                                      (uint8_t*)dst, T, H, W, h, w, (float)h / (float)H,
+                                                      (float)w / (float)W, mode, g0, g1, g2);
   return (int)hipGetLastError();
 }
 

@@ -48,6 +48,8 @@ def parse_args(argv=None):
                     help="SD family: tasks solved lock-step per stream (one batch-2k UNet launch sequence; "
                          "batch-invariant plans keep every CID equal to its solo solve)")
     ap.add_argument("--res", type=int, default=None, help="default 512 (anythingv3) / 768 (kandinsky2)")
+    ap.add_argument("--height", type=int, default=None,
+                    help="image height when it differs from --res (default: --res; zeroscope 320, matting 1080)")
     ap.add_argument("--denoise-steps", type=int, default=None, help="default 50 / 100")
     ap.add_argument("--scheduler", default="DPMSolverMultistep")
     ap.add_argument("--guidance", type=float, default=12.0)
@@ -71,7 +73,7 @@ def parse_args(argv=None):
     args.frames = args.frames or (48 if rvm else 24)
     args.res = args.res or (768 if k2 else 576 if args.model == "zeroscopev2xl" else 256 if vid else
                             1920 if rvm else 512)
-    args.height = 320 if args.model == "zeroscopev2xl" else 1080 if rvm else args.res
+    args.height = args.height or (320 if args.model == "zeroscopev2xl" else 1080 if rvm else args.res)
     args.denoise_steps = args.denoise_steps or (100 if k2 else 50)
     return args
 
@@ -178,7 +180,7 @@ def run(args):
             pipe.cfg.num_steps = args.denoise_steps
             tids = [tid_of(i, j) for j in range(max(1, args.group))]
             inps = [{"prompt": f"a red cat sitting on a castle wall, oil painting, task {i}.{j}",
-                     "width": args.res, "height": args.res, "seed": taskid2seed(t)} for j, t in enumerate(tids)]
+                     "width": args.res, "height": args.height, "seed": taskid2seed(t)} for j, t in enumerate(tids)]
             if tail is not None and len(inps) > 1:
                 from arbius_amd.node.solver import infer_images
                 return tail.submit(finish_group, t0, tids, *infer_images(pipe, inps))
@@ -188,7 +190,7 @@ def run(args):
             tids = [tid_of(i, j) for j in range(max(1, args.group))]
             inps = [{"prompt": f"a detailed anime illustration of a castle on a hill, task {i}.{j}",
                      "negative_prompt": "lowres, bad anatomy, bad hands, text, error",
-                     "width": args.res, "height": args.res, "num_inference_steps": args.denoise_steps,
+                     "width": args.res, "height": args.height, "num_inference_steps": args.denoise_steps,
                      "guidance_scale": args.guidance, "scheduler": args.scheduler,
                      "seed": taskid2seed(t)} for j, t in enumerate(tids)]
             if tail is not None and len(inps) > 1:
@@ -294,7 +296,7 @@ def run(args):
                 "streams_per_gpu": C,
                 "lockstep_group": G,
                 "seq_len": (args.res // 8) * (args.height // 8),
-                "resolution": f"{args.res}x{args.height}" if (vid or rvm) else args.res,
+                "resolution": f"{args.res}x{args.height}" if (vid or rvm or args.height != args.res) else args.res,
                 "denoise_steps": None if rvm else args.denoise_steps,
                 "scheduler": None if rvm else "p_sampler" if k2 else "DPMSolverMultistep" if vid else args.scheduler,
                 "cfg_batch": 1 if rvm else 2,
@@ -312,6 +314,7 @@ def run(args):
                                  "backend": D.backend_name()},
             "world": winfo,
             "init_s": round(t_init, 2),
+            "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if dev.type == "cuda" else None,
             "native_kernels_loaded": ops.native_loaded(),
             "reference_ops": bool(args.reference_ops),
         }

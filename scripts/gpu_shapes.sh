@@ -2,18 +2,20 @@
 # Per-shape evidence on one MI355X: layer_prof tables (every conv / GEMM / attention / norm launch
 # with shape, tile family, split-K, us and TFLOP/s) for SD1.5 and Kandinsky2 at the lock-step batch
 # (group of 4 = batch 8) and solo (batch 2), and a rocprofv3 kernel summary of the 2-stream K2 bench.
+# MODELS / LP_GROUPS / SKIP_PROF select a subset; EXTRA_ENV (e.g. ARB_ATTN_PP=1) runs a tagged variant.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-shapes}
 mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)"; }
-for m in anythingv3 kandinsky2; do
-  for g in 4 1; do
-    step "layer_prof $m g$g"
-    timeout -k 10 300 python scripts/layer_prof.py --model $m --group $g --steps 2 --md $O/shapes_${m}_g$g.md \
-      --json $O/shapes_${m}_g$g.jsonl > $O/lp_${m}_g$g.log 2>&1 || { tail -30 $O/lp_${m}_g$g.log; exit 1; }
-    head -3 $O/shapes_${m}_g$g.md | cut -c1-300
+for m in ${MODELS:-anythingv3 kandinsky2}; do
+  for g in ${LP_GROUPS:-4 1}; do
+    step "layer_prof $m g$g ${TAGV:-}"
+    env ${EXTRA_ENV:-ARBIUS_NOP=1} timeout -k 10 300 python scripts/layer_prof.py --model $m --group $g --steps 2 \
+      --md $O/shapes_${m}_g$g${TAGV:-}.md --json $O/shapes_${m}_g$g${TAGV:-}.jsonl > $O/lp_${m}_g$g${TAGV:-}.log 2>&1 \
+      || { tail -30 $O/lp_${m}_g$g${TAGV:-}.log; exit 1; }
+    head -1 $O/shapes_${m}_g$g${TAGV:-}.md | cut -c1-300
   done
 done
 if [ "${SKIP_PROF:-0}" != "1" ]; then

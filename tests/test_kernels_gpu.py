@@ -664,3 +664,27 @@ def test_temporal_attention_long_clips_via_flash(cuda, F):
     r = ref.temporal_attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D))
     assert o.shape == (B, F, P, H, D) and _rel(o, r) < 2e-2
     assert torch.equal(o, ops.temporal_attention(q, k, v))
+
+
+@pytest.mark.parametrize("B,N,Nk,H,D,causal", [(8, 4096, 4096, 8, 40, False), (2, 4096, 4096, 8, 40, False),
+                                               (8, 1024, 1024, 8, 80, False), (2, 77, 77, 12, 64, True),
+                                               (2, 2304, 2304, 10, 64, False), (4, 300, 333, 5, 64, False),
+                                               (16, 64, 64, 2, 40, False), (2, 130, 130, 3, 40, True)])
+def test_flash_attention_pipelined_ring_bitwise(cuda, B, N, Nk, H, D, causal):
+    """The software-pipelined K / V ring (PV of tile j-1 under QK + softmax of tile j) applies the
+    same *alpha / +PV sequence to O as the plain loop: outputs bitwise equal."""
+    torch.manual_seed(21)
+    q = torch.randn(B, N, H, D, device=cuda).bfloat16()
+    k = torch.randn(B, Nk, H, D, device=cuda).bfloat16() * 1.5
+    v = torch.randn(B, Nk, H, D, device=cuda).bfloat16()
+    fn = _lib._fn("arb_set_attn_pp")
+    try:
+        fn(0)
+        plain = _lib.flash_attention(q, k, v, 1 / math.sqrt(D), causal)
+        fn(1)
+        piped = _lib.flash_attention(q, k, v, 1 / math.sqrt(D), causal)
+    finally:
+        fn(0)
+    assert torch.equal(plain, piped)
+    r = ref.attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), causal)
+    assert _rel(piped, r) < 2e-2

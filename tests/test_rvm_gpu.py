@@ -86,14 +86,17 @@ def test_conv_ex_padded_channels_and_act(cuda, cx, co, k, stride, act, res):
     assert _rel(y, ref) < 1e-2
 
 
-def test_fast_matting_matches_reference_network(cuda):
+@pytest.mark.parametrize("H,W", [(360, 640), (240, 320), (200, 176)])
+def test_fast_matting_matches_reference_network(cuda, H, W):
     """The whole fast path (stem, encoder with fused epilogues, pooled pyramid, upcat, in-place
-    ConvGRU over 2 chunks, guided filter, composite) against the PyTorch-op network in fp32."""
+    ConvGRU over 2 chunks, guided filter - or, for inputs <= 512 px, the full-resolution head -
+    composite) against the PyTorch-op network in fp32."""
     from arbius_amd.models.rvm import RVMConfig, RVMPipeline
     cfg = RVMConfig(chunk=4)
     fast = RVMPipeline(cfg, device=cuda)
+    assert fast._fast_ok(min(1.0, cfg.max_side / max(H, W)))
     rng = np.random.default_rng(3)
-    yy, xx = np.mgrid[0:360, 0:640]
+    yy, xx = np.mgrid[0:H, 0:W]
     base = ((xx[None] + 9 * np.arange(6)[:, None, None]) % 256).astype(np.uint8)
     clip = np.stack([base, (yy[None] % 256).astype(np.uint8).repeat(6, 0),
                      rng.integers(0, 256, base.shape, dtype=np.uint8)], axis=-1)
