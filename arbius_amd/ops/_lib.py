@@ -48,7 +48,7 @@ _SIGS = {
     "arb_convgru_gates": (c_int, [c_int] + [c_void_p] * 4 + [c_long, c_int, c_int, c_int, c_void_p]),
     "arb_sampler_step": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "arb_dwconv_f16": (c_int, [c_void_p] * 4 + [c_int] * 8 + [c_void_p]),
-    "arb_softmax_rows": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "arb_softmax_rows": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p]),
     "arb_group_norm_table_cat": (c_int, [c_void_p] * 2 + [c_int] + [c_void_p] * 3 + [c_float] + [c_void_p] * 2
                                  + [c_int] * 4 + [c_float, c_void_p]),
     "arb_norm_table_apply_cat": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_long, c_int, c_int,
@@ -265,38 +265,41 @@ def temporal_attention(q, k, v, scale):
     return o
 
 
-def softmax_rows(s, scale):
-    """P = softmax(scale * S) over the last dim (csrc/elementwise.hip), S bf16 [..., N], N % 8 == 0."""
+def softmax_rows(s, scale, valid=None):
+    """P = softmax(scale * S) over the first `valid` columns of the last dim (default all; the rest
+    written 0) (csrc/elementwise.hip), S bf16 [..., N], N % 8 == 0."""
     _bf16(s)
     s = s.contiguous()
     N = s.shape[-1]
     p = torch.empty_like(s)
-    _check(_fn("arb_softmax_rows")(_p(s), _p(p), s.numel() // N, N, float(scale), _stream()), "softmax_rows")
+    _check(_fn("arb_softmax_rows")(_p(s), _p(p), s.numel() // N, N, N if valid is None else int(valid),
+                                   float(scale), _stream()), "softmax_rows")
     return p
 
 
 def _large_head_attention(q, k, v, scale):
     """Head dims > 160 (the single-head d = 512 VAE / MoVQ mid-block attention, once per task):
     S = Q K^T on the implicit-GEMM kernel, the HIP row softmax, O = P V on the implicit-GEMM kernel
-    (per batch and head; V^T made contiguous once).  Shapes the GEMM does not tile (Nk or D not a
-    multiple of 64) take the library GEMMs around an fp32 softmax."""
+    (per batch and head; V^T made contiguous once).  Key counts off the 64-tile are zero-padded: the
+    padded score columns are excluded by the softmax (written 0), so P V never sees them."""
     B, Nq, H, D = q.shape
     Nk = k.shape[1]
-    if D % 64 == 0 and Nk % 64 == 0:
-        o = torch.empty(B, Nq, H, D, dtype=q.dtype, device=q.device)
-        for b in range(B):
-            for h in range(H):
-                s = gemm(q[b, :, h], k[b, :, h].contiguous())                 # [Nq, Nk] = q k^T
-                o[b, :, h] = gemm(softmax_rows(s, scale), v[b, :, h].t().contiguous())
-        return o
-    from . import _library
-    _library("attention", f"head dim {D} with {Nk} keys (the GEMM path needs D % 64 == Nk % 64 == 0)")
-    qf = q.transpose(1, 2)
-    kf = k.transpose(1, 2)
-    vf = v.transpose(1, 2)
-    s = torch.matmul(qf, kf.transpose(-1, -2)).float() * scale
-    p = torch.softmax(s, dim=-1).to(q.dtype)
-    return torch.matmul(p, vf).transpose(1, 2).contiguous()
+    if D % 64:
+        from . import _library
+        _library("attention", f"head dim {D} (the GEMM path needs D % 64 == 0)")
+        qf, kf, vf = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        s = torch.matmul(qf, kf.transpose(-1, -2)).float() * scale
+        return torch.matmul(torch.softmax(s, dim=-1).to(q.dtype), vf).transpose(1, 2).contiguous()
+    Np = -(-Nk // 64) * 64
+    if Np != Nk:
+        k = torch.nn.functional.pad(k, (0, 0, 0, 0, 0, Np - Nk))
+        v = torch.nn.functional.pad(v, (0, 0, 0, 0, 0, Np - Nk))
+    o = torch.empty(B, Nq, H, D, dtype=q.dtype, device=q.device)
+    for b in range(B):
+        for h in range(H):
+            s = gemm(q[b, :, h], k[b, :, h].contiguous())                     # [Nq, Np] = q k^T
+            o[b, :, h] = gemm(softmax_rows(s, scale, Nk), v[b, :, h].t().contiguous())
+    return o
 
 
 # --------------------------------------------------------------------------- ConvGRU (fp16)

@@ -140,12 +140,13 @@ static bool apply2_on() {
   return on;
 }
 
-// Row softmax of a score matrix: P = softmax(scale * S) per row, S / P [R, N] bf16 (N % 8 == 0), fp32
+// Row softmax of a score matrix: P = softmax(scale * S) per row over the first nv columns (the rest
+// of the row, key padding up to the GEMM tile, is written 0), S / P [R, N] bf16 (N % 8 == 0), fp32
 // math, one wave per row (three sweeps of the row: max, sum of exp, write; the row stays in L1/L2).
 // The middle launch of the large-head attention (d = 512 single-head VAE / MoVQ mid-block
 // attention): S = Q K^T and O = P V run on the implicit-GEMM kernel.  Fixed reduction order.
 __global__ void __launch_bounds__(256) softmax_rows_kernel(const bf16_t* __restrict__ s, bf16_t* __restrict__ p,
-                                                           int R, int N, float scale) {
+                                                           int R, int N, int nv, float scale) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= R) return;
   const bf16_t* sr = s + (size_t)row * N;
@@ -155,7 +156,7 @@ __global__ void __launch_bounds__(256) softmax_rows_kernel(const bf16_t* __restr
     float f[8];
     unpack8(ld16(sr + c), f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) m = fmaxf(m, f[e] * scale);
+    for (int e = 0; e < 8; ++e) m = c + e < nv ? fmaxf(m, f[e] * scale) : m;
   }
   m = wave_max(m);
   float sum = 0.f;
@@ -163,21 +164,21 @@ __global__ void __launch_bounds__(256) softmax_rows_kernel(const bf16_t* __restr
     float f[8];
     unpack8(ld16(sr + c), f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) sum += __expf(f[e] * scale - m);
+    for (int e = 0; e < 8; ++e) sum += c + e < nv ? __expf(f[e] * scale - m) : 0.f;
   }
   const float inv = 1.f / wave_sum(sum);
   for (int c = lane * 8; c < N; c += 512) {
     float f[8];
     unpack8(ld16(sr + c), f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = __expf(f[e] * scale - m) * inv;
+    for (int e = 0; e < 8; ++e) f[e] = c + e < nv ? __expf(f[e] * scale - m) * inv : 0.f;
     st16(pr + c, pack8(f));
   }
 }
 
-ARB_API int arb_softmax_rows(const void* s, void* p, int R, int N, float scale, hipStream_t stream) {
-  if (N % 8 != 0 || R <= 0) return -1;
-  softmax_rows_kernel<<<(R + 3) / 4, 256, 0, stream>>>((const bf16_t*)s, (bf16_t*)p, R, N, scale);
+ARB_API int arb_softmax_rows(const void* s, void* p, int R, int N, int nv, float scale, hipStream_t stream) {
+  if (N % 8 != 0 || R <= 0 || nv <= 0 || nv > N) return -1;
+  softmax_rows_kernel<<<(R + 3) / 4, 256, 0, stream>>>((const bf16_t*)s, (bf16_t*)p, R, N, nv, scale);
   return (int)hipGetLastError();
 }
 

@@ -16,7 +16,7 @@ if [ $rc -ne 0 ]; then grep -B5 -A40 "^E " $O/pytest_gpu.log | head -120; exit $
 step smoke
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log | cut -c1-200
-for v in default 1x1 pp lnfold; do
+for v in ${VARIANTS:-default 1x1 lnfold}; do
   step "bench $v"
   if [ $v = default ]; then
     timeout -k 10 400 python bench.py --steps 12 --warmup 3 > $O/bench_$v.log 2>$O/bench_$v.err || { tail -20 $O/bench_$v.err; exit 1; }
