@@ -62,24 +62,14 @@ class SSResBlock(nn.Module):
         self.up, self.down = up, down
         self.cout = cout
 
-    @staticmethod
-    def _resample(x, up, down):
-        if up:
-            return x.repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
-        if down:
-            B, H, W, C = x.shape
-            return x.view(B, H // 2, 2, W // 2, 2, C).float().mean(dim=(2, 4)).to(x.dtype)
-        return x
-
     def forward(self, x, emb_act):
-        if self.down:                                   # avg-pool does not commute with SiLU
-            h = self._resample(self.norm1(x), False, True)
-            x = self._resample(x, False, True)
+        if self.down:                                   # avg-pool does not commute with SiLU:
+            h, x = ops.pool2(x, self.norm1.table(x))    # pool(GN+SiLU(x)) and pool(x), one pass
             h = self.conv1(h)
         else:                                           # GN+SiLU (and nearest-up) fused into conv1
             h = self.conv1(x, upsample=self.up, norm=self.norm1.table(x))
             if self.up:
-                x = self._resample(x, True, False)
+                x = ops.upsample2(x)
         ss = self.emb(emb_act)                          # [B, 2C] = [scale | shift]
         # scale-shift norm + SiLU folded into one per-(b, c) affine table: conv2's prologue
         norm = self.norm2.table(h, mod=ss, one_plus=1.0, silu=True)

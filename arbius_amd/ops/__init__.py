@@ -530,6 +530,31 @@ def apply_norm_table(x, table, silu=False):
     if silu:
         y = F.silu(y)
     return y.to(x.dtype)
+def pool2(x, norm=None):
+    """2x2 average pool of x (channels-last [B, H, W, C]) and, with ``norm`` (a ``NormSpec`` /
+    ``(table, silu)``), of its GroupNorm(+SiLU) in the same pass: returns (pool(norm(x)), pool(x))
+    (the first is None without ``norm``).  The GLIDE down-sampling ResBlock: both branches pool.
+    The normalised values round to bf16 before pooling, as the unfused norm-then-pool would."""
+    x = materialize(x)
+    table, silu = norm if norm is not None else (None, False)
+    if _hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and x.shape[1] % 2 == 0 and x.shape[2] % 2 == 0:
+        return _lib.norm_pool2(x, table, silu)
+
+    def pool(t):
+        B, H, W, C = t.shape
+        v = t.float().view(B, H // 2, 2, W // 2, 2, C)
+        return (((v[:, :, 0, :, 0] + v[:, :, 0, :, 1]) + (v[:, :, 1, :, 0] + v[:, :, 1, :, 1])) * 0.25).to(t.dtype)
+    return (pool(apply_norm_table(x, table, silu)) if table is not None else None), pool(x)
+
+
+def upsample2(x):
+    """Nearest 2x up-sampling of a channels-last tensor (one HIP pass on the GPU)."""
+    x = materialize(x)
+    if _hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+        return _lib.upsample2(x)
+    return x.repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
+
+
 def group_norm(x, gamma, beta, groups, eps, silu=False):
     if _hip(x):
         return _lib.group_norm_nhwc(x, gamma, beta, groups, eps, silu)

@@ -33,6 +33,8 @@ _SIGS = {
     "arb_geglu": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "arb_silu": (c_int, [c_void_p, c_void_p, c_long, c_void_p]),
     "arb_norm_table_apply": (c_int, [c_void_p] * 3 + [c_int, c_long, c_int, c_int, c_void_p]),
+    "arb_norm_pool2": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "arb_upsample2": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "arb_conv2d_nhwc": (c_int, [c_void_p] * 8 + [c_int] * 12 + [c_void_p]),
     "arb_set_gn_table_lds": (None, [c_int]),
     "arb_set_attn_pp": (None, [c_int]),
@@ -382,6 +384,35 @@ def _cat_parts(x, x2):
     if x.shape[:-1] != x2.shape[:-1] or x.shape[-1] % 64 or x2.shape[-1] % 8:
         raise ValueError(f"channel concat: bad parts {tuple(x.shape)} | {tuple(x2.shape)}")
     return x, x2
+
+
+def norm_pool2(x, table=None, silu=False, raw=True):
+    """2x2 average pool of x [B, H, W, C] (``raw``) and of its GroupNorm-table transform (``table``
+    [B, C, 2] fp32, +SiLU, rounded to bf16 before pooling) in one pass (csrc/elementwise.hip).
+    Returns (pooled normalised or None, pooled x or None)."""
+    _bf16(x)
+    x = x.contiguous()
+    B, H, W, C = x.shape
+    if C % 8 or H % 2 or W % 2 or (table is not None and (tuple(table.shape) != (B, C, 2)
+                                                         or table.dtype != torch.float32)):
+        raise ValueError(f"norm_pool2: unsupported x {tuple(x.shape)}")
+    yn = torch.empty(B, H // 2, W // 2, C, dtype=x.dtype, device=x.device) if table is not None else None
+    yx = torch.empty(B, H // 2, W // 2, C, dtype=x.dtype, device=x.device) if raw else None
+    _check(_fn("arb_norm_pool2")(_p(x), _p(None if table is None else table.contiguous()), int(bool(silu)), _p(yn),
+                                 _p(yx), B, H, W, C, _stream()), "norm_pool2")
+    return yn, yx
+
+
+def upsample2(x):
+    """Nearest 2x up-sampling of a channels-last bf16 tensor [B, H, W, C] -> [B, 2H, 2W, C]."""
+    _bf16(x)
+    x = x.contiguous()
+    B, H, W, C = x.shape
+    if C % 8:
+        raise ValueError(f"upsample2: C % 8 != 0 ({tuple(x.shape)})")
+    y = torch.empty(B, 2 * H, 2 * W, C, dtype=x.dtype, device=x.device)
+    _check(_fn("arb_upsample2")(_p(x), _p(y), B, H, W, C, _stream()), "upsample2")
+    return y
 
 
 def norm_table_apply(x, table, silu=False, x2=None):

@@ -54,6 +54,9 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// round-to-nearest-even to bf16 and back (an intermediate the unfused op would store as bf16)
+__device__ __forceinline__ float bf16_round(float v) { return __uint_as_float((uint32_t)f2bf(v) << 16); }
+
 // raw v_exp_f32 / v_rcp_f32 (no denormal range fix-up sequences; results are bf16-rounded anyway)
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.f + fast_exp(-x)); }

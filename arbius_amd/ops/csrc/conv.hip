@@ -134,7 +134,6 @@ __device__ __forceinline__ void tile_coords(const ConvArgs& p, int BN, int BM, i
   }
 }
 
-__device__ __forceinline__ float bf16_round(float v) { return __uint_as_float((uint32_t)f2bf(v) << 16); }
 
 // Epilogue activation (after bias / temb / residual): 1 ReLU, 2 hardswish (RVM, either dtype);
 // 3 GELU(erf) and 4 quick-GELU x * sigmoid(1.702 x) (text towers / prior MLPs, bf16): the

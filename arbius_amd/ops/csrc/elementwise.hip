@@ -225,3 +225,85 @@ ARB_API int arb_norm_table_apply_cat(const void* x, const void* x2, int C1, void
                                                                 HW, C, total8, silu, (const bf16_t*)x2, C1);
   return (int)hipGetLastError();
 }
+
+// 2x2 average pool (GLIDE down-sampling ResBlock, guided-diffusion AvgPool2d) of x and, with a
+// GroupNorm table, of its normalised form in the same pass: yx = pool(x), yn = pool(bf16(act(x *
+// scale + shift))).  The normalised values are rounded to bf16 before pooling (the unfused
+// norm-then-pool arithmetic); sums in fixed order (p00 + p01) + (p10 + p11), times 0.25 (exact).
+// x [B, H, W, C] (H, W even), yn / yx [B, H/2, W/2, C]; either output may be null.
+__global__ void __launch_bounds__(256) norm_pool2_kernel(const bf16_t* __restrict__ x, const float2* __restrict__ table,
+                                                         int silu, bf16_t* __restrict__ yn, bf16_t* __restrict__ yx,
+                                                         int Ho, int Wo, int C, long total8) {
+  const int CV = C >> 3;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
+    const long pix = i / CV;                     // output pixel (b, oy, ox)
+    const int c = (int)(i - pix * CV) * 8;
+    const long b = pix / ((long)Ho * Wo);
+    const int rem = (int)(pix - b * Ho * Wo), oy = rem / Wo, ox = rem - oy * Wo;
+    const long W = 2L * Wo;
+    const bf16_t* p0 = x + ((b * 2 * Ho + 2 * oy) * W + 2 * ox) * C + c;
+    float f[4][8];
+    unpack8(ld16(p0), f[0]);
+    unpack8(ld16(p0 + C), f[1]);
+    unpack8(ld16(p0 + W * C), f[2]);
+    unpack8(ld16(p0 + W * C + C), f[3]);
+    if (yx != nullptr) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = ((f[0][e] + f[1][e]) + (f[2][e] + f[3][e])) * 0.25f;
+      st16(yx + i * 8, pack8(o));
+    }
+    if (yn != nullptr) {
+      const float2* t = table + b * C + c;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float2 ss = t[e];
+        float q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = fmaf(f[j][e], ss.x, ss.y);
+          q[j] = bf16_round(silu ? silu_f(v) : v);
+        }
+        o[e] = ((q[0] + q[1]) + (q[2] + q[3])) * 0.25f;
+      }
+      st16(yn + i * 8, pack8(o));
+    }
+  }
+}
+
+ARB_API int arb_norm_pool2(const void* x, const void* table, int silu, void* yn, void* yx, int B, int H, int W, int C,
+                           hipStream_t stream) {
+  if (C % 8 != 0 || H % 2 != 0 || W % 2 != 0 || B <= 0 || (yn != nullptr && table == nullptr)) return -1;
+  const long total8 = (long)B * (H / 2) * (W / 2) * (C / 8);
+  norm_pool2_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (const float2*)table, silu, (bf16_t*)yn,
+                                                          (bf16_t*)yx, H / 2, W / 2, C, total8);
+  return (int)hipGetLastError();
+}
+
+// Nearest 2x up-sampling of a channels-last tensor (GLIDE up-sampling ResBlock skip path):
+// y [B, 2H, 2W, C] from x [B, H, W, C]; one read of x, 16-byte stores.
+__global__ void __launch_bounds__(256) upsample2_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int H,
+                                                        int W, int C, long total8) {
+  const int CV = C >> 3;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
+    const long pix = i / CV;                     // input pixel (b, iy, ix)
+    const int c = (int)(i - pix * CV) * 8;
+    const long b = pix / ((long)H * W);
+    const int rem = (int)(pix - b * H * W), iy = rem / W, ix = rem - iy * W;
+    const uint4 v = ld16(x + i * 8);
+    const long W2 = 2L * W;
+    bf16_t* q = y + ((b * 2 * H + 2 * iy) * W2 + 2 * ix) * C + c;
+    st16(q, v);
+    st16(q + C, v);
+    st16(q + W2 * C, v);
+    st16(q + W2 * C + C, v);
+  }
+}
+
+ARB_API int arb_upsample2(const void* x, void* y, int B, int H, int W, int C, hipStream_t stream) {
+  if (C % 8 != 0 || B <= 0) return -1;
+  const long total8 = (long)B * H * W * (C / 8);
+  upsample2_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, H, W, C, total8);
+  return (int)hipGetLastError();
+}

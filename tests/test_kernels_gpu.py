@@ -493,6 +493,30 @@ def test_norm_table_apply(cuda, B, H, W, C, silu):
     assert _rel(y, r) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,W,C,silu", [(8, 96, 96, 384, True), (2, 48, 48, 768, True), (1, 24, 24, 1152, False),
+                                         (3, 6, 10, 64, True)])
+def test_norm_pool2(cuda, B, H, W, C, silu):
+    """GLIDE down-sampling: one pass == fp32 avg-pool of x and of bf16(GN-table transform(x)),
+    bitwise equal to the unfused CPU-order arithmetic on the same bf16 intermediates."""
+    torch.manual_seed(14)
+    x = (torch.randn(B, H, W, C, device=cuda) * 2 + 0.3).bfloat16()
+    table = torch.randn(B, C, 2, device=cuda)
+    yn, yx = _lib.norm_pool2(x, table, silu)
+    pool = torch.nn.functional.avg_pool2d
+    rx = pool(x.float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    rn = pool(ops.apply_norm_table(x.float(), table, silu).bfloat16().float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    assert _rel(yx, rx) < 5e-3 and _rel(yn, rn) < 5e-3
+    yn2, yx2 = ops.pool2(x.cpu(), (table.cpu(), silu))          # CPU path: same formula, fp32
+    assert _rel(yx, yx2.to(cuda)) < 5e-3 and _rel(yn, yn2.to(cuda)) < 1e-2
+    assert torch.equal(yx, _lib.norm_pool2(x, None, False)[1])
+
+
+@pytest.mark.parametrize("B,H,W,C", [(8, 48, 48, 768), (2, 12, 12, 1536), (1, 3, 5, 8)])
+def test_upsample2(cuda, B, H, W, C):
+    x = torch.randn(B, H, W, C, device=cuda).bfloat16()
+    assert torch.equal(ops.upsample2(x), x.repeat_interleave(2, dim=1).repeat_interleave(2, dim=2))
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride", [(12, 72, 128, 64, 128, 3, 1), (12, 36, 64, 80, 40, 1, 1),
                                                      (4, 144, 256, 16, 24, 3, 2), (2, 18, 32, 960, 128, 1, 1),
                                                      (1, 9, 16, 64, 64, 3, 1)])
