@@ -61,7 +61,7 @@ __device__ __attribute__((aligned(16))) uint4 g_attn_ones[1] = {{0x3F80u, 0u, 0u
 // by (row & 7) on the SOURCE address (lane-linear LDS image, rule 21) and on the QK read; V rows
 // are VROW/8 chunks, already lane-linear; padding chunks read a zero page, V's row-sum column a
 // ones page.  One LDS array for everything (hipcc's vmcnt trap with two __shared__ objects).
-template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false, bool PP = false>
+template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false, bool PP = false, bool PS = true>
 __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   static_assert(!GLDS || KSTEPS == 2, "LDS-DMA staging: 8-chunk K rows only");
   constexpr int KROW = GLDS ? KSTEPS * 32 : KSTEPS * 32 + 8;   // K tile row (elements)
@@ -109,6 +109,13 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       const int d = 32 * s + 8 * g;
       uint4 raw = make_uint4(0, 0, 0, 0);
       if (qidx[qt] < a.Nq && d < D) raw = ld16(qbase + (long)qidx[qt] * a.q_sn + d);
+      if constexpr (PS) {   // Q * scale * log2(e), rounded to bf16 once
+        float f[8];
+        unpack8(raw, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] *= a.scale_log2;
+        raw = pack8(f);
+      }
       qf[qt][s] = __builtin_bit_cast(bf16x8, raw);
     }
   }
@@ -245,10 +252,13 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
 
   // ---- S^T tiles of one 64-key tile: 4 key tiles x QT query tiles
   auto qk = [&](const bf16_t* cK, f32x4 (&st)[QT][4]) __attribute__((always_inline)) {
+    float mi[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) mi[qt] = (PS && m_run[qt] != -INFINITY) ? -m_run[qt] : 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
 #pragma unroll
-      for (int qt = 0; qt < QT; ++qt) st[qt][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int qt = 0; qt < QT; ++qt) st[qt][t] = (f32x4){mi[qt], mi[qt], mi[qt], mi[qt]};
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
         const int krw = 16 * t + lq;
@@ -284,6 +294,41 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     // lazy rescale (T13): keep the running max unless it grew by > 8 (log2 units), so
     // p <= 2^8; the O/l rescale then runs only on the (rare) tiles where some lane needs it.
+    if constexpr (PS) {
+      // st = S' - m_use already (log2 units; m_use = 0 before the first finite max)
+      const float m_old = m_run[qt];
+      const float m_cand = (m_old == -INFINITY ? 0.f : m_old) + mloc;
+      const bool need = m_cand > m_old + 8.f;
+      alpha = 1.f;
+      if (need) {
+        alpha = (m_old == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_old - m_cand);
+        m_run[qt] = m_cand;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) st[qt][t][r] -= mloc;
+      }
+      float lsum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          st[qt][t][r] = __builtin_amdgcn_exp2f(st[qt][t][r]);
+          if (!ONES) lsum += st[qt][t][r];
+        }
+      if (!ONES) l_run[qt] = l_run[qt] * alpha + lsum;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 p;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          p[j] = (__bf16)st[qt][2 * ks][j];
+          p[j + 4] = (__bf16)st[qt][2 * ks + 1][j];
+        }
+        pf[qt][ks] = p;
+      }
+      return __any(need);
+    }
     const float m_cand = mloc * a.scale_log2;
     const bool need = m_cand > m_run[qt] + 8.f;
     alpha = 1.f;
@@ -514,9 +559,22 @@ static bool attn_pp_enabled() {
   return g_attn_pp == 1;
 }
 ARB_API void arb_set_attn_pp(int on) { g_attn_pp = on ? 1 : 0; }
+// PS (prescaled-Q softmax, default): Q is scaled by scale * log2(e) once (bf16) and every S^T MFMA
+// chain starts from -m_run, so the accumulators leave the matrix core as exp2 arguments - one VALU
+// op less per score (the fma of the raw-score form).  ARB_ATTN_PRESCALE=0 / arb_set_attn_prescale(0):
+// the raw-score form (different bytes: Q rounds to bf16 after the scale).
+static int g_attn_prescale = -1;
+static bool attn_prescale_enabled() {
+  if (g_attn_prescale < 0) {
+    const char* e = std::getenv("ARB_ATTN_PRESCALE");
+    g_attn_prescale = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_prescale == 1;
+}
+ARB_API void arb_set_attn_prescale(int on) { g_attn_prescale = on ? 1 : 0; }
 
-template <int KSTEPS, int DT, int QT>
-static void launch_fa(const AttnArgs& a, hipStream_t s) {
+template <int KSTEPS, int DT, int QT, bool PS>
+static void launch_fa_ps(const AttnArgs& a, hipStream_t s) {
   constexpr int QBLK = 4 * QT * 16;
   const int nqb = (a.Nq + QBLK - 1) / QBLK;
   dim3 grid(nqb * a.H * a.B);
@@ -524,20 +582,27 @@ static void launch_fa(const AttnArgs& a, hipStream_t s) {
     if (a.Np == 0 && attn_glds_enabled()) {     // LDS-DMA staging (no prefix segment)
       // pipelined variants that fit the 256-VGPR budget of two waves per SIMD without spilling
       // (the 4-q-tile d = 48 / 64 ones carry two S tile sets + P(j-1) past it)
-      if constexpr (QT <= 2 || DT == 3) {
+      if constexpr (PS && (QT <= 2 || DT == 3)) {
         if (attn_pp_enabled() && (QT <= 2 || (a.D & 15))) {
-          if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true, true><<<grid, 256, 0, s>>>(a);
-          else if constexpr (QT <= 2) flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, true><<<grid, 256, 0, s>>>(a);
+          if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true, true, PS><<<grid, 256, 0, s>>>(a);
+          else if constexpr (QT <= 2)
+            flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, true, PS><<<grid, 256, 0, s>>>(a);
           return;
         }
       }
-      if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true><<<grid, 256, 0, s>>>(a);
-      else flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true><<<grid, 256, 0, s>>>(a);
+      if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true, false, PS><<<grid, 256, 0, s>>>(a);
+      else flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, false, PS><<<grid, 256, 0, s>>>(a);
       return;
     }
   }
-  if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true><<<grid, 256, 0, s>>>(a);
-  else flash_attn_fwd_kernel<KSTEPS, DT, QT, false><<<grid, 256, 0, s>>>(a);
+  if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, false, false, PS><<<grid, 256, 0, s>>>(a);
+  else flash_attn_fwd_kernel<KSTEPS, DT, QT, false, false, false, PS><<<grid, 256, 0, s>>>(a);
+}
+
+template <int KSTEPS, int DT, int QT>
+static void launch_fa(const AttnArgs& a, hipStream_t s) {
+  if (attn_prescale_enabled()) launch_fa_ps<KSTEPS, DT, QT, true>(a, s);
+  else launch_fa_ps<KSTEPS, DT, QT, false>(a, s);
 }
 
 // kp/vp (may be null): prefix K/V segment of Np keys with strides pstrides = {kp_sb, kp_sn, vp_sb, vp_sn}

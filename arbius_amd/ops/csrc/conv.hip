@@ -2334,8 +2334,31 @@ struct FamilyPlan {
 };
 #include "conv_family.inc"
 
+// Optional run-time family table (A/B of a re-tuned table without a rebuild): ARB_CONV_FAMILY names a
+// file in conv_family.inc format ("{M, N, K, split, ratio, cfg},"); its entries take precedence.
+static const std::vector<FamilyPlan>& env_families() {
+  static const std::vector<FamilyPlan> fams = [] {
+    std::vector<FamilyPlan> v;
+    const char* path = std::getenv("ARB_CONV_FAMILY");
+    if (path == nullptr || path[0] == 0) return v;
+    FILE* f = std::fopen(path, "r");
+    if (f == nullptr) return v;
+    char line[256];
+    while (std::fgets(line, sizeof line, f)) {
+      FamilyPlan fp;
+      if (std::sscanf(line, " {%d, %d, %d, %d, %d, %d}", &fp.M, &fp.N, &fp.K, &fp.split, &fp.ratio, &fp.cfg) == 6)
+        v.push_back(fp);
+    }
+    std::fclose(f);
+    return v;
+  }();
+  return fams;
+}
+
 ARB_API int arb_conv_family(int M, int N, int K, int split, int ratio, int cfg) {
   if (std::getenv("ARB_NO_FAMILY") != nullptr) return cfg;
+  for (const FamilyPlan& fp : env_families())
+    if (fp.M == M && fp.N == N && fp.K == K && fp.split == split && fp.ratio == ratio) return fp.cfg;
   for (const FamilyPlan& fp : kFamilyPlans)
     if (fp.M == M && fp.N == N && fp.K == K && fp.split == split && fp.ratio == ratio) return fp.cfg;
   return cfg;

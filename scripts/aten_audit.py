@@ -13,7 +13,6 @@ import os
 import sys
 import traceback
 
-import torch
 from torch.utils._python_dispatch import TorchDispatchMode
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

@@ -57,11 +57,11 @@ def collect_shapes(models=("sd15",), res=512, batch=2):
             convs.add((B, H, W, C, w.shape[0], w.shape[1], w.shape[2], padding, int(bool(upsample)), stride))
         return orig_conv(x, w, b, stride, padding, upsample, residual, temb, norm)
 
-    def lin(x, w, b=None, residual=None):
+    def lin(x, w, b=None, residual=None, act=None):
         # every linear: under batch-invariant planning plain projections run on this kernel too
         if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
             gemms.add((x.numel() // x.shape[-1], x.shape[-1], w.shape[0], residual is not None))
-        return orig_lin(x, w, b, residual)
+        return orig_lin(x, w, b, residual, act=act)
 
     ops.conv2d, ops.linear = conv, lin
     try:

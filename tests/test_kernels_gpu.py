@@ -504,7 +504,8 @@ def test_norm_pool2(cuda, B, H, W, C, silu):
     yn, yx = _lib.norm_pool2(x, table, silu)
     pool = torch.nn.functional.avg_pool2d
     rx = pool(x.float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
-    rn = pool(ops.apply_norm_table(x.float(), table, silu).bfloat16().float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    xn = ops.apply_norm_table(x.float(), table, silu).bfloat16().float()
+    rn = pool(xn.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
     assert _rel(yx, rx) < 5e-3 and _rel(yn, rn) < 5e-3
     yn2, yx2 = ops.pool2(x.cpu(), (table.cpu(), silu))          # CPU path: same formula, fp32
     assert _rel(yx, yx2.to(cuda)) < 5e-3 and _rel(yn, yn2.to(cuda)) < 1e-2
@@ -712,3 +713,26 @@ def test_flash_attention_pipelined_ring_bitwise(cuda, B, N, Nk, H, D, causal):
     assert torch.equal(plain, piped)
     r = ref.attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), causal)
     assert _rel(piped, r) < 2e-2
+
+
+@pytest.mark.parametrize("B,N,Nk,H,D,causal", [(8, 4096, 4096, 8, 40, False), (8, 1024, 1024, 8, 80, False),
+                                               (2, 77, 77, 12, 64, True), (2, 256, 256, 8, 160, False),
+                                               (4, 300, 333, 5, 64, False), (2, 130, 130, 3, 40, True)])
+def test_flash_attention_prescaled_q(cuda, B, N, Nk, H, D, causal):
+    """Prescaled-Q softmax (S^T chains start from -m_run, exp2 straight off the accumulators; the
+    default) against the raw-score form and the fp32 reference; deterministic on re-run."""
+    torch.manual_seed(22)
+    q = torch.randn(B, N, H, D, device=cuda).bfloat16()
+    k = torch.randn(B, Nk, H, D, device=cuda).bfloat16()
+    v = torch.randn(B, Nk, H, D, device=cuda).bfloat16()
+    fn = _lib._fn("arb_set_attn_prescale")
+    try:
+        fn(0)
+        raw = ops.attention(q, k, v, causal=causal)
+        fn(1)
+        ps = ops.attention(q, k, v, causal=causal)
+    finally:
+        fn(1)
+    r = ref.attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), causal)
+    assert _rel(ps, r) < 2e-2 and _rel(raw, r) < 2e-2 and _rel(ps, raw) < 1e-2
+    assert torch.equal(ps, ops.attention(q, k, v, causal=causal))
