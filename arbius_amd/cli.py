@@ -72,10 +72,12 @@ def build_pool(cfg, models):
     if n > 1 or (n == 1 and cfg.mi355x.worker_processes):
         from .parallel.workers import MultiGPUSolverPool
         return MultiGPUSolverPool(n, names, "cuda", streams_per_gpu=cfg.mi355x.workers_per_gpu,
+                                  model_streams=cfg.mi355x.model_streams,
                                   lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir,
                                   hang_timeout=cfg.mi355x.hang_timeout_s, force_group=n == 1)
     from .node.pool import LocalSolverPool
     return LocalSolverPool("cuda:0" if n == 1 else "cpu", capacity=cfg.mi355x.workers_per_gpu,
+                           model_streams=cfg.mi355x.model_streams,
                            lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir)
 
 

@@ -13,6 +13,10 @@ from typing import Dict, List, Literal, Optional
 
 from pydantic import BaseModel, ConfigDict, Field, model_validator
 
+# Task streams per GPU where a model's best differs from ``mi355x.workers_per_gpu`` (bench.py sweeps:
+# profiles/bench_r4_stream_group_sweep.md).
+DEFAULT_MODEL_STREAMS = {"kandinsky2": 2, "zeroscopev2xl": 2, "damo": 2, "robust_video_matting": 2}
+
 
 class _Base(BaseModel):
     model_config = ConfigDict(extra="ignore", populate_by_name=True)
@@ -97,8 +101,11 @@ class MI355XConfig(_Base):
     mock_chain: bool = False              # in-process MockEngine (testing / plumbing config)
     selftest: bool = True                 # boot CID self-test (index.ts:981-1001)
     selftest_table: Optional[str] = None  # override of config/selftest.json
-    workers_per_gpu: int = 2              # concurrent task streams per GPU (pipeline forks): the benched
-                                          # default (bench.py --concurrent 2); 1 = latency mode
+    workers_per_gpu: int = 4              # concurrent task streams per GPU (pipeline forks): the benched
+                                          # SD1.5 default (bench.py --concurrent 4); 1 = latency mode
+    # per-model cap on those streams (measured: Kandinsky2 7.2k tasks/h at 2 streams x groups of 4,
+    # 6.6k at 3, 5.9k at 4 x 2; the video UNet's activations fill the GPU at 2)
+    model_streams: Dict[str, int] = Field(default_factory=lambda: dict(DEFAULT_MODEL_STREAMS))
     lockstep_group: int = 4               # queued compatible SD tasks solved per stream in ONE batch
                                           # (batch-invariant plans: same CIDs as solo; a lone task
                                           # never waits for company)

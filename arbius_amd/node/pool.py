@@ -13,7 +13,7 @@ import asyncio
 import hashlib
 import queue
 import threading
-from typing import Callable, Dict
+from typing import Callable, Dict, Optional
 
 import numpy as np
 
@@ -67,10 +67,12 @@ class LocalSolverPool:
     and hipGraphs each) - concurrency never changes a solution's bytes."""
 
     def __init__(self, device="cpu", pipeline_factory: Callable = None, capacity: int = 1, lockstep: int = 1,
-                 **factory_kw):
+                 model_streams: Optional[Dict[str, int]] = None, **factory_kw):
         from ..models.registry import build_pipeline
         self.device = device
         self.streams = max(1, int(capacity))
+        # per-model cap on the streams (forks) a model gets: its solves beyond that wait for a fork
+        self.model_streams = dict(model_streams or {})
         # lock-step groups only where launches are batch-invariant (the HIP kernels); the CPU
         # reference path's library GEMMs are not, so grouping there would change CIDs
         self.lockstep = max(1, int(lockstep)) if str(device).startswith("cuda") else 1
@@ -94,8 +96,9 @@ class LocalSolverPool:
                 base = self.factory(model.name, device=self.device, **self.factory_kw)
                 self.pipes[model.name] = base
                 q = queue.Queue()
-                for _ in range(self.streams):
-                    q.put(base if self.streams == 1 or not hasattr(base, "fork") else base.fork())
+                n = max(1, min(self.streams, int(self.model_streams.get(model.name, self.streams))))
+                for _ in range(n):
+                    q.put(base if n == 1 or not hasattr(base, "fork") else base.fork())
                 self._free[model.name] = q
             return self._free[model.name]
 

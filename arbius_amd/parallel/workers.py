@@ -50,7 +50,8 @@ def _free_port() -> int:
 
 def _worker_main(rank: int, world: int, port: int, device_type: str, models: List[str], tiny: bool,
                  in_q, out_q, group: bool, weight_seed: int, streams: int = 1, lockstep: int = 1,
-                 weights_dir: Optional[str] = None, beats=None, force_group: bool = False):
+                 weights_dir: Optional[str] = None, beats=None, force_group: bool = False,
+                 model_streams: Optional[Dict[str, int]] = None):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import queue as _queue
     import threading
@@ -104,6 +105,9 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
         # per slot: one thread for a lock-step group's PNG + CID tail, so the slot's stream starts
         # its next group while the previous one encodes
         tails = [ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"tail{k}") for k in range(streams)]
+        # per-model cap on concurrently solving slots (e.g. Kandinsky2 peaks at 2 streams per GPU)
+        caps = {n: threading.Semaphore(max(1, min(streams, int((model_streams or {}).get(n, streams)))))
+                for n in pipes}
 
         def finish(batch, imgs, tm, t0):
             try:
@@ -124,6 +128,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 # lock-step group: queued compatible image tasks share one batch (same bytes as solo)
                 batch = take_group(jobs, msg, lockstep, lambda m: m[2], lambda m: m[5], lambda m: m[1])
                 jid, mname, kind, mid, taskid, inp = msg
+                caps[msg[1]].acquire()              # idle (beat 0) while the model's cap is full
                 progress.beat()                     # busy from now on (0 = idle)
                 try:
                     if inp.get("__fault__") == "hang" and os.environ.get("ARBIUS_FAULT_INJECTION") == "1":
@@ -143,6 +148,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                     for m in batch:
                         out_q.put(("err", m[0], rank, traceback.format_exc()))
                 finally:
+                    caps[msg[1]].release()
                     if beats is not None:
                         beats[rank * streams + k] = 0.0
 
@@ -176,8 +182,9 @@ class MultiGPUSolverPool:
     def __init__(self, n: int, models: List[str], device_type: str = "cuda", tiny: bool = False,
                  weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1,
                  lockstep: int = 1, weights_dir: Optional[str] = None, hang_timeout: float = 300.0,
-                 force_group: bool = False):
+                 force_group: bool = False, model_streams: Optional[Dict[str, int]] = None):
         self.n = n
+        self.model_streams = dict(model_streams or {})
         self.force_group = bool(force_group)
         self.arch = None                         # gcnArchName reported by the workers (no GPU call here)
         self.models = models
@@ -271,7 +278,8 @@ class MultiGPUSolverPool:
         p = self.ctx.Process(target=_worker_main, daemon=True,
                              args=(rank, self.n, port, self.device_type, self.models, self.tiny,
                                    self.in_qs[rank], self.out_qs[rank], group, self.weight_seed, self.streams,
-                                   self.lockstep, self.weights_dir, self.beats, group and self.force_group))
+                                   self.lockstep, self.weights_dir, self.beats, group and self.force_group,
+                                   self.model_streams))
         p.start()
         self.procs[rank] = p
 

@@ -42,8 +42,10 @@ def parse_args(argv=None):
                          "robust_video_matting = #5 (1080p clip per task)")
     ap.add_argument("--frames", type=int, default=None,
                     help="video models: frames (config #4: 24); matting: clip length (default 48 = 2 s at 24 fps)")
-    ap.add_argument("--concurrent", type=int, default=2,
-                    help="tasks solved concurrently per GPU (pipeline forks on private HIP streams)")
+    ap.add_argument("--concurrent", type=int, default=None,
+                    help="task streams per GPU (pipeline forks on private HIP streams); default: the node's "
+                         "(mi355x.workers_per_gpu = 4, capped per model by mi355x.model_streams: 2 for "
+                         "kandinsky2 / video / matting)")
     ap.add_argument("--group", type=int, default=4,
                     help="SD family: tasks solved lock-step per stream (one batch-2k UNet launch sequence; "
                          "batch-invariant plans keep every CID equal to its solo solve)")
@@ -67,6 +69,9 @@ def parse_args(argv=None):
     ap.add_argument("--node-outstanding", type=int, default=0,
                     help="--node: tasks kept in flight (default 2 x pool capacity: a saturated node)")
     args = ap.parse_args(argv)
+    if args.concurrent is None:
+        from arbius_amd.config.mining_config import DEFAULT_MODEL_STREAMS, MI355XConfig
+        args.concurrent = DEFAULT_MODEL_STREAMS.get(args.model, MI355XConfig().workers_per_gpu)
     k2 = args.model == "kandinsky2"
     vid = args.model in ("zeroscopev2xl", "damo")
     rvm = args.model == "robust_video_matting"

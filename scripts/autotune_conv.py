@@ -40,6 +40,15 @@ def _run_meta(models, res, batch=2):
             GlideUNet()(torch.zeros(batch, 96, 96, 4), torch.tensor([500.0]), torch.zeros(batch, 77, 1024),
                         torch.zeros(batch, 768), torch.zeros(batch, 768))
             MoVQDecoder()(torch.zeros(1, 96, 96, 4))
+        if "kandinsky2_prior" in models:   # the diffusion prior (CFG batch 2 per task): M = batch x 81 tokens
+            from arbius_amd.models.clip_text import CLIPTextConfig
+            from arbius_amd.models.prior import PriorConfig, PriorTransformer
+            pcfg = PriorConfig.kandinsky21()
+            prior = PriorTransformer(pcfg)
+            lens = [5, 77] * (batch // 2)
+            layout = prior.layout(lens, torch.device("meta"))
+            prior(torch.zeros(batch, pcfg.clip_dim), 500, torch.zeros(batch, 77, CLIPTextConfig.vit_l14().width),
+                  torch.zeros(batch, pcfg.clip_dim), lens, layout)
         if "video" in models:   # BASELINE config #4: zeroscope 576x320x24f; VAE in chunks of 8 frames
             from arbius_amd.models.unet3d import UNet3DCondition
             from arbius_amd.models.vae import VAEDecoder
@@ -63,11 +72,31 @@ def collect_shapes(models=("sd15",), res=512, batch=2):
             gemms.add((x.numel() // x.shape[-1], x.shape[-1], w.shape[0], residual is not None))
         return orig_lin(x, w, b, residual, act=act)
 
+    orig_ln, orig_lng, orig_geglu = ops.ln_linear, ops.ln_linear_geglu, ops.linear_geglu
+
+    def note(x, w, residual=None):
+        if x.shape[-1] % 64 == 0 and w.shape[0] % 8 == 0:
+            gemms.add((x.numel() // x.shape[-1], x.shape[-1], w.shape[0], residual is not None))
+
+    def ln_lin(x, gamma, beta, eps, w, b=None, residual=None, act=None):
+        note(x, w, residual)    # LayerNorm-folded GEMMs share the (M, N, K) plan table
+        return orig_ln(x, gamma, beta, eps, w, b, residual=residual, act=act)
+
+    def ln_lin_geglu(x, gamma, beta, eps, w, b=None):
+        note(x, w)
+        return orig_lng(x, gamma, beta, eps, w, b)
+
+    def lin_geglu(x, w, b=None):
+        note(x, w)
+        return orig_geglu(x, w, b)
+
     ops.conv2d, ops.linear = conv, lin
+    ops.ln_linear, ops.ln_linear_geglu, ops.linear_geglu = ln_lin, ln_lin_geglu, lin_geglu
     try:
         _run_meta(models, res, batch)
     finally:
         ops.conv2d, ops.linear = orig_conv, orig_lin
+        ops.ln_linear, ops.ln_linear_geglu, ops.linear_geglu = orig_ln, orig_lng, orig_geglu
     return sorted(convs), sorted(gemms)
 
 
