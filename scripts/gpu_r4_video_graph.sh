@@ -1,0 +1,23 @@
+#!/bin/bash
+# Zeroscope evidence (per-shape table of one 576x320x24 clip, one PMC pass) and the VAE-graph
+# stream-serialisation measurement (scripts/graph_serialisation.py, eager VAE vs graph-replayed).
+set -o pipefail
+TAG=${1:-vidg}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+for v in eager graph; do
+  echo "== vae $v $(date +%T)"
+  a=""; [ $v = graph ] && a="--vae-graph"
+  timeout -k 10 400 python -u scripts/graph_serialisation.py $a --groups 3 --json $O/graph_ser_$v.json > $O/graph_ser_$v.log 2>&1 \
+    || { tail -20 $O/graph_ser_$v.log; exit 1; }
+  head -3 $O/graph_ser_$v.log | cut -c1-300
+done
+echo "== layer_prof zeroscope $(date +%T)"
+timeout -k 10 400 python scripts/layer_prof.py --model zeroscopev2xl --steps 2 --md $O/shapes_zeroscope.md \
+  --json $O/shapes_zeroscope.jsonl > $O/lp_zs.log 2>&1 || { tail -30 $O/lp_zs.log; exit 1; }
+head -1 $O/shapes_zeroscope.md | cut -c1-300
+echo "== pmc zeroscope $(date +%T)"
+MODEL=zeroscopev2xl STEPS=3 bash scripts/gpu_pmc_bench.sh ${TAG}_pmc_zs
+echo "== done $(date +%T)"

@@ -120,11 +120,13 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--md", default=None)
     ap.add_argument("--top", type=int, default=80)
+    ap.add_argument("--frames", type=int, default=24, help="video models: frames per clip")
     args = ap.parse_args()
     from arbius_amd.models.registry import build_pipeline
     from arbius_amd.node.solver import solve_images
     k2 = args.model == "kandinsky2"
-    res = args.res or (768 if k2 else 512)
+    vid = args.model in ("zeroscopev2xl", "damo")
+    res = args.res or (768 if k2 else 576 if args.model == "zeroscopev2xl" else 256 if vid else 512)
     pipe = build_pipeline(args.model, device="cuda:0", use_graphs=False)
     if k2:
         pipe.cfg.num_steps = args.steps
@@ -135,10 +137,22 @@ def main():
         inps = [{"prompt": f"castle {j}", "negative_prompt": "x", "width": res, "height": res,
                  "num_inference_steps": args.steps, "guidance_scale": 7, "scheduler": "DPMSolverMultistep",
                  "seed": 1000 + j} for j in range(args.group)]
-    solve_images(pipe, inps)            # warm: plans, workspaces, caches
+    if vid:     # one clip (BASELINE config #4: 576x320, 24 frames); lock-step groups do not apply
+        height = 320 if args.model == "zeroscopev2xl" else 256
+        vinp = {"prompt": "a red cat walking", "negative_prompt": "blurry", "num_frames": args.frames,
+                "width": res, "height": height, "num_inference_steps": args.steps, "guidance_scale": 9.0,
+                "fps": 8, "seed": 1337}
+        args.group = 1
+
+        def run():
+            pipe.solve(vinp)
+    else:
+        def run():
+            solve_images(pipe, inps)
+    run()                               # warm: plans, workspaces, caches
     torch.cuda.synchronize()
     wrap()
-    solve_images(pipe, inps)
+    run()
     torch.cuda.synchronize()
     agg = defaultdict(lambda: [0.0, 0, 0.0, None])
     for n, key, flops, fam, s, e in REC:
@@ -152,8 +166,10 @@ def main():
     by_op = defaultdict(float)
     for (n, _), v in agg.items():
         by_op[n] += v[0]
-    lines = [f"total op time {total / 1000:.2f} ms over {len(REC)} calls ({args.model} {res}^2, group {args.group} "
-             f"= batch {2 * args.group}, {args.steps} steps, eager, each op timed in isolation); "
+    what = (f"{res}x{vinp['height']}x{args.frames}f, CFG batch 2" if vid else
+            f"{res}^2, group {args.group} = batch {2 * args.group}")
+    lines = [f"total op time {total / 1000:.2f} ms over {len(REC)} calls ({args.model} {what}, "
+             f"{args.steps} steps, eager, each op timed in isolation); "
              f"{tot_fl / 1e12:.1f} TFLOP of matmul work -> {tot_fl / (total * 1e-6) / 1e12:.0f} TFLOP/s overall", ""]
     lines += ["| op | % | ms |", "|---|---:|---:|"]
     for n, t in sorted(by_op.items(), key=lambda kv: -kv[1]):
