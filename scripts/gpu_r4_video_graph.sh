@@ -14,6 +14,12 @@ for v in eager graph; do
     || { tail -20 $O/graph_ser_$v.log; exit 1; }
   head -3 $O/graph_ser_$v.log | cut -c1-300
 done
+for v in 0 1; do
+  echo "== k2 prior graph $v $(date +%T)"
+  ARB_PRIOR_GRAPH=$v timeout -k 10 400 python bench.py --model kandinsky2 --steps 4 --warmup 1 > $O/k2_pg$v.log 2>$O/k2_pg$v.err \
+    || { tail -20 $O/k2_pg$v.err; exit 1; }
+  tail -1 $O/k2_pg$v.log | cut -c1-160
+done
 echo "== layer_prof zeroscope $(date +%T)"
 timeout -k 10 400 python scripts/layer_prof.py --model zeroscopev2xl --steps 2 --md $O/shapes_zeroscope.md \
   --json $O/shapes_zeroscope.jsonl > $O/lp_zs.log 2>&1 || { tail -30 $O/lp_zs.log; exit 1; }
