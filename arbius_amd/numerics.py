@@ -16,7 +16,7 @@ import os
 from typing import Callable, Dict, List, Tuple
 
 # bump on ANY change of output bytes (kernels, conv plans, sampler arithmetic, PNG/MP4 encoders)
-NUMERICS_VERSION = "r3.0-bs8-2stream-plans-lnfold"
+NUMERICS_VERSION = "r4.0-bs8-gelu-epilogue-prescaled-attn"
 
 # Environment knobs that select a different kernel library, plan table, tiling or reference ops.
 # They exist for A/B measurement only; ``start`` refuses to mine with any of them set.
@@ -25,7 +25,7 @@ NUMERICS_ENV_KNOBS = (
     "ARBIUS_EXPERIMENT_SKIP", "ARBIUS_REFERENCE_OPS", "ARB_ATTN_GLDS", "ARB_ATTN_QT", "ARB_LN_ROWS",
     "ARB_SPLITK_INLAUNCH", "ARBIUS_GEGLU_FUSED", "ARBIUS_CROSS_KV_HOIST", "ARBIUS_FAULT_INJECTION",
     "ARBIUS_SAMPLER_REF", "ARB_GN_TABLE_LDS", "ARB_VAE_GRAPH", "ARB_PINNED_D2H", "ARB_PRIOR_GRAPH",
-    "ARB_ATTN_PP", "ARB_LN_FOLD_NARROW", "ARB_LN_FOLD_NARROW_N", "ARBIUS_LIBRARY_FALLBACK",
+    "ARB_ATTN_PP", "ARB_LN_FOLD_NARROW", "ARB_LN_FOLD_NARROW_N", "ARBIUS_LIBRARY_FALLBACK", "ARB_ATTN_PRESCALE",
 )
 
 

@@ -1121,11 +1121,16 @@ __device__ __forceinline__ T* half_slot(T* s0, T* s1, T* s2, T* s3, T* s4, T* s5
   else return s5;
 }
 
-template <int BN, int BM, int WN, int WM, int HS, bool SPLIT>
+// PD = prefetch distance in halves (half P + PD is issued in phase P).  WAR needs HS - PD >= 2 when
+// a group's ds_reads may still be in flight at the barrier ending its load part (they retire by the
+// next barrier), HS - PD >= 1 when every wave retires them (lgkmcnt(0)) before that barrier - the PD 4
+// form on a 5-slot ring, which buys one more phase (two barriers) of DMA lead time.
+template <int BN, int BM, int WN, int WM, int HS, bool SPLIT, int PD = 3>
 __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
   constexpr int EL = 0, BK = 64, HK = 32, NT = 512;
   static_assert(WN * WM == 8, "8 waves");
   static_assert(HS == 5 || HS == 6, "half-slot ring depth");
+  static_assert(PD == 3 || (PD == 4 && HS - PD >= 1), "prefetch distance");
   static_assert(BN % 16 == 0 && BM % 16 == 0, "16-row DMA wave-instructions");
   constexpr int TN = BN / WN / 16, TM = BM / WM / 16;
   constexpr int WINS = BN / 16, XINS = BM / 16;      // DMA wave-instructions per operand and half
@@ -1233,19 +1238,24 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
 #pragma unroll
     for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // prologue: halves 0..2 in flight (H >= 2 always), half 0 landed for every wave before any read
+  // prologue: halves 0..PD-1 in flight (H is even and >= 2), half 0 landed for every wave before any read
   issue(IC<0>(), IC<0>());
   issue(IC<1>(), IC<1>());
   if (2 < H) {
     issue(IC<2>(), IC<0>());
-    wait_vmcnt<2 * LPH>();
+    if constexpr (PD == 4) {
+      issue(IC<3>(), IC<1>());     // H even: 2 < H -> half 3 exists
+      wait_vmcnt<3 * LPH>();
+    } else {
+      wait_vmcnt<2 * LPH>();
+    }
   } else {
     wait_vmcnt<LPH>();
   }
   bar();
   if (grp1) bar();   // group 1 runs one barrier behind group 0
 
-  // phase P (K = P % U static): reads slot K % HS, issues half P + 3 into slot (K + 3) % HS
+  // phase P (K = P % U static): reads slot K % HS, issues half P + PD into slot (K + PD) % HS
   auto phase = [&](auto k_c, int P) __attribute__((always_inline)) {
     constexpr int K = decltype(k_c)::value;
     const bf16_t* sW = half_slot<K % HS>(hs0, hs1, hs2, hs3, hs4, hs5);
@@ -1261,14 +1271,17 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
       const int row = wm * (BM / WM) + b * 16 + l16;
       bfr[b] = ld16(&sX[row * HK + ((g ^ half_swz(row)) << 3)]);
     }
-    if (P + 3 < H) {
-      issue(IC<(K + 3) % HS>(), IC<(K + 3) & 1>());
-      wait_vmcnt<2 * LPH>();      // half P+1 landed (P+2, P+3 may be in flight)
-    } else if (P + 2 < H) {
+    if (P + PD < H) {
+      issue(IC<(K + PD) % HS>(), IC<(K + PD) & 1>());
+      wait_vmcnt<(PD - 1) * LPH>();   // half P+1 landed (P+2 .. P+PD may be in flight)
+    } else if (P + PD - 1 < H) {
+      wait_vmcnt<(PD - 2) * LPH>();
+    } else if (PD == 4 && P + 2 < H) {
       wait_vmcnt<LPH>();
     } else {
       wait_vmcnt<0>();
     }
+    if constexpr (PD == 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slot reads retired (WAR)
     bar();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -2059,6 +2072,18 @@ static void launch_stag(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   }
 }
 
+// Prefetch distance of the half-slot tiles (bitwise-equal variants: the MFMA sequence is the same):
+// ARB_STAG2_PD=4 or arb_set_stag2_pd(4) -> one more phase of DMA lead time (A/B switch).
+static int g_stag2_pd = -1;
+static int stag2_pd() {
+  if (g_stag2_pd < 0) {
+    const char* e = std::getenv("ARB_STAG2_PD");
+    g_stag2_pd = (e != nullptr && e[0] == '4') ? 4 : 3;
+  }
+  return g_stag2_pd;
+}
+ARB_API void arb_set_stag2_pd(int pd) { g_stag2_pd = pd == 4 ? 4 : 3; }
+
 // Half-slot staggered tiles (cfg 42 + i): 8 waves, HS-deep ring of K-half slots.
 template <int BN, int BM, int WN, int WM, int HS>
 static void launch_stag2(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
@@ -2071,12 +2096,14 @@ static void launch_stag2(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   p.counters = nullptr;
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
-    conv_stag2_kernel<BN, BM, WN, WM, HS, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
+    if (stag2_pd() == 4) conv_stag2_kernel<BN, BM, WN, WM, HS, true, 4><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
+    else conv_stag2_kernel<BN, BM, WN, WM, HS, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
     long blocks = ((long)p.M * (p.N / 8) + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     splitk_reduce_kernel<0><<<(int)blocks, 256, 0, s>>>(p, pl.split);
   } else {
-    conv_stag2_kernel<BN, BM, WN, WM, HS, false><<<p.tiles_total, 512, 0, s>>>(p);
+    if (stag2_pd() == 4) conv_stag2_kernel<BN, BM, WN, WM, HS, false, 4><<<p.tiles_total, 512, 0, s>>>(p);
+    else conv_stag2_kernel<BN, BM, WN, WM, HS, false><<<p.tiles_total, 512, 0, s>>>(p);
   }
 }
 

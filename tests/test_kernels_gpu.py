@@ -736,3 +736,27 @@ def test_flash_attention_prescaled_q(cuda, B, N, Nk, H, D, causal):
     r = ref.attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), causal)
     assert _rel(ps, r) < 2e-2 and _rel(raw, r) < 2e-2 and _rel(ps, raw) < 1e-2
     assert torch.equal(ps, ops.attention(q, k, v, causal=causal))
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,cfg,split", [(8, 48, 48, 768, 768, 43, 1), (8, 24, 24, 1152, 1152, 44, 1),
+                                                  (8, 12, 12, 1536, 1536, 43, 4), (2, 64, 64, 320, 320, 42, 1),
+                                                  (1, 7, 9, 256, 192, 44, 1), (2, 16, 16, 1280, 1280, 43, 3)])
+def test_stag2_prefetch_distance_bitwise(cuda, B, H, W, C, Co, cfg, split):
+    """K-half staggered tiles with the DMA issued 4 halves ahead (lgkmcnt-retired slot reads) ==
+    3 halves ahead, bit for bit, over repeated launches (a WAR race would show as a flipped tile)."""
+    torch.manual_seed(23)
+    x = torch.randn(B, H, W, C, device=cuda).bfloat16()
+    w = (torch.randn(Co, 3, 3, C, device=cuda) / math.sqrt(9 * C)).bfloat16()
+    b = torch.randn(Co, device=cuda).bfloat16()
+    fn = _lib._fn("arb_set_stag2_pd")
+    try:
+        fn(3)
+        ref3 = _lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split)
+        fn(4)
+        outs = [_lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split) for _ in range(5)]
+    finally:
+        fn(3)
+    assert all(torch.equal(o, ref3) for o in outs)
+    r = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b.float(),
+                                   padding=1).permute(0, 2, 3, 1)
+    assert _rel(ref3, r) < 1e-2
