@@ -2073,12 +2073,14 @@ static void launch_stag(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
 }
 
 // Prefetch distance of the half-slot tiles (bitwise-equal variants: the MFMA sequence is the same):
-// ARB_STAG2_PD=4 or arb_set_stag2_pd(4) -> one more phase of DMA lead time (A/B switch).
+// 4 (default) = one more phase of DMA lead time; ARB_STAG2_PD=3 or arb_set_stag2_pd(3) -> the r3 form.
+// Same-process A/B (profiles/stag2_pd_ab_r4.jsonl): +0..2 % per shape, most on the under-filled
+// 24x24 / 16x16-level tiles, never slower beyond noise.
 static int g_stag2_pd = -1;
 static int stag2_pd() {
   if (g_stag2_pd < 0) {
     const char* e = std::getenv("ARB_STAG2_PD");
-    g_stag2_pd = (e != nullptr && e[0] == '4') ? 4 : 3;
+    g_stag2_pd = (e != nullptr && e[0] == '3') ? 3 : 4;
   }
   return g_stag2_pd;
 }

@@ -7,8 +7,8 @@ the host time spent inside each VAE call is recorded.  For each decode the repor
 
 * host_ms  - wall time of the decode call on the CPU (graph replay + the copy out + D2H),
 * gpu_ms   - its stream's event span (when the stream reached the decode -> decode finished),
-* other_unet - how many UNet evaluations of the OTHER stream ran inside that span, and their
-  mean GPU time vs. the other stream's UNet evaluations outside any decode span.
+* other_unet - how many UNet evaluations of the OTHER stream overlap that span, and their mean
+  GPU time vs. the other stream's UNet evaluations that overlap no decode.
 
 A decode whose GPU span holds many of the other stream's evaluations while its own kernels take
 ~40 ms means the two streams were serialised on the device; a long host_ms with a short gpu_ms
@@ -107,7 +107,7 @@ def main():
         spans = []
         for e0, e1, host in rec[k]["vae"]:
             s, e = ts(e0), ts(e1)
-            inside = [b - a_ for a_, b in other if a_ >= s and b <= e]
+            inside = [b - a_ for a_, b in other if a_ < e and b > s]      # overlapping the decode span
             spans.append((s, e))
             rows.append({"stream": k, "host_ms": round(host, 2), "gpu_ms": round(e - s, 2),
                          "other_unet_inside": len(inside),
@@ -117,12 +117,14 @@ def main():
         spans = [(ts(e0), ts(e1)) for e0, e1, _ in rec[1 - k]["vae"]]
         for e0, e1 in rec[k]["unet"]:
             s, e = ts(e0), ts(e1)
-            if not any(a_ <= s <= b for a_, b in spans):
+            if not any(s < b and e > a_ for a_, b in spans):
                 outside.append(e - s)
     summ = {"vae_graph": a.vae_graph, "wall_s": round(wall, 2), "groups_per_stream": a.groups,
             "decodes": len(rows), "decode_host_ms_median": statistics.median(r["host_ms"] for r in rows),
             "decode_gpu_ms_median": statistics.median(r["gpu_ms"] for r in rows),
             "other_unet_inside_per_decode": statistics.mean(r["other_unet_inside"] for r in rows),
+            "other_unet_ms_overlapping_decodes": round(statistics.mean(
+                [x for r in rows if r["other_unet_inside_mean_ms"] for x in [r["other_unet_inside_mean_ms"]]] or [0]), 2),
             "unet_eval_ms_outside_decodes_median": round(statistics.median(outside), 2) if outside else None,
             "tasks_per_hour": round(2 * 4 * a.groups * 3600 / wall, 1)}
     print(json.dumps(summ))

@@ -52,7 +52,7 @@ def main():
             for pd in (3, 4):
                 setpd(pd)
                 ts[pd].append(at.graph_time(run, reps=10, rounds=3))
-        setpd(3)
+        setpd(4)
         fl = 2.0 * B * H * W * Co * k * k * C
         m3, m4 = statistics.median(ts[3]), statistics.median(ts[4])
         rec = {"shape": [B, H, W, C, Co, k], "cfg": cfg, "split": sp, "bitwise": same, "pd3_us": round(m3, 1),

@@ -755,7 +755,7 @@ def test_stag2_prefetch_distance_bitwise(cuda, B, H, W, C, Co, cfg, split):
         fn(4)
         outs = [_lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split) for _ in range(5)]
     finally:
-        fn(3)
+        fn(4)
     assert all(torch.equal(o, ref3) for o in outs)
     r = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b.float(),
                                    padding=1).permute(0, 2, 3, 1)
