@@ -39,6 +39,7 @@ _SIGS = {
     "arb_set_gn_table_lds": (None, [c_int]),
     "arb_set_attn_prescale": (None, [c_int]),
     "arb_set_stag2_pd": (None, [c_int]),
+    "arb_set_stag2_buf": (None, [c_int]),
     "arb_set_attn_pp": (None, [c_int]),
     "arb_conv2d_nhwc_tld": (c_int, [c_void_p] * 4 + [c_int] + [c_void_p] * 4 + [c_int] * 12 + [c_void_p]),
     "arb_conv2d_nhwc_f16": (c_int, [c_void_p] * 7 + [c_int] * 11 + [c_void_p]),

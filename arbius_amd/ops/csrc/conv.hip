@@ -1125,7 +1125,11 @@ __device__ __forceinline__ T* half_slot(T* s0, T* s1, T* s2, T* s3, T* s4, T* s5
 // a group's ds_reads may still be in flight at the barrier ending its load part (they retire by the
 // next barrier), HS - PD >= 1 when every wave retires them (lgkmcnt(0)) before that barrier - the PD 4
 // form on a 5-slot ring, which buys one more phase (two barriers) of DMA lead time.
-template <int BN, int BM, int WN, int WM, int HS, bool SPLIT, int PD = 3>
+// BUF: the DMA goes through buffer_load ... lds on two buffer resources (W, X) with 32-bit byte
+// offsets - one VALU add per DMA instead of a 64-bit address plus the zero-page select: padding taps
+// and rows past N / M carry an offset beyond the resource's size (0x80000000; sizes < 2 GiB), which
+// the hardware range check turns into zero-filled LDS (tests/test_kernels_gpu.py probes it).
+template <int BN, int BM, int WN, int WM, int HS, bool SPLIT, int PD = 3, bool BUF = false>
 __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
   constexpr int EL = 0, BK = 64, HK = 32, NT = 512;
   static_assert(WN * WM == 8, "8 waves");
@@ -1167,6 +1171,15 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
     const int jj = wave + 8 * i, row = 16 * jj + (lane >> 2);
     woff[i] = (jj < WINS && n0 + row < p.N) ? (n0 + row) * p.K + ((pos ^ half_swz(row)) << 3) : -1;
   }
+  constexpr unsigned kOOB = 0x80000000u;            // BUF: byte offset past every resource (range check)
+  unsigned wbo[WCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) wbo[i] = woff[i] >= 0 ? 2u * (unsigned)woff[i] : kOOB;
+  __amdgpu_buffer_rsrc_t rsw, rsx;
+  if constexpr (BUF) {
+    rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, 2 * p.N * p.K, 0x00020000);
+    rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, 2 * p.B * p.H * p.W * p.Cin, 0x00020000);
+  }
   int xb[XCH], xho[XCH], xwo[XCH], xcc[XCH];
   bool xok[XCH];
   const int hw = p.Ho * p.Wo;
@@ -1187,6 +1200,7 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
   int wk = kt0 * BK, wc = wk % p.Cin, wrs = wk / p.Cin;
   int wr = wrs / p.kw, ws = wrs - wr * p.kw;
   int xoff[XCH];
+  unsigned xbo[XCH];
   auto set_tap = [&]() {
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
@@ -1194,6 +1208,7 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
       const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
       if (p.upsample) { hi >>= 1; wi >>= 1; }
       xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + xcc[i] * 8 : -1;
+      if constexpr (BUF) xbo[i] = ok ? 2u * (unsigned)xoff[i] : kOOB;
     }
   };
   set_tap();
@@ -1205,16 +1220,26 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       const int jj = wave + 8 * i;
-      const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk + PAR * HK) : (const void*)g_conv_zero_page;
       bf16_t* dst = (!DUMMY || jj < WINS) ? sW + 16 * jj * HK : ldsd;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      if constexpr (BUF) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (lptr_t)dst, 16, wbo[i] + 2u * (unsigned)(wk + PAR * HK), 0, 0,
+                                                 0);
+      } else {
+        const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk + PAR * HK) : (const void*)g_conv_zero_page;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
       const int jj = wave + 8 * i;
-      const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc + PAR * HK) : (const void*)g_conv_zero_page;
       bf16_t* dst = (!DUMMY || jj < XINS) ? sX + 16 * jj * HK : ldsd;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      if constexpr (BUF) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (lptr_t)dst, 16, xbo[i] + 2u * (unsigned)(wc + PAR * HK), 0, 0,
+                                                 0);
+      } else {
+        const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc + PAR * HK) : (const void*)g_conv_zero_page;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      }
     }
     if constexpr (PAR == 1) {       // both halves of this K tile issued: next tile
       wk += BK;
@@ -2085,6 +2110,16 @@ static int stag2_pd() {
   return g_stag2_pd;
 }
 ARB_API void arb_set_stag2_pd(int pd) { g_stag2_pd = pd == 4 ? 4 : 3; }
+// Buffer-resource DMA addressing for the PD 4 form (bitwise equal): ARB_STAG2_BUF=1 / arb_set_stag2_buf(1).
+static int g_stag2_buf = -1;
+static bool stag2_buf() {
+  if (g_stag2_buf < 0) {
+    const char* e = std::getenv("ARB_STAG2_BUF");
+    g_stag2_buf = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return g_stag2_buf == 1;
+}
+ARB_API void arb_set_stag2_buf(int on) { g_stag2_buf = on ? 1 : 0; }
 
 // Half-slot staggered tiles (cfg 42 + i): 8 waves, HS-deep ring of K-half slots.
 template <int BN, int BM, int WN, int WM, int HS>
@@ -2096,15 +2131,21 @@ static void launch_stag2(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;
   p.norm = nullptr;
   p.counters = nullptr;
+  // buffer resources: byte sizes below the out-of-range offset (2 GiB) and one X source
+  const bool buf = stag2_pd() == 4 && stag2_buf() && 2L * p.N * p.K < (1L << 31) &&
+                   2L * p.B * p.H * p.W * p.Cin < (1L << 31) && p.x2 == nullptr && (p.Cx == 0 || p.Cx == p.Cin);
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
-    if (stag2_pd() == 4) conv_stag2_kernel<BN, BM, WN, WM, HS, true, 4><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
+    if (buf) conv_stag2_kernel<BN, BM, WN, WM, HS, true, 4, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
+    else if (stag2_pd() == 4)
+      conv_stag2_kernel<BN, BM, WN, WM, HS, true, 4><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
     else conv_stag2_kernel<BN, BM, WN, WM, HS, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
     long blocks = ((long)p.M * (p.N / 8) + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     splitk_reduce_kernel<0><<<(int)blocks, 256, 0, s>>>(p, pl.split);
   } else {
-    if (stag2_pd() == 4) conv_stag2_kernel<BN, BM, WN, WM, HS, false, 4><<<p.tiles_total, 512, 0, s>>>(p);
+    if (buf) conv_stag2_kernel<BN, BM, WN, WM, HS, false, 4, true><<<p.tiles_total, 512, 0, s>>>(p);
+    else if (stag2_pd() == 4) conv_stag2_kernel<BN, BM, WN, WM, HS, false, 4><<<p.tiles_total, 512, 0, s>>>(p);
     else conv_stag2_kernel<BN, BM, WN, WM, HS, false><<<p.tiles_total, 512, 0, s>>>(p);
   }
 }

@@ -124,7 +124,7 @@ def main():
             "decode_gpu_ms_median": statistics.median(r["gpu_ms"] for r in rows),
             "other_unet_inside_per_decode": statistics.mean(r["other_unet_inside"] for r in rows),
             "other_unet_ms_overlapping_decodes": round(statistics.mean(
-                [x for r in rows if r["other_unet_inside_mean_ms"] for x in [r["other_unet_inside_mean_ms"]]] or [0]), 2),
+                [r["other_unet_inside_mean_ms"] for r in rows if r["other_unet_inside_mean_ms"]] or [0]), 2),
             "unet_eval_ms_outside_decodes_median": round(statistics.median(outside), 2) if outside else None,
             "tasks_per_hour": round(2 * 4 * a.groups * 3600 / wall, 1)}
     print(json.dumps(summ))

@@ -742,20 +742,24 @@ def test_flash_attention_prescaled_q(cuda, B, N, Nk, H, D, causal):
                                                   (8, 12, 12, 1536, 1536, 43, 4), (2, 64, 64, 320, 320, 42, 1),
                                                   (1, 7, 9, 256, 192, 44, 1), (2, 16, 16, 1280, 1280, 43, 3)])
 def test_stag2_prefetch_distance_bitwise(cuda, B, H, W, C, Co, cfg, split):
-    """K-half staggered tiles with the DMA issued 4 halves ahead (lgkmcnt-retired slot reads) ==
-    3 halves ahead, bit for bit, over repeated launches (a WAR race would show as a flipped tile)."""
+    """K-half staggered tiles with the DMA issued 4 halves ahead (lgkmcnt-retired slot reads), and that
+    form with buffer-resource DMA addressing, == 3 halves ahead, bit for bit, over repeated launches
+    (a WAR race would show as a flipped tile, a missing zero fill as garbage at the borders)."""
     torch.manual_seed(23)
     x = torch.randn(B, H, W, C, device=cuda).bfloat16()
     w = (torch.randn(Co, 3, 3, C, device=cuda) / math.sqrt(9 * C)).bfloat16()
     b = torch.randn(Co, device=cuda).bfloat16()
-    fn = _lib._fn("arb_set_stag2_pd")
+    fn, fb = _lib._fn("arb_set_stag2_pd"), _lib._fn("arb_set_stag2_buf")
     try:
         fn(3)
         ref3 = _lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split)
         fn(4)
         outs = [_lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split) for _ in range(5)]
+        fb(1)   # buffer-resource DMA: padding taps / rows past N zero-filled by the range check
+        outs += [_lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split) for _ in range(5)]
     finally:
         fn(4)
+        fb(0)
     assert all(torch.equal(o, ref3) for o in outs)
     r = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b.float(),
                                    padding=1).permute(0, 2, 3, 1)
