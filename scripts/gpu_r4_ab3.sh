@@ -6,6 +6,12 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-ab3}
 mkdir -p $O
 export TMPDIR=/tmp
+echo "== stag2 tests + A/B $(date +%T)"
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "stag2 or tile or families" \
+  > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 400 python -u scripts/stag2_pd_ab.py --rounds 5 > $O/stag2_ab.jsonl 2>$O/stag2_ab.err || { tail -20 $O/stag2_ab.err; exit 1; }
+cut -c1-260 $O/stag2_ab.jsonl
 for c in 4 2; do
   for v in 0 1 0 1; do
     echo "== bench c$c vae_graph=$v $(date +%T)"
