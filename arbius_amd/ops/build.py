@@ -67,6 +67,12 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+    # every symbol must resolve (hipcc can emit a kernel launch whose host stub it silently dropped)
+    import ctypes
+    try:
+        ctypes.CDLL(str(LIB), mode=os.RTLD_NOW | os.RTLD_LOCAL)
+    except OSError as e:
+        raise RuntimeError(f"built {LIB.name} does not load: {e}") from None
     return LIB
 
 

@@ -1111,6 +1111,14 @@ __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
 // MFMA order per output (K tiles ascending, k-halves ascending) = every other family: bitwise equal.
 __device__ __forceinline__ int half_swz(int r) { return ((r >> 3) & 1) << 1; }
 
+// One 16-byte-per-lane LDS-DMA through a raw buffer resource over [base, base + nbytes): lanes whose
+// byte offset is past nbytes get zeros (range check).  A separate device function: hipcc drops a
+// kernel's host stub when the target-only resource type appears in the kernel's own (lambda) body.
+__device__ __forceinline__ void buf_lds16(const void* base, int nbytes, void* lds, unsigned off) {
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
+}
+
 template <int S, typename T>
 __device__ __forceinline__ T* half_slot(T* s0, T* s1, T* s2, T* s3, T* s4, T* s5) {
   if constexpr (S == 0) return s0;
@@ -1175,11 +1183,6 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
   unsigned wbo[WCH];
 #pragma unroll
   for (int i = 0; i < WCH; ++i) wbo[i] = woff[i] >= 0 ? 2u * (unsigned)woff[i] : kOOB;
-  __amdgpu_buffer_rsrc_t rsw, rsx;
-  if constexpr (BUF) {
-    rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, 2 * p.N * p.K, 0x00020000);
-    rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, 2 * p.B * p.H * p.W * p.Cin, 0x00020000);
-  }
   int xb[XCH], xho[XCH], xwo[XCH], xcc[XCH];
   bool xok[XCH];
   const int hw = p.Ho * p.Wo;
@@ -1222,8 +1225,7 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
       const int jj = wave + 8 * i;
       bf16_t* dst = (!DUMMY || jj < WINS) ? sW + 16 * jj * HK : ldsd;
       if constexpr (BUF) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (lptr_t)dst, 16, wbo[i] + 2u * (unsigned)(wk + PAR * HK), 0, 0,
-                                                 0);
+        buf_lds16(p.w, 2 * p.N * p.K, dst, wbo[i] + 2u * (unsigned)(wk + PAR * HK));
       } else {
         const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk + PAR * HK) : (const void*)g_conv_zero_page;
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
@@ -1234,8 +1236,7 @@ __global__ void __launch_bounds__(512, 1) conv_stag2_kernel(ConvArgs p) {
       const int jj = wave + 8 * i;
       bf16_t* dst = (!DUMMY || jj < XINS) ? sX + 16 * jj * HK : ldsd;
       if constexpr (BUF) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (lptr_t)dst, 16, xbo[i] + 2u * (unsigned)(wc + PAR * HK), 0, 0,
-                                                 0);
+        buf_lds16(p.x, 2 * p.B * p.H * p.W * p.Cin, dst, xbo[i] + 2u * (unsigned)(wc + PAR * HK));
       } else {
         const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc + PAR * HK) : (const void*)g_conv_zero_page;
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
