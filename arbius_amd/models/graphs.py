@@ -9,7 +9,9 @@ from __future__ import annotations
 
 import contextlib
 import copy
+import os
 import threading
+import time
 from typing import Callable, Sequence
 
 import torch
@@ -17,6 +19,14 @@ import torch
 # Captures are serialised process-wide; "thread_local" capture mode lets other threads keep
 # launching work on their own streams while one thread captures (concurrent task streams).
 CAPTURE_LOCK = threading.Lock()
+# ARB_GRAPH_DEBUG=1: log every capture and every replay whose host call takes > 20 ms (stderr)
+_DEBUG = os.environ.get("ARB_GRAPH_DEBUG", "0") == "1"
+
+
+def _dbg(msg):
+    import logging
+    logging.getLogger("arbius_amd.graphs").warning("[graph %.3f %s] %s", time.perf_counter(),
+                                                   threading.current_thread().name, msg)
 
 
 class GraphedCall:
@@ -24,6 +34,8 @@ class GraphedCall:
         dev = example_args[0].device
         self.fn = fn
         self.inputs = [a.detach().clone() for a in example_args]
+        if _DEBUG:
+            _dbg(f"capture {getattr(fn, '__qualname__', fn)} {[tuple(a.shape) for a in example_args]}")
         with CAPTURE_LOCK:
             s = torch.cuda.Stream(device=dev)
             s.wait_stream(torch.cuda.current_stream(dev))
@@ -39,6 +51,13 @@ class GraphedCall:
         for dst, src in zip(self.inputs, args):
             if src.data_ptr() != dst.data_ptr():
                 dst.copy_(src)
+        if _DEBUG:
+            t0 = time.perf_counter()
+            self.graph.replay()
+            dt = time.perf_counter() - t0
+            if dt > 0.02:
+                _dbg(f"replay {getattr(self.fn, '__qualname__', self.fn)} took {dt * 1e3:.1f} ms on the host")
+            return self.out
         self.graph.replay()
         return self.out
 

@@ -689,7 +689,17 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // NT = 64 * WN * WM threads: 4 waves (one per SIMD), or 8 waves for the 256-wide tiles (two per
 // SIMD: one wave's MFMA cluster runs while the other issues its LDS reads / DMA).
-template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
+// One 16-byte-per-lane LDS-DMA through a raw buffer resource over [base, base + nbytes): lanes whose
+// byte offset is past nbytes get zeros (range check).  A separate device function: hipcc drops a
+// kernel's host stub when the target-only resource type appears in the kernel's own (lambda) body.
+__device__ __forceinline__ void buf_lds16(const void* base, int nbytes, void* lds, unsigned off) {
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
+}
+
+// BUF: LDS-DMA through buffer resources (conv_stag2_kernel BUF): one VALU add per DMA, range-checked
+// zero fill for padding taps and rows past N / M instead of the zero-page select.
+template <int BN, int BM, int WN, int WM, int NS, bool SPLIT, bool BUF = false>
 __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) {
   constexpr int EL = 0;   // LDS-DMA variant: bf16 only (fp16 convs use the register-staged kernel)
   constexpr int BK = 64;
@@ -752,6 +762,10 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
     const int n = n0 + wrow[i];
     woff[i] = n < p.N ? n * p.K + wcc[i] * 8 : -1;
   }
+  constexpr unsigned kOOB = 0x80000000u;            // BUF: byte offset past every resource (range check)
+  unsigned wbo[WCH], xbo[XCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) wbo[i] = woff[i] >= 0 ? 2u * (unsigned)woff[i] : kOOB;
   int wk = kt0 * BK, wc = wk % p.Cin, wrs = wk / p.Cin;
   int wr = wrs / p.kw, ws = wrs - wr * p.kw;
   int xoff[XCH];
@@ -762,6 +776,7 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
       const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
       if (p.upsample) { hi >>= 1; wi >>= 1; }
       xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + xcc[i] * 8 : -1;
+      if constexpr (BUF) xbo[i] = ok ? 2u * (unsigned)xoff[i] : kOOB;
     }
   };
   set_tap();
@@ -770,16 +785,24 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
     bf16_t* sX = sW + BN * BK;
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
-      const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
       // wave-uniform destination: first row of this wave's 8-row slab
       bf16_t* dst = sW + ((wave * 8) + RPI * i) * BK;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      if constexpr (BUF) {
+        buf_lds16(p.w, 2 * p.N * p.K, dst, wbo[i] + 2u * (unsigned)wk);
+      } else {
+        const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
-      const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
       bf16_t* dst = sX + ((wave * 8) + RPI * i) * BK;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      if constexpr (BUF) {
+        buf_lds16(p.x, 2 * p.B * p.H * p.W * p.Cin, dst, xbo[i] + 2u * (unsigned)wc);
+      } else {
+        const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      }
     }
     wk += BK;
     wc += BK;
@@ -1111,13 +1134,6 @@ __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
 // MFMA order per output (K tiles ascending, k-halves ascending) = every other family: bitwise equal.
 __device__ __forceinline__ int half_swz(int r) { return ((r >> 3) & 1) << 1; }
 
-// One 16-byte-per-lane LDS-DMA through a raw buffer resource over [base, base + nbytes): lanes whose
-// byte offset is past nbytes get zeros (range check).  A separate device function: hipcc drops a
-// kernel's host stub when the target-only resource type appears in the kernel's own (lambda) body.
-__device__ __forceinline__ void buf_lds16(const void* base, int nbytes, void* lds, unsigned off) {
-  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
-}
 
 template <int S, typename T>
 __device__ __forceinline__ T* half_slot(T* s0, T* s1, T* s2, T* s3, T* s4, T* s5) {
@@ -2035,10 +2051,28 @@ ARB_API size_t arb_conv2d_workspace(int B, int H, int W, int Cin, int Cout, int 
   return pl.split > 1 ? slab_bytes(pl.split, a.M, a.N) : 0;
 }
 
+// Buffer-resource LDS-DMA addressing (conv_glds_kernel / conv_stag2_kernel BUF; bitwise equal): default
+// on; ARB_DMA_BUF=0 / arb_set_stag2_buf(0) -> the global_load_lds + zero-page form.  Used when W and X
+// are below the 2 GiB out-of-range offset and X is one source.
+static int g_stag2_buf = -1;
+static bool stag2_buf() {
+  if (g_stag2_buf < 0) {
+    const char* e = std::getenv("ARB_DMA_BUF");
+    g_stag2_buf = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return g_stag2_buf == 1;
+}
+ARB_API void arb_set_stag2_buf(int on) { g_stag2_buf = on ? 1 : 0; }
+static bool dma_buf_ok(const ConvArgs& p) {
+  return stag2_buf() && 2L * p.N * p.K < (1L << 31) && 2L * p.B * p.H * p.W * p.Cin < (1L << 31) &&
+         p.x2 == nullptr && (p.Cx == 0 || p.Cx == p.Cin);
+}
+
 template <int BN, int BM, int WN, int WM, int NS, bool SPLIT>
 static void launch_glds(const ConvArgs& p, dim3 grid, hipStream_t s) {
   static_assert((size_t)NS * (BN + BM) * 64 * sizeof(bf16_t) <= 160 * 1024, "LDS");
-  conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT><<<grid, 64 * WN * WM, 0, s>>>(p);   // static LDS ring
+  if (dma_buf_ok(p)) conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT, true><<<grid, 64 * WN * WM, 0, s>>>(p);
+  else conv_glds_kernel<BN, BM, WN, WM, NS, SPLIT><<<grid, 64 * WN * WM, 0, s>>>(p);   // static LDS ring
 }
 
 // Persistent short-K tiles (cfg 24 + i): grid = min(tiles, 256 CUs).
@@ -2111,16 +2145,7 @@ static int stag2_pd() {
   return g_stag2_pd;
 }
 ARB_API void arb_set_stag2_pd(int pd) { g_stag2_pd = pd == 4 ? 4 : 3; }
-// Buffer-resource DMA addressing for the PD 4 form (bitwise equal): ARB_STAG2_BUF=1 / arb_set_stag2_buf(1).
-static int g_stag2_buf = -1;
-static bool stag2_buf() {
-  if (g_stag2_buf < 0) {
-    const char* e = std::getenv("ARB_STAG2_BUF");
-    g_stag2_buf = (e != nullptr && e[0] == '1') ? 1 : 0;
-  }
-  return g_stag2_buf == 1;
-}
-ARB_API void arb_set_stag2_buf(int on) { g_stag2_buf = on ? 1 : 0; }
+
 
 // Half-slot staggered tiles (cfg 42 + i): 8 waves, HS-deep ring of K-half slots.
 template <int BN, int BM, int WN, int WM, int HS>
@@ -2132,9 +2157,7 @@ static void launch_stag2(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   p.m_fastest = (long)p.N * p.K > (long)p.M * p.Cin;
   p.norm = nullptr;
   p.counters = nullptr;
-  // buffer resources: byte sizes below the out-of-range offset (2 GiB) and one X source
-  const bool buf = stag2_pd() == 4 && stag2_buf() && 2L * p.N * p.K < (1L << 31) &&
-                   2L * p.B * p.H * p.W * p.Cin < (1L << 31) && p.x2 == nullptr && (p.Cx == 0 || p.Cx == p.Cin);
+  const bool buf = stag2_pd() == 4 && dma_buf_ok(p);
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
     if (buf) conv_stag2_kernel<BN, BM, WN, WM, HS, true, 4, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);

@@ -57,7 +57,7 @@ def main():
             for pd in (3, 4, 5):
                 setpd(pd)
                 ts[pd].append(at.graph_time(run, reps=10, rounds=3))
-        setpd(4)
+        setpd(5)
         fl = 2.0 * B * H * W * Co * k * k * C
         m3, m4, m5 = statistics.median(ts[3]), statistics.median(ts[4]), statistics.median(ts[5])
         rec = {"shape": [B, H, W, C, Co, k], "cfg": cfg, "split": sp, "bitwise": same, "pd3_us": round(m3, 1),

@@ -752,6 +752,7 @@ def test_stag2_prefetch_distance_bitwise(cuda, B, H, W, C, Co, cfg, split):
     fn, fb = _lib._fn("arb_set_stag2_pd"), _lib._fn("arb_set_stag2_buf")
     try:
         fn(3)
+        fb(0)
         ref3 = _lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split)
         fn(4)
         outs = [_lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split) for _ in range(5)]
@@ -759,8 +760,28 @@ def test_stag2_prefetch_distance_bitwise(cuda, B, H, W, C, Co, cfg, split):
         outs += [_lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, split) for _ in range(5)]
     finally:
         fn(4)
-        fb(0)
+        fb(1)
     assert all(torch.equal(o, ref3) for o in outs)
     r = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b.float(),
                                    padding=1).permute(0, 2, 3, 1)
     assert _rel(ref3, r) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [0, 3, 5, 9, 20, 21, 22, 23, 28, 29, 30, 31, 42, 43, 44])
+def test_lds_dma_buffer_resource_bitwise(cuda, cfg):
+    """LDS-DMA through buffer resources (range-checked zero fill for padding taps / rows past N and M)
+    == the global_load_lds + zero-page form, bit for bit, on a shape with borders and ragged tiles."""
+    torch.manual_seed(24)
+    B, H, W, C, Co = 2, 13, 11, 192, 200
+    x = torch.randn(B, H, W, C, device=cuda).bfloat16()
+    w = (torch.randn(Co, 3, 3, C, device=cuda) / math.sqrt(9 * C)).bfloat16()
+    b = torch.randn(Co, device=cuda).bfloat16()
+    fb = _lib._fn("arb_set_stag2_buf")
+    try:
+        fb(0)
+        ref = _lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, 1)
+        fb(1)
+        got = [_lib.conv2d_nhwc(x, w, b, 1, False, None, None, 1, cfg, 1) for _ in range(3)]
+    finally:
+        fb(1)
+    assert all(torch.equal(g, ref) for g in got)
