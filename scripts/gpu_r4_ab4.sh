@@ -18,6 +18,13 @@ for v in 1 0 1 0; do
   ARB_DMA_BUF=$v timeout -k 10 400 python bench.py --steps 6 --warmup 2 > $O/bench_buf$v.log 2>$O/bench_buf$v.err || { tail -20 $O/bench_buf$v.err; exit 1; }
   tail -1 $O/bench_buf$v.log | cut -c1-150
 done
+for spec in "4 8" "3 8"; do
+  set -- $spec
+  echo "== bench c$1 g$2 (group-of-8 families) $(date +%T)"
+  timeout -k 10 400 python bench.py --steps 4 --warmup 2 --concurrent $1 --group $2 > $O/bench_c$1g$2.log 2>$O/bench_c$1g$2.err \
+    || { tail -20 $O/bench_c$1g$2.err; exit 1; }
+  tail -1 $O/bench_c$1g$2.log | cut -c1-150
+done
 echo "== vae graph debug $(date +%T)"
 ARB_VAE_GRAPH=1 ARB_GRAPH_DEBUG=1 timeout -k 10 400 python bench.py --steps 4 --warmup 2 --concurrent 2 > $O/vg_dbg.log 2>$O/vg_dbg.err \
   || { tail -20 $O/vg_dbg.err; exit 1; }
