@@ -936,7 +936,7 @@ __global__ void __launch_bounds__(64 * WN * WM, 1) conv_glds_kernel(ConvArgs p) 
 // A tile operand of R rows is R/8 DMA wave-instructions (8 rows of 128 B each); wave w issues
 // instructions w, w+8, ... - when R/8 is not a multiple of 8 (BN = 160) the surplus ones of a round
 // write a 1 KiB dummy buffer nobody reads, so every wave keeps the same vmcnt count per tile.
-template <int BN, int BM, int WN, int WM, bool SPLIT>
+template <int BN, int BM, int WN, int WM, bool SPLIT, bool BUF = false>
 __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
   constexpr int EL = 0, BK = 64, NT = 512, NS = 3;
   static_assert(WN * WM == 8, "8 waves");
@@ -970,6 +970,10 @@ __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
     const int j = wave + 8 * i, row = 8 * j + (lane >> 3);
     woff[i] = (j < WINS && n0 + row < p.N) ? (n0 + row) * p.K + ((pos ^ (row & 7)) << 3) : -1;
   }
+  constexpr unsigned kOOB = 0x80000000u;            // BUF: byte offset past every resource (range check)
+  unsigned wbo[WCH], xbo[XCH];
+#pragma unroll
+  for (int i = 0; i < WCH; ++i) wbo[i] = woff[i] >= 0 ? 2u * (unsigned)woff[i] : kOOB;
   int xb[XCH], xho[XCH], xwo[XCH], xcc[XCH];
   bool xok[XCH];
   const int hw = p.Ho * p.Wo;
@@ -997,6 +1001,7 @@ __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
       const bool ok = xok[i] && hi >= 0 && hi < p.Hl && wi >= 0 && wi < p.Wl;
       if (p.upsample) { hi >>= 1; wi >>= 1; }
       xoff[i] = ok ? ((xb[i] * p.H + hi) * p.W + wi) * p.Cin + xcc[i] * 8 : -1;
+      if constexpr (BUF) xbo[i] = ok ? 2u * (unsigned)xoff[i] : kOOB;
     }
   };
   set_tap();
@@ -1006,16 +1011,24 @@ __global__ void __launch_bounds__(512, 1) conv_stag_kernel(ConvArgs p) {
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       const int j = wave + 8 * i;
-      const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
       bf16_t* dst = (!DUMMY || j < WINS) ? sW + 8 * j * BK : ldsd;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      if constexpr (BUF) {
+        buf_lds16(p.w, 2 * p.N * p.K, dst, wbo[i] + 2u * (unsigned)wk);
+      } else {
+        const void* src = woff[i] >= 0 ? (const void*)(p.w + woff[i] + wk) : (const void*)g_conv_zero_page;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      }
     }
 #pragma unroll
     for (int i = 0; i < XCH; ++i) {
       const int j = wave + 8 * i;
-      const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
       bf16_t* dst = (!DUMMY || j < XINS) ? sX + 8 * j * BK : ldsd;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      if constexpr (BUF) {
+        buf_lds16(p.x, 2 * p.B * p.H * p.W * p.Cin, dst, xbo[i] + 2u * (unsigned)wc);
+      } else {
+        const void* src = xoff[i] >= 0 ? (const void*)(p.x + xoff[i] + wc) : (const void*)g_conv_zero_page;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)dst, 16, 0, 0);
+      }
     }
     wk += BK;
     wc += BK;
@@ -2123,12 +2136,14 @@ static void launch_stag(const ConvArgs& a, const ConvPlan& pl, hipStream_t s) {
   p.counters = nullptr;
   if (pl.split > 1) {
     p.kt_per_split = pl.kt_per_split;
-    conv_stag_kernel<BN, BM, WN, WM, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
+    if (dma_buf_ok(p)) conv_stag_kernel<BN, BM, WN, WM, true, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
+    else conv_stag_kernel<BN, BM, WN, WM, true><<<p.tiles_total * pl.split, 512, 0, s>>>(p);
     long blocks = ((long)p.M * (p.N / 8) + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     splitk_reduce_kernel<0><<<(int)blocks, 256, 0, s>>>(p, pl.split);
   } else {
-    conv_stag_kernel<BN, BM, WN, WM, false><<<p.tiles_total, 512, 0, s>>>(p);
+    if (dma_buf_ok(p)) conv_stag_kernel<BN, BM, WN, WM, false, true><<<p.tiles_total, 512, 0, s>>>(p);
+    else conv_stag_kernel<BN, BM, WN, WM, false><<<p.tiles_total, 512, 0, s>>>(p);
   }
 }
 

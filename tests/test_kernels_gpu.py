@@ -767,7 +767,7 @@ def test_stag2_prefetch_distance_bitwise(cuda, B, H, W, C, Co, cfg, split):
     assert _rel(ref3, r) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [0, 3, 5, 9, 20, 21, 22, 23, 28, 29, 30, 31, 42, 43, 44])
+@pytest.mark.parametrize("cfg", [0, 3, 5, 9, 20, 21, 22, 23, 28, 29, 30, 31, 36, 37, 38, 39, 40, 41, 42, 43, 44])
 def test_lds_dma_buffer_resource_bitwise(cuda, cfg):
     """LDS-DMA through buffer resources (range-checked zero fill for padding taps / rows past N and M)
     == the global_load_lds + zero-page form, bit for bit, on a shape with borders and ragged tiles."""
