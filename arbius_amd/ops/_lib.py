@@ -299,12 +299,17 @@ def _large_head_attention(q, k, v, scale):
     if Np != Nk:
         k = torch.nn.functional.pad(k, (0, 0, 0, 0, 0, Np - Nk))
         v = torch.nn.functional.pad(v, (0, 0, 0, 0, 0, Np - Nk))
-    o = torch.empty(B, Nq, H, D, dtype=q.dtype, device=q.device)
+    # each (b, h) output is the GEMM's own [Nq, D] tensor: no strided write into a preallocated output
+    # (a contiguous-to-contiguous copy_ is a memcpy - inside a captured hipGraph a memcpy node, which
+    # serialised the other task streams' graphs: profiles/graph_serialisation_r4.md)
+    outs = []
     for b in range(B):
         for h in range(H):
             s = gemm(q[b, :, h], k[b, :, h].contiguous())                     # [Nq, Np] = q k^T
-            o[b, :, h] = gemm(softmax_rows(s, scale, Nk), v[b, :, h].t().contiguous())
-    return o
+            outs.append(gemm(softmax_rows(s, scale, Nk), v[b, :, h].t().contiguous()))
+    if B * H == 1:
+        return outs[0].view(1, Nq, 1, D)
+    return torch.stack(outs).view(B, H, Nq, D).transpose(1, 2).contiguous()
 
 
 # --------------------------------------------------------------------------- ConvGRU (fp16)
