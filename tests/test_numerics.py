@@ -48,8 +48,9 @@ def test_repository_lint_clean():
 
 def test_family_table_well_formed():
     """csrc/conv_family.inc (scripts/tune_family.py): unique (M, N, K, split, ratio) keys, ratios of the
-    canonical batch 8 over the actual batch (4 solo, 2 groups of 2, 1 groups of 4), known tile cfgs and
-    no family that lacks split-K at a split > 1 (persistent kernels 24-27)."""
+    canonical batch 8 over the actual batch (4 solo, 2 groups of 2, 1 groups of 4, 0 groups larger than
+    4 - keyed by their own M), known tile cfgs and no family that lacks split-K at a split > 1
+    (persistent kernels 24-27)."""
     import os
     import re
     path = os.path.join(os.path.dirname(__file__), "..", "arbius_amd", "ops", "csrc", "conv_family.inc")
@@ -59,7 +60,7 @@ def test_family_table_well_formed():
     keys = [r[:5] for r in rows]
     assert len(keys) == len(set(keys))
     for M, N, K, split, ratio, cfg in rows:
-        assert ratio in (1, 2, 4) and split >= 1 and K % 64 == 0
+        assert ratio in (0, 1, 2, 4) and split >= 1 and K % 64 == 0
         assert 0 <= cfg < 45 and not (24 <= cfg < 28 and split > 1)   # 0..44: conv.hip tile cfgs
 
 
