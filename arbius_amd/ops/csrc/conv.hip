@@ -246,10 +246,27 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&ac
       }
       continue;
     }
-    for (int c = tid; c < PR * CPR; c += NT) {
+    // this thread's chunks of the row block: every residual load (the HBM-bound operand) is issued
+    // before the first store (the compiler cannot hoist a later chunk's residual load above an
+    // earlier chunk's store to out - they may alias), so the block's residual reads overlap instead
+    // of running one chunk at a time; bias / temb stay in the loop (L2-hot, and registers: the
+    // X-in-registers tiles keep their two blocks per CU).  Same arithmetic and order per element.
+    constexpr int ITER = (PR * CPR + NT - 1) / NT;
+    uint4 rr[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int c = tid + it * NT;
       const int rl = c / CPR, ch = (c - rl * CPR) * 8;
       const int m = m0 + r0 + rl, n = n0 + ch;
-      if (m >= p.M || n >= p.N) continue;
+      const bool ok = c < PR * CPR && m < p.M && n < p.N;
+      rr[it] = (ok && p.res) ? ld16(p.res + (size_t)m * p.N + n) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int c = tid + it * NT;
+      const int rl = c / CPR, ch = (c - rl * CPR) * 8;
+      const int m = m0 + r0 + rl, n = n0 + ch;
+      if (c >= PR * CPR || m >= p.M || n >= p.N) continue;
       const f32x4 s0 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch]);
       const f32x4 s1 = *reinterpret_cast<const f32x4*>(&stage[rl * OROW + ch + 4]);
       float v[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
@@ -266,7 +283,7 @@ __device__ __forceinline__ void epilogue_lds(const ConvArgs& p, const f32x4 (&ac
         for (int e = 0; e < 8; ++e) v[e] += t[e];
       }
       if (p.res) {
-        unpack8e<EL>(ld16(p.res + (size_t)m * p.N + n), t);
+        unpack8e<EL>(rr[it], t);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += t[e];
       }
