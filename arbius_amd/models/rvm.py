@@ -430,15 +430,27 @@ class RVMPipeline(PipelineBase):
         self.timings = {"matting_s": time.perf_counter() - t0}
         return res
 
-    def solve(self, inp: dict):
-        from ..node.solver import solve_files
-        from ..utils.mp4 import encode_mp4
+    def infer(self, inp: dict):
+        """GPU part of a solve (input hydration + matting): host arrays for ``finish``."""
         from ..utils.video_io import load_video
         t0 = time.perf_counter()
         frames, fps = load_video(inp["input_video"])
         out = self(frames, inp.get("output_type") or "green-screen")
-        t1 = time.perf_counter()
-        mp4 = encode_mp4(list(out), fps)
         tm = dict(self.timings)
-        tm.update({"infer_s": t1 - t0, "encode_cid_s": time.perf_counter() - t1})
+        tm["infer_s"] = time.perf_counter() - t0
+        return out, fps, tm
+
+    @staticmethod
+    def finish(raw) -> "Solution":
+        """CPU tail of a solve, no GPU and no pipeline state: H.264 encode + MP4 + CID.  Task slots
+        run it while their pipeline mattes the next clip (node/solver.py ``infer_task``)."""
+        from ..node.solver import solve_files
+        from ..utils.mp4 import encode_mp4
+        out, fps, tm = raw
+        t1 = time.perf_counter()
+        mp4 = encode_mp4(out, fps)
+        tm = dict(tm, encode_cid_s=time.perf_counter() - t1)
         return solve_files([("out-1.mp4", mp4)], tm)
+
+    def solve(self, inp: dict):
+        return self.finish(self.infer(inp))

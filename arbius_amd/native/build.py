@@ -24,7 +24,8 @@ def build(force: bool = False) -> Path:
     if out.exists() and not force and all(out.stat().st_mtime >= f.stat().st_mtime for f in SOURCES + HEADERS):
         return out
     import pybind11
-    cmd = ["g++", "-O3", "-shared", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-pthread",
+    # x86-64-v2 (SSE4.2): every x86 server CPU since 2009; lets the H.264 quantiser loops use pmulld
+    cmd = ["g++", "-O3", "-march=x86-64-v2", "-shared", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-pthread",
            "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], *map(str, SOURCES), "-lz", "-o",
            str(out)]
     subprocess.run(cmd, check=True)

@@ -21,6 +21,8 @@
 // task's input undecodable instead of failing the solve).
 #include "h264.h"
 
+#include <emmintrin.h>   // SSE2 (x86-64 baseline): psadbw for the mode-decision SADs
+
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -698,25 +700,80 @@ struct Frame {
 
 // Reconstruction of an Intra_16x16 macroblock from its levels (normative, shared enc/dec).
 // dc: 16 levels in scan order; ac[blk][0..14]: levels of scan positions 1..15 (blkIdx order)
+// AC dequantisation of one QP as a table: dequant(c, qp, r) == (c * mul[r] + add) >> sh (qp >= 24:
+// c * ls * 2^n == c * (ls << n), add = sh = 0) - the same integers, without the per-coefficient
+// position class / qp split.
+struct AcDequant {
+  int mul[16], add, sh;
+  explicit AcDequant(int qp) {
+    const int q6 = qp / 6;
+    for (int r = 0; r < 16; ++r) mul[r] = qp >= 24 ? level_scale(qp % 6, r) * (1 << (q6 - 4)) : level_scale(qp % 6, r);
+    add = qp >= 24 ? 0 : 1 << (3 - q6);
+    sh = qp >= 24 ? 0 : 4 - q6;
+  }
+  int operator()(int c, int r) const { return (c * mul[r] + add) >> sh; }
+};
+
+// Residual of one 4x4 block into an n x n int16 residual plane (saturated to int16: pred + r is
+// clipped to [0, 255] afterwards, and any |r| beyond the int16 range clips to the same 0 / 255).
+// A block whose only non-zero coefficient is the DC has the constant residual (d0 + 32) >> 6
+// (inv4x4's rows and columns pass d0 through unchanged).
+inline int16_t sat16(int v) { return int16_t(v < -32768 ? -32768 : v > 32767 ? 32767 : v); }
+inline void put_residual(int16_t* rs, int n, int bx, int by, int* d, bool any_ac) {
+  int16_t* o = rs + n * 4 * by + 4 * bx;
+  if (!any_ac) {
+    const int16_t v = sat16((d[0] + 32) >> 6);
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) o[n * y + x] = v;
+    return;
+  }
+  int r[16];
+  inv4x4(d, r);
+  for (int y = 0; y < 4; ++y)
+    for (int x = 0; x < 4; ++x) o[n * y + x] = sat16(r[4 * y + x]);
+}
+// dst = clip255(pred + rs) over a 16 x 16 (n = 16) or 8 x 8 (n = 8) block: saturating int16 adds
+// and an unsigned-saturating pack, the same values as the scalar clip.
+inline void add_residual(uint8_t* dst, int dstride, const uint8_t* pred, const int16_t* rs, int n) {
+  const __m128i z = _mm_setzero_si128();
+  for (int y = 0; y < n; ++y) {
+    const int16_t* r = rs + n * y;
+    if (n == 16) {
+      const __m128i p = _mm_loadu_si128(reinterpret_cast<const __m128i*>(pred + 16 * y));
+      const __m128i lo = _mm_adds_epi16(_mm_unpacklo_epi8(p, z), _mm_loadu_si128(reinterpret_cast<const __m128i*>(r)));
+      const __m128i hi = _mm_adds_epi16(_mm_unpackhi_epi8(p, z), _mm_loadu_si128(reinterpret_cast<const __m128i*>(r + 8)));
+      _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + size_t(y) * dstride), _mm_packus_epi16(lo, hi));
+    } else {
+      const __m128i p = _mm_loadl_epi64(reinterpret_cast<const __m128i*>(pred + 8 * y));
+      const __m128i lo = _mm_adds_epi16(_mm_unpacklo_epi8(p, z), _mm_loadu_si128(reinterpret_cast<const __m128i*>(r)));
+      _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + size_t(y) * dstride), _mm_packus_epi16(lo, lo));
+    }
+  }
+}
+
 void recon_luma16(Frame& f, int mx, int my, const uint8_t* pred, const int* dc, const int (*ac)[15], int qp) {
   int c[16], fdc[16];
   for (int k = 0; k < 16; ++k) c[kZigzag[k]] = dc[k];
   hadamard4(c, fdc);
   const int ls = level_scale(qp % 6, 0);
+  const AcDequant dq(qp);
+  alignas(16) int16_t rs[256];
   for (int blk = 0; blk < 16; ++blk) {
     const int bx = kBlkX[blk], by = kBlkY[blk];
     const int fv = fdc[4 * by + bx];
-    int d[16] = {0}, r[16];
+    int d[16] = {0};
     d[0] = qp >= 36 ? fv * ls * (1 << (qp / 6 - 6)) : (fv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+    bool any = false;
     for (int k = 0; k < 15; ++k) {
       const int rp = kZigzag[k + 1];
-      if (ac[blk][k]) d[rp] = dequant(ac[blk][k], qp, rp);
+      if (ac[blk][k]) {
+        d[rp] = dq(ac[blk][k], rp);
+        any = true;
+      }
     }
-    inv4x4(d, r);
-    uint8_t* dst = f.y.data() + size_t(my * 16 + 4 * by) * f.W + mx * 16 + 4 * bx;
-    for (int y = 0; y < 4; ++y)
-      for (int x = 0; x < 4; ++x) dst[y * f.W + x] = clip255(pred[16 * (4 * by + y) + 4 * bx + x] + r[4 * y + x]);
+    put_residual(rs, 16, bx, by, d, any);
   }
+  add_residual(f.y.data() + size_t(my * 16) * f.W + mx * 16, f.W, pred, rs, 16);
 }
 
 // chroma component: dc[4] raster (blkIdx) order, ac[4][15]
@@ -726,19 +783,23 @@ void recon_chroma(std::vector<uint8_t>& pl, int Wc, int mx, int my, const uint8_
   const int f2 = dc[0] + dc[1] - dc[2] - dc[3], f3 = dc[0] - dc[1] - dc[2] + dc[3];
   const int fv[4] = {f0, f1, f2, f3};
   const int ls = level_scale(qpc % 6, 0);
+  const AcDequant dq(qpc);
+  alignas(16) int16_t rs[64];
   for (int blk = 0; blk < 4; ++blk) {
     const int bx = blk & 1, by = blk >> 1;
-    int d[16] = {0}, r[16];
+    int d[16] = {0};
     d[0] = (fv[blk] * ls * (1 << (qpc / 6))) >> 5;
+    bool any = false;
     for (int k = 0; k < 15; ++k) {
       const int rp = kZigzag[k + 1];
-      if (ac[blk][k]) d[rp] = dequant(ac[blk][k], qpc, rp);
+      if (ac[blk][k]) {
+        d[rp] = dq(ac[blk][k], rp);
+        any = true;
+      }
     }
-    inv4x4(d, r);
-    uint8_t* dst = pl.data() + size_t(my * 8 + 4 * by) * Wc + mx * 8 + 4 * bx;
-    for (int y = 0; y < 4; ++y)
-      for (int x = 0; x < 4; ++x) dst[y * Wc + x] = clip255(pred[8 * (4 * by + y) + 4 * bx + x] + r[4 * y + x]);
+    put_residual(rs, 8, bx, by, d, any);
   }
+  add_residual(pl.data() + size_t(my * 8) * Wc + mx * 8, Wc, pred, rs, 8);
 }
 
 // ------------------------------------------------------------------------------------ inter (P) tools
@@ -1206,11 +1267,43 @@ inline int quant(int w, int mf, int f, int qbits) {
   return w < 0 ? -z : z;
 }
 
+// Sum of absolute differences of an n x n source block against a packed n x n prediction, n = 8
+// or 16: one psadbw per row (integer: the same value as the scalar sum).
+inline int hsum_sad(__m128i acc) { return _mm_cvtsi128_si32(acc) + _mm_cvtsi128_si32(_mm_srli_si128(acc, 8)); }
 int sad(const uint8_t* src, int stride, const uint8_t* pred, int n) {
-  int s = 0;
-  for (int y = 0; y < n; ++y)
-    for (int x = 0; x < n; ++x) s += std::abs(int(src[y * stride + x]) - int(pred[n * y + x]));
-  return s;
+  __m128i acc = _mm_setzero_si128();
+  if (n == 16) {
+    for (int y = 0; y < 16; ++y)
+      acc = _mm_add_epi64(acc, _mm_sad_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(src + y * stride)),
+                                            _mm_loadu_si128(reinterpret_cast<const __m128i*>(pred + 16 * y))));
+  } else {
+    for (int y = 0; y < n; ++y)
+      acc = _mm_add_epi64(acc, _mm_sad_epu8(_mm_loadl_epi64(reinterpret_cast<const __m128i*>(src + y * stride)),
+                                            _mm_loadl_epi64(reinterpret_cast<const __m128i*>(pred + n * y))));
+  }
+  return hsum_sad(acc);
+}
+
+// SAD of a 16x16 source block against Intra_16x16 mode 0 / 1 / 2 (V / H / DC) without building
+// the prediction: row y is compared against the top row, the broadcast left sample or the DC.
+int sad16_mode(const uint8_t* src, int stride, const uint8_t* pl, int pstride, int x0, int y0, const Nb& nb, int mode) {
+  __m128i acc = _mm_setzero_si128();
+  if (mode == 0) {
+    const __m128i top = _mm_loadu_si128(reinterpret_cast<const __m128i*>(pl + (y0 - 1) * pstride + x0));
+    for (int y = 0; y < 16; ++y)
+      acc = _mm_add_epi64(acc, _mm_sad_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(src + y * stride)), top));
+  } else if (mode == 1) {
+    for (int y = 0; y < 16; ++y)
+      acc = _mm_add_epi64(acc, _mm_sad_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(src + y * stride)),
+                                            _mm_set1_epi8(char(pl[(y0 + y) * pstride + x0 - 1]))));
+  } else {
+    uint8_t dc[256];
+    pred16(pl, pstride, x0, y0, nb, 2, dc);
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(dc));
+    for (int y = 0; y < 16; ++y)
+      acc = _mm_add_epi64(acc, _mm_sad_epu8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(src + y * stride)), v));
+  }
+  return hsum_sad(acc);
 }
 
 void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, const uint8_t* scr, int mx, int my,
@@ -1223,23 +1316,38 @@ void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, c
   const uint8_t* src = sy + size_t(my * 16) * W + mx * 16;
   for (int m : {0, 1, 2, 3}) {
     if ((m == 0 && !nb.top) || (m == 1 && !nb.left) || (m == 3 && !(nb.top && nb.left && nb.topleft))) continue;
-    pred16(f.y.data(), W, mx * 16, my * 16, nb, m, pred);
-    const int s = sad(src, W, pred, 16);
+    int s;
+    if (m < 3) {
+      s = sad16_mode(src, W, f.y.data(), W, mx * 16, my * 16, nb, m);
+    } else {
+      pred16(f.y.data(), W, mx * 16, my * 16, nb, m, pred);
+      s = sad(src, W, pred, 16);
+    }
     if (s < best_sad) {
       best_sad = s;
       mode = m;
-      std::memcpy(best, pred, 256);
     }
   }
+  if (mode == 3) std::memcpy(best, pred, 256);
+  else pred16(f.y.data(), W, mx * 16, my * 16, nb, mode, best);
   // ---- luma residual -> levels
   const int qp6 = qp % 6, qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
   int W4[16][16], dcm[16], ac[16][15];
+  alignas(16) int16_t rsd[256];   // src - pred, 16 x 16 (one unpack + subtract per 8 samples)
+  {
+    const __m128i z = _mm_setzero_si128();
+    for (int y = 0; y < 16; ++y) {
+      const __m128i sv = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + size_t(y) * W));
+      const __m128i pv = _mm_loadu_si128(reinterpret_cast<const __m128i*>(best + 16 * y));
+      _mm_store_si128(reinterpret_cast<__m128i*>(rsd + 16 * y), _mm_sub_epi16(_mm_unpacklo_epi8(sv, z), _mm_unpacklo_epi8(pv, z)));
+      _mm_store_si128(reinterpret_cast<__m128i*>(rsd + 16 * y + 8), _mm_sub_epi16(_mm_unpackhi_epi8(sv, z), _mm_unpackhi_epi8(pv, z)));
+    }
+  }
   for (int blk = 0; blk < 16; ++blk) {
     const int bx = kBlkX[blk], by = kBlkY[blk];
     int res[16];
     for (int y = 0; y < 4; ++y)
-      for (int x = 0; x < 4; ++x)
-        res[4 * y + x] = int(src[(4 * by + y) * W + 4 * bx + x]) - int(best[16 * (4 * by + y) + 4 * bx + x]);
+      for (int x = 0; x < 4; ++x) res[4 * y + x] = rsd[16 * (4 * by + y) + 4 * bx + x];
     fwd4x4(res, W4[blk]);
     dcm[4 * by + bx] = W4[blk][0];
   }
@@ -1247,12 +1355,17 @@ void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, c
   hadamard4(dcm, hd);
   bool any_ac = false;
   for (int k = 0; k < 16; ++k) dc[k] = quant(hd[kZigzag[k]] / 2, kMF[qp6][0], 2 * fq, qbits + 1);
-  for (int blk = 0; blk < 16; ++blk)
+  int mfz[15];   // quantiser multiplier per scan position 1..15
+  for (int k = 0; k < 15; ++k) mfz[k] = kMF[qp6][pos_class(kZigzag[k + 1])];
+  for (int blk = 0; blk < 16; ++blk) {
+    int zz[15], nz = 0;   // scan order first, so the quantiser loop is contiguous (vectorised)
+    for (int k = 0; k < 15; ++k) zz[k] = W4[blk][kZigzag[k + 1]];
     for (int k = 0; k < 15; ++k) {
-      const int rp = kZigzag[k + 1];
-      ac[blk][k] = quant(W4[blk][rp], kMF[qp6][pos_class(rp)], fq, qbits);
-      any_ac |= ac[blk][k] != 0;
+      ac[blk][k] = quant(zz[k], mfz[k], fq, qbits);
+      nz |= ac[blk][k];
     }
+    any_ac |= nz != 0;
+  }
   const int cbp_luma = any_ac ? 15 : 0;
   if (!any_ac) std::memset(ac, 0, sizeof(ac));
   // ---- chroma
@@ -1275,7 +1388,8 @@ void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, c
       std::memcpy(cpred, p, sizeof(p));
     }
   }
-  int cdc[2][4], cac[2][4][15];
+  int cdc[2][4], cac[2][4][15], mfc[15];
+  for (int k = 0; k < 15; ++k) mfc[k] = kMF[qc6][pos_class(kZigzag[k + 1])];
   bool c_any_dc = false, c_any_ac = false;
   for (int c = 0; c < 2; ++c) {
     int Wb[4][16];
@@ -1286,11 +1400,13 @@ void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, c
         for (int x = 0; x < 4; ++x)
           res[4 * y + x] = int(csrc[c][(4 * by + y) * Wc + 4 * bx + x]) - int(cpred[c][8 * (4 * by + y) + 4 * bx + x]);
       fwd4x4(res, Wb[blk]);
+      int zz[15], nz = 0;
+      for (int k = 0; k < 15; ++k) zz[k] = Wb[blk][kZigzag[k + 1]];
       for (int k = 0; k < 15; ++k) {
-        const int rp = kZigzag[k + 1];
-        cac[c][blk][k] = quant(Wb[blk][rp], kMF[qc6][pos_class(rp)], fqc, qcbits);
-        c_any_ac |= cac[c][blk][k] != 0;
+        cac[c][blk][k] = quant(zz[k], mfc[k], fqc, qcbits);
+        nz |= cac[c][blk][k];
       }
+      c_any_ac |= nz != 0;
     }
     const int d0 = Wb[0][0], d1 = Wb[1][0], d2 = Wb[2][0], d3 = Wb[3][0];
     const int h[4] = {d0 + d1 + d2 + d3, d0 - d1 + d2 - d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3};

@@ -19,7 +19,7 @@ import numpy as np
 
 from ..ipfs.unixfs import wrap_directory
 from ..utils.png import encode_png
-from .solver import Solution, solve_task
+from .solver import Solution, infer_task
 
 
 class FakeSolverPool:
@@ -115,9 +115,10 @@ class LocalSolverPool:
         free = self._pipe(model)
         pipe = free.get()
         try:
-            return solve_task(model, pipe, inp)
+            tail = infer_task(model, pipe, inp)
         finally:
-            free.put(pipe)
+            free.put(pipe)          # the CPU tail (encode + CID) runs after the fork is back
+        return tail()
 
     def _solve_waiting(self, model, pending: "queue.Queue"):
         """A stream's turn: this request plus any queued compatible ones, solved lock-step.  A group's
@@ -126,7 +127,7 @@ class LocalSolverPool:
         from .solver import encode_images, infer_images, take_group
         free = self._pipe(model)
         pipe = free.get()
-        batch, imgs, tm = [], None, None
+        batch, imgs, tm, tails = [], None, None, None
         try:
             try:
                 first = pending.get_nowait()
@@ -137,9 +138,7 @@ class LocalSolverPool:
             if len(batch) > 1 and hasattr(pipe, "run_group"):
                 imgs, tm = infer_images(pipe, [r[1] for r in batch])
             else:
-                sols = [solve_task(r[0], pipe, r[1]) for r in batch]
-                for r, sol in zip(batch, sols):
-                    r[2].set_result(sol)
+                tails = [infer_task(r[0], pipe, r[1]) for r in batch]
         except BaseException as e:  # noqa: BLE001
             for r in batch:
                 if not r[2].done():
@@ -147,6 +146,13 @@ class LocalSolverPool:
             return
         finally:
             free.put(pipe)
+        if tails is not None:           # CPU tails after the fork went back (RVM: H.264 encode)
+            for r, tail in zip(batch, tails):
+                try:
+                    r[2].set_result(tail())
+                except BaseException as e:  # noqa: BLE001
+                    r[2].set_exception(e)
+            return
         if imgs is None:
             return
         try:

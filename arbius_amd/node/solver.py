@@ -154,3 +154,18 @@ def solve_task(model, pipe, inp: dict) -> Solution:
     if model.kind == "image":
         return solve_image(pipe, inp)
     raise ValueError(f"no solver for model kind {model.kind}")
+
+
+def infer_task(model, pipe, inp: dict):
+    """Two-phase solve for task slots: the GPU part runs now, while the caller holds the pipeline;
+    the returned callable is the CPU tail (encode + CID) and touches no pipeline state, so the slot
+    can hand its pipeline / stream to the next task first.  Pipelines with a separable tail expose
+    ``infer(inp) -> raw`` and a static ``finish(raw) -> Solution`` (RVM: the 1080p H.264 encode is
+    longer than the matting); for the rest the tail is the finished solution.  Same bytes as
+    ``solve_task``."""
+    if hasattr(pipe, "infer") and hasattr(type(pipe), "finish"):
+        raw = pipe.infer(inp)
+        fin = type(pipe).finish
+        return lambda: fin(raw)
+    sol = solve_task(model, pipe, inp)
+    return lambda: sol

@@ -61,7 +61,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
 
     from ..models.registry import build_pipeline
     from ..node.models import Model
-    from ..node.solver import encode_images, infer_images, solve_task, take_group
+    from ..node.solver import encode_images, infer_images, infer_task, take_group
     from . import dist as D
 
     try:
@@ -105,6 +105,7 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
         # per slot: one thread for a lock-step group's PNG + CID tail, so the slot's stream starts
         # its next group while the previous one encodes
         tails = [ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"tail{k}") for k in range(streams)]
+        last_tail = [None] * streams        # a slot's solo-task tail in flight (at most one: RVM clips are 300 MB)
         # per-model cap on concurrently solving slots (e.g. Kandinsky2 peaks at 2 streams per GPU)
         caps = {n: threading.Semaphore(max(1, min(streams, int((model_streams or {}).get(n, streams)))))
                 for n in pipes}
@@ -117,6 +118,16 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                     out_q.put(("ok", m[0], rank, sol))
             except Exception:  # noqa: BLE001
                 for m in batch:
+                    out_q.put(("err", m[0], rank, traceback.format_exc()))
+
+        def finish_solo(batch, tail_fns, t0):
+            for m, fn in zip(batch, tail_fns):
+                try:
+                    sol = fn()
+                    sol.dag = None  # blocks are recomputed by the pinner; keep the message small
+                    sol.timings["worker_s"] = time.perf_counter() - t0
+                    out_q.put(("ok", m[0], rank, sol))
+                except Exception:  # noqa: BLE001
                     out_q.put(("err", m[0], rank, traceback.format_exc()))
 
         def slot_loop(k):
@@ -139,11 +150,12 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                         imgs, tm = infer_images(slots[k][mname], [m[5] for m in batch])
                         tails[k].submit(finish, batch, imgs, tm, t0)
                         continue
-                    sols = [solve_task(Model(m[3], m[1], {}, True, [], m[2]), slots[k][m[1]], m[5]) for m in batch]
-                    for m, sol in zip(batch, sols):
-                        sol.dag = None  # blocks are recomputed by the pinner; keep the message small
-                        sol.timings["worker_s"] = time.perf_counter() - t0
-                        out_q.put(("ok", m[0], rank, sol))
+                    # GPU part now; the CPU tail (e.g. RVM's H.264 encode) on the slot's tail thread
+                    # while the slot takes its next task
+                    fns = [infer_task(Model(m[3], m[1], {}, True, [], m[2]), slots[k][m[1]], m[5]) for m in batch]
+                    if last_tail[k] is not None:
+                        last_tail[k].result()
+                    last_tail[k] = tails[k].submit(finish_solo, batch, fns, t0)
                 except Exception:  # noqa: BLE001
                     for m in batch:
                         out_q.put(("err", m[0], rank, traceback.format_exc()))

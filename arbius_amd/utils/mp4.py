@@ -223,8 +223,16 @@ def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False, sync=None
 
 
 def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra", threads: int = 16) -> bytes:
-    """uint8 RGB frames [H, W, 3] (all the same size) -> MP4 bytes (deterministic)."""
-    frames = list(frames)
+    """uint8 RGB frames [H, W, 3] (all the same size), or one uint8 array [F, H, W, 3] (passed to
+    the native encoder without a copy) -> MP4 bytes (deterministic)."""
+    if isinstance(frames, np.ndarray) and frames.ndim == 4:
+        if frames.dtype != np.uint8 or frames.shape[3] != 3:
+            raise ValueError("encode_mp4: frames must be uint8 [F, H, W, 3]")
+        clip = np.ascontiguousarray(frames)
+        frames = list(clip)
+    else:
+        frames = list(frames)
+        clip = None
     if not frames:
         raise ValueError("encode_mp4: no frames")
     if codec not in CODECS:
@@ -245,11 +253,12 @@ def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra",
             raise RuntimeError("encode_mp4: the native runtime (H.264 encoder) is not built; "
                                "run python -m arbius_amd.native.build")
         sps, pps = sps_pps(W, H, INTRA_QP)
+        clip = np.stack(frames) if clip is None else clip
         if codec == "avc":
-            _, _, pics = native.h264_encode_rgb_stream(np.stack(frames), INTRA_QP, GOP, threads, ROWS_PER_SLICE)
+            _, _, pics = native.h264_encode_rgb_stream(clip, INTRA_QP, GOP, threads, ROWS_PER_SLICE)
             sync = list(range(0, len(frames), GOP))
         else:
-            _, _, nals = native.h264_encode_rgb(np.stack(frames), INTRA_QP, threads)
+            _, _, nals = native.h264_encode_rgb(clip, INTRA_QP, threads)
             pics = [[n] for n in nals]
     samples = [b"".join(struct.pack(">I", len(n)) + n for n in p) for p in pics]
     sizes = [len(s) for s in samples]

@@ -161,20 +161,28 @@ def run(args):
         lat.extend([time.perf_counter() - t0] * len(sols))
         return sols[-1]
 
+    def finish_clip(t0, tid, raw):
+        """CPU tail of an RVM task: MP4 encode + CID + commitment."""
+        sol = type(pipe).finish(raw)
+        generate_commitment(wallet, tid, sol.cid)
+        lat.append(time.perf_counter() - t0)
+        return sol
+
     def one_task(i, pipe=pipe, tail=None):
         """Solve this slot's task(s) of step i; every solution gets its own task id's commitment.
         ``tail``: executor for a lock-step group's CPU tail (returns its future)."""
         t0 = time.perf_counter()
         if rvm:
-            from arbius_amd.node.solver import solve_files
-            from arbius_amd.utils.mp4 import encode_mp4
+            # the node's two-phase solve (node/solver.py infer_task): matting on the slot's stream,
+            # then the H.264 encode + CID (RVMPipeline.finish, CPU only) on the slot's tail thread
+            # while the stream mattes the next clip
             out = pipe(clip, "green-screen")
-            t1 = time.perf_counter()
             tm = dict(pipe.timings)
-            tm.update({"infer_s": t1 - t0})
-            sol = solve_files([("out-1.mp4", encode_mp4(list(out), 24))], tm)
-            sol.timings["encode_cid_s"] = time.perf_counter() - t1
-            done = [(tid_of(i), sol)]
+            tm.update({"infer_s": time.perf_counter() - t0})
+            raw = (out, 24, tm)
+            if tail is not None:
+                return tail.submit(finish_clip, t0, tid_of(i), raw)
+            return finish_clip(t0, tid_of(i), raw)
         elif vid:  # BASELINE config #4: 576x320x24f text-to-video
             inp = {"prompt": f"a red cat walking on a castle wall, cinematic, task {i}", "num_frames": args.frames,
                    "width": args.res, "height": args.height, "num_inference_steps": args.denoise_steps,

@@ -41,16 +41,16 @@ def test_capped_model_solves_at_most_cap_at_once(monkeypatch):
     import arbius_amd.node.pool as P
     live, peak, lock = [0], [0], threading.Lock()
 
-    def fake_solve(model, pipe, inp):
+    def fake_infer(model, pipe, inp):      # the GPU part (holds the fork); the tail is free
         with lock:
             live[0] += 1
             peak[0] = max(peak[0], live[0])
         time.sleep(0.05)
         with lock:
             live[0] -= 1
-        return inp
+        return lambda: inp
 
-    monkeypatch.setattr(P, "solve_task", fake_solve)
+    monkeypatch.setattr(P, "infer_task", fake_infer)
     pool = LocalSolverPool("cpu", pipeline_factory=lambda name, **kw: _Pipe(), capacity=4,
                            model_streams={"kandinsky2": 2})
     ts = [threading.Thread(target=pool.solve_sync, args=(_Model("kandinsky2"), i, {"i": i})) for i in range(4)]
@@ -59,3 +59,56 @@ def test_capped_model_solves_at_most_cap_at_once(monkeypatch):
     for t in ts:
         t.join()
     assert peak[0] == 2
+
+
+def test_two_phase_solve_releases_fork_before_tail(monkeypatch):
+    """A pipeline with ``infer`` / static ``finish`` (RVM): the fork goes back to the pool before the
+    CPU tail runs, so a second solve's GPU part overlaps the first one's tail; same result as solve."""
+    import arbius_amd.node.pool as P
+    events, lock = [], threading.Lock()
+
+    class _Split:
+        def fork(self):
+            return _Split()
+
+        def infer(self, inp):
+            with lock:
+                events.append(("infer", inp["i"]))
+            return inp["i"]
+
+        @staticmethod
+        def finish(raw):
+            time.sleep(0.1)
+            with lock:
+                events.append(("finish", raw))
+            return raw * 10
+
+        def solve(self, inp):
+            return self.finish(self.infer(inp))
+
+    pool = P.LocalSolverPool("cpu", pipeline_factory=lambda name, **kw: _Split(), capacity=1)
+    out = {}
+    ts = [threading.Thread(target=lambda i=i: out.__setitem__(i, pool.solve_sync(_Model("rvm"), i, {"i": i})))
+          for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert out == {0: 0, 1: 10}
+    # one fork: the second infer ran before the first tail finished
+    assert [e[0] for e in events][:2] == ["infer", "infer"]
+
+
+def test_encode_mp4_array_equals_frame_list():
+    """``encode_mp4`` on one [F, H, W, 3] array (no stack copy) writes the frame list's bytes."""
+    import numpy as np
+
+    from arbius_amd import native
+    from arbius_amd.utils.mp4 import encode_mp4
+    if not native.loaded:
+        import pytest
+        pytest.skip("native runtime not built")
+    rng = np.random.default_rng(3)
+    clip = rng.integers(0, 256, (3, 48, 64, 3), dtype=np.uint8)
+    assert encode_mp4(clip, 12) == encode_mp4(list(clip), 12)
+    assert encode_mp4(clip, 12, codec="avc") == encode_mp4(list(clip), 12, codec="avc")
