@@ -18,6 +18,7 @@ place by the gate kernel.  BatchNorm is folded into conv biases (inference).
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass
 from typing import List, Tuple
@@ -29,6 +30,15 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..utils.progress import beat
+
+def _host_copy(dst: np.ndarray, src: "torch.Tensor"):
+    """Pinned staging buffer -> result array through ATen's CPU copy: it drops the GIL (a numpy
+    slice assignment of a 37 MB chunk holds it, stalling the other task slots' kernel launches)."""
+    torch.from_numpy(dst).view(-1).copy_(src.view(-1))
+
+
+# CPU priority of the output encode's threads (RVMPipeline.finish); 0 = same as the caller
+ENCODE_NICE = int(os.environ.get("ARB_ENCODE_NICE", "10"))
 from .graphs import PipelineBase
 
 CL = torch.channels_last
@@ -392,14 +402,14 @@ class RVMPipeline(PipelineBase):
             if len(pending) >= 2:         # the staging buffer's previous download must be drained first
                 e, v, sl = pending.pop(0)
                 e.synchronize()
-                res[sl] = v.numpy().reshape(res[sl].shape)
+                _host_copy(res[sl], v)
             ob.copy_(out.view(-1), non_blocking=True)
             e = torch.cuda.Event()
             e.record(stream)
             pending.append((e, ob, slice(i, i + t)))
         for e, v, sl in pending:
             e.synchronize()
-            res[sl] = v.numpy().reshape(res[sl].shape)
+            _host_copy(res[sl], v)
         return res
 
     def _matte(self, frames: np.ndarray, output_type: str) -> np.ndarray:
@@ -448,7 +458,8 @@ class RVMPipeline(PipelineBase):
         from ..utils.mp4 import encode_mp4
         out, fps, tm = raw
         t1 = time.perf_counter()
-        mp4 = encode_mp4(out, fps)
+        # encode threads at nice 10: the slot's next clip's staging copies keep their CPU
+        mp4 = encode_mp4(out, fps, nice=ENCODE_NICE)
         tm = dict(tm, encode_cid_s=time.perf_counter() - t1)
         return solve_files([("out-1.mp4", mp4)], tm)
 

@@ -533,19 +533,18 @@ void pred4(const int* t, const int* l, int mode, bool has_top, bool has_left, in
 
 // ------------------------------------------------------------------------------------ CAVLC
 void write_block(BitWriter& bw, const int* coef, int max_num, int nC) {
-  int levels[16], runs[16], tc = 0, last = max_num - 1;
-  while (last >= 0 && !coef[last]) --last;
-  int zeros = 0;
-  for (int i = last; i >= 0; --i) {   // reverse scan: runs[k] = zeros just below level k
-    if (coef[i]) {
-      if (tc) runs[tc - 1] = zeros;
-      levels[tc++] = coef[i];
-      zeros = 0;
-    } else {
-      ++zeros;
-    }
+  int levels[16], runs[16], tc = 0;
+  // non-zero mask of the max_num (4 / 15 / 16) levels, then a reverse walk over its set bits:
+  // runs[k] = zeros just below level k (the gap to the next set bit)
+  uint32_t nzm = 0;
+  for (int i = 0; i < max_num; ++i) nzm |= uint32_t(coef[i] != 0) << i;
+  const int last = nzm ? 31 - __builtin_clz(nzm) : -1;
+  for (uint32_t m = nzm; m;) {
+    const int i = 31 - __builtin_clz(m);
+    m &= ~(1u << i);
+    levels[tc] = coef[i];
+    runs[tc++] = m ? i - 1 - (31 - __builtin_clz(m)) : i;
   }
-  if (tc) runs[tc - 1] = zeros;
   const int total_zeros = last + 1 - tc;
   int t1 = 0;
   while (t1 < tc && t1 < 3 && (levels[t1] == 1 || levels[t1] == -1)) ++t1;
@@ -763,15 +762,13 @@ void recon_luma16(Frame& f, int mx, int my, const uint8_t* pred, const int* dc, 
     const int fv = fdc[4 * by + bx];
     int d[16] = {0};
     d[0] = qp >= 36 ? fv * ls * (1 << (qp / 6 - 6)) : (fv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
-    bool any = false;
+    int any = 0;   // a zero level dequantises to 0 ((0 * mul + add) >> sh, add < 2^sh): no branch
     for (int k = 0; k < 15; ++k) {
       const int rp = kZigzag[k + 1];
-      if (ac[blk][k]) {
-        d[rp] = dq(ac[blk][k], rp);
-        any = true;
-      }
+      d[rp] = dq(ac[blk][k], rp);
+      any |= ac[blk][k];
     }
-    put_residual(rs, 16, bx, by, d, any);
+    put_residual(rs, 16, bx, by, d, any != 0);
   }
   add_residual(f.y.data() + size_t(my * 16) * f.W + mx * 16, f.W, pred, rs, 16);
 }
@@ -789,15 +786,13 @@ void recon_chroma(std::vector<uint8_t>& pl, int Wc, int mx, int my, const uint8_
     const int bx = blk & 1, by = blk >> 1;
     int d[16] = {0};
     d[0] = (fv[blk] * ls * (1 << (qpc / 6))) >> 5;
-    bool any = false;
+    int any = 0;
     for (int k = 0; k < 15; ++k) {
       const int rp = kZigzag[k + 1];
-      if (ac[blk][k]) {
-        d[rp] = dq(ac[blk][k], rp);
-        any = true;
-      }
+      d[rp] = dq(ac[blk][k], rp);
+      any |= ac[blk][k];
     }
-    put_residual(rs, 8, bx, by, d, any);
+    put_residual(rs, 8, bx, by, d, any != 0);
   }
   add_residual(pl.data() + size_t(my * 8) * Wc + mx * 8, Wc, pred, rs, 8);
 }

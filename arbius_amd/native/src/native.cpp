@@ -22,6 +22,10 @@
 
 #include "secp256k1.h"
 
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <functional>
 #include <cstdint>
@@ -233,9 +237,14 @@ static void rgb_to_420(const uint8_t* src, int H, int W, int H16, int W16, uint8
     }
 }
 
-static void run_parallel(int n, int threads, const std::function<void(int)>& fn) {
+// nice > 0: every item runs on a spawned thread that first lowers its own scheduling priority
+// (Linux setpriority on the thread id; raising nice needs no privilege) and the caller only joins.
+// A background encode then yields the CPU to the threads that feed the GPU (the next clip's
+// host<->device staging copies) instead of time-slicing with them.
+static void run_parallel(int n, int threads, const std::function<void(int)>& fn, int nice = 0) {
   std::vector<std::string> errors(n);
   auto work = [&](int t, int nt) {
+    if (nice > 0) setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice);
     for (int i = t; i < n; i += nt) {
       try {
         fn(i);
@@ -246,8 +255,8 @@ static void run_parallel(int n, int threads, const std::function<void(int)>& fn)
   };
   const int nt = std::max(1, std::min(threads, n));
   std::vector<std::thread> pool;
-  for (int t = 1; t < nt; ++t) pool.emplace_back(work, t, nt);
-  work(0, nt);
+  for (int t = nice > 0 ? 0 : 1; t < nt; ++t) pool.emplace_back(work, t, nt);
+  if (nice <= 0) work(0, nt);
   for (auto& th : pool) th.join();
   for (auto& e : errors)
     if (!e.empty()) throw std::runtime_error(e);
@@ -256,7 +265,7 @@ static void run_parallel(int n, int threads, const std::function<void(int)>& fn)
 // frames uint8 [F, H, W, 3] -> (sps, pps, [IDR NAL per frame]); frames are independent pictures,
 // so they are encoded in parallel (the output does not depend on the thread count).
 static py::tuple h264_encode_rgb(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> frames, int qp,
-                                 int threads) {
+                                 int threads, int nice) {
   auto b = frames.request();
   if (b.ndim != 4 || b.shape[3] != 3 || b.shape[0] < 1 || b.shape[1] < 1 || b.shape[2] < 1)
     throw std::invalid_argument("h264_encode_rgb: frames [F, H, W, 3]");
@@ -272,7 +281,7 @@ static py::tuple h264_encode_rgb(py::array_t<uint8_t, py::array::c_style | py::a
       std::vector<uint8_t> y((size_t)H16 * W16), cb((size_t)H16 * W16 / 4), cr((size_t)H16 * W16 / 4);
       rgb_to_420(src + (size_t)i * H * W * 3, H, W, H16, W16, y.data(), cb.data(), cr.data());
       nals[i] = h264::encode_idr(y.data(), cb.data(), cr.data(), W16, H16, qp, i, nullptr, nullptr, nullptr);
-    });
+    }, nice);
   }
   py::list out;
   for (auto& n : nals) out.append(py::bytes(n));
@@ -535,7 +544,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("pcm_slice_body", &pcm_slice_body, py::arg("frame"), py::arg("threads") = 8,
         "H.264 I_PCM macroblock payload of one RGB frame");
   m.def("h264_encode_rgb", &h264_encode_rgb, py::arg("frames"), py::arg("qp"), py::arg("threads") = 8,
-        "H.264 CAVLC intra: RGB frames [F, H, W, 3] -> (sps, pps, [IDR NAL])");
+        py::arg("nice") = 0, "H.264 CAVLC intra: RGB frames [F, H, W, 3] -> (sps, pps, [IDR NAL]); nice > 0 runs "
+        "the encode threads at that lower priority");
   m.def("h264_encode_yuv", &h264_encode_yuv, py::arg("y"), py::arg("cb"), py::arg("cr"), py::arg("qp"),
         py::arg("idr_pic_id") = 0, "one 4:2:0 picture -> (IDR NAL, recon Y, Cb, Cr)");
   m.def("h264_parameter_sets", &h264_parameter_sets, py::arg("width"), py::arg("height"), py::arg("qp"),

@@ -222,9 +222,12 @@ def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False, sync=None
     return _box(b"moov", mvhd, _box(b"trak", tkhd, mdia))
 
 
-def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra", threads: int = 16) -> bytes:
+def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra", threads: int = 16,
+               nice: int = 0) -> bytes:
     """uint8 RGB frames [H, W, 3] (all the same size), or one uint8 array [F, H, W, 3] (passed to
-    the native encoder without a copy) -> MP4 bytes (deterministic)."""
+    the native encoder without a copy) -> MP4 bytes (deterministic).  ``nice`` > 0 runs the intra
+    encode's threads at that lower CPU priority (a background tail next to GPU-feeding threads);
+    bytes never depend on it."""
     if isinstance(frames, np.ndarray) and frames.ndim == 4:
         if frames.dtype != np.uint8 or frames.shape[3] != 3:
             raise ValueError("encode_mp4: frames must be uint8 [F, H, W, 3]")
@@ -258,7 +261,7 @@ def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra",
             _, _, pics = native.h264_encode_rgb_stream(clip, INTRA_QP, GOP, threads, ROWS_PER_SLICE)
             sync = list(range(0, len(frames), GOP))
         else:
-            _, _, nals = native.h264_encode_rgb(clip, INTRA_QP, threads)
+            _, _, nals = native.h264_encode_rgb(clip, INTRA_QP, threads, nice)
             pics = [[n] for n in nals]
     samples = [b"".join(struct.pack(">I", len(n)) + n for n in p) for p in pics]
     sizes = [len(s) for s in samples]

@@ -6,6 +6,7 @@
 //
 //   g++ -O3 -std=c++17 -pthread -I arbius_amd/native/src scripts/h264_bench.cpp
 //       arbius_amd/native/src/h264.cpp -o build/h264_bench && build/h264_bench [frames]
+#include <algorithm>
 #include <chrono>
 #include <ctime>
 #include <cmath>
@@ -17,16 +18,35 @@
 
 #include "h264.h"
 
+// argv[2] (optional): raw 1920x1088 4:2:0 pictures (Y, Cb, Cr planes back to back) to cycle
+// through instead of the synthetic ones, e.g. real matting output converted by the probe script.
 int main(int argc, char** argv) {
   const int F = argc > 1 ? std::atoi(argv[1]) : 8;
   const int W = 1920, H = 1088, Wc = W / 2, Hc = H / 2;
   std::vector<uint8_t> y((size_t)W * H), cb((size_t)Wc * Hc), cr((size_t)Wc * Hc);
+  std::vector<uint8_t> file;
+  if (argc > 2) {
+    FILE* fp = std::fopen(argv[2], "rb");
+    if (!fp) return 1;
+    uint8_t buf[1 << 16];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof(buf), fp)) > 0) file.insert(file.end(), buf, buf + n);
+    std::fclose(fp);
+  }
+  const size_t pic = y.size() + cb.size() + cr.size();
+  const int nfile = (int)(file.size() / pic);
   uint32_t rng = 12345u;
   auto rnd = [&]() { rng = rng * 1664525u + 1013904223u; return (rng >> 24) & 15; };
   uint64_t h = 1469598103934665603ull;
   size_t bytes = 0;
   double secs = 0;
   for (int f = 0; f < F; ++f) {
+    if (nfile > 0) {
+      const uint8_t* p = file.data() + (size_t)(f % nfile) * pic;
+      std::copy(p, p + y.size(), y.begin());
+      std::copy(p + y.size(), p + y.size() + cb.size(), cb.begin());
+      std::copy(p + y.size() + cb.size(), p + pic, cr.begin());
+    } else {
     // smooth shading + a moving edge + low-amplitude grain: a matted subject over a flat screen
     for (int r = 0; r < H; ++r)
       for (int c = 0; c < W; ++c) {
@@ -39,6 +59,7 @@ int main(int argc, char** argv) {
         cb[(size_t)r * Wc + c] = (uint8_t)(44 + ((r * 3 + c + f) & 7));
         cr[(size_t)r * Wc + c] = (uint8_t)(21 + ((r + c * 2) & 3));
       }
+    }
     timespec a, b;
     clock_gettime(CLOCK_THREAD_CPUTIME_ID, &a);   // thread CPU time: robust to preemption on a busy host
     const std::string nal = h264::encode_idr(y.data(), cb.data(), cr.data(), W, H, 20, f, nullptr, nullptr, nullptr);
