@@ -32,9 +32,10 @@ from .. import ops
 from ..utils.progress import beat
 
 def _host_copy(dst: np.ndarray, src: "torch.Tensor"):
-    """Pinned staging buffer -> result array through ATen's CPU copy: it drops the GIL (a numpy
-    slice assignment of a 37 MB chunk holds it, stalling the other task slots' kernel launches)."""
-    torch.from_numpy(dst).view(-1).copy_(src.view(-1))
+    """Pinned staging buffer -> result array.  A numpy assignment: an ATen copy (GIL released, but
+    OpenMP-parallel) measured 4-7 % slower on the 2-stream bench, its worker threads competing with
+    the encode (profiles/bench_r4_rvm/staging_copy_ab.md)."""
+    dst[...] = src.numpy().reshape(dst.shape)
 
 
 # CPU priority of the output encode's threads (RVMPipeline.finish); 0 = same as the caller
