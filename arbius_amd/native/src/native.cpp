@@ -220,21 +220,36 @@ static py::bytes pcm_slice_body(py::array_t<uint8_t, py::array::c_style | py::ar
 // ------------------------------------------------------------------------------------ H.264 CAVLC
 // RGB -> 4:2:0 (the same integer BT.601 conversion as pcm_slice_body / mp4.rgb_to_yuv420) of an
 // H x W frame edge-replicated to H16 x W16 (whole macroblocks; the SPS crops it back)
+// RGB -> 4:2:0 at macroblock-padded size (rows / columns past H / W replicate the last one).  Per
+// row: the columns inside the picture run as a plain stride-3 loop (no per-sample clamping, so
+// the compiler vectorises it), the padding columns reuse the last sample.
 static void rgb_to_420(const uint8_t* src, int H, int W, int H16, int W16, uint8_t* y, uint8_t* cb, uint8_t* cr) {
-  auto px = [&](int r, int x) { return src + ((size_t)std::min(r, H - 1) * W + std::min(x, W - 1)) * 3; };
-  for (int r = 0; r < H16; ++r)
-    for (int x = 0; x < W16; ++x) {
-      const uint8_t* p = px(r, x);
-      y[(size_t)r * W16 + x] = clip1(((66 * p[0] + 129 * p[1] + 25 * p[2] + 128) >> 8) + 16);
+  auto row = [&](int r) { return src + (size_t)std::min(r, H - 1) * W * 3; };
+  for (int r = 0; r < H16; ++r) {
+    const uint8_t* p = row(r);
+    uint8_t* o = y + (size_t)r * W16;
+    for (int x = 0; x < W; ++x)
+      o[x] = clip1(((66 * p[3 * x] + 129 * p[3 * x + 1] + 25 * p[3 * x + 2] + 128) >> 8) + 16);
+    for (int x = W; x < W16; ++x) o[x] = o[W - 1];
+  }
+  const int Wc = W16 / 2, Wi = W / 2;   // chroma columns whose 2x2 source lies inside the picture
+  for (int r = 0; r < H16 / 2; ++r) {
+    const uint8_t *p0 = row(2 * r), *p1 = row(2 * r + 1);
+    uint8_t *ob = cb + (size_t)r * Wc, *orr = cr + (size_t)r * Wc;
+    for (int x = 0; x < Wi; ++x) {
+      const uint8_t *a = p0 + 6 * x, *c = p1 + 6 * x;
+      const int rr = a[0] + a[3] + c[0] + c[3], g = a[1] + a[4] + c[1] + c[4], bl = a[2] + a[5] + c[2] + c[5];
+      ob[x] = clip1(((-38 * rr - 74 * g + 112 * bl + 512) >> 10) + 128);
+      orr[x] = clip1(((112 * rr - 94 * g - 18 * bl + 512) >> 10) + 128);
     }
-  for (int r = 0; r < H16 / 2; ++r)
-    for (int x = 0; x < W16 / 2; ++x) {
-      const uint8_t *a = px(2 * r, 2 * x), *b = px(2 * r, 2 * x + 1);
-      const uint8_t *c = px(2 * r + 1, 2 * x), *d = px(2 * r + 1, 2 * x + 1);
+    for (int x = Wi; x < Wc; ++x) {       // odd W / padding: clamp the source columns
+      const int x0 = std::min(2 * x, W - 1), x1 = std::min(2 * x + 1, W - 1);
+      const uint8_t *a = p0 + 3 * x0, *b = p0 + 3 * x1, *c = p1 + 3 * x0, *d = p1 + 3 * x1;
       const int rr = a[0] + b[0] + c[0] + d[0], g = a[1] + b[1] + c[1] + d[1], bl = a[2] + b[2] + c[2] + d[2];
-      cb[(size_t)r * (W16 / 2) + x] = clip1(((-38 * rr - 74 * g + 112 * bl + 512) >> 10) + 128);
-      cr[(size_t)r * (W16 / 2) + x] = clip1(((112 * rr - 94 * g - 18 * bl + 512) >> 10) + 128);
+      ob[x] = clip1(((-38 * rr - 74 * g + 112 * bl + 512) >> 10) + 128);
+      orr[x] = clip1(((112 * rr - 94 * g - 18 * bl + 512) >> 10) + 128);
     }
+  }
 }
 
 // nice > 0: every item runs on a spawned thread that first lowers its own scheduling priority
