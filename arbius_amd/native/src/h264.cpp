@@ -739,8 +739,10 @@ inline void add_residual(uint8_t* dst, int dstride, const uint8_t* pred, const i
     const int16_t* r = rs + n * y;
     if (n == 16) {
       const __m128i p = _mm_loadu_si128(reinterpret_cast<const __m128i*>(pred + 16 * y));
-      const __m128i lo = _mm_adds_epi16(_mm_unpacklo_epi8(p, z), _mm_loadu_si128(reinterpret_cast<const __m128i*>(r)));
-      const __m128i hi = _mm_adds_epi16(_mm_unpackhi_epi8(p, z), _mm_loadu_si128(reinterpret_cast<const __m128i*>(r + 8)));
+      const __m128i r0 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(r));
+      const __m128i r1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(r + 8));
+      const __m128i lo = _mm_adds_epi16(_mm_unpacklo_epi8(p, z), r0);
+      const __m128i hi = _mm_adds_epi16(_mm_unpackhi_epi8(p, z), r1);
       _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + size_t(y) * dstride), _mm_packus_epi16(lo, hi));
     } else {
       const __m128i p = _mm_loadl_epi64(reinterpret_cast<const __m128i*>(pred + 8 * y));
@@ -1334,8 +1336,10 @@ void encode_mb(BitWriter& bw, Frame& f, const uint8_t* sy, const uint8_t* scb, c
     for (int y = 0; y < 16; ++y) {
       const __m128i sv = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + size_t(y) * W));
       const __m128i pv = _mm_loadu_si128(reinterpret_cast<const __m128i*>(best + 16 * y));
-      _mm_store_si128(reinterpret_cast<__m128i*>(rsd + 16 * y), _mm_sub_epi16(_mm_unpacklo_epi8(sv, z), _mm_unpacklo_epi8(pv, z)));
-      _mm_store_si128(reinterpret_cast<__m128i*>(rsd + 16 * y + 8), _mm_sub_epi16(_mm_unpackhi_epi8(sv, z), _mm_unpackhi_epi8(pv, z)));
+      const __m128i lo = _mm_sub_epi16(_mm_unpacklo_epi8(sv, z), _mm_unpacklo_epi8(pv, z));
+      const __m128i hi = _mm_sub_epi16(_mm_unpackhi_epi8(sv, z), _mm_unpackhi_epi8(pv, z));
+      _mm_store_si128(reinterpret_cast<__m128i*>(rsd + 16 * y), lo);
+      _mm_store_si128(reinterpret_cast<__m128i*>(rsd + 16 * y + 8), hi);
     }
   }
   for (int blk = 0; blk < 16; ++blk) {
