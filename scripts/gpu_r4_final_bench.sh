@@ -17,4 +17,5 @@ run k2_c2g4 400 --model kandinsky2 --steps 4 --warmup 1
 run k2_solo 300 --model kandinsky2 --steps 4 --warmup 1 --concurrent 1 --group 1
 run sd_solo 300 --steps 6 --warmup 2 --concurrent 1 --group 1
 run zs_c2 600 --model zeroscopev2xl --steps 6 --warmup 1
+run rvm_c2 300 --model robust_video_matting --steps 6 --warmup 1
 echo "== done $(date +%T)"
