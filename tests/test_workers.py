@@ -93,3 +93,33 @@ def test_pool_reports_the_formed_world_and_closes():
         assert not any(p.is_alive() for p in pool.procs)
 
     asyncio.run(go())
+
+
+@pytest.mark.timeout(600)
+def test_worker_two_phase_solve_matches_solo():
+    """RVM's two-phase solve in a worker slot (matting on the slot, MP4 encode + CID on the slot's
+    tail thread while the slot takes the next clip): the CIDs of solo pipeline solves."""
+    import base64
+
+    import numpy as np
+
+    from arbius_amd.utils.mp4 import encode_mp4
+    rvm = Model("0x" + "cd" * 32, "robust_video_matting", load_template("robust_video_matting"), True, [], "video")
+    inps = []
+    for s in (4, 5, 6):
+        frames = np.random.default_rng(s).integers(0, 256, (2, 48, 64, 3), dtype=np.uint8)
+        src = "data:video/mp4;base64," + base64.b64encode(encode_mp4(list(frames), 5)).decode()
+        inps.append({"input_video": src, "output_type": "green-screen"})
+    local = LocalSolverPool("cpu", tiny=True)
+    ref = [local.solve_sync(rvm, f"r{i}", inp).cid for i, inp in enumerate(inps)]
+
+    async def go():
+        pool = MultiGPUSolverPool(1, ["robust_video_matting"], device_type="cpu", tiny=True, streams_per_gpu=2)
+        try:
+            sols = await asyncio.gather(*[pool.solve(rvm, f"t{i}", inp) for i, inp in enumerate(inps)])
+            assert [s.cid for s in sols] == ref
+            assert all("encode_cid_s" in s.timings for s in sols)
+        finally:
+            await pool.close()
+
+    asyncio.run(go())
