@@ -38,6 +38,9 @@ def _host_copy(dst: np.ndarray, src: "torch.Tensor"):
     dst[...] = src.numpy().reshape(dst.shape)
 
 
+# download the composites straight into a pinned result array (A/B switch; same bytes)
+_PINNED_OUT = os.environ.get("ARB_RVM_PINNED_OUT", "1") == "1"
+
 # CPU priority of the output encode's threads (RVMPipeline.finish); 0 = same as the caller
 ENCODE_NICE = int(os.environ.get("ARB_ENCODE_NICE", "10"))
 from .graphs import PipelineBase
@@ -381,6 +384,8 @@ class RVMPipeline(PipelineBase):
             self._fast = FastMatting(self.net)
         T, H, W, _ = frames.shape
         n = self.cfg.chunk
+        if _PINNED_OUT:
+            return self._matte_fast_pinned(frames, output_type, ratio)
         res = np.empty((T, H, W, 3), dtype=np.uint8)
         stream = torch.cuda.current_stream(self.device)
         rec = [None] * 4
@@ -412,6 +417,39 @@ class RVMPipeline(PipelineBase):
             e.synchronize()
             _host_copy(res[sl], v)
         return res
+
+    def _matte_fast_pinned(self, frames: np.ndarray, output_type: str, ratio: float) -> np.ndarray:
+        """As ``_matte_fast``, but every chunk's composite is downloaded straight into one page-locked
+        result array (PyTorch's caching host allocator: a freed clip's block is reused), so the
+        300 MB host copy out of a staging buffer is gone; the result is that array's numpy view
+        (it keeps the block alive until the encode has read it).  Same bytes."""
+        from .rvm_fast import FastMatting
+        if getattr(self, "_fast", None) is None:
+            self._fast = FastMatting(self.net)
+        T, H, W, _ = frames.shape
+        n = self.cfg.chunk
+        fb = H * W * 3
+        res = torch.empty(T * fb, dtype=torch.uint8, pin_memory=True)
+        stream = torch.cuda.current_stream(self.device)
+        rec = [None] * 4
+        ups = []
+        for j, i in enumerate(range(0, T, n)):
+            beat()
+            t = min(n, T - i)
+            st = self._pinned(("in", j % 2), n * fb)[:t * fb]
+            if len(ups) >= 2:
+                ups[-2].synchronize()     # the staging buffer's previous upload has been consumed
+            st.copy_(torch.from_numpy(np.ascontiguousarray(frames[i:i + t]).reshape(-1)))
+            dev = st.to(self.device, non_blocking=True).view(t, H, W, 3)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            ups.append(ev)
+            out, rec = self._fast(dev, rec, ratio, output_type, GREEN)
+            res[i * fb:(i + t) * fb].copy_(out.view(-1), non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(stream)
+        done.synchronize()
+        return res.view(T, H, W, 3).numpy()
 
     def _matte(self, frames: np.ndarray, output_type: str) -> np.ndarray:
         t0 = time.perf_counter()

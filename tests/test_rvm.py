@@ -202,3 +202,22 @@ def test_gateway_fetch_is_capped_while_streaming_and_cached(monkeypatch, tmp_pat
             V.fetch(cid + "/big")
     finally:
         srv.shutdown()
+
+
+@pytest.mark.gpu
+def test_rvm_pinned_result_equals_staged_download(monkeypatch):
+    """The composites downloaded straight into one pinned result array (default) are bitwise the
+    double-buffered staging path's; the array stays valid after the pipeline's next clip."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    import arbius_amd.models.rvm as R
+    pipe = RVMPipeline(RVMConfig(), device="cuda")
+    rng = np.random.default_rng(9)
+    clips = [rng.integers(0, 256, (26, 144, 256, 3), dtype=np.uint8) for _ in range(2)]   # 3 chunks
+    monkeypatch.setattr(R, "_PINNED_OUT", False)
+    staged = [pipe(c, "green-screen") for c in clips]
+    monkeypatch.setattr(R, "_PINNED_OUT", True)
+    first = pipe(clips[0], "green-screen")
+    second = pipe(clips[1], "green-screen")
+    assert np.array_equal(first, staged[0]) and np.array_equal(second, staged[1])
