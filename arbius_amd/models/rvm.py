@@ -41,6 +41,9 @@ def _host_copy(dst: np.ndarray, src: "torch.Tensor"):
 # download the composites straight into a pinned result array (A/B switch; same bytes)
 _PINNED_OUT = os.environ.get("ARB_RVM_PINNED_OUT", "1") == "1"
 
+# the input chunk's copy into its pinned staging buffer as a numpy assignment (A/B switch)
+_NUMPY_IN = os.environ.get("ARB_RVM_NUMPY_IN", "1") == "1"
+
 # CPU priority of the output encode's threads (RVMPipeline.finish); 0 = same as the caller
 ENCODE_NICE = int(os.environ.get("ARB_ENCODE_NICE", "10"))
 from .graphs import PipelineBase
@@ -439,7 +442,10 @@ class RVMPipeline(PipelineBase):
             st = self._pinned(("in", j % 2), n * fb)[:t * fb]
             if len(ups) >= 2:
                 ups[-2].synchronize()     # the staging buffer's previous upload has been consumed
-            st.copy_(torch.from_numpy(np.ascontiguousarray(frames[i:i + t]).reshape(-1)))
+            if _NUMPY_IN:                 # one thread (ATen's copy wakes its OpenMP pool)
+                st.numpy()[:] = frames[i:i + t].reshape(-1)
+            else:
+                st.copy_(torch.from_numpy(np.ascontiguousarray(frames[i:i + t]).reshape(-1)))
             dev = st.to(self.device, non_blocking=True).view(t, H, W, 3)
             ev = torch.cuda.Event()
             ev.record(stream)
