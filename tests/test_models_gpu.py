@@ -220,7 +220,7 @@ def test_cold_cache_concurrent_first_use_matches_solo(cuda, graphs):
 
 
 def test_kandinsky2_prior_graph_bitwise_equals_eager(cuda):
-    """The opt-in hipGraph replay of the diffusion-prior step (``prior_graph``) gives the eager CIDs:
+    """The hipGraph replay of the diffusion-prior step (``prior_graph``, default on) gives the eager CIDs:
     a lock-step group of 2 with different prompt lengths and a mixed prior_steps group."""
     from arbius_amd.node.solver import solve_images
     pipe = build_pipeline("kandinsky2", device=cuda)
