@@ -71,6 +71,12 @@ class ChainClient(abc.ABC):
     async def block_number(self) -> int: ...
 
     @abc.abstractmethod
+    async def commitment_block(self, commitment: str) -> int: ...   # commitments(bytes32): 0 = none
+
+    @abc.abstractmethod
+    async def contestation_vote_counts(self, taskid: str) -> Tuple[int, int]: ...   # (yeas, nays) on chain
+
+    @abc.abstractmethod
     async def get_submit_task_input(self, txid: str) -> Optional[bytes]:
         """Decode ``submitTask`` calldata of ``txid`` -> ``input_`` bytes (index.ts:151-159)."""
 
@@ -114,12 +120,18 @@ class ChainClient(abc.ABC):
 class MockChainClient(ChainClient):
     """ChainClient over an in-process MockEngine, acting as ``address``."""
 
-    def __init__(self, engine: MockEngine, address: str, eth_balance: int = 10 ** 18):
+    def __init__(self, engine: MockEngine, address: str, eth_balance: int = 10 ** 18, batch_blocks: bool = False):
         self.engine = engine
         self.address = address.lower()
         self._eth = eth_balance
         self.sent: List[Tuple[str, tuple]] = []  # tx log for tests / fault injection
         self.fail_next: Dict[str, str] = {}       # method -> revert reason (fault injection)
+        self.reverted: List[Tuple[str, tuple, str]] = []   # (method, args, reason) of reverted txs
+        # batch_blocks: a transaction sent without waiting for its receipt stays pending and is mined
+        # in ONE block together with the next transaction (a real chain's sequencing); hardhat
+        # automine (every transaction its own block) otherwise
+        self.batch_blocks = batch_blocks
+        self._pending: List[Tuple[str, tuple]] = []
 
     @property
     def engine_address(self) -> str:
@@ -132,10 +144,35 @@ class MockChainClient(ChainClient):
             fn = getattr(self.engine, method)
             fn(self.address, *args)
         except Revert as e:
+            self.reverted.append((method, args, str(e)))
             raise TxError(str(e)) from None
         self.sent.append((method, args))
         ev = self.engine.events[-1] if self.engine.events else None
         return ev.tx if ev else "0x"
+
+    def _send(self, method, *args, wait: bool = True):
+        if not self.batch_blocks:
+            return self._call(method, *args)
+        self._pending.append((method, args))
+        if not wait:
+            return "0x"
+        return self.flush()
+
+    def flush(self):
+        """Mine the pending transactions in one block; raises the LAST one's revert (the caller
+        waits on that one's receipt; earlier ones fail silently, as unawaited sends do)."""
+        pend, self._pending = self._pending, []
+        if not pend:
+            return "0x"
+        out = None
+        with self.engine.one_block():
+            for i, (m, a) in enumerate(pend):
+                try:
+                    out = self._call(m, *a)
+                except TxError:
+                    if i == len(pend) - 1:
+                        raise
+        return out
 
     async def get_task(self, taskid):
         t = self.engine.get_task(taskid)
@@ -174,7 +211,15 @@ class MockChainClient(ChainClient):
         return self._eth
 
     async def block_number(self):
+        self.flush() if self.batch_blocks else None
         return self.engine.block_number
+
+    async def commitment_block(self, commitment):
+        return self.engine.commitments.get(commitment.lower(), 0)
+
+    async def contestation_vote_counts(self, taskid):
+        t = taskid.lower()
+        return len(self.engine.vote_yeas.get(t, [])), len(self.engine.vote_nays.get(t, []))
 
     async def get_submit_task_input(self, txid):
         r = self.engine.get_transaction(txid)
@@ -183,25 +228,25 @@ class MockChainClient(ChainClient):
         return r[1][4]
 
     async def signal_commitment(self, commitment, wait=False):
-        return self._call("signal_commitment", commitment)
+        return self._send("signal_commitment", commitment, wait=wait)
 
     async def submit_solution(self, taskid, cid):
-        return self._call("submit_solution", taskid, cid)
+        return self._send("submit_solution", taskid, cid)
 
     async def claim_solution(self, taskid):
-        return self._call("claim_solution", taskid)
+        return self._send("claim_solution", taskid)
 
     async def submit_contestation(self, taskid):
-        return self._call("submit_contestation", taskid)
+        return self._send("submit_contestation", taskid)
 
     async def vote_on_contestation(self, taskid, yea):
-        return self._call("vote_on_contestation", taskid, yea)
+        return self._send("vote_on_contestation", taskid, yea)
 
     async def contestation_vote_finish(self, taskid, amnt):
-        return self._call("contestation_vote_finish", taskid, amnt)
+        return self._send("contestation_vote_finish", taskid, amnt)
 
     async def validator_deposit(self, validator, amount):
-        return self._call("validator_deposit", validator, amount)
+        return self._send("validator_deposit", validator, amount)
 
     async def token_approve(self, spender, amount):
         self.engine.token.approve(self.address, spender, amount)

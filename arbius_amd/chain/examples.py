@@ -38,15 +38,28 @@ class _Integration:
 
 
 class SubmitTask(_Integration):
-    """SubmitTask.sol:6-33: approves the engine for max, submits version 0 with fee 0.1 AIUS."""
+    """SubmitTask.sol:6-33: approves the engine for max, submits version 0 with fee 0.1 AIUS.
 
-    def __init__(self, engine, token, model: str, input_: bytes, address: str | None = None):
+    The transaction that carries it is an EOA's call of the contract's ``submitTask()``, not of the
+    engine's ``submitTask(uint8,address,bytes32,uint256,bytes)``: its calldata holds no task input
+    (the reference miner throws on it).  The engine's transaction record is
+    rewritten to that outer call, so a node has to recover the input by the task's on-chain CID."""
+
+    SELECTOR_SIG = "submitTask()"
+
+    def __init__(self, engine, token, model: str, input_: bytes, address: str | None = None,
+                 caller: str = "0x" + "ca" * 20):
         super().__init__(engine, address)
-        self.token, self.model, self.input = token, model, input_
+        self.token, self.model, self.input, self.caller = token, model, input_, caller
 
     def submit_task(self) -> str:
         self.token.approve(self.address, self.engine.address, 2 ** 256 - 1)
-        return self.engine.submit_task(self.address, 0, self.address, self.model, E18 // 10, self.input)
+        tid = self.engine.submit_task(self.address, 0, self.address, self.model, E18 // 10, self.input)
+        txin = getattr(self.engine, "_tx_inputs", None)
+        if txin is not None:
+            tx = next(ev.tx for ev in reversed(self.engine.events) if ev.name == "TaskSubmitted")
+            txin[tx] = (self.SELECTOR_SIG, (self.address,), self.caller)
+        return tid
 
 
 class RegisterModel(_Integration):

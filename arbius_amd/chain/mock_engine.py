@@ -10,6 +10,8 @@ Amounts are integers in wei (18 decimals).  Addresses are lowercase 0x-hex.
 """
 from __future__ import annotations
 
+import contextlib
+
 import itertools
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
@@ -190,10 +192,28 @@ class MockEngine:
 
     # ------------------------------------------------------------------ chain mechanics
     def _tx(self) -> str:
-        """Mine one block for a transaction (hardhat automine)."""
+        """Mine one block for a transaction (hardhat automine); inside ``one_block()`` every
+        transaction lands in the block that context opened (a real chain's batching)."""
+        if not getattr(self, "_open_block", False):
+            self.block_number += 1
+            self.arb_block_number += 1
+        return "0x" + keccak256(f"tx{next(self._txc)}".encode()).hex()
+
+    @contextlib.contextmanager
+    def one_block(self):
+        """Execute the enclosed transactions in ONE new block (the same ``block.number`` /
+        ``arbBlockNumber``), as a sequencer does with transactions that arrive together."""
         self.block_number += 1
         self.arb_block_number += 1
-        return "0x" + keccak256(f"tx{next(self._txc)}".encode()).hex()
+        prev, self._open_block = getattr(self, "_open_block", False), True
+        try:
+            yield
+        finally:
+            self._open_block = prev
+
+    def _current_block(self) -> int:
+        """``getBlockNumberNow()`` as seen by the executing transaction: the block it is mined in."""
+        return self.get_block_number_now() + (0 if getattr(self, "_open_block", False) else 1)
 
     def increase_time(self, seconds: int):
         """evm_increaseTime + evm_mine."""
@@ -516,7 +536,7 @@ class MockEngine:
         blk = self.commitments.get(commitment, 0)
         if blk == 0:
             raise Revert("non existent commitment")
-        if not blk < self.get_block_number_now() + 1:  # block this tx is mined in
+        if not blk < self._current_block():  # EngineV1.sol:797-802
             raise Revert("commitment must be in past")
         tx = self._tx()
         self.solutions[taskid] = Solution(_addr(sender), self.timestamp, False, cid)

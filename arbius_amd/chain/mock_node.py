@@ -102,6 +102,13 @@ class MockNode:
             return abi.encode(rets, [getattr(e, name)])
         if name in ENGINE_PARAMS:
             return abi.encode(rets, [int(getattr(e, _snake(name)))])
+        if name == "commitments":
+            return abi.encode(rets, [e.commitments.get(args[0].lower(), 0)])
+        if name in ("contestationVoteYeas", "contestationVoteNays"):
+            lst = (e.vote_yeas if name.endswith("Yeas") else e.vote_nays).get(args[0].lower(), [])
+            if args[1] >= len(lst):
+                raise Revert("index out of bounds")      # solidity array getter: Panic(0x32)
+            return abi.encode(rets, [lst[args[1]]])
         if name == "models":
             m = e.models.get(args[0].lower())
             return abi.encode(rets, [m.fee, m.addr, m.rate, m.cid] if m else [0, "0x" + "00" * 20, 0, b""])

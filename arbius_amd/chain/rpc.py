@@ -110,6 +110,35 @@ class RpcChainClient(ChainClient):
     async def block_number(self):
         return int(await self.rpc("eth_blockNumber", []), 16)
 
+    async def commitment_block(self, commitment):
+        return (await self._call(self._engine, "commitments", commitment))[0]
+
+    async def contestation_vote_counts(self, taskid):
+        """Lengths of ``contestationVoteYeas/Nays[taskid]``: the public array getters revert past the
+        end, so each length is found by an exponential + binary search over indices (O(log n) calls)."""
+        async def has(name, i):
+            try:
+                await self._call(self._engine, name, taskid, i)
+                return True
+            except RpcError:
+                return False
+
+        async def length(name):
+            if not await has(name, 0):
+                return 0
+            hi = 1
+            while await has(name, hi):
+                hi *= 2
+            lo = hi // 2                     # has(lo), not has(hi)
+            while hi - lo > 1:
+                mid = (lo + hi) // 2
+                if await has(name, mid):
+                    lo = mid
+                else:
+                    hi = mid
+            return hi
+        return await length("contestationVoteYeas"), await length("contestationVoteNays")
+
     async def get_submit_task_input(self, txid):
         tx = await self.rpc("eth_getTransactionByHash", [txid])
         if not tx:

@@ -106,6 +106,11 @@ class MI355XConfig(_Base):
     # per-model cap on those streams (measured: Kandinsky2 7.2k tasks/h at 2 streams x groups of 4,
     # 6.6k at 3, 5.9k at 4 x 2; the video UNet's activations fill the GPU at 2)
     model_streams: Dict[str, int] = Field(default_factory=lambda: dict(DEFAULT_MODEL_STREAMS))
+    # IPFS gateway (http(s) base URL) for the input of a task whose transaction is not a plain
+    # submitTask call (submitted through a contract): the bytes are fetched by the
+    # task's on-chain CID and accepted only if their on-chain CIDv0 matches.  None: $ARBIUS_IPFS_GATEWAY,
+    # else only the configured pinner (kubo cat / the local store) is asked.
+    ipfs_gateway: Optional[str] = None
     lockstep_group: int = 4               # queued compatible SD tasks solved per stream in ONE batch
                                           # (batch-invariant plans: same CIDs as solo; a lone task
                                           # never waits for company)

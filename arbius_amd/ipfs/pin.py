@@ -12,7 +12,7 @@ import os
 from pathlib import Path
 from typing import Dict, List, Optional, Sequence, Tuple
 
-from .unixfs import CHUNK, add_file, b58encode, wrap_directory
+from .unixfs import CHUNK, add_file, b58decode, b58encode, read_file, wrap_directory
 
 KUBO_ADD_PARAMS = {"cid-version": "0", "hash": "sha2-256", "chunker": f"size-{CHUNK}", "raw-leaves": "false"}
 
@@ -24,6 +24,11 @@ class Pinner:
 
     async def pin_file(self, content: bytes, name: str) -> str:
         raise NotImplementedError
+
+    async def cat(self, cid: str, max_bytes: int) -> Optional[bytes]:
+        """The bytes of a UnixFS file by base58 CIDv0, at most ``max_bytes`` (None: this strategy
+        cannot read content back; the caller tries the configured gateway instead)."""
+        return None
 
     async def close(self):
         pass
@@ -59,8 +64,14 @@ class LocalPinner(Pinner):
         self.pins.append(r.cid_str)
         return r.cid_str
 
-    def cat(self, cid_mh: bytes) -> bytes:
+    def block(self, cid_mh: bytes) -> bytes:
         return self.blocks[cid_mh]
+
+    async def cat(self, cid, max_bytes):
+        try:
+            return read_file(self.block, b58decode(cid), max_bytes)
+        except KeyError:
+            return None
 
 
 class KuboPinner(Pinner):
@@ -87,6 +98,13 @@ class KuboPinner(Pinner):
                                    files=[("file", (name, content, "application/octet-stream"))])
         r.raise_for_status()
         return json.loads(r.text.strip().splitlines()[-1])["Hash"]
+
+    async def cat(self, cid, max_bytes):
+        """``/api/v0/cat`` capped while streaming (kubo checks every block against its hash)."""
+        async with self.client.stream("POST", f"{self.url}/api/v0/cat",
+                                      params={"arg": cid, "length": str(max_bytes + 1)}) as r:
+            r.raise_for_status()
+            return await _read_capped(r, max_bytes)
 
     async def close(self):
         await self.client.aclose()
@@ -118,6 +136,42 @@ class PinataPinner(Pinner):
 
     async def close(self):
         await self.client.aclose()
+
+
+async def _read_capped(resp, max_bytes: int) -> bytes:
+    buf = bytearray()
+    async for chunk in resp.aiter_bytes():
+        buf.extend(chunk)
+        if len(buf) > max_bytes:
+            raise ValueError(f"content exceeds {max_bytes} bytes")
+    return bytes(buf)
+
+
+def _gateway_base(gateway: str) -> str:
+    """Operator-configured gateway (``mi355x.ipfs_gateway`` / ``$ARBIUS_IPFS_GATEWAY``): an
+    http(s) URL without query or fragment."""
+    from urllib.parse import urlsplit
+    u = urlsplit(gateway)
+    if u.scheme not in ("http", "https") or not u.netloc or u.query or u.fragment:
+        raise ValueError(f"bad IPFS gateway URL {gateway!r}")
+    return gateway.rstrip("/")
+
+
+async def gateway_cat(gateway: str, cid: str, max_bytes: int, client=None, timeout: float = 60.0) -> bytes:
+    """``GET <gateway>/ipfs/<cid>`` capped at ``max_bytes``.  A gateway is untrusted: callers check
+    the bytes against the CID they asked for (``onchain_cid`` / ``add_file``)."""
+    import httpx
+    if not cid.isalnum():
+        raise ValueError("CID must be base58")
+    own = client is None
+    client = client or httpx.AsyncClient(timeout=timeout, follow_redirects=False)
+    try:
+        async with client.stream("GET", f"{_gateway_base(gateway)}/ipfs/{cid}") as r:
+            r.raise_for_status()
+            return await _read_capped(r, max_bytes)
+    finally:
+        if own:
+            await client.aclose()
 
 
 async def pinata_gc(jwt: str, max_age_s: float = 7200.0, base: str = "https://api.pinata.cloud", client=None,

@@ -209,3 +209,88 @@ def cid_str_to_hex(cid: str) -> str:
 
 def cid_hex_to_str(h: str) -> str:
     return b58encode(bytes.fromhex(h[2:] if h.startswith("0x") else h))
+
+
+# ---------------------------------------------------------------------------------------------
+# Reader: the inverse of add_file over a block store (LocalPinner.cat; the bytes behind an
+# on-chain task CID when its input cannot be read from the transaction).
+
+def _read_varint(b: bytes, i: int) -> Tuple[int, int]:
+    n = shift = 0
+    while True:
+        if i >= len(b) or shift > 63:
+            raise ValueError("truncated protobuf varint")
+        c = b[i]
+        i += 1
+        n |= (c & 0x7F) << shift
+        shift += 7
+        if not c & 0x80:
+            return n, i
+
+
+def _pb_fields(b: bytes):
+    """(field number, wire type, value) of a protobuf message (varint / length-delimited only)."""
+    i = 0
+    while i < len(b):
+        key, i = _read_varint(b, i)
+        num, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _read_varint(b, i)
+        elif wt == 2:
+            n, i = _read_varint(b, i)
+            if i + n > len(b):
+                raise ValueError("truncated protobuf field")
+            v, i = b[i:i + n], i + n
+        else:
+            raise ValueError(f"unsupported protobuf wire type {wt}")
+        yield num, wt, v
+
+
+def parse_pb_node(block: bytes) -> Tuple[list, bytes]:
+    """dag-pb PBNode -> ([Link], Data bytes)."""
+    links, data = [], b""
+    for num, wt, v in _pb_fields(block):
+        if num == 2 and wt == 2:
+            h, name, ts = b"", "", 0
+            for n2, w2, v2 in _pb_fields(v):
+                if n2 == 1 and w2 == 2:
+                    h = bytes(v2)
+                elif n2 == 2 and w2 == 2:
+                    name = bytes(v2).decode("utf-8", "replace")
+                elif n2 == 3 and w2 == 0:
+                    ts = v2
+            links.append(Link(h, name, ts))
+        elif num == 1 and wt == 2:
+            data = bytes(v)
+    return links, data
+
+
+def read_file(get_block, cid: bytes, max_bytes: int = 1 << 30) -> bytes:
+    """Bytes of the UnixFS file whose root multihash is ``cid``; ``get_block(mh) -> bytes``.
+    Every block is checked against its multihash (a store cannot substitute content) and the
+    output is capped at ``max_bytes`` (ValueError past it)."""
+    out = bytearray()
+
+    def walk(mh: bytes, depth: int):
+        if depth > 16:
+            raise ValueError("unixfs DAG too deep")
+        blk = get_block(mh)
+        if multihash_sha256(blk) != mh:
+            raise ValueError("block does not match its multihash")
+        links, data = parse_pb_node(blk)
+        typ, chunk = None, b""
+        for num, wt, v in _pb_fields(data):
+            if num == 1 and wt == 0:
+                typ = v
+            elif num == 2 and wt == 2:
+                chunk = bytes(v)
+        if typ not in (0, 2):            # Raw / File only (a directory is not a task input)
+            raise ValueError(f"unixfs node type {typ} is not a file")
+        out.extend(chunk)
+        if len(out) > max_bytes:
+            raise ValueError("file exceeds the size cap")
+        for l in links:
+            walk(l.hash, depth + 1)
+
+    walk(cid, 0)
+    return bytes(out)

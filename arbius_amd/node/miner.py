@@ -140,10 +140,14 @@ class Miner:
             return json.loads(cached["data"])
         raw = await self._retry(lambda: self.chain.get_submit_task_input(txid))
         if raw is None:
-            # reference Q9: non-submitTask calldata (task sent through a contract).  Do NOT mark
-            # invalid (that would contest a valid task); skip it.
-            log.warning("Task (%s) input could not be recovered from tx %s", taskid, txid)
-            return None
+            # reference Q9 (index.ts:151-155 throws): the transaction is not a submitTask call (the task
+            # was sent through a contract, e.g. Example/SubmitTask.sol).  The task's on-chain cid is the
+            # CIDv0 of the input bytes (EngineV1.sol:681-711, IPFS.sol:38-65): fetch them by CID and
+            # accept them only if they hash to it.  Unrecoverable / mismatching bytes: skip the task,
+            # never mark it invalid (that would contest a valid task).
+            raw = await self.recover_input_by_cid(taskid, cid)
+            if raw is None:
+                return None
         try:
             pre_str = raw.decode("utf-8")
             pre = json.loads(pre_str)
@@ -188,6 +192,42 @@ class Miner:
         self.db.store_task_input(taskid, cid, inp)
         self.queue("pinTaskInput", 10, 0, True, {"taskid": taskid, "input": pre_str})
         return inp
+
+    async def recover_input_by_cid(self, taskid: str, cid: str) -> Optional[bytes]:
+        """The bytes behind a task's on-chain input CID (<= 65536 B: IPFS.sol:39), from the pinner
+        (kubo ``cat`` / the local store) or the operator's gateway, verified against the CID."""
+        import os
+        from ..ipfs.pin import gateway_cat
+        from ..ipfs.unixfs import onchain_cid
+        want = bytes.fromhex(cid[2:] if cid.startswith("0x") else cid)
+        cid58 = cid_hex_to_str(cid)
+        sources = [("pinner", lambda: self.pinner.cat(cid58, 65536))]
+        gw = getattr(self.c.mi355x, "ipfs_gateway", None) or os.environ.get("ARBIUS_IPFS_GATEWAY")
+        if gw:
+            sources.append(("gateway", lambda: gateway_cat(gw, cid58, 65536)))
+        for name, fetch in sources:
+            try:
+                data = await fetch()
+            except Exception as e:  # noqa: BLE001 - unreachable source / over the size cap
+                log.warning("Task (%s) input %s from %s failed: %r", taskid, cid58, name, e)
+                continue
+            if data is None:
+                continue
+            try:
+                ok = len(data) <= 65536 and onchain_cid(data) == want
+            except ValueError:
+                ok = False
+            if ok:
+                self.metrics.inc("tasks_input_by_cid")
+                log.info("Task (%s) input recovered by cid %s from %s", taskid, cid58, name)
+                return data
+            self.metrics.inc("tasks_input_cid_mismatch")
+            log.warning("Task (%s) input from %s does not hash to the on-chain cid %s: ignored", taskid, name,
+                        cid58)
+        self.metrics.inc("tasks_input_unrecoverable")
+        log.warning("Task (%s) input could not be recovered (tx not submitTask, cid %s unavailable)", taskid,
+                    cid58)
+        return None
 
     # ------------------------------------------------------------------ event handlers (index.ts:191-333)
     async def on_event(self, ev):
@@ -358,7 +398,14 @@ class Miner:
         commitment = generate_commitment(self.wallet, taskid, cid)
         t_c = time.perf_counter()
         try:
-            await self.chain.signal_commitment(commitment)
+            # wait for the commitment's receipt: submitSolution requires the commitment in an EARLIER
+            # block (EngineV1.sol:797-802); the reference sends both back to back (index.ts:619-639)
+            # and relies on its retry delay, paying for a reverted submit whenever both land in one
+            # block.  The GPU slot was released when the solve returned, so waiting costs no throughput.
+            # (a commitment already on chain - a restarted solve - is not signalled twice: the second
+            # signalCommitment would revert "commitment exists", EngineV1.sol:764-768)
+            if await self.chain.commitment_block(commitment) == 0:
+                await self.chain.signal_commitment(commitment, wait=True)
         except Exception as e:  # noqa: BLE001
             log.error("Commitment submission failed %r", e)
             self.metrics.inc("tx_failures")
@@ -448,21 +495,33 @@ class Miner:
         except TxError as e:
             log.error("Failed voting on contestation %s: %s", taskid, e.reason)
 
+    FINISH_PAGE = 32
+
     async def process_contestation_vote_finish(self, taskid):
-        """Implemented (reference stub, index.ts:392-395): finish in pages of 32 voters."""
+        """Implemented (reference stub, index.ts:392-395): finish in pages of 32 voters, paged by
+        CHAIN state.  The on-chain loop pays the winning side's voters i in [finish_start_index,
+        +amnt) (EngineV1.sol:1043-1106), so pages are sent until ``finish_start_index`` covers that
+        side's vote count as the contract stores it - votes cast before this node's event cursor
+        existed are not in the local DB, and a DB count would stop early and strand their stakes."""
         c = await self._retry(lambda: self.chain.get_contestation(taskid))
         if c["validator"] == ZERO_ADDR:
             return
-        votes = self.db.get_contestation_votes(taskid)
-        total = max(len(votes), 1)
+        yeas, nays = await self._retry(lambda: self.chain.contestation_vote_counts(taskid))
+        need = max(1, yeas if yeas > nays else nays)     # at least one call: it settles the task
         start = int(c["finish_start_index"])
-        while start < total:
+        while start < need:
             try:
-                await self.chain.contestation_vote_finish(taskid, 32)
+                await self.chain.contestation_vote_finish(taskid, self.FINISH_PAGE)
             except TxError as e:
                 log.error("contestationVoteFinish %s failed: %s", taskid, e.reason)
                 return
-            start += 32
+            c = await self._retry(lambda: self.chain.get_contestation(taskid))
+            nxt = int(c["finish_start_index"])
+            if nxt <= start:
+                log.error("contestationVoteFinish %s did not advance (%d)", taskid, nxt)
+                return
+            start = nxt
+            self.metrics.inc("contestation_finish_pages")
 
     async def process_claim(self, taskid):
         async def claim():

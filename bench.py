@@ -244,6 +244,10 @@ def run(args):
     D.barrier(dev)
     sync()
     t0 = time.perf_counter()
+    marks = os.environ.get("ARB_BENCH_MARKS") == "1"   # timed-region bounds on the trace clocks
+    if marks:
+        print(f"[bench] timed t0 monotonic_ns={time.monotonic_ns()} "
+              f"boottime_ns={time.clock_gettime_ns(time.CLOCK_BOOTTIME)}", file=sys.stderr, flush=True)
     last = None
     if ex is None:
         for i in range(args.steps):
@@ -271,6 +275,9 @@ def run(args):
     sync()
     D.barrier(dev)
     elapsed = time.perf_counter() - t0
+    if marks:
+        print(f"[bench] timed t1 monotonic_ns={time.monotonic_ns()} "
+              f"boottime_ns={time.clock_gettime_ns(time.CLOCK_BOOTTIME)}", file=sys.stderr, flush=True)
     my_ms = elapsed * 1000.0 / args.steps
     ms_per_step = D.max_over_ranks(my_ms, dev)
     all_lat = D.all_gather_floats(lat, dev)

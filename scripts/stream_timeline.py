@@ -19,13 +19,18 @@ def _cols(c, table):
     return [r[1] for r in c.execute(f"pragma table_info({table})")]
 
 
-def load(db):
+def load(db, by=None):
     c = sqlite3.connect(db)
     cols = _cols(c, "kernels")
     name = "name" if "name" in cols else "kernel_name"
-    key = next((k for k in ("stream_id", "queue_id") if k in cols), None)
+    key = by if by in cols else next((k for k in ("stream_id", "queue_id") if k in cols), None)
     sel = f"select {name}, start, end, {key or 0} from kernels order by start"
-    return [(n, s, e, q) for n, s, e, q in c.execute(sel).fetchall()], key or "none", cols
+    rows = [(n, s, e, q) for n, s, e, q in c.execute(sel).fetchall()]
+    qmap = {}
+    if "stream_id" in cols and "queue_id" in cols:
+        for st, q, n in c.execute("select stream_id, queue_id, count(*) from kernels group by stream_id, queue_id"):
+            qmap.setdefault(st, []).append((q, n))
+    return rows, key or "none", cols, qmap
 
 
 def union(iv):
@@ -44,8 +49,25 @@ def main():
     ap.add_argument("--md", default=None)
     ap.add_argument("--gap-ms", type=float, default=2.0)
     ap.add_argument("--top", type=int, default=8)
+    ap.add_argument("--by", default=None, help="group by this column (stream_id / queue_id)")
+    ap.add_argument("--window", nargs=2, type=int, default=None, metavar=("T0_NS", "T1_NS"),
+                    help="keep only kernels inside [T0, T1] (trace clock; bench.py ARB_BENCH_MARKS=1 prints "
+                         "the timed region's bounds)")
+    ap.add_argument("--skip-ms", type=float, default=0.0,
+                    help="drop the first N ms of the trace (warm-up captures) when no --window is given")
     a = ap.parse_args()
-    rows, key, cols = load(a.db)
+    rows, key, cols, qmap = load(a.db, a.by)
+    if a.window:
+        w0, w1 = a.window
+        inside = [(n, max(s, w0), min(e, w1), q) for n, s, e, q in rows if e > w0 and s < w1]
+        if not inside:
+            print(f"window {w0}..{w1} misses the trace ({rows[0][1]}..{rows[-1][2]}): clocks differ; "
+                  "falling back to --skip-ms")
+        else:
+            rows = inside
+    elif a.skip_ms > 0:
+        cut = rows[0][1] + int(a.skip_ms * 1e6)
+        rows = [(n, max(s, cut), e, q) for n, s, e, q in rows if e > cut]
     t0, t1 = min(r[1] for r in rows), max(r[2] for r in rows)
     wall = (t1 - t0) / 1e6
     per = defaultdict(list)
@@ -97,6 +119,17 @@ def main():
             top = sorted(inside.items(), key=lambda kv: -kv[1][1])[:3]
             desc = "; ".join(f"s{q2} {n} x{c} {ms:.2f} ms" for (q2, n), (c, ms) in top) or "nothing"
             lines.append(f"* stream {q}: gap {g / 1e6:.2f} ms at +{(gs - t0) / 1e6:.1f} ms -> {desc}")
+    if qmap:
+        lines += ["", "HIP stream -> HW queue (`queue_id`, dispatches), whole trace:", "",
+                  "| stream | queues |", "|---|---|"]
+        for st, qs in sorted(qmap.items()):
+            lines.append(f"| {st} | {', '.join(f'q{q} ({n})' for q, n in sorted(qs))} |")
+        shared = defaultdict(list)
+        for st, qs in qmap.items():
+            for q, _ in qs:
+                shared[q].append(st)
+        lines += ["", "HW queue -> streams: " + "; ".join(
+            f"q{q}: {', '.join(f's{x}' for x in sorted(sts))}" for q, sts in sorted(shared.items()))]
     lines += ["", f"(kernels columns: {', '.join(cols)})"]
     out = "\n".join(lines)
     print(out)
