@@ -29,6 +29,25 @@ def _dbg(msg):
                                                    threading.current_thread().name, msg)
 
 
+_SIDE = {}
+
+
+def capture_stream(dev) -> "torch.cuda.Stream":
+    """The stream a graph is warmed up and captured on: the calling pipeline fork's own stream (the
+    stream its replays run on), never a new one.  HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware
+    queues and two streams on one queue run their kernels one after the other
+    (profiles/queues_r5_sd15.md), so every extra stream is a chance to land on a task stream's queue.
+    Only an unforked pipeline (current stream = the default stream, which cannot capture) uses one
+    process-wide side stream."""
+    cur = torch.cuda.current_stream(dev)
+    if cur != torch.cuda.default_stream(dev):
+        return cur
+    key = torch.device(dev).index
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
 class GraphedCall:
     def __init__(self, fn: Callable, example_args: Sequence[torch.Tensor], warmup: int = 2):
         dev = example_args[0].device
@@ -37,14 +56,14 @@ class GraphedCall:
         if _DEBUG:
             _dbg(f"capture {getattr(fn, '__qualname__', fn)} {[tuple(a.shape) for a in example_args]}")
         with CAPTURE_LOCK:
-            s = torch.cuda.Stream(device=dev)
+            s = capture_stream(dev)
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
                 for _ in range(warmup):   # allocator + kernel-library load outside capture
                     self.out = fn(*self.inputs)
             torch.cuda.current_stream(dev).wait_stream(s)
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"):
                 self.out = fn(*self.inputs)
 
     def __call__(self, *args):

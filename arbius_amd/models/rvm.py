@@ -40,6 +40,9 @@ def _host_copy(dst: np.ndarray, src: "torch.Tensor"):
 
 # download the composites straight into a pinned result array (A/B switch; same bytes)
 _PINNED_OUT = os.environ.get("ARB_RVM_PINNED_OUT", "1") == "1"
+# largest clip (output bytes) downloaded into one page-locked array: ~100 frames of 1080p; longer clips
+# take the staged path (two reusable pinned chunk buffers + a pageable result)
+_PINNED_OUT_MAX = int(os.environ.get("ARB_RVM_PINNED_OUT_MAX", str(640 << 20)))
 
 # the input chunk's copy into its pinned staging buffer as a numpy assignment (A/B switch)
 _NUMPY_IN = os.environ.get("ARB_RVM_NUMPY_IN", "1") == "1"
@@ -387,8 +390,16 @@ class RVMPipeline(PipelineBase):
             self._fast = FastMatting(self.net)
         T, H, W, _ = frames.shape
         n = self.cfg.chunk
-        if _PINNED_OUT:
-            return self._matte_fast_pinned(frames, output_type, ratio)
+        if _PINNED_OUT and T * H * W * 3 <= _PINNED_OUT_MAX:
+            # the page-locked result array comes from PyTorch's caching host allocator,
+            # which rounds up and never returns memory to the OS - bounded per clip; a failed pin
+            # (host memory exhausted) falls back to the staged download below (same bytes)
+            try:
+                res_pin = torch.empty(T * H * W * 3, dtype=torch.uint8, pin_memory=True)
+            except RuntimeError:
+                res_pin = None
+            if res_pin is not None:
+                return self._matte_fast_pinned(frames, output_type, ratio, res_pin)
         res = np.empty((T, H, W, 3), dtype=np.uint8)
         stream = torch.cuda.current_stream(self.device)
         rec = [None] * 4
@@ -421,7 +432,7 @@ class RVMPipeline(PipelineBase):
             _host_copy(res[sl], v)
         return res
 
-    def _matte_fast_pinned(self, frames: np.ndarray, output_type: str, ratio: float) -> np.ndarray:
+    def _matte_fast_pinned(self, frames: np.ndarray, output_type: str, ratio: float, res) -> np.ndarray:
         """As ``_matte_fast``, but every chunk's composite is downloaded straight into one page-locked
         result array (PyTorch's caching host allocator: a freed clip's block is reused), so the
         300 MB host copy out of a staging buffer is gone; the result is that array's numpy view
@@ -432,7 +443,6 @@ class RVMPipeline(PipelineBase):
         T, H, W, _ = frames.shape
         n = self.cfg.chunk
         fb = H * W * 3
-        res = torch.empty(T * fb, dtype=torch.uint8, pin_memory=True)
         stream = torch.cuda.current_stream(self.device)
         rec = [None] * 4
         ups = []

@@ -25,7 +25,7 @@ from .. import ops
 from ..utils.trace import span
 from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
-from .graphs import CAPTURE_LOCK, GraphCache, PipelineBase
+from .graphs import CAPTURE_LOCK, GraphCache, PipelineBase, capture_stream
 from .layers import init_weights
 from .schedulers import GroupSampler, TaskSampler, make_scheduler
 from .tokenizer import CLIPTokenizer
@@ -76,7 +76,7 @@ class _GraphedUNet:
                 self.kv[id(m)] = m.context_kv(self.ctx)
 
     def _capture(self, unet, dev):
-        s = torch.cuda.Stream(device=dev)
+        s = capture_stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for _ in range(2):  # warm-up: allocator + kernel-library load outside capture
@@ -85,10 +85,10 @@ class _GraphedUNet:
                     self.out = unet(self.x, self.t, self.ctx)
         torch.cuda.current_stream(dev).wait_stream(s)
         self.kv_graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.kv_graph, capture_error_mode="thread_local"):
+        with torch.cuda.graph(self.kv_graph, stream=s, capture_error_mode="thread_local"):
             self._project_kv(unet)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+        with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"):
             with cross_kv_mode("consume" if self.HOIST else None, self.kv):
                 self.out = unet(self.x, self.t, self.ctx)
 
@@ -274,6 +274,8 @@ class SD15Pipeline(PipelineBase):
     @torch.no_grad()
     def decode(self, latent):
         z = (latent / self.cfg.vae.scaling_factor).to(self.dtype)
+        if "vae" in ops._EXP_SKIP:      # ablation runs only (numerics knob): no VAE decode
+            return np.zeros((z.shape[1] * 8, z.shape[2] * 8, 3), np.uint8)
         if self.use_graphs and _VAE_GRAPH:
             img = self._vae_graph(z).float()      # .float(): a copy out of the graph's static output
         else:

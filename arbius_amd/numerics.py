@@ -26,6 +26,10 @@ NUMERICS_ENV_KNOBS = (
     "ARB_SPLITK_INLAUNCH", "ARBIUS_GEGLU_FUSED", "ARBIUS_CROSS_KV_HOIST", "ARBIUS_FAULT_INJECTION",
     "ARBIUS_SAMPLER_REF", "ARB_GN_TABLE_LDS", "ARB_VAE_GRAPH", "ARB_PINNED_D2H", "ARB_PRIOR_GRAPH",
     "ARB_ATTN_PP", "ARB_LN_FOLD_NARROW", "ARB_LN_FOLD_NARROW_N", "ARBIUS_LIBRARY_FALLBACK", "ARB_ATTN_PRESCALE",
+    # tile-family / layout switches read by the kernel library (bitwise-neutral by test, but their
+    # neutrality then rests on a run-time file or an untested combination: refused all the same)
+    "ARB_CONV_FAMILY", "ARB_NO_FAMILY", "ARB_DMA_BUF", "ARB_STAG2_PD", "ARB_GN_APPLY2", "ARB_GN_FUSED",
+    "ARB_LN_PACKED",
 )
 
 

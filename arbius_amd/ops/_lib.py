@@ -154,6 +154,18 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+# ARBIUS_EXPERIMENT_SKIP (numerics.NUMERICS_ENV_KNOBS; never when mining): op classes whose kernels
+# are NOT launched (the output stays uninitialised) - ablation runs that measure what each class
+# costs inside the deployed concurrent-stream mix.  Classes: shortk (GEMM / 1x1 conv, K <= 640),
+# geglu, gemmbig (GEMM / 1x1 conv, K > 640), conv3 (3x3 / temporal convs), attn, attn512, lnorm
+# (LayerNorm + row stats), gnstats / gnapply (ops/__init__.py).
+_SKIP = frozenset(filter(None, os.environ.get("ARBIUS_EXPERIMENT_SKIP", "").split(",")))
+
+
+def _skip(cls: str) -> bool:
+    return cls in _SKIP
+
+
 def _check(rc, what):
     if rc != 0:
         raise RuntimeError(f"{what}: HIP launch failed (rc={rc})")
@@ -210,6 +222,8 @@ def layer_norm(x, gamma, beta, eps, plan_rows=None):
         raise ValueError(f"layer_norm: unsupported C={C}")
     M = x.numel() // C
     y = torch.empty_like(x)
+    if _skip("lnorm"):
+        return y
     _check(_fn("arb_layer_norm")(_p(x), _p(y), _p(gamma), _p(beta), M, C, float(eps),
                                  int(M if plan_rows is None else plan_rows), _stream()), "layer_norm")
     return y
@@ -223,6 +237,8 @@ def flash_attention(q, k, v, scale, causal, kv_prefix=None):
     B, Nq, H, D = q.shape
     Nk = k.shape[1]
     if D > 160:
+        if _skip("attn512"):
+            return torch.empty_like(q)
         if kv_prefix is not None:
             k, v = torch.cat([kv_prefix[0], k], 1), torch.cat([kv_prefix[1], v], 1)
         return _large_head_attention(q, k, v, scale)
@@ -243,6 +259,8 @@ def flash_attention(q, k, v, scale, causal, kv_prefix=None):
     if D % 8:
         raise ValueError(f"flash_attention: D={D} not a multiple of 8")
     o = torch.empty(B, Nq, H, D, dtype=q.dtype, device=q.device)
+    if _skip("attn"):
+        return o
     strides = (ctypes.c_long * 12)(q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
                                    v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2))
     _check(_fn("arb_flash_attention")(_p(q), _p(k), _p(v), _p(o), strides, B, H, Nq, Nk + Np, D, float(scale),
@@ -590,6 +608,8 @@ def conv2d_nhwc(x, w, b, padding, upsample, residual, temb=None, stride=1, cfg=-
     args = (B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride, int(cfg), int(split))
     audit_note("conv", M=B * Ho * Wo, N=Cout, K=kh * kw * Cin, cfg=int(cfg), split=int(split), plan_b=plan_b,
                batch=B, shape=(B, H, W, Cin, Cout, kcode, padding, int(bool(upsample)), stride), dtype=str(x.dtype))
+    if _skip("conv3" if kh > 1 else "shortk" if Cin <= 640 else "gemmbig"):
+        return y
     ws_bytes = _fn("arb_conv2d_workspace")(*args)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
     if f16:
@@ -628,6 +648,8 @@ def gemm(x, w, b=None, residual=None, cfg=-1, split=-1, plan_batch=None, act=Non
     audit_note("gemm", M=M, N=N, K=K, cfg=int(cfg), split=int(split), plan_b=plan_batch and plan_batch[1],
                batch=plan_batch and plan_batch[0], dtype=str(x.dtype))
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    if _skip("shortk" if K <= 640 else "gemmbig"):
+        return y.reshape(*x.shape[:-1], N)
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
@@ -656,6 +678,8 @@ def gemm_geglu(x, w_il, b_il=None, cfg=-1, split=-1, plan_batch=None):
     audit_note("gemm", M=M, N=N, K=K, cfg=int(cfg), split=int(split), plan_b=plan_batch and plan_batch[1],
                batch=plan_batch and plan_batch[0], dtype=str(x.dtype))
     y = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+    if _skip("geglu"):
+        return y.reshape(*x.shape[:-1], N // 2)
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None
     _check(_fn("arb_gemm_geglu")(_p(x2), _p(w_il.contiguous()), _p(b_il), _p(y), _p(ws), M, N, K, int(cfg),
@@ -673,6 +697,8 @@ def row_stats(x, eps, plan_rows=None):
         raise ValueError(f"row_stats: unsupported C={C}")
     M = x.numel() // C
     rs = torch.empty(M, 2, dtype=torch.float32, device=x.device)
+    if _skip("lnorm"):
+        return rs
     _check(_fn("arb_row_stats")(_p(x), _p(rs), M, C, float(eps), int(M if plan_rows is None else plan_rows),
                                 _stream()), "row_stats")
     return rs
@@ -695,6 +721,8 @@ def gemm_ln(x, w, b, wsum, rs, residual=None, geglu=False, cfg=-1, split=-1, pla
     audit_note("gemm", M=M, N=N, K=K, cfg=int(cfg), split=int(split), plan_b=plan_batch and plan_batch[1],
                batch=plan_batch and plan_batch[0], dtype=str(x.dtype))
     y = torch.empty(M, N // 2 if geglu else N, dtype=x.dtype, device=x.device)
+    if _skip("geglu" if geglu else "shortk" if K <= 640 else "gemmbig"):
+        return y.reshape(*x.shape[:-1], y.shape[-1])
     r2 = residual.reshape(M, N).contiguous() if residual is not None else None
     ws_bytes = _fn("arb_conv2d_workspace")(1, 1, M, K, N, 1, 0, 0, 1, int(cfg), int(split))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device) if ws_bytes else None

@@ -1925,7 +1925,10 @@ static const std::vector<PinnedPlan>& env_plans() {
     const char* path = std::getenv("ARB_CONV_PLANS");
     if (path == nullptr || path[0] == 0) return v;
     FILE* f = std::fopen(path, "r");
-    if (f == nullptr) return v;
+    if (f == nullptr) {
+      std::fprintf(stderr, "[arbius] ARB_CONV_PLANS=%s cannot be read: the built-in table is used\n", path);
+      return v;
+    }
     char line[256];
     while (std::fgets(line, sizeof line, f)) {
       PinnedPlan pp;
@@ -2468,7 +2471,10 @@ static const std::vector<FamilyPlan>& env_families() {
     const char* path = std::getenv("ARB_CONV_FAMILY");
     if (path == nullptr || path[0] == 0) return v;
     FILE* f = std::fopen(path, "r");
-    if (f == nullptr) return v;
+    if (f == nullptr) {
+      std::fprintf(stderr, "[arbius] ARB_CONV_FAMILY=%s cannot be read: the built-in table is used\n", path);
+      return v;
+    }
     char line[256];
     while (std::fgets(line, sizeof line, f)) {
       FamilyPlan fp;

@@ -98,34 +98,60 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 if hasattr(pipe, "_reset_graphs"):
                     pipe._reset_graphs()
             pipes[name] = pipe
-        # `streams` task slots: slot k solves on its own pipeline forks (private HIP stream + graphs)
-        slots = [{n: (p if streams == 1 else p.fork()) for n, p in pipes.items()} for _ in range(streams)]
+        # `streams` task slots share, per model, a pool of min(streams, model cap) pipeline forks (private
+        # HIP stream + hipGraphs each; ADVICE r4: one fork per slot gave a capped model - Kandinsky2,
+        # video, matting - 4 graph memory pools per GPU for the 2 solves its cap allows).  A slot takes
+        # a fork of its job's model for the GPU part and returns it before the CPU tail.
+        caps_n = {n: max(1, min(streams, int((model_streams or {}).get(n, streams)))) for n in pipes}
+        forks = {}
+        for n, p in pipes.items():
+            q = _queue.Queue()
+            for _ in range(caps_n[n]):
+                q.put(p if streams == 1 or not hasattr(p, "fork") else p.fork())
+            forks[n] = q
+        fork_stats = {n: {"forks": caps_n[n], "in_use": 0, "peak": 0} for n in pipes}
+        fork_mu = threading.Lock()
         jobs: "_queue.Queue" = _queue.Queue()
         from concurrent.futures import ThreadPoolExecutor
         # per slot: one thread for a lock-step group's PNG + CID tail, so the slot's stream starts
         # its next group while the previous one encodes
         tails = [ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"tail{k}") for k in range(streams)]
         last_tail = [None] * streams        # a slot's solo-task tail in flight (at most one: RVM clips are 300 MB)
-        # per-model cap on concurrently solving slots (e.g. Kandinsky2 peaks at 2 streams per GPU)
-        caps = {n: threading.Semaphore(max(1, min(streams, int((model_streams or {}).get(n, streams)))))
-                for n in pipes}
 
-        def finish(batch, imgs, tm, t0):
+        def finish(batch, imgs, tm, t0, k=None):
+            if k is not None:
+                tail_clock(k, True)
             try:
                 for m, sol in zip(batch, encode_images(imgs, tm)):
                     sol.dag = None
                     sol.timings["worker_s"] = time.perf_counter() - t0
+                    sol.timings["fork_peak"] = fork_stats[m[1]]["peak"]
                     out_q.put(("ok", m[0], rank, sol))
             except Exception:  # noqa: BLE001
                 for m in batch:
                     out_q.put(("err", m[0], rank, traceback.format_exc()))
+            finally:
+                if k is not None:
+                    tail_clock(k, False)
 
-        def finish_solo(batch, tail_fns, t0):
+        def tail_clock(k, on):
+            if beats is not None:
+                beats[(world + rank) * streams + k] = time.time() if on else 0.0
+
+        def finish_solo(batch, tail_fns, t0, k):
+            tail_clock(k, True)
+            try:
+                _finish_solo(batch, tail_fns, t0)
+            finally:
+                tail_clock(k, False)
+
+        def _finish_solo(batch, tail_fns, t0):
             for m, fn in zip(batch, tail_fns):
                 try:
                     sol = fn()
                     sol.dag = None  # blocks are recomputed by the pinner; keep the message small
                     sol.timings["worker_s"] = time.perf_counter() - t0
+                    sol.timings["fork_peak"] = fork_stats[m[1]]["peak"]
                     out_q.put(("ok", m[0], rank, sol))
                 except Exception:  # noqa: BLE001
                     out_q.put(("err", m[0], rank, traceback.format_exc()))
@@ -139,28 +165,43 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 # lock-step group: queued compatible image tasks share one batch (same bytes as solo)
                 batch = take_group(jobs, msg, lockstep, lambda m: m[2], lambda m: m[5], lambda m: m[1])
                 jid, mname, kind, mid, taskid, inp = msg
-                caps[msg[1]].acquire()              # idle (beat 0) while the model's cap is full
+                pipe = forks[mname].get()           # idle (beat 0) while every fork of the model solves
+                with fork_mu:
+                    st = fork_stats[mname]
+                    st["in_use"] += 1
+                    st["peak"] = max(st["peak"], st["in_use"])
                 progress.beat()                     # busy from now on (0 = idle)
+                released = False
+
+                def release():
+                    nonlocal released
+                    if not released:
+                        released = True
+                        with fork_mu:
+                            fork_stats[mname]["in_use"] -= 1
+                        forks[mname].put(pipe)
                 try:
                     if inp.get("__fault__") == "hang" and os.environ.get("ARBIUS_FAULT_INJECTION") == "1":
                         while True:                 # test hook: a hung kernel - no beats, no result
                             time.sleep(1.0)
                     t0 = time.perf_counter()
-                    if len(batch) > 1 and hasattr(slots[k][mname], "run_group"):
-                        imgs, tm = infer_images(slots[k][mname], [m[5] for m in batch])
-                        tails[k].submit(finish, batch, imgs, tm, t0)
+                    if len(batch) > 1 and hasattr(pipe, "run_group"):
+                        imgs, tm = infer_images(pipe, [m[5] for m in batch])
+                        release()
+                        tails[k].submit(finish, batch, imgs, tm, t0, k)
                         continue
                     # GPU part now; the CPU tail (e.g. RVM's H.264 encode) on the slot's tail thread
                     # while the slot takes its next task
-                    fns = [infer_task(Model(m[3], m[1], {}, True, [], m[2]), slots[k][m[1]], m[5]) for m in batch]
+                    fns = [infer_task(Model(m[3], m[1], {}, True, [], m[2]), pipe, m[5]) for m in batch]
+                    release()
                     if last_tail[k] is not None:
                         last_tail[k].result()
-                    last_tail[k] = tails[k].submit(finish_solo, batch, fns, t0)
+                    last_tail[k] = tails[k].submit(finish_solo, batch, fns, t0, k)
                 except Exception:  # noqa: BLE001
                     for m in batch:
                         out_q.put(("err", m[0], rank, traceback.format_exc()))
                 finally:
-                    caps[msg[1]].release()
+                    release()
                     if beats is not None:
                         beats[rank * streams + k] = 0.0
 
@@ -171,7 +212,8 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
         log.info("worker %d ready: %s", rank, world_info)
         from ..node.pool import hardware_id
         # the dispatcher never touches the GPU: the worker reports its device's arch (self-test key)
-        out_q.put(("ready", rank, dict(bstats, world=world_info, arch=hardware_id(dev))))
+        out_q.put(("ready", rank, dict(bstats, world=world_info, arch=hardware_id(dev),
+                                       forks={n: st["forks"] for n, st in fork_stats.items()})))
         while True:
             msg = in_q.get()
             if msg is None:
@@ -213,7 +255,10 @@ class MultiGPUSolverPool:
         self.streams = max(1, int(streams_per_gpu))
         # per task slot: time of its last progress beat, 0.0 while idle (shared memory, no lock:
         # one writer per slot, the watchdog only reads)
-        self.beats = self.ctx.Array("d", n * self.streams, lock=False)
+        # second half: per task slot, the start time of its CPU tail in flight (0.0 when none; ADVICE r4:
+        # a tail - RVM's H.264 encode + CID - runs after the slot's beat went idle, so the watchdog
+        # times it separately)
+        self.beats = self.ctx.Array("d", 2 * n * self.streams, lock=False)
         # tasks per lock-step group on one stream (HIP kernels only: batch-invariant launches)
         self.lockstep = max(1, int(lockstep)) if device_type == "cuda" else 1
         # one more lock-step group per stream queued in the worker (node/pool.py LocalSolverPool.depth)
@@ -287,6 +332,7 @@ class MultiGPUSolverPool:
     def _spawn(self, rank, port, group):
         for k in range(self.streams):
             self.beats[rank * self.streams + k] = 0.0
+            self.beats[(self.n + rank) * self.streams + k] = 0.0
         p = self.ctx.Process(target=_worker_main, daemon=True,
                              args=(rank, self.n, port, self.device_type, self.models, self.tiny,
                                    self.in_qs[rank], self.out_qs[rank], group, self.weight_seed, self.streams,
@@ -346,7 +392,8 @@ class MultiGPUSolverPool:
         out = []
         for r in range(self.n):
             stamps = [self.beats[r * self.streams + k] for k in range(self.streams)]
-            if any(t > 0.0 and now - t > self.hang_timeout for t in stamps):
+            tails = [self.beats[(self.n + r) * self.streams + k] for k in range(self.streams)]
+            if any(t > 0.0 and now - t > self.hang_timeout for t in stamps + tails):
                 out.append(r)
         return out
 

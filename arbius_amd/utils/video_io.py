@@ -26,6 +26,8 @@ from __future__ import annotations
 
 import base64
 import io
+import json
+import logging
 import os
 import re
 import shutil
@@ -34,6 +36,8 @@ import tempfile
 from typing import List, Tuple
 
 import numpy as np
+
+log = logging.getLogger("arbius.video")
 
 
 MAX_VIDEO_BYTES = 512 << 20
@@ -183,35 +187,49 @@ def _cid_matches(ref: str, data: bytes) -> bool:
 
 
 def _cache_get(ref: str):
+    """Cached bytes of ``ref``, or None.  An entry is used only with its sidecar (written by
+    ``_cache_put`` after the download was checked once, ADVICE r4: no re-hash of up to 512 MB per
+    task) and only when file and sidecar are ours and agree on the size."""
     if not _cache_dir_ok(False):
         return None
     p = _cache_path(ref)
     try:
-        st = os.lstat(p)
-        if st.st_uid != os.getuid() or not os.path.isfile(p):
-            return None
+        for q in (p, p + ".meta"):
+            st = os.lstat(q)
+            if st.st_uid != os.getuid() or not os.path.isfile(q):
+                return None
+        with open(p + ".meta") as f:
+            meta = json.load(f)
         with open(p, "rb") as f:
             data = f.read(MAX_VIDEO_BYTES + 1)
         os.utime(p)
-    except OSError:
+    except (OSError, ValueError):
         return None
-    if len(data) > MAX_VIDEO_BYTES or not _cid_matches(ref, data):
+    if meta.get("ref") != ref or meta.get("size") != len(data) or len(data) > MAX_VIDEO_BYTES:
         return None
     return data
 
 
-def _cache_put(ref: str, data: bytes):
+def _cache_put(ref: str, data: bytes, verified: bool):
     try:
         if not _cache_dir_ok(True):
             return
-        tmp = _cache_path(ref) + f".{os.getpid()}.tmp"
+        p = _cache_path(ref)
+        tmp = p + f".{os.getpid()}.tmp"
         with open(tmp, "wb") as f:
             f.write(data)
-        os.replace(tmp, _cache_path(ref))
+        os.replace(tmp, p)
+        with open(tmp, "w") as f:
+            json.dump({"ref": ref, "size": len(data), "verified": bool(verified)}, f)
+        os.replace(tmp, p + ".meta")
         ents = sorted((os.path.getmtime(os.path.join(_CACHE_DIR, e)), e) for e in os.listdir(_CACHE_DIR)
-                      if not e.endswith(".tmp"))
+                      if not e.endswith((".tmp", ".meta")))
         for _, e in ents[:-_CACHE_KEEP]:
-            os.unlink(os.path.join(_CACHE_DIR, e))
+            for q in (e, e + ".meta"):
+                try:
+                    os.unlink(os.path.join(_CACHE_DIR, q))
+                except FileNotFoundError:
+                    pass
     except OSError:
         pass
 
@@ -231,7 +249,14 @@ def fetch(ref: str) -> bytes:
                 with httpx.stream("GET", f"{gw.rstrip('/')}/ipfs/{ref.replace('ipfs://', '')}", timeout=120.0) as r:
                     r.raise_for_status()
                     data = _read_capped(r)                 # capped while streaming, never read whole first
-            _cache_put(ref, data)
+            # checked ONCE, here: a bare CIDv0 must be the bytes' UnixFS CID under kubo's defaults.  A
+            # file added with another chunker / layout cannot be re-derived: it is kept as unverified
+            # (the operator's gateway served it) instead of being fetched again on every use.
+            verified = _cid_matches(ref, data)
+            if not verified:
+                log.warning("input %s: bytes do not re-derive the CID under kubo's default layout "
+                            "(another chunker?) - used unverified", ref[:80])
+            _cache_put(ref, data, verified)
     if len(data) > MAX_VIDEO_BYTES:
         raise VideoSourceError("input video exceeds MAX_VIDEO_BYTES")
     return data

@@ -22,7 +22,7 @@ from arbius_amd.node.pool import FakeSolverPool
 from arbius_amd.store.db import DB
 from arbius_amd.utils.protocol import generate_commitment
 
-from test_node_e2e import DEPLOYER, MINER, MINER2, USER, make_world, submit
+from test_node_e2e import DEPLOYER, MINER, MINER2, make_world, submit
 
 INPUT = {"prompt": "a lighthouse at dusk", "negative_prompt": "blurry"}
 

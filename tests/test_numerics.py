@@ -73,3 +73,19 @@ def test_plan_rows_is_batch_invariant():
     with ops.plan_batch(2):
         assert ops._plan_rows(solo) == ops._plan_rows(group) == ops.PLAN_CANON * 1024
     assert ops._plan_rows(solo) == 2 * 1024 and ops._plan_rows(group) == 8 * 1024
+
+
+def test_every_kernel_env_knob_is_refused_when_mining():
+    """Every environment variable the HIP kernel library reads (std::getenv in csrc/) selects a kernel,
+    plan or layout: ``start`` must refuse to mine with any of them set."""
+    import re
+    from pathlib import Path
+
+    from arbius_amd.numerics import NUMERICS_ENV_KNOBS
+    csrc = Path(__file__).resolve().parents[1] / "arbius_amd" / "ops" / "csrc"
+    names = set()
+    for f in csrc.glob("*.hip"):
+        names |= set(re.findall(r'getenv\("([A-Z0-9_]+)"\)', f.read_text()))
+    assert names, "no getenv found"
+    missing = sorted(n for n in names if n not in NUMERICS_ENV_KNOBS)
+    assert missing == [], missing

@@ -114,3 +114,17 @@ def test_fast_matting_matches_reference_network(cuda, H, W):
     assert d.mean() < 1.5 and np.percentile(d, 99) <= 8, (d.mean(), np.percentile(d, 99))
     for mode in ("alpha-mask", "foreground-mask"):
         assert fast(clip, mode).shape == clip.shape
+
+
+def test_long_clip_takes_the_staged_download_with_the_same_bytes(cuda, monkeypatch):
+    """a clip above the pinned-result cap (or a failed pin) downloads through the reusable
+    staging buffers instead of one page-locked array of the whole clip - same bytes either way."""
+    from arbius_amd.models import rvm
+    from arbius_amd.models.rvm import RVMConfig, RVMPipeline
+    pipe = RVMPipeline(RVMConfig(chunk=4), device=cuda)
+    rng = np.random.default_rng(5)
+    clip = rng.integers(0, 256, (9, 240, 320, 3), dtype=np.uint8)
+    pinned = pipe(clip, "green-screen")
+    monkeypatch.setattr(rvm, "_PINNED_OUT_MAX", 0)
+    staged = pipe(clip, "green-screen")
+    assert np.array_equal(pinned, staged)

@@ -123,3 +123,37 @@ def test_worker_two_phase_solve_matches_solo():
             await pool.close()
 
     asyncio.run(go())
+
+
+def test_capped_model_gets_cap_forks_and_never_exceeds_its_cap():
+    """with 4 slots and a model capped at 2 streams the worker builds 2 forks of that model
+    (not 4: each fork owns hipGraphs and their memory pools) and never solves more than 2 at once."""
+    ref = [LocalSolverPool("cpu", tiny=True).solve_sync(MODEL, "t", dict(INP, seed=s)).cid for s in range(1, 7)]
+
+    async def go():
+        pool = MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, streams_per_gpu=4,
+                                  model_streams={"anythingv3": 2})
+        try:
+            assert pool.broadcast_stats[0]["forks"] == {"anythingv3": 2}
+            sols = await asyncio.gather(*[pool.solve(MODEL, f"t{s}", dict(INP, seed=s)) for s in range(1, 7)])
+            assert [x.cid for x in sols] == ref
+            assert max(x.timings["fork_peak"] for x in sols) <= 2
+        finally:
+            await pool.close()
+
+    asyncio.run(go())
+
+
+def test_watchdog_times_cpu_tails_too():
+    """a slot's CPU tail (RVM encode + CID, a group's PNGs) runs after the slot's progress
+    beat went idle; the tail's own clock (second half of the beats array) is watched as well."""
+    pool = MultiGPUSolverPool.__new__(MultiGPUSolverPool)
+    pool.n, pool.streams, pool.hang_timeout = 2, 2, 10.0
+    pool.beats = [0.0] * (2 * pool.n * pool.streams)
+    assert pool.hung_ranks(now=1000.0) == []
+    pool.beats[(pool.n + 1) * pool.streams + 1] = 985.0      # rank 1, slot 1: tail started 15 s ago
+    assert pool.hung_ranks(now=1000.0) == [1]
+    pool.beats[(pool.n + 1) * pool.streams + 1] = 995.0
+    assert pool.hung_ranks(now=1000.0) == []
+    pool.beats[0 * pool.streams + 0] = 980.0                 # rank 0, slot 0: solve silent for 20 s
+    assert pool.hung_ranks(now=1000.0) == [0]
