@@ -75,6 +75,8 @@ _SIGS = {
     "arb_rvm_gate": (c_int, [c_void_p, c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "arb_gemm_ln": (c_int, [c_void_p] * 8 + [c_int] * 7 + [c_void_p]),
     "arb_gemm_act": (c_int, [c_void_p] * 6 + [c_int] * 6 + [c_void_p]),
+    "arb_attention512": (c_int, [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p, c_void_p]),
+    "arb_attention512_workspace": (c_long, [c_int] * 4),
 }
 
 
@@ -112,7 +114,7 @@ def loaded() -> bool:
 # selection of this module (no GPU, no data).  Host-only queries still call the library.
 _AUDIT = None
 _HOST_SYMBOLS = ("arb_conv2d_plan", "arb_conv_family", "arb_conv2d_workspace", "arb_group_norm_workspace",
-                 "arb_rvm_args_sizes")
+                 "arb_rvm_args_sizes", "arb_attention512_workspace")
 
 
 def auditing() -> bool:
@@ -300,13 +302,43 @@ def softmax_rows(s, scale, valid=None):
     return p
 
 
-def _large_head_attention(q, k, v, scale):
-    """Head dims > 160 (the single-head d = 512 VAE / MoVQ mid-block attention, once per task):
-    S = Q K^T on the implicit-GEMM kernel, the HIP row softmax, O = P V on the implicit-GEMM kernel
-    (per batch and head; V^T made contiguous once).  Key counts off the 64-tile are zero-padded: the
-    padded score columns are excluded by the softmax (written 0), so P V never sees them."""
+def attention512(q, k, v, scale):
+    """Blockwise (O(N) memory) attention at head dim 512 (csrc/attention512.hip): the single-head
+    VAE / MoVQ mid-block attention.  q/k/v [B, N, H, 512], last dim contiguous."""
+    _bf16(q, k, v)
     B, Nq, H, D = q.shape
     Nk = k.shape[1]
+    if D != 512 or k.shape[-1] != 512 or v.shape[-1] != 512 or tuple(k.shape) != tuple(v.shape):
+        raise ValueError(f"attention512: q {tuple(q.shape)} k {tuple(k.shape)} v {tuple(v.shape)}")
+    for t in (q, k, v):
+        if t.stride(-1) != 1 or any(s % 8 for s in t.stride()[:3]) or t.data_ptr() % 16:
+            raise ValueError("attention512: last dim must be contiguous, strides/base 16B aligned")
+    o = torch.empty(B, Nq, H, D, dtype=q.dtype, device=q.device)
+    if _skip("attn512"):
+        return o
+    wsb = _fn("arb_attention512_workspace")(B, H, Nq, Nk)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=q.device) if wsb else None
+    strides = (ctypes.c_long * 12)(q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),
+                                   v.stride(0), v.stride(1), v.stride(2), o.stride(0), o.stride(1), o.stride(2))
+    _check(_fn("arb_attention512")(_p(q), _p(k), _p(v), _p(o), strides, B, H, Nq, Nk, float(scale), _p(ws),
+                                   _stream()), "attention512")
+    return o
+
+
+# ARB_ATTN512=0: the round-4 GEMM -> row softmax -> GEMM path for d = 512 (A/B; other bytes)
+_A512 = os.environ.get("ARB_ATTN512", "1") != "0"
+
+
+def _large_head_attention(q, k, v, scale):
+    """Head dims > 160: d = 512 (the single-head VAE / MoVQ mid-block attention, once per task) on the
+    blockwise kernel (``attention512``).  Other large heads (none in the templates): S = Q K^T on the
+    implicit-GEMM kernel, the HIP row softmax, O = P V on the implicit-GEMM kernel (per batch and
+    head; V^T made contiguous once).  Key counts off the 64-tile are zero-padded: the padded score
+    columns are excluded by the softmax (written 0), so P V never sees them."""
+    B, Nq, H, D = q.shape
+    Nk = k.shape[1]
+    if D == 512 and k.shape[-1] == 512 and _A512:
+        return attention512(q, k, v, scale)
     if D % 64:
         from . import _library
         _library("attention", f"head dim {D} (the GEMM path needs D % 64 == 0)")
@@ -502,7 +534,8 @@ _CFG_NAMES = {20: "glds<256,256>", 21: "glds<320,128>", 22: "glds<256,128>", 23:
               32: "xreg<160,8,2>", 33: "xreg<128,8,2>", 34: "xreg<160,8,1>", 35: "xreg<256,8,1>",
               36: "stag<256,128>", 37: "stag<128,256>", 38: "stag<192,192>", 39: "stag<320,64>",
               40: "stag<160,256>", 41: "stag<160,128>", 42: "stag2<320,128>", 43: "stag2<256,256>",
-              44: "stag2<256,192>"}
+              44: "stag2<256,192>", 45: "stag2<192,192>",
+              46: "sk<160>", 47: "sk<80>"}
 
 
 def cfg_name(cfg: int) -> str:

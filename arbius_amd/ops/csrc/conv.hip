@@ -1943,14 +1943,14 @@ static const std::vector<PinnedPlan>& env_plans() {
 // cfg ids: 0..9 LDS-DMA 4-wave, 10..19 register-staged 4-wave, 20..23 8-wave LDS-DMA 2-stage,
 // 24..27 persistent short-K, 28..31 8-wave LDS-DMA 3-stage ring (two K-tiles in flight),
 // 32..35 8-wave X-in-registers (weights-only LDS-DMA ring), 36..41 8-wave staggered two-group ring,
-// 42..44 the same on K-half slots
+// 42..45 the same on K-half slots, 46..47 W-stationary short-K GEMM (conv_sk.inc)
 static inline bool is_persist(int cfg) { return cfg >= 24 && cfg < 28; }
 // 32..35 X-in-registers 8-wave tiles (weights through an LDS-DMA ring, activations straight to VGPRs)
 static inline bool is_xreg(int cfg) { return cfg >= 32 && cfg < 36; }
 
 static ConvPlan conv_plan(int M, int N, int ktiles, int want_cfg, int want_split) {
   const int K = ktiles * 64;
-  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 45))) {
+  if (want_cfg >= 0 && (want_cfg < 2 * kNumCfgs || (want_cfg >= 20 && want_cfg < 48))) {
     if (is_persist(want_cfg)) return {want_cfg, 1, ktiles};   // persistent: no split-K
     int split = want_split < 1 ? 1 : want_split;
     if (split > ktiles) split = ktiles;
@@ -2296,6 +2296,8 @@ static void launch_conv(const ConvArgs& a, const ConvPlan& pl, bool glds, hipStr
 // cfg/split = -1: planned; >= 0: forced (autotuning).
 // norm: optional [B, Cin, 2] fp32 (scale, shift) GroupNorm table applied to x in the prologue
 // (+ SiLU when norm_silu) - see arb_group_norm_table.  Register-staged kernels only.
+#include "conv_sk.inc"
+
 template <int EL>
 static int conv_run(const void* x, const void* w, const void* bias, const void* temb, const void* res, void* out,
                     void* ws, const void* norm, int B, int H, int W, int Cin, int Cout, int k, int pad, int upsample,
@@ -2340,12 +2342,22 @@ static int conv_run(const void* x, const void* w, const void* bias, const void* 
     else if (pl.cfg < kNumCfgs) pl.cfg += kNumCfgs;
   }
   if (pl.split > 1 && ws == nullptr) return -3;
+  if (pl.cfg == 46 || pl.cfg == 47) {   // W-stationary short-K GEMM (conv_sk.inc)
+    if (EL == 0 && pl.split == 1 && sk_ok(a, pl.cfg)) {
+      if (pl.cfg == 46) launch_sk<160, 320>(a, stream);
+      else if (a.K == 640) launch_sk<80, 640>(a, stream);
+      else launch_sk<80, 320>(a, stream);
+      return (int)hipGetLastError();
+    }
+    pl.cfg = 34;   // outside its shapes: the X-in-registers 160-wide tile at the same split (same bytes)
+  }
   if (pl.cfg >= 42) {   // half-slot staggered 8-wave tiles (bf16, no norm prologue / dual source)
     if (EL != 0 || a.norm != nullptr) return -4;
     switch (pl.cfg - 42) {
       case 0: launch_stag2<320, 128, 4, 2, 5>(a, pl, stream); break;
       case 1: launch_stag2<256, 256, 2, 4, 5>(a, pl, stream); break;
-      default: launch_stag2<256, 192, 4, 2, 5>(a, pl, stream); break;
+      case 2: launch_stag2<256, 192, 4, 2, 5>(a, pl, stream); break;
+      default: launch_stag2<192, 192, 2, 4, 5>(a, pl, stream); break;   // cfg 45 (120 KiB ring)
     }
     return (int)hipGetLastError();
   }

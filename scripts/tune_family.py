@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from arbius_amd.ops import _lib  # noqa: E402
 from scripts.autotune_conv import collect_shapes, graph_time  # noqa: E402
 
-FAMILIES = list(range(20)) + [20, 21, 22, 23] + list(range(28, 45))
+FAMILIES = list(range(20)) + [20, 21, 22, 23] + list(range(28, 48))
 NOSPLIT = [24, 25, 26, 27]   # persistent: split 1 only
 
 
@@ -48,7 +48,13 @@ def main():
     ap.add_argument("--models", default="sd15", help="comma list: sd15,kandinsky2")
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--plans", action="store_true", help="rewrite conv_plans.inc cfgs (any batch, own plans)")
+    ap.add_argument("--families", default=None, help="comma list of candidate cfgs (default: every family)")
+    ap.add_argument("--gemms-only", action="store_true", help="tune the GEMM shapes only (keep the conv entries)")
     a = ap.parse_args()
+    if a.families:
+        global FAMILIES, NOSPLIT
+        FAMILIES = [int(c) for c in a.families.split(",")]
+        NOSPLIT = [c for c in NOSPLIT if c in FAMILIES]
     if a.plans:
         return tune_plans(a)
     import scripts.autotune_conv as at
@@ -64,7 +70,7 @@ def main():
                 kept[(M, N, K, sp, r)] = c
     torch.manual_seed(0)
     for (B, H, W, C, Co, kh, kw, pad, up, stride) in convs:
-        if B != a.batch or kh != kw:
+        if B != a.batch or kh != kw or a.gemms_only:
             continue
         x = torch.randn(B, H, W, C, device=dev).bfloat16()
         w = (torch.randn(Co, kh, kw, C, device=dev) / math.sqrt(kh * kw * C)).bfloat16()
@@ -106,7 +112,10 @@ def main():
         ref = _lib.gemm(x, w, b, r, cfg0, sp)
         best = (graph_time(lambda: _lib.gemm(x, w, b, r, cfg0, sp)), cfg0)
         base = best[0]
-        for cfg in FAMILIES + (NOSPLIT if sp == 1 else []):
+        cands = FAMILIES + (NOSPLIT if sp == 1 else [])
+        if key in kept and kept[key] not in cands:     # a restricted search still weighs the current family
+            cands = cands + [kept[key]]
+        for cfg in cands:
             if cfg == cfg0:
                 continue
             try:

@@ -133,7 +133,7 @@ def test_gemm(cuda, M, K, N):
     assert _rel(y, x.float() @ w.float().t() + b.float() + r.float()) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", list(range(20)) + list(range(20, 28)) + list(range(32, 45)))
+@pytest.mark.parametrize("cfg", list(range(20)) + list(range(20, 28)) + list(range(32, 46)))
 @pytest.mark.parametrize("split", [1, 3])
 def test_conv2d_all_tile_configs(cuda, cfg, split):
     """Every tile config of both kernel variants (LDS-DMA ring / register staged) and split-K."""
@@ -159,7 +159,7 @@ def test_conv_tile_families_bitwise_equal(cuda, B, H, W, C, Co, k):
     b = torch.randn(Co, device=cuda).bfloat16()
     pad = k // 2
     ref_y = _lib.conv2d_nhwc(x, w, b, pad, False, None, None, 1, 10, 1)
-    for cfg in (0, 3, 5, 6, 13, 15, 16, 20, 21, 22, 28, 29, 31, 36, 37, 38, 39, 40, 41, 42, 43, 44):
+    for cfg in (0, 3, 5, 6, 13, 15, 16, 20, 21, 22, 28, 29, 31, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45):
         y = _lib.conv2d_nhwc(x, w, b, pad, False, None, None, 1, cfg, 1)
         assert torch.equal(y, ref_y), cfg
 
@@ -180,7 +180,7 @@ def test_conv_tile_families_bitwise_equal_at_split(cuda, split, B, H, W, C, Co, 
     pad = k // 2
     ref_y = _lib.conv2d_nhwc(x, w, b, pad, False, r, None, 1, 15, split)
     for cfg in (0, 3, 4, 5, 10, 13, 14, 16, 20, 21, 22, 28, 29, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42,
-                43, 44):
+                43, 44, 45):
         y = _lib.conv2d_nhwc(x, w, b, pad, False, r, None, 1, cfg, split)
         assert torch.equal(y, ref_y), cfg
 
@@ -205,7 +205,8 @@ def test_gemm_persistent_many_tiles(cuda, cfg, res):
 @pytest.mark.parametrize("M,K,N,cfg,split", [
     (8200, 320, 2560, -1, -1), (8200, 320, 2560, 15, 1), (8200, 320, 2560, 25, 1), (8200, 320, 2560, 21, 1),
     (8200, 320, 2560, 0, 1), (512, 1280, 10240, 13, 3), (512, 1280, 10240, 22, 2), (300, 640, 5120, 3, 1),
-    (8200, 320, 2560, 32, 1), (300, 640, 5120, 35, 1)])
+    (8200, 320, 2560, 32, 1), (300, 640, 5120, 35, 1), (8200, 320, 2560, 46, 1), (8192, 640, 5120, 47, 1),
+    (300, 640, 5120, 47, 1), (1000, 320, 2576, 47, 1)])
 def test_gemm_geglu_bitwise_equals_unfused(cuda, M, K, N, cfg, split):
     """GEGLU in the GEMM epilogue (interleaved value/gate rows) == geglu(gemm(x, w, b)) bitwise,
     for register / LDS-DMA / 8-wave tiles, split-K (reduce kernel) and the persistent remap."""
@@ -583,7 +584,7 @@ def test_fused_sampler_hip_vs_fp32_reference(cuda, name):
 @pytest.mark.parametrize("M,K,N,geglu,res", [(8 * 4096, 320, 960, False, False), (8 * 1024, 640, 640, False, False),
                                              (8 * 256, 1280, 10240, True, False), (2 * 77, 768, 3072, False, False),
                                              (300, 320, 2560, True, False), (1000, 1280, 1280, False, True)])
-@pytest.mark.parametrize("cfg,split", [(-1, -1), (10, 1), (12, 3), (24, 1), (5, 2), (32, 1)])
+@pytest.mark.parametrize("cfg,split", [(-1, -1), (10, 1), (12, 3), (24, 1), (5, 2), (32, 1), (46, 1), (47, 1)])
 def test_gemm_with_folded_layer_norm(cuda, M, K, N, geglu, res, cfg, split):
     """LayerNorm folded into the GEMM epilogue (row stats + gamma-scaled weights + wsum) against the
     fp32 reference LN -> linear (-> GEGLU), on every epilogue path: planned, register-staged,
@@ -767,7 +768,7 @@ def test_stag2_prefetch_distance_bitwise(cuda, B, H, W, C, Co, cfg, split):
     assert _rel(ref3, r) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [0, 3, 5, 9, 20, 21, 22, 23, 28, 29, 30, 31, 36, 37, 38, 39, 40, 41, 42, 43, 44])
+@pytest.mark.parametrize("cfg", [0, 3, 5, 9, 20, 21, 22, 23, 28, 29, 30, 31, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45])
 def test_lds_dma_buffer_resource_bitwise(cuda, cfg):
     """LDS-DMA through buffer resources (range-checked zero fill for padding taps / rows past N and M)
     == the global_load_lds + zero-page form, bit for bit, on a shape with borders and ragged tiles."""
@@ -785,3 +786,75 @@ def test_lds_dma_buffer_resource_bitwise(cuda, cfg):
     finally:
         fb(1)
     assert all(torch.equal(g, ref) for g in got)
+
+
+@pytest.mark.parametrize("B,Nq,Nk", [(1, 4096, 4096), (1, 9216, 9216), (1, 300, 777), (3, 64, 2048), (1, 16, 5000),
+                                     (2, 2880, 2880)])
+def test_attention512_blockwise(cuda, B, Nq, Nk):
+    """Blockwise d = 512 attention (csrc/attention512.hip: key splits merged in order at 4096 / 9216
+    keys, partial 32-key tiles, Nq != Nk) vs the fp32 reference; bitwise rerun."""
+    torch.manual_seed(11)
+    q = torch.randn(B, Nq, 1, 512, device=cuda).bfloat16()
+    kv = torch.randn(B, Nk, 2, 1, 512, device=cuda).bfloat16()
+    k, v = kv[:, :, 0], kv[:, :, 1]
+    o = _lib.attention512(q, k, v, 1 / math.sqrt(512))
+    r = ref.attention(q.float(), k.float(), v.float(), 1 / math.sqrt(512), False)
+    assert _rel(o, r) < 1e-2
+    assert torch.equal(o, _lib.attention512(q, k, v, 1 / math.sqrt(512)))
+
+
+def test_attention512_rescale_spike(cuda):
+    """One key tile far above the running max (forces the lazy rescale mid-row, and in one key split
+    only): still the reference within bf16 rounding."""
+    torch.manual_seed(12)
+    B, N = 1, 4096
+    q = torch.randn(B, N, 1, 512, device=cuda) * 0.5
+    k = torch.randn(B, N, 1, 512, device=cuda) * 0.5
+    k[:, 2500] = q[:, 7] * 4.0               # query 7 locks onto key 2500 (third split)
+    k[:, 40] = -q[:, 9] * 4.0
+    v = torch.randn(B, N, 1, 512, device=cuda)
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    o = _lib.attention512(q, k, v, 1 / math.sqrt(512))
+    r = ref.attention(q.float(), k.float(), v.float(), 1 / math.sqrt(512), False)
+    assert _rel(o, r) < 1e-2 and _rel(o[:, 7], r[:, 7]) < 1e-2
+
+
+def test_attention512_memory_is_linear(cuda):
+    """16,384 tokens (anythingv3 at 1024^2): no score matrix - the call allocates only its output (the
+    GEMM path's [N, N] bf16 scores alone are 512 MiB)."""
+    q = torch.randn(1, 16384, 1, 512, device=cuda).bfloat16()
+    k = torch.randn(1, 16384, 1, 512, device=cuda).bfloat16()
+    v = torch.randn(1, 16384, 1, 512, device=cuda).bfloat16()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    o = ops.attention(q, k, v)
+    torch.cuda.synchronize()
+    assert torch.cuda.max_memory_allocated() - base <= 2 * o.numel() * o.element_size()
+    assert torch.isfinite(o.float()).all()
+
+
+@pytest.mark.parametrize("cfg", [46, 47])
+@pytest.mark.parametrize("M,K,N,res,act", [(32768, 320, 320, False, None), (8200, 320, 960, True, None),
+                                           (8192, 640, 640, True, None), (4100, 640, 1920, False, None),
+                                           (300, 320, 328, True, None), (1000, 640, 88, False, "gelu"),
+                                           (333, 320, 1280, True, "quick_gelu"), (8192, 1280, 640, True, None)])
+def test_gemm_w_stationary_bitwise_equal_tiled(cuda, cfg, M, K, N, res, act):
+    """W-stationary short-K kernel (csrc/conv_sk.inc, cfg 46 / 47: resident weight panel, activation
+    rows straight to VGPRs, epilogue from registers): ragged M, partial weight panels, bias +
+    residual / activation epilogues, bitwise equal to the register-staged tile at split 1; shapes
+    outside its range (K = 1280, K = 640 on cfg 46) take the X-in-registers tile (same bytes)."""
+    torch.manual_seed(21)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    r = torch.randn(M, N, device=cuda).bfloat16() if res else None
+    y = _lib.gemm(x, w, b, r, cfg, 1, act=act)
+    assert torch.equal(y, _lib.gemm(x, w, b, r, 15, 1, act=act))
+    assert torch.equal(y, _lib.gemm(x, w, b, r, cfg, 1, act=act))
+    h = x.float() @ w.float().t() + b.float() + (r.float() if res else 0)
+    if act == "gelu":
+        h = torch.nn.functional.gelu(h)
+    elif act == "quick_gelu":
+        h = h * torch.sigmoid(1.702 * h)
+    assert _rel(y, h) < 1.5e-2

@@ -61,7 +61,7 @@ def test_family_table_well_formed():
     assert len(keys) == len(set(keys))
     for M, N, K, split, ratio, cfg in rows:
         assert ratio in (0, 1, 2, 4) and split >= 1 and K % 64 == 0
-        assert 0 <= cfg < 45 and not (24 <= cfg < 28 and split > 1)   # 0..44: conv.hip tile cfgs
+        assert 0 <= cfg < 46 and not (24 <= cfg < 28 and split > 1)   # 0..45: conv.hip tile cfgs
 
 
 def test_plan_rows_is_batch_invariant():
