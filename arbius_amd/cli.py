@@ -74,7 +74,8 @@ def build_pool(cfg, models):
         return MultiGPUSolverPool(n, names, "cuda", streams_per_gpu=cfg.mi355x.workers_per_gpu,
                                   model_streams=cfg.mi355x.model_streams,
                                   lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir,
-                                  hang_timeout=cfg.mi355x.hang_timeout_s, force_group=n == 1)
+                                  hang_timeout=cfg.mi355x.hang_timeout_s, force_group=n == 1,
+                                  dispatch=cfg.mi355x.dispatch_policy)
     from .node.pool import LocalSolverPool
     return LocalSolverPool("cuda:0" if n == 1 else "cpu", capacity=cfg.mi355x.workers_per_gpu,
                            model_streams=cfg.mi355x.model_streams,

@@ -111,6 +111,9 @@ class MI355XConfig(_Base):
     # task's on-chain CID and accepted only if their on-chain CIDv0 matches.  None: $ARBIUS_IPFS_GATEWAY,
     # else only the configured pinner (kubo cat / the local store) is asked.
     ipfs_gateway: Optional[str] = None
+    # task -> GPU policy of the multi-GPU pool (parallel/dispatch.py): "spread" = least-loaded GPU
+    # first (lowest latency below saturation, profiles/dispatch_r5.md), "pack" = fill one GPU first
+    dispatch_policy: Literal["spread", "pack"] = "spread"
     lockstep_group: int = 4               # queued compatible SD tasks solved per stream in ONE batch
                                           # (batch-invariant plans: same CIDs as solo; a lone task
                                           # never waits for company)

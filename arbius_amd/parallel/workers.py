@@ -37,6 +37,8 @@ import time
 import traceback
 from typing import Dict, List, Optional
 
+from .dispatch import POLICIES, pick_rank
+
 log = logging.getLogger("arbius.workers")
 
 
@@ -236,7 +238,11 @@ class MultiGPUSolverPool:
     def __init__(self, n: int, models: List[str], device_type: str = "cuda", tiny: bool = False,
                  weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1,
                  lockstep: int = 1, weights_dir: Optional[str] = None, hang_timeout: float = 300.0,
-                 force_group: bool = False, model_streams: Optional[Dict[str, int]] = None):
+                 force_group: bool = False, model_streams: Optional[Dict[str, int]] = None,
+                 dispatch: str = "spread"):
+        if dispatch not in POLICIES:
+            raise ValueError(f"dispatch policy {dispatch!r} not in {POLICIES}")
+        self.dispatch = dispatch
         self.n = n
         self.model_streams = dict(model_streams or {})
         self.force_group = bool(force_group)
@@ -426,9 +432,11 @@ class MultiGPUSolverPool:
             await asyncio.sleep(0.01)
             self._watchdog()
             self._drain_nowait()
-        # least-loaded GPU first: spread concurrent tasks over GPUs before doubling up on one
+        # dispatch policy (parallel/dispatch.py): "spread" (default) = least-loaded GPU first - below
+        # saturation a task starts at once on an idle GPU (p50 354 ms vs ~3.7 s when GPUs are packed,
+        # profiles/dispatch_r5.md); groups still form where a GPU's own queue builds up
         load = {r: sum(1 for rr in self.busy.values() if rr == r) for r in set(self.idle)}
-        rank = min(set(self.idle), key=lambda r: (load[r], r))
+        rank = pick_rank(self.dispatch, self.idle, load)
         self.idle.remove(rank)
         jid = next(self._ids)
         fut = asyncio.get_running_loop().create_future()

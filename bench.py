@@ -66,6 +66,9 @@ def parse_args(argv=None):
     ap.add_argument("--node", action="store_true",
                     help="whole-node mode: tasks flow through the node's own stack (MockEngine events -> "
                          "orchestrator -> solver pool -> commit/submit); one process, N GPU worker processes")
+    ap.add_argument("--dispatch-sim", action="store_true",
+                    help="no GPU: the multi-GPU dispatch model (parallel/dispatch.py) under Poisson arrival at "
+                         "25/50/75/100 %% of node capacity, spread vs pack policy (one JSON line per point)")
     ap.add_argument("--node-outstanding", type=int, default=0,
                     help="--node: tasks kept in flight (default 2 x pool capacity: a saturated node)")
     args = ap.parse_args(argv)
@@ -435,6 +438,16 @@ def spawn(argv, world: int) -> int:
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
+    if args.dispatch_sim:
+        from arbius_amd.parallel.dispatch import node_capacity_per_s, simulate
+        n = max(1, args.gpus)
+        cap = node_capacity_per_s(n_gpus=n, streams=args.concurrent, group=args.group)
+        for frac in (0.25, 0.5, 0.75, 1.0):
+            for pol in ("spread", "pack"):
+                r = simulate(pol, cap * frac, n_gpus=n, streams=args.concurrent, group=args.group, n_tasks=4000)
+                print(json.dumps(dict(r, load=frac, n_gpus=n, model="anythingv3 service model (measured r4 points)")),
+                      flush=True)
+        return
     launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
     if args.node:
         if launched > 1:

@@ -157,3 +157,24 @@ def test_watchdog_times_cpu_tails_too():
     assert pool.hung_ranks(now=1000.0) == []
     pool.beats[0 * pool.streams + 0] = 980.0                 # rank 0, slot 0: solve silent for 20 s
     assert pool.hung_ranks(now=1000.0) == [0]
+
+
+def test_dispatch_policies_and_model():
+    """pick_rank: spread = least-loaded GPU, pack = most-loaded GPU with a free slot; the dispatch model
+    (parallel/dispatch.py) reproduces the measured single-GPU points it was fitted to, and below
+    saturation spread answers faster than pack at the same completed throughput."""
+    from arbius_amd.parallel.dispatch import SD15_MODEL, pick_rank, simulate, node_capacity_per_s
+    load = {0: 3, 1: 0, 2: 5, 3: 1}
+    assert pick_rank("spread", [0, 1, 2, 3], load) == 1
+    assert pick_rank("pack", [0, 1, 2, 3], load) == 2
+    with pytest.raises(ValueError):
+        pick_rank("random", [0], load)
+    for (s, g, ms) in ((4, 4, 1995), (4, 2, 1254), (3, 4, 1541), (1, 1, 354)):
+        assert abs(SD15_MODEL.work(g) * s / SD15_MODEL.eff[s - 1] - ms) / ms < 0.02
+    cap = node_capacity_per_s()
+    sp = simulate("spread", 0.5 * cap, n_tasks=1500)
+    pk = simulate("pack", 0.5 * cap, n_tasks=1500)
+    assert sp["p50_ms"] * 3 < pk["p50_ms"]
+    assert sp["completed_per_h"] >= 0.97 * pk["completed_per_h"]
+    with pytest.raises(ValueError):
+        MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, dispatch="random")
