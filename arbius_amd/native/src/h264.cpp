@@ -1,24 +1,22 @@
-// Deterministic H.264 Constrained-Baseline intra codec (CAVLC), see h264.h.
+// Deterministic H.264 Constrained-Baseline codec (CAVLC), see h264.h.
 //
-// Why it exists (SURVEY.md §2.6(c,d), VERDICT r1 "Harden video input and shrink video output"):
-// the video templates (/root/reference/templates/zeroscopev2xl.json:1,
-// robust_video_matting.json:6-31) return out-1.mp4 whose CID is the solution, so the encoder
-// must be a pure function of the frames on every node, and there is no ffmpeg / libx264 in the
-// image.  Round 1 wrote raw I_PCM macroblocks (~149 MB per 1080p 48-frame clip); this codec
-// writes I_16x16 macroblocks with the integer 4x4 transform at a fixed QP, which is ~10-40x
-// smaller and still decodable by every H.264 decoder (Constrained Baseline, CAVLC, deblocking
-// disabled in the slice header so the reconstruction is exactly the decoder's output).
+// Why it exists (SURVEY.md §2.6(c,d)): the video templates (/root/reference/templates/zeroscopev2xl.json:1,
+// robust_video_matting.json:6-31) return out-1.mp4 whose CID is the solution, so the encoder must be a
+// pure function of the frames on every node, and there is no ffmpeg / libx264 in the image; the matting
+// template's input_video has to be decoded without one too.
 //
-// Encoder: per macroblock the Intra_16x16 luma mode (V / H / DC / plane) and the chroma mode
-// (DC / H / V / plane) are chosen by SAD over the source (integer, ties -> lowest mode);
-// forward core transform + Hadamard DC, dead-zone quantisation (intra rounding 1/3), coded
-// block patterns from the quantised levels; the reconstruction is the normative decoding
-// process (ITU-T H.264 8.3.3, 8.3.4, 8.5.10-8.5.12) shared with the decoder below, so the
-// encoder's recon == any decoder's output, bit for bit.
+// Encoder: IPPP GOPs.  I macroblocks choose the Intra_16x16 luma / chroma mode by SAD (SSE2 psadbw,
+// integer, ties -> lowest mode); P macroblocks a quarter-sample motion vector by a fixed search order
+// (P_L0_16x16 / P_Skip); forward core transform + Hadamard DC, dead-zone quantisation at a fixed QP,
+// CAVLC over a non-zero bit mask; in-loop deblocking ON.  The reconstruction is the normative decoding
+// process (ITU-T H.264 8.3-8.7) shared with the decoder below, so the encoder's reference pictures are
+// every decoder's output, bit for bit; slices encode in parallel (same bytes at any thread count).
 //
-// Decoder: SPS/PPS/IDR + non-IDR I slices, CAVLC, I_PCM / I_16x16 / I_NxN (intra 4x4), multiple
-// slices, 4:2:0 8-bit, deblocking disabled.  Everything else throws (the node then marks the
-// task's input undecodable instead of failing the solve).
+// Decoder (input_video): SPS / PPS, IDR and non-IDR I and P slices, CAVLC, I_PCM / I_16x16 / I_NxN /
+// P partitions with quarter-sample MC, multiple reference frames with list modification and MMCO,
+// in-loop deblocking (wavefront-parallel), multiple slices, 4:2:0 8-bit.  CABAC, B slices, High-profile
+// tools (8x8 transform), weighted prediction and long-term references throw: the node then skips the
+// task as undecodable (never marks it invalid: another miner's decoder may read it).
 #include "h264.h"
 
 #include <emmintrin.h>   // SSE2 (x86-64 baseline): psadbw for the mode-decision SADs

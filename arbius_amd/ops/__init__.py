@@ -46,8 +46,8 @@ _NORM_PROLOGUE = _NORM_PROLOGUE_MODE == "1"
 def _norm_prologue(w) -> bool:
     return _NORM_PROLOGUE or (_NORM_PROLOGUE_MODE == "1x1" and w.shape[1] == 1 and w.shape[2] == 1)
 
-# Library convolutions (MIOpen: depthwise / 3-4 channel / fp16 RVM convs) must pick the
-# same deterministic solver on every call and every GPU: a solution CID is consensus.
+# GPU tensors never reach a library convolution (LibraryFallback above); these flags only matter for
+# the ARBIUS_LIBRARY_FALLBACK=1 A/B runs, where MIOpen must at least pick the same solver every call.
 torch.backends.cudnn.deterministic = True
 torch.backends.cudnn.benchmark = False
 
