@@ -30,6 +30,8 @@ def _dbg(msg):
 
 
 _SIDE = {}
+# ARB_CAPTURE_SIDE=1: warm up and capture on one process-wide side stream instead (A/B; same graphs)
+_CAPTURE_SIDE = os.environ.get("ARB_CAPTURE_SIDE", "0") == "1"
 
 
 def capture_stream(dev) -> "torch.cuda.Stream":
@@ -40,7 +42,7 @@ def capture_stream(dev) -> "torch.cuda.Stream":
     Only an unforked pipeline (current stream = the default stream, which cannot capture) uses one
     process-wide side stream."""
     cur = torch.cuda.current_stream(dev)
-    if cur != torch.cuda.default_stream(dev):
+    if cur != torch.cuda.default_stream(dev) and not _CAPTURE_SIDE:
         return cur
     key = torch.device(dev).index
     if key not in _SIDE:

@@ -278,8 +278,11 @@ class Kandinsky2Pipeline(PipelineBase):
 
     @torch.no_grad()
     def decode(self, latent):
-        img = self.movq(latent.to(self.dtype))[0].float()
-        img = ((img + 1.0) * 127.5).clamp(0, 255).round().to(torch.uint8)
+        img = self.movq(latent.to(self.dtype))[0]
+        if img.is_cuda and img.dtype == torch.bfloat16 and not ops.reference_ops():
+            img = ops.image_u8(img, 1)            # one HIP pass, the ATen chain's bytes
+        else:
+            img = ((img.float() + 1.0) * 127.5).clamp(0, 255).round().to(torch.uint8)
         return img.cpu().numpy()
 
     def solve(self, inp: dict):

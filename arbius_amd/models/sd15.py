@@ -277,8 +277,11 @@ class SD15Pipeline(PipelineBase):
         if "vae" in ops._EXP_SKIP:      # ablation runs only (numerics knob): no VAE decode
             return np.zeros((z.shape[1] * 8, z.shape[2] * 8, 3), np.uint8)
         if self.use_graphs and _VAE_GRAPH:
-            img = self._vae_graph(z).float()      # .float(): a copy out of the graph's static output
+            img = self._vae_graph(z).clone()      # a copy out of the graph's static output
         else:
-            img = self.vae(z)[0].float()
-        img = ((img / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
+            img = self.vae(z)[0]
+        if img.is_cuda and img.dtype == torch.bfloat16 and not ops.reference_ops():
+            img = ops.image_u8(img, 0)            # one HIP pass, the ATen chain's bytes
+        else:
+            img = ((img.float() / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
         return _to_host(img)  # [H, W, 3]

@@ -23,6 +23,7 @@ import torch
 from ..utils.mp4 import encode_mp4
 from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
+from .. import ops
 from .graphs import GraphCache, PipelineBase
 from .layers import init_weights
 from .schedulers import GroupSampler, TaskSampler, make_scheduler
@@ -155,8 +156,7 @@ class VideoPipeline(PipelineBase):
         out = []
         for i in range(0, z.shape[0], self.cfg.vae_chunk):
             beat()
-            img = self.vae(z[i:i + self.cfg.vae_chunk]).float()
-            out.append(((img / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8).cpu())
+            out.append(ops.image_u8(self.vae(z[i:i + self.cfg.vae_chunk]), 0).cpu())
         return torch.cat(out).numpy()                             # [F, H, W, 3]
 
     def solve(self, inp: dict):

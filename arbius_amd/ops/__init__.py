@@ -658,3 +658,13 @@ def sampler_step(tasks):
 def native_loaded() -> bool:
     """True when the HIP kernel library is loaded in this process."""
     return _lib.loaded()
+
+
+def image_u8(x, mode: int):
+    """Decoded image -> uint8 RGB: mode 0 KL-VAE round(clamp(x / 2 + 0.5, 0, 1) * 255), mode 1 MoVQ
+    round(clamp((x + 1) * 127.5, 0, 255)).  GPU bf16: one HIP pass; otherwise the PyTorch chain."""
+    if _hip(x) and x.dtype == torch.bfloat16:
+        return _lib.image_u8(x, mode)
+    x = x.float()
+    v = (x / 2 + 0.5).clamp(0, 1) * 255 if mode == 0 else ((x + 1.0) * 127.5).clamp(0, 255)
+    return v.round().to(torch.uint8)

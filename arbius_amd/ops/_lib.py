@@ -75,6 +75,7 @@ _SIGS = {
     "arb_rvm_gate": (c_int, [c_void_p, c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "arb_gemm_ln": (c_int, [c_void_p] * 8 + [c_int] * 7 + [c_void_p]),
     "arb_gemm_act": (c_int, [c_void_p] * 6 + [c_int] * 6 + [c_void_p]),
+    "arb_image_u8": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
     "arb_attention512": (c_int, [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p, c_void_p]),
     "arb_attention512_workspace": (c_long, [c_int] * 4),
 }
@@ -959,3 +960,13 @@ def rvm_gate(x, w, mode):
 
 def rvm_args_size(which: int) -> int:
     return int(_fn("arb_rvm_args_sizes")(which))
+
+
+def image_u8(x, mode: int):
+    """Decoded bf16 image [..., 3] -> uint8 (csrc/elementwise.hip image_u8_kernel): mode 0 the KL-VAE's
+    round(clamp(x / 2 + 0.5, 0, 1) * 255), mode 1 the MoVQ's round(clamp((x + 1) * 127.5, 0, 255))."""
+    _bf16(x)
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    _check(_fn("arb_image_u8")(_p(x), _p(y), x.numel(), int(mode), _stream()), "image_u8")
+    return y

@@ -17,7 +17,7 @@
 //     transposing reads).  Two stages (131 KiB of LDS),
 //     the next tile's DMA in flight under the current tile's MFMAs.
 //   * the key axis is split over S workgroups when (batch x query blocks) alone cannot fill the chip
-//     (S from the launch geometry only, at most 4): each writes an fp32 partial O^T and its (max, sum);
+//     (S from the launch geometry only, at most 8): each writes an fp32 partial O^T and its (max, sum);
 //     attn512_combine_kernel merges the S partials in split order.  S = 1 normalises in place.
 //   * no atomics, fixed reduction order -> bitwise deterministic.
 #include "common.h"
@@ -294,13 +294,18 @@ __global__ void __launch_bounds__(256) attn512_combine_kernel(A5Args a) {
   st16(a.o + b * a.o_sb + h * a.o_sh + (long)qi * a.o_sn + d, pack8(acc));
 }
 
-// Key splits of one call: only when the query blocks alone leave most of the 256 CUs idle; from the
-// launch geometry only (B, H, Nq), so equal calls split equally.
+// Key splits of one call, from the launch geometry only (equal calls split equally): only when the
+// query blocks alone leave CUs idle (< 256 workgroups; one workgroup per CU), then the split count
+// 1..8 (>= 512 keys each) whose workgroups fill the last round of 256 best, a larger split only for a
+// clearly fuller chip (4096 tokens: 4 splits, 256 workgroups; 9216: 5 splits, 720 of 768 slots).
 static int a5_splits(int B, int H, int Nq, int Nk) {
   const long blocks = (long)B * H * ((Nq + A5_QB - 1) / A5_QB);
-  int s = 1;
-  while (s < 4 && blocks * s < 256 && Nk >= 2 * s * 1024) s *= 2;
-  return s;
+  if (blocks >= 256) return 1;
+  auto fill = [&](int s) { const long n = blocks * s; return (double)n / (256.0 * ((n + 255) / 256)); };
+  int best = 1;
+  for (int s = 2; s <= 8 && Nk >= s * 512; ++s)
+    if (fill(s) > fill(best) + 0.05) best = s;
+  return best;
 }
 
 // workspace bytes for arb_attention512 (0 when the call does not split)

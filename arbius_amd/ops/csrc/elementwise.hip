@@ -307,3 +307,30 @@ ARB_API int arb_upsample2(const void* x, void* y, int B, int H, int W, int C, hi
   upsample2_kernel<<<grid_for(total8), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, H, W, C, total8);
   return (int)hipGetLastError();
 }
+
+// Decoded image -> uint8 RGB in one pass (the tail of every VAE / MoVQ decode; was 5-6 ATen launches):
+// mode 0 (SD KL-VAE): round(clamp(x / 2 + 0.5, 0, 1) * 255); mode 1 (MoVQ): round(clamp((x + 1) * 127.5, 0, 255)).
+// fp32 arithmetic in the order of the PyTorch expressions (x / 2 exact, so a contracted fma rounds the
+// same), round half to even - bitwise the ATen chain for finite inputs.
+__global__ void __launch_bounds__(256) image_u8_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ y, long n,
+                                                       int mode) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float f = bf2f(x[i]);
+    float v;
+    if (mode == 0) {
+      v = fminf(fmaxf(f * 0.5f + 0.5f, 0.f), 1.f) * 255.f;
+    } else {
+      const float s = f + 1.f;
+      v = fminf(fmaxf(s * 127.5f, 0.f), 255.f);
+    }
+    y[i] = (uint8_t)rintf(v);
+  }
+}
+
+ARB_API int arb_image_u8(const void* x, void* y, long n, int mode, hipStream_t stream) {
+  if (n <= 0 || mode < 0 || mode > 1) return -1;
+  long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  image_u8_kernel<<<dim3((unsigned)blocks), 256, 0, stream>>>((const bf16_t*)x, (uint8_t*)y, n, mode);
+  return (int)hipGetLastError();
+}

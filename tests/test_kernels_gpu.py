@@ -858,3 +858,16 @@ def test_gemm_w_stationary_bitwise_equal_tiled(cuda, cfg, M, K, N, res, act):
     elif act == "quick_gelu":
         h = h * torch.sigmoid(1.702 * h)
     assert _rel(y, h) < 1.5e-2
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_image_u8_equals_aten_chain(cuda, mode):
+    """The decode tail in one HIP pass == the PyTorch expression chain, byte for byte (incl. values
+    exactly at .5 after scaling, and out-of-range inputs)."""
+    torch.manual_seed(30)
+    x = (torch.randn(333, 517, 3, device=cuda) * 1.3).bfloat16()
+    x.view(-1)[:8] = torch.tensor([-1.0, 1.0, 0.0, 2.5, -3.0, 1 / 255, 0.5, -0.5], device=cuda).bfloat16()
+    got = _lib.image_u8(x, mode)
+    f = x.float()
+    want = ((f / 2 + 0.5).clamp(0, 1) * 255).round() if mode == 0 else ((f + 1.0) * 127.5).clamp(0, 255).round()
+    assert torch.equal(got, want.to(torch.uint8))
