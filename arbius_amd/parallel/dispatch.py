@@ -18,7 +18,6 @@ dispatch decision itself is ``pick_rank`` - the same function the pool calls.
 """
 from __future__ import annotations
 
-import heapq
 import random
 import statistics
 from dataclasses import dataclass, field
