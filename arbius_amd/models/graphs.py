@@ -50,6 +50,74 @@ def capture_stream(dev) -> "torch.cuda.Stream":
     return _SIDE[key]
 
 
+_HELD = []              # rejected candidates, kept alive so their queue stays counted
+QUEUE_STATS = {"checked": 0, "rejected": 0, "shared": 0}
+_SPIN = 4_000_000       # torch.cuda._sleep cycles: ~1.7 ms on MI355X (50M cycles = 20.9 ms, queue_probe_r5)
+
+
+def _spin_wall(dev, streams) -> float:
+    best = float("inf")
+    for _ in range(2):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for s in streams:
+            with torch.cuda.stream(s):
+                torch.cuda._sleep(_SPIN)
+        torch.cuda.synchronize(dev)
+        best = min(best, time.perf_counter() - t0)
+    return best
+
+
+def task_stream(dev, peers=()) -> "torch.cuda.Stream":
+    """A stream for one concurrent task (a pipeline fork) on a hardware queue that none of ``peers``
+    (the other task streams of the same pipeline) uses.  HIP binds a stream to one of
+    GPU_MAX_HW_QUEUES (4) HSA queues at its first use, and two streams on one queue run their kernels
+    strictly one after the other.  Which queue a stream gets depends on which streams were used before
+    it, so changing an unrelated side stream can put two task streams on one queue.  Round 5 measured
+    exactly that: slots 2 and 3 of the 4-stream SD bench ran at half the rate of slots 0 and 1
+    (profiles/queues_r5_sd15.md).  This function does not assume any mapping; it measures it.  It runs
+    a one-workgroup spin kernel on the candidate together with every peer.  If the run takes more than
+    1.5 spin lengths, the candidate shares a queue.  The candidate is then held (so its queue stays
+    counted) and the next one is tried.  Past GPU_MAX_HW_QUEUES task streams, sharing cannot be avoided
+    and the stream is taken as is.  ARB_QUEUE_CHECK=0 turns the check off (A/B)."""
+    dev = torch.device(dev)
+    if dev.type != "cuda":
+        return None
+    live = list(peers)
+    nq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    cand = torch.cuda.Stream(device=dev)
+    if live and len(live) < nq and os.environ.get("ARB_QUEUE_CHECK", "1") != "0":
+        QUEUE_STATS["checked"] += 1
+        one = _spin_wall(dev, [cand])
+        for _ in range(4 * nq):
+            if _spin_wall(dev, live + [cand]) < 1.5 * one:
+                break
+            QUEUE_STATS["rejected"] += 1
+            _HELD.append(cand)
+            cand = torch.cuda.Stream(device=dev)
+        else:
+            QUEUE_STATS["shared"] += 1
+            import logging
+            logging.getLogger("arbius_amd.graphs").warning(
+                "task stream %d shares a hardware queue with another task stream", len(live))
+    return cand
+
+
+def live_table(tensors) -> list:
+    """(tensor, address, storage bytes) of every buffer a captured graph reads or writes; the tensors
+    are held by the table, so the caching allocator cannot hand their blocks to anyone else."""
+    return [(t, t.data_ptr(), t.untyped_storage().nbytes()) for t in tensors]
+
+
+def check_live(table) -> None:
+    """Before a replay: every captured buffer is still the tensor it was captured on (same address, same
+    storage size).  A replay into a moved or re-sized block would write another tensor's memory."""
+    for t, ptr, nbytes in table:
+        if t.data_ptr() != ptr or t.untyped_storage().nbytes() != nbytes:
+            raise RuntimeError(f"graph buffer moved: {ptr:#x} -> {t.data_ptr():#x} "
+                               f"({nbytes} -> {t.untyped_storage().nbytes()} bytes)")
+
+
 class GraphedCall:
     def __init__(self, fn: Callable, example_args: Sequence[torch.Tensor], warmup: int = 2):
         dev = example_args[0].device
@@ -67,8 +135,14 @@ class GraphedCall:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"):
                 self.out = fn(*self.inputs)
+        outs = self.out if isinstance(self.out, (tuple, list)) else [self.out]
+        self._live = live_table(list(self.inputs) + [o for o in outs if isinstance(o, torch.Tensor)])
+
+    def check_live(self):
+        check_live(self._live)
 
     def __call__(self, *args):
+        check_live(self._live)
         for dst, src in zip(self.inputs, args):
             if src.data_ptr() != dst.data_ptr():
                 dst.copy_(src)
@@ -114,9 +188,12 @@ class PipelineBase:
         raise NotImplementedError
 
     def fork(self):
+        peers = self.__dict__.setdefault("_fork_streams", [])   # shared by every fork of this pipeline
         c = copy.copy(self)
         c._reset_graphs()
-        c.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        c.stream = task_stream(self.device, peers) if self.device.type == "cuda" else None
+        if c.stream is not None:
+            peers.append(c.stream)
         c.timings = {}
         return c
 

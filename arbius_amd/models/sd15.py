@@ -25,7 +25,7 @@ from .. import ops
 from ..utils.trace import span
 from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
-from .graphs import CAPTURE_LOCK, GraphCache, PipelineBase, capture_stream
+from .graphs import CAPTURE_LOCK, GraphCache, PipelineBase, capture_stream, check_live, live_table
 from .layers import init_weights
 from .schedulers import GroupSampler, TaskSampler, make_scheduler
 from .tokenizer import CLIPTokenizer
@@ -91,8 +91,10 @@ class _GraphedUNet:
         with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"):
             with cross_kv_mode("consume" if self.HOIST else None, self.kv):
                 self.out = unet(self.x, self.t, self.ctx)
+        self._live = live_table([self.x, self.t, self.ctx, self.out] + list(self.kv.values()))
 
     def __call__(self, x, t, ctx):
+        check_live(self._live)
         if x.data_ptr() != self.x.data_ptr():       # the sampler writes the static buffer itself
             self.x.copy_(x)
         self.t.fill_(float(t))
@@ -106,10 +108,11 @@ class _GraphedUNet:
         return self.out
 
 
-# A/B switches (bitwise-equal paths): ARB_VAE_GRAPH=1 replays the VAE decode as a hipGraph per
-# image (measured: the 2-stream bench fell from 26.4k to 19.0k tasks/h with it); ARB_PINNED_D2H=1
-# copies the image to the host through a pinned buffer instead of a pageable ``.cpu()``
-_VAE_GRAPH = os.environ.get("ARB_VAE_GRAPH", "0") == "1"
+# A/B switches (bitwise-equal paths): ARB_VAE_GRAPH=0 runs the VAE decode eagerly instead of as one
+# hipGraph replay per image (r5, 4 x 4 bench on one box: 30,960 graph vs 30,308-30,572 eager; the r4
+# "VAE-graph stall" was two task streams bound to one hardware queue - profiles/graph_serialisation_r5.md);
+# ARB_PINNED_D2H=1 copies the image to the host through a pinned buffer instead of a pageable ``.cpu()``
+_VAE_GRAPH = os.environ.get("ARB_VAE_GRAPH", "1") == "1"
 _PINNED_D2H = os.environ.get("ARB_PINNED_D2H", "0") == "1"
 
 

@@ -16,7 +16,7 @@ import os
 from typing import Callable, Dict, List, Tuple
 
 # bump on ANY change of output bytes (kernels, conv plans, sampler arithmetic, PNG/MP4 encoders)
-NUMERICS_VERSION = "r4.0-bs8-gelu-epilogue-prescaled-attn"
+NUMERICS_VERSION = "r5.0-blockwise-d512-attn-fast-gelu"
 
 # Environment knobs that select a different kernel library, plan table, tiling or reference ops.
 # They exist for A/B measurement only; ``start`` refuses to mine with any of them set.

@@ -102,6 +102,7 @@ def run(args):
     import torch
 
     from arbius_amd import ops
+    from arbius_amd.models import graphs
     from arbius_amd.models.registry import build_pipeline
     from arbius_amd.node.solver import solve_image
     from arbius_amd.parallel import dist as D
@@ -251,6 +252,9 @@ def run(args):
     if marks:
         print(f"[bench] timed t0 monotonic_ns={time.monotonic_ns()} "
               f"boottime_ns={time.clock_gettime_ns(time.CLOCK_BOOTTIME)}", file=sys.stderr, flush=True)
+    if os.environ.get("ARB_DUMP_MAPS"):     # library load addresses: symbolise a native crash stack offline
+        with open("/proc/self/maps") as src, open(os.environ["ARB_DUMP_MAPS"], "w") as dst:
+            dst.write(src.read())
     last = None
     if ex is None:
         for i in range(args.steps):
@@ -340,6 +344,7 @@ def run(args):
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2) if dev.type == "cuda" else None,
             "native_kernels_loaded": ops.native_loaded(),
             "reference_ops": bool(args.reference_ops),
+            "task_stream_queue_check": dict(graphs.QUEUE_STATS),
         }
         print(json.dumps(out), flush=True)
     if ex is not None:

@@ -23,7 +23,7 @@ mode = sys.argv[1] if len(sys.argv) > 1 else "task"
 dev = torch.device("cuda", 0)
 streams, side = [], []
 for i in range(4):
-    streams.append(graphs.task_stream(dev) if mode == "task" else torch.cuda.Stream(device=dev))
+    streams.append(graphs.task_stream(dev, streams) if mode == "task" else torch.cuda.Stream(device=dev))
     if mode != "plain":
         s = torch.cuda.Stream(device=dev)
         with torch.cuda.stream(s):
@@ -41,6 +41,5 @@ del streams, side, s
 gc.collect()
 mark("clear module state")
 graphs._HELD.clear()
-graphs._TASK_STREAMS.clear()
 gc.collect()
 mark("exit")

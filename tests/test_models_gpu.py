@@ -244,3 +244,24 @@ def test_kandinsky2_group_with_mixed_steps_splits(cuda):
     inps = [{"prompt": "cat", "width": 256, "height": 256, "seed": 5, "num_inference_steps": 2},
             {"prompt": "cat", "width": 256, "height": 256, "seed": 6, "num_inference_steps": 3}]
     assert [s.cid for s in solve_images(pipe, inps)] == [pipe.solve(i).cid for i in inps]
+
+
+def test_vae_graph_two_concurrent_forks_bitwise_equal_eager(cuda, monkeypatch):
+    """the VAE decode replayed as a hipGraph on 2 forks solving concurrently from two
+    threads gives the eager CIDs.  Every replay first checks that each captured input and output buffer
+    is still the tensor the graph was captured on (GraphedCall.check_live)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from arbius_amd.models import sd15
+    from arbius_amd.node.solver import solve_image
+    pipe = build_pipeline("anythingv3", device=cuda)
+    inps = [{"prompt": f"harbour {i}", "negative_prompt": "", "width": 256, "height": 256,
+             "num_inference_steps": 3, "guidance_scale": 7.5, "scheduler": "DPMSolverMultistep",
+             "seed": 500 + i} for i in range(2)]
+    eager = [solve_image(pipe, inp).cid for inp in inps]
+    monkeypatch.setattr(sd15, "_VAE_GRAPH", True)
+    forks = [pipe.fork() for _ in range(2)]
+    with ThreadPoolExecutor(2) as ex:
+        for _ in range(3):
+            conc = list(ex.map(lambda a: solve_image(a[0], a[1]).cid, zip(forks, inps)))
+            assert conc == eager
+    assert all(len(f._vae_graph.graphs) == 1 for f in forks)
