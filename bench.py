@@ -248,6 +248,7 @@ def run(args):
     D.barrier(dev)
     sync()
     t0 = time.perf_counter()
+    cpu0 = os.times()          # host CPU seconds of this process (every thread) over the timed region
     marks = os.environ.get("ARB_BENCH_MARKS") == "1"   # timed-region bounds on the trace clocks
     if marks:
         print(f"[bench] timed t0 monotonic_ns={time.monotonic_ns()} "
@@ -282,13 +283,15 @@ def run(args):
     sync()
     D.barrier(dev)
     elapsed = time.perf_counter() - t0
+    cpu1 = os.times()
+    my_cpu_s = (cpu1.user - cpu0.user) + (cpu1.system - cpu0.system)
     if marks:
         print(f"[bench] timed t1 monotonic_ns={time.monotonic_ns()} "
               f"boottime_ns={time.clock_gettime_ns(time.CLOCK_BOOTTIME)}", file=sys.stderr, flush=True)
     my_ms = elapsed * 1000.0 / args.steps
     ms_per_step = D.max_over_ranks(my_ms, dev)
     all_lat = D.all_gather_floats(lat, dev)
-    per_rank = D.all_gather_floats([my_ms, float(len(lat)), float(bstats["bytes"])], dev)
+    per_rank = D.all_gather_floats([my_ms, float(len(lat)), float(bstats["bytes"]), my_cpu_s], dev)
     flat = sorted(x for r in all_lat for x in r)
     p50 = statistics.median(flat) * 1000.0 if flat else float("nan")
 
@@ -334,7 +337,9 @@ def run(args):
             "p50_task_latency_ms": round(p50, 2),
             "per_rank": [{"rank": r, "ms_per_step": round(v[0], 2), "tasks": int(v[1]),
                           "tasks_per_hour": round(per_gpu_tasks * 3600.0 * 1000.0 / v[0], 2),
-                          "weight_broadcast_bytes": int(v[2])} for r, v in enumerate(per_rank)],
+                          "weight_broadcast_bytes": int(v[2]),
+                          "host_cpu_s_per_task": round(v[3] / max(1.0, v[1]), 3),
+                          "host_cores_busy": round(v[3] * 1000.0 / (v[0] * args.steps), 2)} for r, v in enumerate(per_rank)],
             **({"frames_per_second": round(n * C * args.frames * 1000.0 / ms_per_step, 1)} if (rvm or vid) else {}),
             "stage_s": {k: round(v, 4) for k, v in (last.timings.items() if last else [])},
             "weight_broadcast": {"bytes": int(max(v[2] for v in per_rank)), "seconds": round(bstats["seconds"], 4),

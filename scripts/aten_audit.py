@@ -7,6 +7,7 @@ executed) under a TorchDispatchMode that records every ATen op which would launc
 
     python scripts/aten_audit.py sd15 512 4
     python scripts/aten_audit.py kandinsky2 768 4
+    python scripts/aten_audit.py zeroscopev2xl 576 1 24      (width; height = width * 320 / 576)
 """
 import collections
 import os
@@ -58,10 +59,13 @@ def main():
     model = sys.argv[1] if len(sys.argv) > 1 else "sd15"
     size = int(sys.argv[2]) if len(sys.argv) > 2 else 512
     group = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-    fn = {"sd15": audit.sd15, "kandinsky2": audit.kandinsky2}[model]
+    frames = int(sys.argv[4]) if len(sys.argv) > 4 else 24
+    fn = {"sd15": audit.sd15, "kandinsky2": audit.kandinsky2,
+          "zeroscopev2xl": lambda w, h, g: audit.video("zeroscopev2xl", w, h, frames),
+          "damo": lambda w, h, g: audit.video("damo", w, h, frames)}[model]
     rec = _Rec()
     with rec:
-        fn(size, size, group)
+        fn(size, size * 320 // 576 if model == "zeroscopev2xl" else size, group)
     total = sum(rec.hits.values())
     print(f"{model} {size}^2 group {group}: {total} ATen kernel launches outside the HIP ops")
     for (name, where), n in rec.hits.most_common():

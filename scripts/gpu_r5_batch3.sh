@@ -7,7 +7,7 @@ O=gpurun_out/${1:-r5b3}; mkdir -p $O
 export TMPDIR=/tmp
 FAM=${FAM:-arbius_amd/ops/csrc/conv_family.inc}
 echo "== k2 tune $(date +%T)"
-timeout -k 10 800 python -u scripts/tune_family.py $O/f.inc --batch 8 --conc 2 --models kandinsky2 --res 768 --merge $FAM > $O/tune_k2.log 2>&1 || { tail $O/tune_k2.log; exit 1; }
+timeout -k 10 800 python -u scripts/tune_family.py $O/f.inc --batch 8 --conc 2 --models kandinsky2 --res 768 --merge $FAM ${FAMS:+--families $FAMS} > $O/tune_k2.log 2>&1 || { tail $O/tune_k2.log; exit 1; }
 grep -E "re-tuned|-> cfg 4[567]" $O/tune_k2.log | head -20
 i=0
 for v in base tuned base tuned; do
