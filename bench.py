@@ -339,7 +339,8 @@ def run(args):
                           "tasks_per_hour": round(per_gpu_tasks * 3600.0 * 1000.0 / v[0], 2),
                           "weight_broadcast_bytes": int(v[2]),
                           "host_cpu_s_per_task": round(v[3] / max(1.0, v[1]), 3),
-                          "host_cores_busy": round(v[3] * 1000.0 / (v[0] * args.steps), 2)} for r, v in enumerate(per_rank)],
+                          "host_cores_busy": round(v[3] * 1000.0 / (v[0] * args.steps), 2)}
+                         for r, v in enumerate(per_rank)],
             **({"frames_per_second": round(n * C * args.frames * 1000.0 / ms_per_step, 1)} if (rvm or vid) else {}),
             "stage_s": {k: round(v, 4) for k, v in (last.timings.items() if last else [])},
             "weight_broadcast": {"bytes": int(max(v[2] for v in per_rank)), "seconds": round(bstats["seconds"], 4),

@@ -6,6 +6,9 @@ set -o pipefail
 O=gpurun_out/${1:-r5b3}; mkdir -p $O
 export TMPDIR=/tmp
 FAM=${FAM:-arbius_amd/ops/csrc/conv_family.inc}
+echo "== k2 aten sites $(date +%T)"
+timeout -k 10 300 python -u scripts/aten_gpu_sites.py kandinsky2 --steps 20 > $O/aten_sites.jsonl 2> $O/aten_sites.err || { tail -20 $O/aten_sites.err; exit 1; }
+head -12 $O/aten_sites.jsonl | cut -c1-220
 echo "== k2 tune $(date +%T)"
 timeout -k 10 800 python -u scripts/tune_family.py $O/f.inc --batch 8 --conc 2 --models kandinsky2 --res 768 --merge $FAM ${FAMS:+--families $FAMS} > $O/tune_k2.log 2>&1 || { tail $O/tune_k2.log; exit 1; }
 grep -E "re-tuned|-> cfg 4[567]" $O/tune_k2.log | head -20
