@@ -43,6 +43,9 @@ _PINNED_OUT = os.environ.get("ARB_RVM_PINNED_OUT", "1") == "1"
 # largest clip (output bytes) downloaded into one page-locked array: ~100 frames of 1080p; longer clips
 # take the staged path (two reusable pinned chunk buffers + a pageable result)
 _PINNED_OUT_MAX = int(os.environ.get("ARB_RVM_PINNED_OUT_MAX", str(640 << 20)))
+# the solve path downloads GPU-converted 4:2:0 planes instead of RGB (ARB_RVM_GPU_YUV=0: RGB + host
+# conversion, A/B; same bytes)
+_GPU_YUV = os.environ.get("ARB_RVM_GPU_YUV", "1") != "0"
 
 # the input chunk's copy into its pinned staging buffer as a numpy assignment (A/B switch)
 _NUMPY_IN = os.environ.get("ARB_RVM_NUMPY_IN", "1") == "1"
@@ -381,7 +384,7 @@ class RVMPipeline(PipelineBase):
             bufs[key] = b
         return b[:nbytes]
 
-    def _matte_fast(self, frames: np.ndarray, output_type: str, ratio: float) -> np.ndarray:
+    def _matte_fast(self, frames: np.ndarray, output_type: str, ratio: float, yuv: bool = False):
         """HIP fast path (models/rvm_fast.py): uint8 chunks in through pinned double buffers (async
         H2D), uint8 composites out the same way; chunk i+1's upload and chunk i-1's download overlap
         chunk i's kernels.  Bytes are those of the fast path, bitwise, for any chunk timing."""
@@ -390,16 +393,18 @@ class RVMPipeline(PipelineBase):
             self._fast = FastMatting(self.net)
         T, H, W, _ = frames.shape
         n = self.cfg.chunk
-        if _PINNED_OUT and T * H * W * 3 <= _PINNED_OUT_MAX:
+        yuv = yuv and _GPU_YUV
+        nout = T * ((H + 15) // 16 * 16) * ((W + 15) // 16 * 16) * 3 // 2 if yuv else T * H * W * 3
+        if _PINNED_OUT and nout <= _PINNED_OUT_MAX:
             # the page-locked result array comes from PyTorch's caching host allocator,
             # which rounds up and never returns memory to the OS - bounded per clip; a failed pin
             # (host memory exhausted) falls back to the staged download below (same bytes)
             try:
-                res_pin = torch.empty(T * H * W * 3, dtype=torch.uint8, pin_memory=True)
+                res_pin = torch.empty(nout, dtype=torch.uint8, pin_memory=True)
             except RuntimeError:
                 res_pin = None
             if res_pin is not None:
-                return self._matte_fast_pinned(frames, output_type, ratio, res_pin)
+                return self._matte_fast_pinned(frames, output_type, ratio, res_pin, yuv)
         res = np.empty((T, H, W, 3), dtype=np.uint8)
         stream = torch.cuda.current_stream(self.device)
         rec = [None] * 4
@@ -432,11 +437,15 @@ class RVMPipeline(PipelineBase):
             _host_copy(res[sl], v)
         return res
 
-    def _matte_fast_pinned(self, frames: np.ndarray, output_type: str, ratio: float, res) -> np.ndarray:
+    def _matte_fast_pinned(self, frames: np.ndarray, output_type: str, ratio: float, res, yuv: bool = False):
         """As ``_matte_fast``, but every chunk's composite is downloaded straight into one page-locked
         result array (PyTorch's caching host allocator: a freed clip's block is reused), so the
         300 MB host copy out of a staging buffer is gone; the result is that array's numpy view
-        (it keeps the block alive until the encode has read it).  Same bytes."""
+        (it keeps the block alive until the encode has read it).  Same bytes.
+        ``yuv``: each chunk's composite is converted on the GPU to the encoder's macroblock-padded
+        4:2:0 planes (``ops.rgb_to_yuv420``) and those are downloaded instead (1.5 instead of 3 bytes
+        per pixel, no host colour conversion): returns a ``utils.mp4.Yuv420Clip`` that encodes to the
+        RGB path's bytes."""
         from .rvm_fast import FastMatting
         if getattr(self, "_fast", None) is None:
             self._fast = FastMatting(self.net)
@@ -446,6 +455,11 @@ class RVMPipeline(PipelineBase):
         stream = torch.cuda.current_stream(self.device)
         rec = [None] * 4
         ups = []
+        if yuv:
+            H16, W16 = (H + 15) // 16 * 16, (W + 15) // 16 * 16
+            ly, lc = H16 * W16, H16 * W16 // 4
+            planes = (res[:T * ly].view(T, H16, W16), res[T * ly:T * (ly + lc)].view(T, H16 // 2, W16 // 2),
+                      res[T * (ly + lc):T * (ly + 2 * lc)].view(T, H16 // 2, W16 // 2))
         for j, i in enumerate(range(0, T, n)):
             beat()
             t = min(n, T - i)
@@ -461,18 +475,32 @@ class RVMPipeline(PipelineBase):
             ev.record(stream)
             ups.append(ev)
             out, rec = self._fast(dev, rec, ratio, output_type, GREEN)
-            res[i * fb:(i + t) * fb].copy_(out.view(-1), non_blocking=True)
+            if yuv:
+                for dst, src in zip(planes, ops.rgb_to_yuv420(out)):
+                    dst[i:i + t].copy_(src, non_blocking=True)
+            else:
+                res[i * fb:(i + t) * fb].copy_(out.view(-1), non_blocking=True)
         done = torch.cuda.Event()
         done.record(stream)
         done.synchronize()
+        if yuv:
+            from ..utils.mp4 import Yuv420Clip
+            return Yuv420Clip(*(pl.numpy() for pl in planes), W, H, keep=res)
         return res.view(T, H, W, 3).numpy()
 
-    def _matte(self, frames: np.ndarray, output_type: str) -> np.ndarray:
+    @torch.no_grad()
+    def matte_for_encode(self, frames: np.ndarray, output_type: str = "green-screen"):
+        """As ``__call__``, but on the HIP fast path the result is the encoder's 4:2:0 planes, converted
+        on the GPU (``utils.mp4.Yuv420Clip``, the same MP4 bytes); otherwise uint8 RGB frames."""
+        with self._stream_ctx():
+            return self._matte(frames, output_type, yuv=True)
+
+    def _matte(self, frames: np.ndarray, output_type: str, yuv: bool = False):
         t0 = time.perf_counter()
         T, H, W, _ = frames.shape
         ratio = min(1.0, self.cfg.max_side / max(H, W))
         if self._fast_ok(ratio):
-            res = self._matte_fast(frames, output_type, ratio)
+            res = self._matte_fast(frames, output_type, ratio, yuv)
             self.timings = {"matting_s": time.perf_counter() - t0}
             return res
         rec = [None] * 4
@@ -500,7 +528,7 @@ class RVMPipeline(PipelineBase):
         from ..utils.video_io import load_video
         t0 = time.perf_counter()
         frames, fps = load_video(inp["input_video"])
-        out = self(frames, inp.get("output_type") or "green-screen")
+        out = self.matte_for_encode(frames, inp.get("output_type") or "green-screen")
         tm = dict(self.timings)
         tm["infer_s"] = time.perf_counter() - t0
         return out, fps, tm

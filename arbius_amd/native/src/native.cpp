@@ -305,6 +305,51 @@ static py::tuple h264_encode_rgb(py::array_t<uint8_t, py::array::c_style | py::a
 
 using u8arr = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 
+// Macroblock-padded 4:2:0 planes y [F, H16, W16], cb / cr [F, H16 / 2, W16 / 2] of an H x W picture
+// (the GPU's rgb_to_yuv420 output, same samples as rgb_to_420) -> (sps, pps, [IDR NAL per frame]):
+// h264_encode_rgb without the host colour conversion.  Same bytes for the same planes.
+static py::tuple h264_encode_yuv420_frames(u8arr y, u8arr cb, u8arr cr, int W, int H, int qp, int threads,
+                                           int nice) {
+  auto by = y.request(), bcb = cb.request(), bcr = cr.request();
+  const int H16 = (H + 15) / 16 * 16, W16 = (W + 15) / 16 * 16;
+  if (W < 1 || H < 1 || by.ndim != 3 || bcb.ndim != 3 || bcr.ndim != 3 || by.shape[1] != H16 || by.shape[2] != W16 ||
+      bcb.shape[0] != by.shape[0] || bcr.shape[0] != by.shape[0] || bcb.shape[1] != H16 / 2 ||
+      bcb.shape[2] != W16 / 2 || bcr.shape[1] != H16 / 2 || bcr.shape[2] != W16 / 2 || by.shape[0] < 1)
+    throw std::invalid_argument("h264_encode_yuv420_frames: y [F, H16, W16], cb / cr [F, H16/2, W16/2]");
+  const int F = (int)by.shape[0];
+  const uint8_t* py_ = static_cast<const uint8_t*>(by.ptr);
+  const uint8_t* pcb = static_cast<const uint8_t*>(bcb.ptr);
+  const uint8_t* pcr = static_cast<const uint8_t*>(bcr.ptr);
+  const size_t ly = (size_t)H16 * W16, lc = ly / 4;
+  std::vector<std::string> nals(F);
+  std::string sps, pps;
+  h264::parameter_sets(W, H, qp, sps, pps);
+  {
+    py::gil_scoped_release nogil;
+    run_parallel(F, threads, [&](int i) {
+      nals[i] = h264::encode_idr(py_ + i * ly, pcb + i * lc, pcr + i * lc, W16, H16, qp, i, nullptr, nullptr, nullptr);
+    }, nice);
+  }
+  py::list out;
+  for (auto& n : nals) out.append(py::bytes(n));
+  return py::make_tuple(py::bytes(sps), py::bytes(pps), out);
+}
+
+// the host conversion on its own (tests: the GPU planes equal these)
+static py::tuple rgb_to_yuv420_planes(u8arr frames) {
+  auto b = frames.request();
+  if (b.ndim != 4 || b.shape[3] != 3 || b.shape[0] < 1 || b.shape[1] < 1 || b.shape[2] < 1)
+    throw std::invalid_argument("rgb_to_yuv420_planes: frames [F, H, W, 3]");
+  const int F = (int)b.shape[0], H = (int)b.shape[1], W = (int)b.shape[2];
+  const int H16 = (H + 15) / 16 * 16, W16 = (W + 15) / 16 * 16;
+  u8arr y({F, H16, W16}), cb({F, H16 / 2, W16 / 2}), cr({F, H16 / 2, W16 / 2});
+  const uint8_t* src = static_cast<const uint8_t*>(b.ptr);
+  for (int i = 0; i < F; ++i)
+    rgb_to_420(src + (size_t)i * H * W * 3, H, W, H16, W16, y.mutable_data() + (size_t)i * H16 * W16,
+               cb.mutable_data() + (size_t)i * H16 * W16 / 4, cr.mutable_data() + (size_t)i * H16 * W16 / 4);
+  return py::make_tuple(y, cb, cr);
+}
+
 // One picture from 4:2:0 planes -> (IDR NAL, recon Y, recon Cb, recon Cr) (tests: recon == decoder output)
 static py::tuple h264_encode_yuv(u8arr y, u8arr cb, u8arr cr, int qp, int idr_pic_id) {
   auto by = y.request(), bcb = cb.request(), bcr = cr.request();
@@ -558,6 +603,9 @@ PYBIND11_MODULE(_native, m) {
   m.def("png_encode", &png_encode, py::arg("img"), py::arg("level") = 6, "deterministic filter-0 PNG");
   m.def("pcm_slice_body", &pcm_slice_body, py::arg("frame"), py::arg("threads") = 8,
         "H.264 I_PCM macroblock payload of one RGB frame");
+  m.def("h264_encode_yuv420_frames", &h264_encode_yuv420_frames, py::arg("y"), py::arg("cb"), py::arg("cr"),
+        py::arg("width"), py::arg("height"), py::arg("qp"), py::arg("threads") = 8, py::arg("nice") = 0);
+  m.def("rgb_to_yuv420_planes", &rgb_to_yuv420_planes, py::arg("frames"));
   m.def("h264_encode_rgb", &h264_encode_rgb, py::arg("frames"), py::arg("qp"), py::arg("threads") = 8,
         py::arg("nice") = 0, "H.264 CAVLC intra: RGB frames [F, H, W, 3] -> (sps, pps, [IDR NAL]); nice > 0 runs "
         "the encode threads at that lower priority");

@@ -29,7 +29,7 @@ NUMERICS_ENV_KNOBS = (
     # tile-family / layout switches read by the kernel library (bitwise-neutral by test, but their
     # neutrality then rests on a run-time file or an untested combination: refused all the same)
     "ARB_CONV_FAMILY", "ARB_NO_FAMILY", "ARB_DMA_BUF", "ARB_STAG2_PD", "ARB_GN_APPLY2", "ARB_GN_FUSED",
-    "ARB_LN_PACKED", "ARB_ATTN512", "ARB_CAPTURE_SIDE",
+    "ARB_LN_PACKED", "ARB_ATTN512", "ARB_CAPTURE_SIDE", "ARB_QUEUE_CHECK", "ARB_RVM_GPU_YUV",
 )
 
 

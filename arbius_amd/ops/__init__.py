@@ -660,6 +660,16 @@ def native_loaded() -> bool:
     return _lib.loaded()
 
 
+def rgb_to_yuv420(x):
+    """uint8 RGB frames [T, H, W, 3] -> the H.264 encoder's macroblock-padded BT.601 4:2:0 planes
+    (y [T, H16, W16], cb, cr [T, H16 / 2, W16 / 2]).  GPU: one HIP pass; CPU: the native host
+    conversion (the same integer arithmetic, so the same samples)."""
+    if _hip(x):
+        return _lib.rgb_to_yuv420(x)
+    from .. import native
+    return tuple(torch.from_numpy(p) for p in native.rgb_to_yuv420_planes(x.contiguous().numpy()))
+
+
 def image_u8(x, mode: int):
     """Decoded image -> uint8 RGB: mode 0 KL-VAE round(clamp(x / 2 + 0.5, 0, 1) * 255), mode 1 MoVQ
     round(clamp((x + 1) * 127.5, 0, 255)).  GPU bf16: one HIP pass; otherwise the PyTorch chain."""

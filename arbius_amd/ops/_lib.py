@@ -76,6 +76,7 @@ _SIGS = {
     "arb_gemm_ln": (c_int, [c_void_p] * 8 + [c_int] * 7 + [c_void_p]),
     "arb_gemm_act": (c_int, [c_void_p] * 6 + [c_int] * 6 + [c_void_p]),
     "arb_image_u8": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
+    "arb_rgb_to_yuv420": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "arb_attention512": (c_int, [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p, c_void_p]),
     "arb_attention512_workspace": (c_long, [c_int] * 4),
 }
@@ -970,3 +971,25 @@ def image_u8(x, mode: int):
     y = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
     _check(_fn("arb_image_u8")(_p(x), _p(y), x.numel(), int(mode), _stream()), "image_u8")
     return y
+
+
+def rgb_to_yuv420(x, out=None):
+    """uint8 RGB frames [T, H, W, 3] -> macroblock-padded BT.601 4:2:0 planes (y [T, H16, W16], cb, cr
+    [T, H16 / 2, W16 / 2]) (csrc/elementwise.hip rgb_to_yuv420_kernel; the H.264 encoder's input, same
+    samples as native rgb_to_420).  ``out``: optional (y, cb, cr) destination tensors."""
+    if x.dtype != torch.uint8 or x.dim() != 4 or x.shape[-1] != 3:
+        raise ValueError("rgb_to_yuv420: uint8 [T, H, W, 3]")
+    x = x.contiguous()
+    T, H, W, _ = x.shape
+    H16, W16 = (H + 15) // 16 * 16, (W + 15) // 16 * 16
+    if out is None:
+        out = (torch.empty(T, H16, W16, dtype=torch.uint8, device=x.device),
+               torch.empty(T, H16 // 2, W16 // 2, dtype=torch.uint8, device=x.device),
+               torch.empty(T, H16 // 2, W16 // 2, dtype=torch.uint8, device=x.device))
+    y, cb, cr = out
+    if (tuple(y.shape) != (T, H16, W16) or tuple(cb.shape) != (T, H16 // 2, W16 // 2)
+            or tuple(cr.shape) != tuple(cb.shape) or not all(t.is_contiguous() for t in out)):
+        raise ValueError("rgb_to_yuv420: bad destination planes")
+    _check(_fn("arb_rgb_to_yuv420")(_p(x), _p(y), _p(cb), _p(cr), T, H, W, _stream()), "rgb_to_yuv420")
+    return y, cb, cr
+

@@ -334,3 +334,52 @@ ARB_API int arb_image_u8(const void* x, void* y, long n, int mode, hipStream_t s
   image_u8_kernel<<<dim3((unsigned)blocks), 256, 0, stream>>>((const bf16_t*)x, (uint8_t*)y, n, mode);
   return (int)hipGetLastError();
 }
+
+// uint8 RGB frames [T, H, W, 3] -> BT.601 limited-range 4:2:0 planes padded to whole macroblocks:
+// Y [T, H16, W16], Cb / Cr [T, H16 / 2, W16 / 2] - the H.264 encoder's input, so the video tail
+// downloads 1.5 bytes per pixel instead of 3 and the host skips the colour conversion.  Integer
+// arithmetic identical to native/src/native.cpp rgb_to_420 (samples clipped to [1, 254]; rows and
+// columns past the picture replicate the last one; chroma = the 2x2 sum's matrix, >> 10 with
+// rounding), so the encoded bytes are the same.  One thread per chroma sample: its 2x2 luma samples
+// and Cb, Cr.
+__global__ void rgb_to_yuv420_kernel(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ yp,
+                                     uint8_t* __restrict__ cbp, uint8_t* __restrict__ crp, int T, int H, int W,
+                                     int H16, int W16) {
+  const int Wc = W16 / 2, Hc = H16 / 2;
+  const long total = (long)T * Hc * Wc;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % Wc);
+    const long rest = i / Wc;
+    const int r = (int)(rest % Hc), t = (int)(rest / Hc);
+    const uint8_t* f = rgb + (size_t)t * H * W * 3;
+    int sr = 0, sg = 0, sb = 0;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const int yy = 2 * r + dy;
+      const uint8_t* row = f + (size_t)min(yy, H - 1) * W * 3;
+      uint8_t* yo = yp + ((size_t)t * H16 + yy) * W16;
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int xx = 2 * x + dx;
+        const uint8_t* p = row + 3 * min(xx, W - 1);
+        const int R = p[0], G = p[1], B = p[2];
+        yo[xx] = (uint8_t)min(max(((66 * R + 129 * G + 25 * B + 128) >> 8) + 16, 1), 254);
+        sr += R; sg += G; sb += B;
+      }
+    }
+    const size_t co = ((size_t)t * Hc + r) * Wc + x;
+    cbp[co] = (uint8_t)min(max(((-38 * sr - 74 * sg + 112 * sb + 512) >> 10) + 128, 1), 254);
+    crp[co] = (uint8_t)min(max(((112 * sr - 94 * sg - 18 * sb + 512) >> 10) + 128, 1), 254);
+  }
+}
+
+ARB_API int arb_rgb_to_yuv420(const void* rgb, void* y, void* cb, void* cr, int T, int H, int W, hipStream_t stream) {
+  if (T <= 0 || H <= 0 || W <= 0) return -1;
+  const int H16 = (H + 15) / 16 * 16, W16 = (W + 15) / 16 * 16;
+  const long total = (long)T * (H16 / 2) * (W16 / 2);
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  rgb_to_yuv420_kernel<<<dim3((unsigned)blocks), 256, 0, stream>>>((const uint8_t*)rgb, (uint8_t*)y, (uint8_t*)cb,
+                                                                   (uint8_t*)cr, T, H, W, H16, W16);
+  return (int)hipGetLastError();
+}

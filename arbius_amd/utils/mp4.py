@@ -222,12 +222,30 @@ def _moov(width, height, fps, sizes, sps, pps, mdat_offset, pcm=False, sync=None
     return _box(b"moov", mvhd, _box(b"trak", tkhd, mdia))
 
 
+class Yuv420Clip:
+    """A clip already converted to the encoder's input: macroblock-padded BT.601 4:2:0 planes
+    y [F, H16, W16], cb / cr [F, H16 / 2, W16 / 2] of a ``width`` x ``height`` picture - the samples
+    ``rgb_to_yuv420`` / native ``rgb_to_420`` compute from the RGB frames (the GPU converts the video
+    models' output before the download: ``ops.rgb_to_yuv420``).  ``encode_mp4`` of it gives the bytes
+    of ``encode_mp4`` of the RGB frames."""
+    __slots__ = ("y", "cb", "cr", "width", "height", "keep")
+
+    def __init__(self, y: np.ndarray, cb: np.ndarray, cr: np.ndarray, width: int, height: int, keep=None):
+        self.y, self.cb, self.cr, self.width, self.height = y, cb, cr, int(width), int(height)
+        self.keep = keep          # the pinned host block the planes view (kept alive until the encode)
+
+    def __len__(self):
+        return int(self.y.shape[0])
+
+
 def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra", threads: int = 16,
                nice: int = 0) -> bytes:
     """uint8 RGB frames [H, W, 3] (all the same size), or one uint8 array [F, H, W, 3] (passed to
-    the native encoder without a copy) -> MP4 bytes (deterministic).  ``nice`` > 0 runs the intra
-    encode's threads at that lower CPU priority (a background tail next to GPU-feeding threads);
-    bytes never depend on it."""
+    the native encoder without a copy), or a ``Yuv420Clip`` (``avc-intra`` only) -> MP4 bytes
+    (deterministic).  ``nice`` > 0 runs the intra encode's threads at that lower CPU priority (a
+    background tail next to GPU-feeding threads); bytes never depend on it."""
+    if isinstance(frames, Yuv420Clip):
+        return _encode_mp4_yuv(frames, fps, codec, threads, nice)
     if isinstance(frames, np.ndarray) and frames.ndim == 4:
         if frames.dtype != np.uint8 or frames.shape[3] != 3:
             raise ValueError("encode_mp4: frames must be uint8 [F, H, W, 3]")
@@ -263,6 +281,25 @@ def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra",
         else:
             _, _, nals = native.h264_encode_rgb(clip, INTRA_QP, threads, nice)
             pics = [[n] for n in nals]
+    return _mux(W, H, fps, sps, pps, pics, pcm, sync)
+
+
+def _encode_mp4_yuv(clip: "Yuv420Clip", fps: int, codec: str, threads: int, nice: int) -> bytes:
+    if codec != "avc-intra":
+        raise ValueError("encode_mp4: a Yuv420Clip encodes as avc-intra only")
+    if len(clip) < 1:
+        raise ValueError("encode_mp4: no frames")
+    from .. import native
+    if not native.loaded:
+        raise RuntimeError("encode_mp4: the native runtime (H.264 encoder) is not built; "
+                           "run python -m arbius_amd.native.build")
+    W, H = clip.width, clip.height
+    sps, pps = sps_pps(W, H, INTRA_QP)
+    _, _, nals = native.h264_encode_yuv420_frames(clip.y, clip.cb, clip.cr, W, H, INTRA_QP, threads, nice)
+    return _mux(W, H, max(1, int(fps)), sps, pps, [[n] for n in nals], False, None)
+
+
+def _mux(W, H, fps, sps, pps, pics, pcm, sync) -> bytes:
     samples = [b"".join(struct.pack(">I", len(n)) + n for n in p) for p in pics]
     sizes = [len(s) for s in samples]
     ftyp = _box(b"ftyp", b"isom", struct.pack(">I", 512), b"isomiso2avc1mp41")

@@ -180,7 +180,7 @@ def run(args):
             # the node's two-phase solve (node/solver.py infer_task): matting on the slot's stream,
             # then the H.264 encode + CID (RVMPipeline.finish, CPU only) on the slot's tail thread
             # while the stream mattes the next clip
-            out = pipe(clip, "green-screen")
+            out = pipe.matte_for_encode(clip, "green-screen")      # as RVMPipeline.infer
             tm = dict(pipe.timings)
             tm.update({"infer_s": time.perf_counter() - t0})
             raw = (out, 24, tm)

@@ -128,3 +128,37 @@ def test_long_clip_takes_the_staged_download_with_the_same_bytes(cuda, monkeypat
     monkeypatch.setattr(rvm, "_PINNED_OUT_MAX", 0)
     staged = pipe(clip, "green-screen")
     assert np.array_equal(pinned, staged)
+
+
+@pytest.mark.parametrize("T,H,W", [(2, 37, 53), (3, 180, 320), (1, 1080, 1920)])
+def test_gpu_yuv420_equals_host_conversion(cuda, T, H, W):
+    """csrc/elementwise.hip rgb_to_yuv420_kernel == native rgb_to_420 (the encoder's host conversion),
+    padding rows / columns included, sample for sample."""
+    from arbius_amd import native
+    rng = np.random.default_rng(T * H + W)
+    fr = rng.integers(0, 256, (T, H, W, 3), dtype=np.uint8)
+    fr[0, :4] = 0
+    fr[-1, -4:] = 255                                     # the clip range [1, 254] at both ends
+    ref = native.rgb_to_yuv420_planes(fr)
+    got = ops.rgb_to_yuv420(torch.from_numpy(fr).to(cuda))
+    assert ops.native_loaded()
+    for a, b in zip(got, ref):
+        assert tuple(a.shape) == b.shape and np.array_equal(a.cpu().numpy(), b)
+
+
+def test_rvm_solve_path_yuv_planes_encode_to_the_rgb_bytes(cuda, monkeypatch):
+    """The solve path downloads GPU-converted 4:2:0 planes (RVMPipeline.matte_for_encode): the MP4 is
+    byte-identical to encoding the RGB composite, on the pinned and on the staged download."""
+    from arbius_amd.models import rvm
+    from arbius_amd.models.rvm import RVMConfig, RVMPipeline
+    from arbius_amd.utils.mp4 import Yuv420Clip, encode_mp4
+    pipe = RVMPipeline(RVMConfig(chunk=4), device=cuda)
+    rng = np.random.default_rng(9)
+    clip = rng.integers(0, 256, (9, 181, 322, 3), dtype=np.uint8)
+    rgb = pipe(clip, "green-screen")
+    planes = pipe.matte_for_encode(clip, "green-screen")
+    assert isinstance(planes, Yuv420Clip) and len(planes) == 9
+    assert encode_mp4(planes, 24) == encode_mp4(rgb, 24)
+    monkeypatch.setattr(rvm, "_PINNED_OUT_MAX", 0)        # staged download: RGB frames, same bytes
+    staged = pipe.matte_for_encode(clip, "green-screen")
+    assert not isinstance(staged, Yuv420Clip) and encode_mp4(staged, 24) == encode_mp4(rgb, 24)
