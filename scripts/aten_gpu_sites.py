@@ -28,7 +28,8 @@ def main():
 
     from arbius_amd.models.registry import build_pipeline
     dev = torch.device("cuda", 0)
-    pipe = build_pipeline(a.model, device=dev, init=True)
+    # eager: kernels inside a replayed hipGraph carry no ATen op / Python stack to attribute them to
+    pipe = build_pipeline(a.model, device=dev, init=True, use_graphs=False)
     res = a.res or (768 if a.model == "kandinsky2" else 512)
     inp = {"prompt": "a lighthouse on a cliff at dusk", "negative_prompt": "", "width": res, "height": res,
            "num_inference_steps": a.steps, "seed": 7}
@@ -43,7 +44,7 @@ def main():
     for ev in prof.events():
         if ev.device_type.name != "CPU" or not ev.name.startswith("aten::"):
             continue
-        dev_us = sum(k.device_time for k in ev.kernels) if ev.kernels else 0.0
+        dev_us = sum(k.duration for k in ev.kernels) if ev.kernels else 0.0
         if dev_us <= 0:
             continue
         where = "?"
