@@ -46,6 +46,14 @@ _PINNED_OUT_MAX = int(os.environ.get("ARB_RVM_PINNED_OUT_MAX", str(640 << 20)))
 # the solve path downloads GPU-converted 4:2:0 planes instead of RGB (ARB_RVM_GPU_YUV=0: RGB + host
 # conversion, A/B; same bytes)
 _GPU_YUV = os.environ.get("ARB_RVM_GPU_YUV", "1") != "0"
+# the slot thread's waits on its uploads / downloads yield the CPU (hipEventBlockingSync) instead of
+# spinning: RVM is host-bound (profiles/cpu_budget_r5.md) and a spinning wait takes a core from the
+# H.264 encoders of the other slots' tails (ARB_RVM_BLOCKING_SYNC=0: spin, A/B)
+_BLOCKING = os.environ.get("ARB_RVM_BLOCKING_SYNC", "1") != "0"
+
+
+def _event():
+    return torch.cuda.Event(blocking=_BLOCKING)
 
 # the input chunk's copy into its pinned staging buffer as a numpy assignment (A/B switch)
 _NUMPY_IN = os.environ.get("ARB_RVM_NUMPY_IN", "1") == "1"
@@ -419,7 +427,7 @@ class RVMPipeline(PipelineBase):
                 ups[-2].synchronize()     # the staging buffer's previous upload has been consumed
             st.copy_(torch.from_numpy(np.ascontiguousarray(frames[i:i + t]).reshape(-1)))
             dev = st.to(self.device, non_blocking=True).view(t, H, W, 3)
-            ev = torch.cuda.Event()
+            ev = _event()
             ev.record(stream)
             ups.append(ev)
             out, rec = self._fast(dev, rec, ratio, output_type, GREEN)
@@ -429,7 +437,7 @@ class RVMPipeline(PipelineBase):
                 e.synchronize()
                 _host_copy(res[sl], v)
             ob.copy_(out.view(-1), non_blocking=True)
-            e = torch.cuda.Event()
+            e = _event()
             e.record(stream)
             pending.append((e, ob, slice(i, i + t)))
         for e, v, sl in pending:
@@ -471,7 +479,7 @@ class RVMPipeline(PipelineBase):
             else:
                 st.copy_(torch.from_numpy(np.ascontiguousarray(frames[i:i + t]).reshape(-1)))
             dev = st.to(self.device, non_blocking=True).view(t, H, W, 3)
-            ev = torch.cuda.Event()
+            ev = _event()
             ev.record(stream)
             ups.append(ev)
             out, rec = self._fast(dev, rec, ratio, output_type, GREEN)
@@ -480,7 +488,7 @@ class RVMPipeline(PipelineBase):
                     dst[i:i + t].copy_(src, non_blocking=True)
             else:
                 res[i * fb:(i + t) * fb].copy_(out.view(-1), non_blocking=True)
-        done = torch.cuda.Event()
+        done = _event()
         done.record(stream)
         done.synchronize()
         if yuv:
