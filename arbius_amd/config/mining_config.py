@@ -15,7 +15,7 @@ from pydantic import BaseModel, ConfigDict, Field, model_validator
 
 # Task streams per GPU where a model's best differs from ``mi355x.workers_per_gpu`` (bench.py sweeps:
 # profiles/bench_r4_stream_group_sweep.md).
-DEFAULT_MODEL_STREAMS = {"kandinsky2": 2, "zeroscopev2xl": 2, "damo": 2, "robust_video_matting": 2}
+DEFAULT_MODEL_STREAMS = {"kandinsky2": 4, "zeroscopev2xl": 2, "damo": 2, "robust_video_matting": 2}
 
 
 class _Base(BaseModel):
@@ -103,8 +103,10 @@ class MI355XConfig(_Base):
     selftest_table: Optional[str] = None  # override of config/selftest.json
     workers_per_gpu: int = 4              # concurrent task streams per GPU (pipeline forks): the benched
                                           # SD1.5 default (bench.py --concurrent 4); 1 = latency mode
-    # per-model cap on those streams (measured: Kandinsky2 7.2k tasks/h at 2 streams x groups of 4,
-    # 6.6k at 3, 5.9k at 4 x 2; the video UNet's activations fill the GPU at 2)
+    # per-model cap on those streams.  Kandinsky2, measured on one box with every task stream on its own
+    # hardware queue (profiles/sweep_r5.md): 7,236 tasks/h at 2 streams x groups of 4, 7,468 at 3 x 4,
+    # 7,591 at 4 x 4, 6,264 at 4 x 2.  Round 4's 3- and 4-stream losses came from task streams sharing a
+    # queue.  The video UNet's activations fill the GPU at 2 streams (zeroscope 3 streams: 1,129).
     model_streams: Dict[str, int] = Field(default_factory=lambda: dict(DEFAULT_MODEL_STREAMS))
     # IPFS gateway (http(s) base URL) for the input of a task whose transaction is not a plain
     # submitTask call (submitted through a contract): the bytes are fetched by the

@@ -33,7 +33,7 @@ from ..utils.png import encode_png
 from ..utils.progress import beat
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .glide_unet import GlideUNet, GlideUNetConfig
-from .graphs import GraphCache, PipelineBase
+from .graphs import GraphCache, PipelineBase, task_stream
 from .layers import Linear, init_weights
 from .movq import MoVQConfig, MoVQDecoder
 from .prior import PriorConfig, PriorTransformer
@@ -73,6 +73,9 @@ class _Buffers(nn.Module):
 # Each diffusion-prior step replays as a hipGraph (bitwise equal to eager; +1.3 % on the 2-stream
 # bench, no stream serialisation: profiles/ab_r4_k2.md).  ARB_PRIOR_GRAPH=0 = eager (A/B only).
 _PRIOR_GRAPH = os.environ.get("ARB_PRIOR_GRAPH", "1") == "1"
+# ARB_K2_SPLIT_CFG=1: a solo task's cond / uncond UNet rows run as two overlapping batch-1 graph replays
+# on two hardware queues (latency mode; bitwise the batch-2 bytes by test)
+_SPLIT_CFG = os.environ.get("ARB_K2_SPLIT_CFG", "0") == "1"
 
 
 class Kandinsky2Pipeline(PipelineBase):
@@ -104,6 +107,9 @@ class Kandinsky2Pipeline(PipelineBase):
         self._prior_graph = GraphCache(self._prior_step, self.use_graphs)
         # A/B switch (bitwise-equal paths, tests/test_models_gpu.py): replay each prior step as a hipGraph
         self.prior_graph = _PRIOR_GRAPH
+        # latency mode: a solo task's cond / uncond UNet rows on two hardware queues (_unet_split)
+        self.split_cfg = _SPLIT_CFG
+        self._split = None
         self.timings: Dict[str, float] = {}
 
     def _prior_step(self, xin, tt, hidden, pooled, idx, q):
@@ -112,6 +118,7 @@ class Kandinsky2Pipeline(PipelineBase):
     def _reset_graphs(self):
         self._unet = GraphCache(self.unet, self.use_graphs)
         self._prior_graph = GraphCache(self._prior_step, self.use_graphs)
+        self._split = None
 
     def modules(self) -> Dict[str, nn.Module]:
         return {"unet": self.unet, "movq": self.movq, "prior": self.prior, "clip": self.clip,
@@ -188,6 +195,33 @@ class Kandinsky2Pipeline(PipelineBase):
         std, mean = self._prior_stats()
         return torch.stack([(ts.x.view(d) * std + mean) for ts in tasks]).to(self.dtype)
 
+    def _split_ok(self) -> bool:
+        return self.split_cfg and self.use_graphs and self.device.type == "cuda"
+
+    def _unet_split(self, xin, tbuf, text_full, text_pooled, img_embs):
+        """Latency mode of a solo task: the cond row's UNet on the calling stream and the uncond row's on
+        a second task stream (its own hardware queue, ``graphs.task_stream``), as two batch-1 graph
+        replays that overlap, joined before the sampler step.  Batch-1 launches under plan_batch(1)
+        plan at the same canonical batch as the batch-2 solo launch and every UNet op is row-local, so
+        each row's bytes are the batch-2 row's (tests/test_models_gpu.py)."""
+        dev = self.device
+        cur = torch.cuda.current_stream(dev)
+        if self._split is None:
+            peers = [cur] if cur != torch.cuda.default_stream(dev) else []
+            self._split = (task_stream(dev, peers), GraphCache(self.unet, True), GraphCache(self.unet, True),
+                           torch.cuda.Event(), torch.cuda.Event())
+        s2, una, unb, ev_in, ev_b = self._split
+        ev_in.record(cur)
+        with torch.cuda.stream(s2):
+            s2.wait_event(ev_in)
+            with ops.plan_batch(1):
+                ob = unb(xin[1:2], tbuf, text_full[1:2], text_pooled[1:2], img_embs[1:2])
+            ev_b.record(s2)
+        with ops.plan_batch(1):
+            oa = una(xin[0:1], tbuf, text_full[0:1], text_pooled[0:1], img_embs[0:1])
+        cur.wait_event(ev_b)
+        return torch.cat([oa, ob])
+
     def _group_sampler(self, tasks, h, w, guidance: List[float]):
         """k decoder tasks on one batch-2k GLIDE UNet input: rows 2k / 2k+1 = (cond, uncond); the
         cond row's channels 4..7 are the learned variance of p_sample."""
@@ -263,11 +297,15 @@ class Kandinsky2Pipeline(PipelineBase):
             t1 = time.perf_counter()
             samp = self._group_sampler(tasks, h, w, [s["guidance"] for s in st])
             tbuf = torch.zeros(1, dtype=torch.float32, device=self.device)
+            split = k == 1 and self._split_ok()
             for i, t in enumerate(tasks[0].sched.timesteps):
                 beat()
                 tbuf.fill_(float(t))
-                with ops.plan_batch(2):      # batch-invariant plans: solo == lock-step group bytes
-                    out = self._unet(samp.xin, tbuf, text_full, text_pooled, img_embs)
+                if split:
+                    out = self._unet_split(samp.xin, tbuf, text_full, text_pooled, img_embs)
+                else:
+                    with ops.plan_batch(2):      # batch-invariant plans: solo == lock-step group bytes
+                        out = self._unet(samp.xin, tbuf, text_full, text_pooled, img_embs)
                 samp.step(i, out)            # ONE fused CFG + sampler launch for the group
             sync()
             t2 = time.perf_counter()

@@ -265,3 +265,17 @@ def test_vae_graph_two_concurrent_forks_bitwise_equal_eager(cuda, monkeypatch):
             conc = list(ex.map(lambda a: solve_image(a[0], a[1]).cid, zip(forks, inps)))
             assert conc == eager
     assert all(len(f._vae_graph.graphs) == 1 for f in forks)
+
+
+def test_kandinsky2_split_cfg_latency_mode_bitwise_equals_batch2(cuda):
+    """Latency mode: a solo task's cond / uncond UNet rows as two batch-1 graph replays on two hardware
+    queues give exactly the batch-2 solo bytes (and so the lock-step group's)."""
+    pipe = build_pipeline("kandinsky2", device=cuda)
+    pipe.cfg.num_steps = 4
+    inps = [{"prompt": "a red fox in snow", "width": 768, "height": 768, "seed": 21},
+            {"prompt": "harbour at night", "width": 512, "height": 512, "seed": 22}]
+    pipe.split_cfg = False
+    ref = [pipe.solve(i).cid for i in inps]
+    pipe.split_cfg = True
+    assert [pipe.solve(i).cid for i in inps] == ref
+    assert pipe._split is not None
