@@ -23,7 +23,7 @@ class _Model:
 def test_defaults():
     cfg = MI355XConfig()
     assert cfg.workers_per_gpu == 4
-    assert cfg.model_streams == DEFAULT_MODEL_STREAMS and cfg.model_streams["kandinsky2"] == 2
+    assert cfg.model_streams == DEFAULT_MODEL_STREAMS and cfg.model_streams["kandinsky2"] == 4
     assert MI355XConfig(model_streams={"kandinsky2": 3}).model_streams == {"kandinsky2": 3}
 
 
