@@ -37,6 +37,7 @@ _SIGS = {
     "arb_upsample2": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "arb_conv2d_nhwc": (c_int, [c_void_p] * 8 + [c_int] * 12 + [c_void_p]),
     "arb_set_gn_table_lds": (None, [c_int]),
+    "arb_set_gn_tail": (None, [c_int]),
     "arb_set_attn_prescale": (None, [c_int]),
     "arb_set_stag2_pd": (None, [c_int]),
     "arb_set_stag2_buf": (None, [c_int]),

@@ -15,6 +15,12 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
+// n zero-initialised int tickets for one launch on stream s (conv.hip's per-device pool): a region
+// of its own per graph-captured launch, one shared region per stream for eager launches (same-
+// stream kernels are serialised).  The launch's last arriving block re-arms its ticket to 0.
+// nullptr: no pool (e.g. the first use is inside a capture) - the caller takes its two-kernel path.
+int* arb_tickets(hipStream_t s, int n);
+
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }

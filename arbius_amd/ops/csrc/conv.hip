@@ -2050,6 +2050,8 @@ static int* split_counters(hipStream_t s, int tiles) {
   return r;
 }
 
+int* arb_tickets(hipStream_t s, int n) { return split_counters(s, n); }
+
 static bool splitk_inlaunch() {
   static const bool on = [] {
     const char* e = std::getenv("ARB_SPLITK_INLAUNCH");

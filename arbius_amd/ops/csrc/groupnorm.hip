@@ -38,6 +38,19 @@ __device__ __forceinline__ Stat chan_combine(Stat a, Stat b) {
   return r;
 }
 
+#define GN_TAIL_GPB 4
+#define GN_TAIL_MAXG 32
+struct GnTail {
+  int* tickets;            // [B], zero on entry; null = partials only (separate table kernel)
+  float2* table;
+  const bf16_t* gamma;
+  const bf16_t* beta;
+  const bf16_t* mod;
+  float one_plus, eps;
+};
+
+__device__ void gn_tail(const Stat* __restrict__ part, const GnTail& tl, int b, int chunks, int C, int G);
+
 // Stats partition, a function of (HW, C) only - so the reduction order never depends on the
 // batch (lock-step groups stay bitwise equal to solo tasks).  Large images (>= 1M elements per
 // image): slabs of 8 rows per thread (16 x 16-B loads in flight with the next slab's), up to
@@ -51,9 +64,10 @@ __host__ __device__ inline int gn_iters(int HW, int C) { return 1; }
 
 // Thread geometry: NV = C/8 channel vectors.  NV < 256: k = 256/NV row lanes, thread
 // (v = t % NV, rl = t / NV).  NV >= 256: one row lane, thread owns vectors t, t+256 (VPT).
-template <int VPT, int GN_SRPT>
+template <int VPT, int GN_SRPT, bool TAIL = false>
 __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict__ x, Stat* __restrict__ part,
-                                                       int HW, int C, int G, const bf16_t* __restrict__ x2, int C1) {
+                                                       int HW, int C, int G, const bf16_t* __restrict__ x2, int C1,
+                                                       GnTail tl) {
   const int chunk = blockIdx.x, b = blockIdx.y, chunks = gridDim.x;
   const int NV = C >> 3;
   const int k = NV >= 256 ? 1 : 256 / NV;
@@ -191,6 +205,7 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
     Stat st = {N, mu, m2, 0.f};
     part[((size_t)b * chunks + chunk) * G + g] = st;
   }
+  if constexpr (TAIL) gn_tail(part, tl, b, chunks, C, G);
 }
 
 __global__ void __launch_bounds__(256) gn_finalize_kernel(const Stat* __restrict__ part, float2* __restrict__ stats,
@@ -302,17 +317,21 @@ static int gn_stat_chunks(int HW, int C) {
 }
 
 static void launch_gn_stats(const void* x, Stat* part, int B, int HW, int C, int G, hipStream_t stream,
-                            const void* x2 = nullptr, int C1 = 0) {
+                            const void* x2 = nullptr, int C1 = 0, GnTail tl = GnTail{}) {
   dim3 grid(gn_stat_chunks(HW, C), B);
   const bool wide = C / 8 > 256, big = gn_srpt(HW, C) == 8;
   const bf16_t* xb = (const bf16_t*)x;
   const bf16_t* xb2 = (const bf16_t*)x2;
+  const bool tail = tl.tickets != nullptr;
   if (wide) {
-    if (big) gn_stats_kernel<2, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1);
-    else gn_stats_kernel<2, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1);
+    if (big) gn_stats_kernel<2, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1, tl);
+    else if (tail) gn_stats_kernel<2, 4, true><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1, tl);
+    else gn_stats_kernel<2, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1, tl);
   } else {
-    if (big) gn_stats_kernel<1, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1);
-    else gn_stats_kernel<1, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1);
+    if (big && tail) gn_stats_kernel<1, 8, true><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1, tl);
+    else if (big) gn_stats_kernel<1, 8><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1, tl);
+    else if (tail) gn_stats_kernel<1, 4, true><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1, tl);
+    else gn_stats_kernel<1, 4><<<grid, 256, 0, stream>>>(xb, part, HW, C, G, xb2, C1, tl);
   }
 }
 
@@ -521,19 +540,23 @@ __global__ void __launch_bounds__(256) gn_table_kernel(const Stat* __restrict__ 
 // t, t+256, ...); levels 128 and 64 combine in-lane, levels 32..1 through __shfl_down (node t takes node
 // t+s) - with no LDS round trips and no block barriers (the 256-thread version was launch/latency bound:
 // 6 us per call, 2 % of the SD1.5 bench's kernel time).
-__global__ void __launch_bounds__(64) gn_table_wave_kernel(const Stat* __restrict__ part, float2* __restrict__ table,
-                                                           const bf16_t* __restrict__ gamma,
-                                                           const bf16_t* __restrict__ beta,
-                                                           const bf16_t* __restrict__ mod, float one_plus,
-                                                           int chunks, int C, int G, float eps) {
-  const int g = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
-  Stat leaf[4];
+// Tree leaves of lane l for group g of image b: leaf q = the sequential Chan combine of chunks l + 64q,
+// l + 64q + 256, ...
+__device__ __forceinline__ void gn_table_leaves(const Stat* __restrict__ part, int b, int chunks, int G, int g, int l,
+                                                Stat (&leaf)[4]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     Stat acc = {0.f, 0.f, 0.f, 0.f};
     for (int c = l + 64 * q; c < chunks; c += 256) acc = chan_combine(acc, part[((size_t)b * chunks + c) * G + g]);
     leaf[q] = acc;
   }
+}
+
+// The rest of the one-wave table: combine tree over the 4 x 64 leaves, then the group's Cg table entries.
+__device__ __forceinline__ void gn_table_tree(Stat (&leaf)[4], float2* __restrict__ table,
+                                              const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
+                                              const bf16_t* __restrict__ mod, float one_plus, int C, int G, float eps,
+                                              int g, int b, int l) {
   // level 128: t <- (t, t + 128) for t < 128  (t = l: leaf 0 with leaf 2; t = l + 64: leaf 1 with leaf 3)
   Stat n0 = chan_combine(leaf[0], leaf[2]);
   const Stat n1 = chan_combine(leaf[1], leaf[3]);
@@ -564,6 +587,73 @@ __global__ void __launch_bounds__(64) gn_table_wave_kernel(const Stat* __restric
   }
 }
 
+__global__ void __launch_bounds__(64) gn_table_wave_kernel(const Stat* __restrict__ part, float2* __restrict__ table,
+                                                           const bf16_t* __restrict__ gamma,
+                                                           const bf16_t* __restrict__ beta,
+                                                           const bf16_t* __restrict__ mod, float one_plus,
+                                                           int chunks, int C, int G, float eps) {
+  const int g = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
+  Stat leaf[4];
+  gn_table_leaves(part, b, chunks, G, g, l, leaf);
+  gn_table_tree(leaf, table, gamma, beta, mod, one_plus, C, G, eps, g, b, l);
+}
+
+// Statistics + table in ONE launch, bitwise equal to gn_stats + gn_table_wave: the stats blocks of
+// image b take a ticket after their partials are stored (agent-scope release before it); the block
+// that draws the last one (acquire) runs gn_table_wave's arithmetic for every group of the image,
+// wave w taking groups w, w + 4, ... with the leaf loads of GPB groups in flight together, then
+// re-arms the ticket.  Saves the table launch and its cross-XCD partials round trip (K2 solo: ~96
+// GroupNorms per UNet step).  G <= GN_TAIL_MAXG (4 waves x 2 batches of GPB).  Not on the wide
+// big-image variant (C > 2048 at >= 1M elements per image): there the tail's registers spill.
+__device__ void gn_tail(const Stat* __restrict__ part, const GnTail& tl, int b, int chunks, int C,
+                                        int G) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this block's partials are stored
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int t = __hip_atomic_fetch_add(&tl.tickets[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == chunks - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __syncthreads();
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int i0 = 0; i0 < GN_TAIL_MAXG / 4; i0 += GN_TAIL_GPB) {
+    Stat leaf[GN_TAIL_GPB][4];
+    if (chunks <= 256) {   // one partial per leaf at most: every load of the batch in flight at once
+      Stat raw[GN_TAIL_GPB][4];
+#pragma unroll
+      for (int i = 0; i < GN_TAIL_GPB; ++i) {
+        const int g = w + 4 * (i0 + i);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = l + 64 * q;
+          raw[i][q] = (g < G && c < chunks) ? part[((size_t)b * chunks + c) * G + g] : Stat{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < GN_TAIL_GPB; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) leaf[i][q] = chan_combine(Stat{0.f, 0.f, 0.f, 0.f}, raw[i][q]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < GN_TAIL_GPB; ++i) {
+        const int g = w + 4 * (i0 + i);
+        if (g < G) gn_table_leaves(part, b, chunks, G, g, l, leaf[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GN_TAIL_GPB; ++i) {
+      const int g = w + 4 * (i0 + i);
+      if (g < G) gn_table_tree(leaf[i], tl.table, tl.gamma, tl.beta, tl.mod, tl.one_plus, C, G, tl.eps, g, b, l);
+    }
+  }
+  if (threadIdx.x == 0) tl.tickets[b] = 0;   // re-arm for the next launch on this region
+}
+
 // A/B switch (bitwise-equal variants): ARB_GN_TABLE_LDS=1 or arb_set_gn_table_lds(1) -> the 256-thread
 // LDS-tree table kernel instead of the one-wave one (tests/test_kernels_gpu.py compares the two).
 static int g_gn_table_lds = -1;
@@ -579,6 +669,20 @@ ARB_API void arb_set_gn_table_lds(int on) { g_gn_table_lds = on ? 1 : 0; }
 static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma, const void* beta, const void* mod,
                         float one_plus, void* workspace, void* table, int B, int HW, int C, int G, float eps,
                         hipStream_t stream);
+
+// Opt-in (ARB_GN_TAIL=1 or arb_set_gn_tail(1)); bitwise equal to the two launches either way.
+// Measured slower everywhere (round 5, same box: SD 4x4 31.0k -> 28.1k tasks/h, K2 solo 1.09 ->
+// 1.26 s): every stats block's agent-scope release before its ticket is an L2 write-back on
+// MI355X, which costs far more than the table launch it saves (profiles/k2_plan_r5.md).
+static int g_gn_tail = -1;
+static bool gn_tail_on() {
+  if (g_gn_tail < 0) {
+    const char* e = std::getenv("ARB_GN_TAIL");
+    g_gn_tail = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return g_gn_tail == 1;
+}
+ARB_API void arb_set_gn_tail(int on) { g_gn_tail = on ? 1 : 0; }
 
 // ---------------------------------------------------------------------------------------------
 // Small images (HW * C <= GN_FUSED_MAX, the deep UNet levels): statistics AND table in ONE launch.
@@ -744,6 +848,15 @@ static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma
   }
   const int chunks = gn_stat_chunks(HW, C);
   Stat* part = (Stat*)workspace;
+  if (gn_tail_on() && !gn_table_lds() && G <= GN_TAIL_MAXG && (gn_srpt(HW, C) == 4 || C / 8 <= 256)) {
+    int* tickets = arb_tickets(stream, B);
+    if (tickets != nullptr) {   // statistics + table in one launch (bitwise equal)
+      launch_gn_stats(x, part, B, HW, C, G, stream, x2, C1,
+                      GnTail{tickets, (float2*)table, (const bf16_t*)gamma, (const bf16_t*)beta, (const bf16_t*)mod,
+                             one_plus, eps});
+      return (int)hipGetLastError();
+    }
+  }
   launch_gn_stats(x, part, B, HW, C, G, stream, x2, C1);
   if (gn_table_lds())
     gn_table_kernel<<<dim3(G, B), 256, 0, stream>>>(part, (float2*)table, (const bf16_t*)gamma, (const bf16_t*)beta,

@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Split-K study for one model's UNet launches: solo (batch 2) vs lock-step group (batch 8).
+
+Consensus pins only the split-K of each canonical (batch-8) plan; at that split every tile family is
+bitwise interchangeable, so a solo task runs the family tuned for its own (4x smaller) shape.  Under
+the throughput-tuned splits the deep UNet levels of a solo Kandinsky2 task launch far fewer
+workgroups than the chip has CUs (e.g. 1152 x 1152 x 10368 on 64 x 64 tiles: 324 workgroups,
+L2-bandwidth bound).  This script times, for every planned conv / GEMM of the model's UNet step
+whose solo row count is at most --max-m, the best tile family at every split-K:
+
+  * solo: batch 2, one stream, hipGraph-replayed;
+  * group: batch 8 with --conc concurrent copies (the deployed task streams), per call of the
+    aggregate;
+
+plus the deployed choice of both.  One JSON line per shape (``--out``), so a re-plan can trade the
+solo latency against the group throughput per shape (scripts/split_plan.py).
+
+    python scripts/split_study.py --model kandinsky2 --out gpurun_out/split/k2.jsonl
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from collections import Counter
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import autotune_conv as at  # noqa: E402
+from arbius_amd.ops import _lib, audit  # noqa: E402
+
+SPLITS = (1, 2, 3, 4, 6, 8)
+SMALL = list(range(20))                                 # 4-wave LDS-DMA (0-9) and register-staged (10-19)
+BIG = [20, 21, 22, 23, 28, 29, 30, 31, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45]
+
+
+def _tile(cfg):
+    if cfg >= 36:
+        return at.KSTAG[cfg - 36] if cfg - 36 < len(at.KSTAG) else (192, 192)
+    if cfg >= 32:
+        return at.KXREG[cfg - 32]
+    if cfg >= 28:
+        return at.KDEEP[cfg - 28]
+    if cfg >= 24:
+        return at.KPERSIST[cfg - 24]
+    if cfg >= 20:
+        return at.KBIG[cfg - 20]
+    return at.KCFG[cfg % 10]
+
+
+def launches(model):
+    if model == "kandinsky2":
+        solo, grp = audit.kandinsky2(768, 768, 1), audit.kandinsky2(768, 768, 4)
+    else:
+        solo, grp = audit.sd15(512, 512, 1), audit.sd15(512, 512, 4)
+    out = Counter()
+    for x, y in zip(audit.launches(solo), audit.launches(grp)):
+        if not x.get("plan_b") or x["M"] == y["M"]:
+            continue       # unplanned (VAE / MoVQ / text) or group-independent launches
+        key = (x["kind"], x.get("shape"), x["M"], x["N"], x["K"], x["cfg"], x["split"], y.get("shape"), y["M"],
+               y["cfg"])
+        out[key] += 1
+    return out
+
+
+def make_run(kind, shape, M, N, K, dev):
+    """(run(cfg, split) -> output, reference output) for one launch at its own batch."""
+    if kind == "conv":
+        B, H, W, C, Co, kc, pad, up, st = shape
+        kh, kw = (3, 1) if kc == 31 else (kc, kc)
+        x = torch.randn(B, H, W, C, device=dev).bfloat16()
+        w = (torch.randn(Co, kh, kw, C, device=dev) / math.sqrt(kh * kw * C)).bfloat16()
+        b = torch.randn(Co, device=dev).bfloat16()
+        return lambda c, s: _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st, c, s)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=dev).bfloat16()
+    return lambda c, s: _lib.gemm(x, w, b, None, c, s)
+
+
+def sweep(run, M, N, K, cfgs, conc, deployed):
+    at.CONC = conc
+    ref = run(*deployed)
+    t_dep = at.graph_time(lambda: run(*deployed))
+    best = {}
+    ktiles = K // 64
+    for sp in SPLITS:
+        if sp > 1 and sp > ktiles // 2:
+            continue
+        for c in cfgs:
+            bn, bm = _tile(c)
+            if c >= 20 and bn > N + N // 2:
+                continue
+            if 24 <= c < 28 and sp > 1:
+                continue
+            try:
+                if not at._agrees(run(c, sp), ref):
+                    continue
+                t = at.graph_time(lambda: run(c, sp))
+            except Exception:  # noqa: BLE001 - a config the shape does not support
+                continue
+            if sp not in best or t < best[sp][0]:
+                best[sp] = (round(t, 2), c)
+    return round(t_dep, 2), {sp: v for sp, v in sorted(best.items())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="kandinsky2")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--max-m", type=int, default=4608, help="solo row count limit (deep levels)")
+    ap.add_argument("--conc", type=int, default=4, help="concurrent copies for the batch-8 timing")
+    a = ap.parse_args()
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    dev = torch.device("cuda")
+    todo = [(k, n) for k, n in launches(a.model).items() if k[2] <= a.max_m]
+    todo.sort(key=lambda kn: -kn[0][2] * kn[0][3] * kn[0][4] * kn[1])
+    print(f"{len(todo)} launches", flush=True)
+    with open(a.out, "w") as f:
+        for (kind, sshape, M, N, K, scfg, ssplit, gshape, GM, gcfg), n in todo:
+            t0 = time.time()
+            rs = make_run(kind, sshape, M, N, K, dev)
+            solo_dep, solo = sweep(rs, M, N, K, SMALL + BIG, 1, (scfg, ssplit))
+            del rs
+            rg = make_run(kind, gshape, GM, N, K, dev)
+            grp_dep, grp = sweep(rg, GM, N, K, BIG + [0, 3, 5, 7, 8, 13], a.conc, (gcfg, ssplit))
+            del rg
+            torch.cuda.empty_cache()
+            rec = {"kind": kind, "solo_shape": sshape, "group_shape": gshape, "MNK": [M, N, K], "GM": GM,
+                   "calls": n, "split": ssplit, "solo_cfg": scfg, "group_cfg": gcfg, "solo_dep_us": solo_dep,
+                   "group_dep_us": grp_dep, "solo_best": solo, "group_best": grp, "sec": round(time.time() - t0, 1)}
+            f.write(json.dumps(rec) + "\n")
+            f.flush()
+            print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

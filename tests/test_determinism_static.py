@@ -2,8 +2,10 @@
 
 A solution CID is consensus, so no floating-point reduction may depend on arrival order: every
 kernel reduces in a fixed order (LDS trees, xor butterflies, ordered split-K slabs).  The one
-atomic in the kernel library is the integer split-K TICKET (which block of a tile reduces the
-slabs - the reduction itself still walks slabs 0..S-1 in order); anything else fails here.
+atomics in the kernel library are integer TICKETS: the split-K ticket (which block of a tile reduces
+the slabs - the reduction itself still walks slabs 0..S-1 in order) and the GroupNorm stats ticket
+(which block of an image builds the table - from the partials in the fixed tree order of the table
+kernel); anything else fails here.
 """
 import os
 import re
@@ -11,7 +13,8 @@ import re
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "arbius_amd", "ops", "csrc")
 ATOMIC = re.compile(r"\b(atomicAdd|atomicCAS|atomicExch|atomicMax|atomicMin|unsafeAtomicAdd|__hip_atomic_\w+|"
                     r"global_atomic_\w+|buffer_atomic_\w+|ds_add_\w+|__atomic_\w+)\b")
-ALLOWED = {("conv.hip", "__hip_atomic_fetch_add")}      # integer split-K ticket, ordered slab reduce
+ALLOWED = {("conv.hip", "__hip_atomic_fetch_add"),      # integer split-K ticket, ordered slab reduce
+           ("groupnorm.hip", "__hip_atomic_fetch_add")}  # integer stats ticket, fixed-tree table
 
 
 def _code_lines(path):
@@ -38,3 +41,11 @@ def test_split_k_ticket_is_integer_and_reduction_is_ordered():
     assert len(calls) == 1 and "counters" in calls[0]            # int* ticket pool, never a float slab
     # the reducer sums slabs sp = 1 .. nsplit-1 in index order onto slab 0
     assert re.search(r"for \(int sp = 1; sp < p\.nsplit; \+\+sp\)", src)
+
+
+def test_group_norm_ticket_is_integer_and_table_tree_is_shared():
+    src = open(os.path.join(CSRC, "groupnorm.hip")).read()
+    calls = re.findall(r"__hip_atomic_fetch_add\(([^;]*)\);", src)
+    assert len(calls) == 1 and "tickets" in calls[0]             # int* ticket per image
+    # the last block builds the table with the table kernel's own tree (one definition, two callers)
+    assert src.count("gn_table_tree(") == 3                        # definition + wave kernel + fused tail

@@ -678,6 +678,41 @@ def test_group_norm_table_wave_kernel_bitwise_equals_lds_tree(cuda, B, HW, C, G,
     assert _rel(t_wave, r) < 1e-4
 
 
+@pytest.mark.parametrize("B,HW,C,G,mod,cat", [(2, 576, 1152, 32, True, False), (2, 144, 1536, 32, False, False),
+                                              (8, 144, 3072, 32, False, True), (2, 2304, 384, 32, True, False),
+                                              (8, 256, 1280, 32, False, False), (8, 64, 2560, 32, False, True),
+                                              (3, 100, 64, 4, False, False), (1, 48, 512, 8, True, False),
+                                              (8, 4096, 320, 32, False, False), (2, 9216, 384, 32, True, False),
+                                              (8, 1024, 1280, 32, False, True)])
+def test_group_norm_fused_tail_bitwise_equals_two_launches(cuda, B, HW, C, G, mod, cat):
+    """Statistics + table in one launch (the image's last stats block builds the table after a ticket)
+    == the stats kernel followed by the one-wave table kernel, bit for bit - also when the input is a
+    skip concat read in place - and every ticket is re-armed (a second call gives the same table)."""
+    torch.manual_seed(16)
+    x = (torch.randn(B, HW, C, device=cuda) * 2 + 0.7).bfloat16()
+    g = (torch.rand(C, device=cuda) + 0.5).bfloat16()
+    bt = torch.randn(C, device=cuda).bfloat16()
+    m = torch.randn(B, 2 * C, device=cuda).bfloat16() if mod else None
+    op = 1.0 if mod else 0.0
+    x2 = None
+    if cat:
+        x, x2 = x[..., :C // 2].contiguous(), x[..., C // 2:].contiguous()
+    fn = _lib._fn("arb_set_gn_tail")
+    try:
+        fn(0)
+        t_two = _lib.group_norm_table(x, g, bt, G, 1e-5, m, op, x2=x2)
+        fn(1)
+        t_one = _lib.group_norm_table(x, g, bt, G, 1e-5, m, op, x2=x2)
+        t_again = _lib.group_norm_table(x, g, bt, G, 1e-5, m, op, x2=x2)
+    finally:
+        fn(0)
+    assert torch.equal(t_one, t_two)
+    assert torch.equal(t_again, t_two)
+    xf = x.float() if x2 is None else torch.cat([x, x2], -1).float()
+    r = ref.group_norm_table(xf, g.float(), bt.float(), G, 1e-5, m.float() if mod else None, op)
+    assert _rel(t_one, r) < 1e-4
+
+
 @pytest.mark.parametrize("F", [97, 200])
 def test_temporal_attention_long_clips_via_flash(cuda, F):
     """damo accepts up to 500 frames: beyond the register-resident kernel's 96 the op gathers the

@@ -26,6 +26,24 @@ def test_png_matches_python(shape):
         assert native.png_encode(img, level) == encode_png_py(img, level)
 
 
+def test_png_segmented_zlib_stream_is_standard():
+    """The IDAT stream is a segmented (pigz-layout) zlib stream: any inflater decodes it to the filtered
+    rows; segments are cut at fixed 128 KiB offsets, so a 768^2 RGB image spans 14 of them and a tiny one
+    is a single segment with the plain zlib framing."""
+    import zlib
+
+    from arbius_amd.utils.png import SEG, decode_png, zlib_segmented
+    rng = np.random.default_rng(5)
+    for n in (0, 1, SEG - 1, SEG, SEG + 1, 5 * SEG + 77):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        z = zlib_segmented(data, 6)
+        assert zlib.decompress(z) == data
+        assert z[:2] == zlib.compress(data, 6)[:2]            # same header bytes as zlib's own framing
+    img = rng.integers(0, 256, (768, 768, 3), dtype=np.uint8)
+    blob = native.png_encode(img, 6)
+    assert np.array_equal(decode_png(blob).reshape(img.shape), img)
+
+
 @pytest.mark.parametrize("hw", [(16, 16), (320, 576), (90, 160), (1080, 1920)])
 def test_pcm_body_matches_python(hw):
     f = _pad16(np.random.default_rng(1).integers(0, 256, (*hw, 3), dtype=np.uint8))
