@@ -35,6 +35,8 @@ def main():
            "num_inference_steps": a.steps, "seed": 7}
     if a.model == "kandinsky2":
         pipe.cfg.num_steps = a.steps
+    if a.model in ("zeroscopev2xl", "damo"):   # BASELINE config #4: 576 x 320 x 24 frames
+        inp.update(width=a.res or 576, height=320 if a.model == "zeroscopev2xl" else inp["height"], num_frames=24)
     pipe.solve(inp)
     torch.cuda.synchronize()
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
