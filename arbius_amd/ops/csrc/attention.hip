@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  const int lq = lane & 15, g = lane >> 4;
+  const int lq = lane & 15, g = lane >> 4, g4 = 4 * g;
   const int D = a.D;
   // ONES: D % 16 != 0 -> the spare zero-padded V column D carries the row sum
 
@@ -277,21 +277,30 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
                      float& alpha) __attribute__((always_inline)) {
     const bool full = !a.causal && kv0 + KV_BLK <= a.Nk;
     if (!full) {
+      // key kv0 + 16t + 4g + r: compare the lane-invariant 4g against per-(t, r) uniform bounds, so
+      // no per-element key index is built (hipcc hoisted those 16 v_or above the branch, onto
+      // every full tile)
+      const int lim = a.Nk - kv0;                                   // keys >= lim are padding
+      const int qrel = a.causal ? qidx[qt] - kv0 : 0x7fffffff;       // keys > qrel are causal-masked
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = kv0 + 16 * t + 4 * g + r;
-          const bool masked = key >= a.Nk || (a.causal && key > qidx[qt]);
+          const bool masked = g4 >= lim - (16 * t + r) || g4 > qrel - (16 * t + r);
           st[qt][t][r] = masked ? -INFINITY : st[qt][t][r];
         }
     }
-    float mloc = fmaxf(fmaxf(st[qt][0][0], st[qt][0][1]), fmaxf(st[qt][0][2], st[qt][0][3]));
-#pragma unroll
-    for (int t = 1; t < 4; ++t)
-      mloc = fmaxf(mloc, fmaxf(fmaxf(st[qt][t][0], st[qt][t][1]), fmaxf(st[qt][t][2], st[qt][t][3])));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    // row max: v_max3 chain (values are finite or -inf: same bits as the fmaxf tree)
+    float mloc = vmax3(st[qt][0][0], st[qt][0][1], st[qt][0][2]);
+    mloc = vmax3(mloc, st[qt][0][3], st[qt][1][0]);
+    mloc = vmax3(mloc, st[qt][1][1], st[qt][1][2]);
+    mloc = vmax3(mloc, st[qt][1][3], st[qt][2][0]);
+    mloc = vmax3(mloc, st[qt][2][1], st[qt][2][2]);
+    mloc = vmax3(mloc, st[qt][2][3], st[qt][3][0]);
+    mloc = vmax3(mloc, st[qt][3][1], st[qt][3][2]);
+    mloc = vmax2(mloc, st[qt][3][3]);
+    mloc = vmax2(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = vmax2(mloc, __shfl_xor(mloc, 32, 64));
     // lazy rescale (T13): keep the running max unless it grew by > 8 (log2 units), so
     // p <= 2^8; the O/l rescale then runs only on the (rare) tiles where some lane needs it.
     if constexpr (PS) {

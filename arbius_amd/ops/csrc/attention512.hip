@@ -175,10 +175,12 @@ __global__ void __launch_bounds__(256, 1) attn512_kernel(A5Args a) {
         for (int r = 0; r < 4; ++r)
           if (kv0 + 16 * t + 4 * g + r >= k1) st[t][r] = -INFINITY;
     }
-    float mloc = fmaxf(fmaxf(st[0][0], st[0][1]), fmaxf(st[0][2], st[0][3]));
-    mloc = fmaxf(mloc, fmaxf(fmaxf(st[1][0], st[1][1]), fmaxf(st[1][2], st[1][3])));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    float mloc = vmax3(st[0][0], st[0][1], st[0][2]);       // single-instruction maxes (common.h)
+    mloc = vmax3(mloc, st[0][3], st[1][0]);
+    mloc = vmax3(mloc, st[1][1], st[1][2]);
+    mloc = vmax2(mloc, st[1][3]);
+    mloc = vmax2(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = vmax2(mloc, __shfl_xor(mloc, 32, 64));
     // lazy rescale (attention.hip T13): the running max moves only when it grew by > 8 (log2 units)
     const float m_old = m_run;
     const float m_cand = (m_old == -INFINITY ? 0.f : m_old) + mloc;

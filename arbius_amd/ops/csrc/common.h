@@ -15,6 +15,21 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
+// max of non-NaN floats as ONE instruction each: hipcc lowers fmaxf on MFMA results with a
+// canonicalising v_max_f32 x, x per operand first (IEEE maxnum quieting), doubling the VALU of a
+// softmax row max (MI355X_MICROARCH.md).  Inputs here are finite or -inf, so max is exact and
+// order-free: bitwise the fmaxf result.
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax2(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // n zero-initialised int tickets for one launch on stream s (conv.hip's per-device pool): a region
 // of its own per graph-captured launch, one shared region per stream for eager launches (same-
 // stream kernels are serialised).  The launch's last arriving block re-arms its ticket to 0.

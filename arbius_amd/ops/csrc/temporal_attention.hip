@@ -102,11 +102,11 @@ __global__ void __launch_bounds__(256) temporal_attn_kernel(TAArgs a) {
         const int key = kt * 16 + 4 * g + r;
         const float v = key < F ? sc[kt][r] * a.scale_log2 : -INFINITY;
         sc[kt][r] = v;
-        mx = fmaxf(mx, v);
       }
+      mx = vmax3(mx, vmax2(sc[kt][0], sc[kt][1]), vmax2(sc[kt][2], sc[kt][3]));   // common.h
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = vmax2(mx, __shfl_xor(mx, 16, 64));
+    mx = vmax2(mx, __shfl_xor(mx, 32, 64));
     float sum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
