@@ -6,8 +6,8 @@ A plan entry {M, N, K, cfg, split} replaces the table's entry for (M, N, K); a f
 {M, N, K, split, ratio, cfg} replaces the one for (M, N, K, split, ratio).  A changed split moves
 output bytes (bump NUMERICS_VERSION and re-pin the goldens); a changed cfg at the same split does not.
 
-    python scripts/merge_plans.py --plans scripts/k2plans/k2w4800_plans.txt \
-        --family scripts/k2plans/k2w4800_family.txt
+    python scripts/merge_plans.py --plans scripts/r5/k2plans/k2w4800_plans.txt \
+        --family scripts/r5/k2plans/k2w4800_family.txt
 """
 import argparse
 import os

@@ -1,6 +1,6 @@
 #!/bin/bash
 # K2 latency mode (split CFG rows on two hardware queues): bitwise test + solo A/B; then the RVM
-# blocking-sync A/B, K2 ATen call sites and a 1-stream K2 kernel summary (scripts/gpu_r5_rvmblk.sh).
+# blocking-sync A/B, K2 ATen call sites and a 1-stream K2 kernel summary (scripts/r5/gpu_r5_rvmblk.sh).
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r5k2}; mkdir -p $O
 export TMPDIR=/tmp
@@ -13,4 +13,4 @@ for v in off on off on; do
   echo "k2 solo split=$v $(tail -1 $O/solo_$v.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["p50_task_latency_ms"], d["stage_s"])')"
 done
 unset ARB_K2_SPLIT_CFG
-bash scripts/gpu_r5_rvmblk.sh ${1:-r5k2}
+bash scripts/r5/gpu_r5_rvmblk.sh ${1:-r5k2}

@@ -1,10 +1,10 @@
 #!/bin/bash
 # GroupNorm stats+table tail (bitwise test) and the Kandinsky2 re-plan candidates (scripts/split_study.py
-# -> scripts/split_plan.py; ARB_CONV_PLANS / ARB_CONV_FAMILY override files under scripts/k2plans/):
+# -> scripts/split_plan.py; ARB_CONV_PLANS / ARB_CONV_FAMILY override files under scripts/r5/k2plans/):
 # K2 solo latency, K2 4x4 throughput and the SD default bench per variant, one box.
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r5k2plan}; mkdir -p $O
-P=$GRAFT_REPO_ROOT/scripts/k2plans
+P=$GRAFT_REPO_ROOT/scripts/r5/k2plans
 export TMPDIR=/tmp
 echo "load $(cat /proc/loadavg)"
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "group_norm or norm_table" -x -q --timeout 120 \

@@ -40,6 +40,12 @@ def main():
     hdr = f"{'S':>3} {'solo us':>9} {'group us':>9}"
     print(f"{'M x N x K':>24} {'calls':>5} {hdr} -> {hdr}")
 
+    for r in rows:   # a one-sided study (--only solo / group): the other side keeps its deployed choice
+        for side in ("solo", "group"):
+            if side + "_best" not in r:
+                r[side + "_dep_us"] = 0.0
+                r[side + "_best"] = {str(r["split"]): (0.0, r[side + "_cfg"])}
+
     def times(r, s):
         """(solo us, solo cfg, group us, group cfg) of launch r at split s (the deployed choice if faster)."""
         sb, gb = r["solo_best"][str(s)], r["group_best"][str(s)]
@@ -81,12 +87,15 @@ def main():
             mark = "" if best is None else (" * split" if best != S0 else " * family")
             print(f"{M:>8} x{N:>6} x{K:>6} {n:>5} {S0:>3} {cur[0]:>9.1f} {cur[1]:>9.1f} -> {s:>3} {su:>9.1f} "
                   f"{gu:>9.1f}{mark}")
-            if best is not None:
+            if best is not None and scfg != r["solo_cfg"] or best not in (None, S0):
                 fams.append(f"{{{M}, {N}, {K}, {best}, {GM // M}, {scfg}}},")
         if best is not None:
             gcfg = times(rs[0], best)[3]
             plans.append(f"{{{GM}, {N}, {K}, {gcfg}, {best}}},")
             fams.append(f"{{{GM}, {N}, {K}, {best}, 1, {gcfg}}},")
+            if best == S0 and gcfg == rs[0]["group_cfg"]:
+                plans.pop()
+                fams.pop()
     print("solo  us/step: %.0f -> %.0f (%+.1f %%)" % (tot["solo_dep"], tot["solo_new"],
                                                      100 * (tot["solo_new"] / tot["solo_dep"] - 1)))
     print("group us/task-step: %.0f -> %.0f (%+.1f %%)" % (tot["grp_dep"], tot["grp_new"],

@@ -66,29 +66,43 @@ def launches(model):
     return out
 
 
-def make_run(kind, shape, M, N, K, dev):
-    """(run(cfg, split) -> output, reference output) for one launch at its own batch."""
+COLD_BYTES = 512 << 20      # > the 256 MB Infinity Cache: weights read cold, as in a real UNet step
+
+
+def make_run(kind, shape, M, N, K, dev, cold=False):
+    """run(cfg, split) -> output for one launch at its own batch.  cold: every call takes the next of
+    a pool of identical weight copies (>= COLD_BYTES in total), so a replay of the timing graph reads
+    its weights from HBM - a UNet step reads each weight once, while the activation it consumes
+    was just written (warm).  Returns (run, pool size)."""
     if kind == "conv":
         B, H, W, C, Co, kc, pad, up, st = shape
         kh, kw = (3, 1) if kc == 31 else (kc, kc)
         x = torch.randn(B, H, W, C, device=dev).bfloat16()
         w = (torch.randn(Co, kh, kw, C, device=dev) / math.sqrt(kh * kw * C)).bfloat16()
-        b = torch.randn(Co, device=dev).bfloat16()
-        return lambda c, s: _lib.conv2d_nhwc(x, w, b, pad, up, None, None, st, c, s)
-    x = torch.randn(M, K, device=dev).bfloat16()
-    w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
-    b = torch.randn(N, device=dev).bfloat16()
-    return lambda c, s: _lib.gemm(x, w, b, None, c, s)
+    else:
+        x = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
+    b = torch.randn(w.shape[0], device=dev).bfloat16()
+    n = max(1, min(256, -(-COLD_BYTES // (w.numel() * 2)))) if cold else 1
+    pool = [w] + [w.clone() for _ in range(n - 1)]
+    cnt = [0]
+
+    def pick():
+        cnt[0] += 1
+        return pool[cnt[0] % n]
+    if kind == "conv":
+        return (lambda c, s: _lib.conv2d_nhwc(x, pick(), b, pad, up, None, None, st, c, s)), n
+    return (lambda c, s: _lib.gemm(x, pick(), b, None, c, s)), n
 
 
-def sweep(run, M, N, K, cfgs, conc, deployed):
+def sweep(run, M, N, K, cfgs, conc, deployed, splits=SPLITS, reps=10):
     at.CONC = conc
     ref = run(*deployed)
-    t_dep = at.graph_time(lambda: run(*deployed))
+    t_dep = at.graph_time(lambda: run(*deployed), reps=reps)
     best = {}
     ktiles = K // 64
-    for sp in SPLITS:
-        if sp > 1 and sp > ktiles // 2:
+    for sp in splits:
+        if sp > 1 and sp > ktiles // 2 and sp != deployed[1]:
             continue
         for c in cfgs:
             bn, bm = _tile(c)
@@ -99,7 +113,7 @@ def sweep(run, M, N, K, cfgs, conc, deployed):
             try:
                 if not at._agrees(run(c, sp), ref):
                     continue
-                t = at.graph_time(lambda: run(c, sp))
+                t = at.graph_time(lambda: run(c, sp), reps=reps)
             except Exception:  # noqa: BLE001 - a config the shape does not support
                 continue
             if sp not in best or t < best[sp][0]:
@@ -109,10 +123,13 @@ def sweep(run, M, N, K, cfgs, conc, deployed):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="kandinsky2")
+    ap.add_argument("--model", default="kandinsky2", help="kandinsky2 | anythingv3")
     ap.add_argument("--out", required=True)
     ap.add_argument("--max-m", type=int, default=4608, help="solo row count limit (deep levels)")
     ap.add_argument("--conc", type=int, default=4, help="concurrent copies for the batch-8 timing")
+    ap.add_argument("--cold", action="store_true", help="weights from a > Infinity-Cache pool (cold reads)")
+    ap.add_argument("--only", default="both", choices=("both", "solo", "group"))
+    ap.add_argument("--keep-split", action="store_true", help="families at the pinned split only (bitwise)")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     dev = torch.device("cuda")
@@ -122,16 +139,21 @@ def main():
     with open(a.out, "w") as f:
         for (kind, sshape, M, N, K, scfg, ssplit, gshape, GM, gcfg), n in todo:
             t0 = time.time()
-            rs = make_run(kind, sshape, M, N, K, dev)
-            solo_dep, solo = sweep(rs, M, N, K, SMALL + BIG, 1, (scfg, ssplit))
-            del rs
-            rg = make_run(kind, gshape, GM, N, K, dev)
-            grp_dep, grp = sweep(rg, GM, N, K, BIG + [0, 3, 5, 7, 8, 13], a.conc, (gcfg, ssplit))
-            del rg
-            torch.cuda.empty_cache()
+            splits = (ssplit,) if a.keep_split else SPLITS
             rec = {"kind": kind, "solo_shape": sshape, "group_shape": gshape, "MNK": [M, N, K], "GM": GM,
-                   "calls": n, "split": ssplit, "solo_cfg": scfg, "group_cfg": gcfg, "solo_dep_us": solo_dep,
-                   "group_dep_us": grp_dep, "solo_best": solo, "group_best": grp, "sec": round(time.time() - t0, 1)}
+                   "calls": n, "split": ssplit, "solo_cfg": scfg, "group_cfg": gcfg, "cold": a.cold}
+            for side, shape, rows, cfgs, conc, dcfg in (("solo", sshape, M, SMALL + BIG, 1, scfg),
+                                                        ("group", gshape, GM, BIG + [0, 3, 5, 7, 8, 13], a.conc,
+                                                         gcfg)):
+                if a.only not in ("both", side):
+                    continue
+                run, npool = make_run(kind, shape, rows, N, K, dev, a.cold)
+                reps = max(10, min(400, -(-npool // conc)))
+                dep, best = sweep(run, rows, N, K, cfgs, conc, (dcfg, ssplit), splits, reps)
+                rec[side + "_dep_us"], rec[side + "_best"] = dep, best
+                del run
+                torch.cuda.empty_cache()
+            rec["sec"] = round(time.time() - t0, 1)
             f.write(json.dumps(rec) + "\n")
             f.flush()
             print(json.dumps(rec), flush=True)
