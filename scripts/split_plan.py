@@ -96,11 +96,9 @@ def main():
             if best == S0 and gcfg == rs[0]["group_cfg"]:
                 plans.pop()
                 fams.pop()
-    print("solo  us/step: %.0f -> %.0f (%+.1f %%)" % (tot["solo_dep"], tot["solo_new"],
-                                                     100 * (tot["solo_new"] / tot["solo_dep"] - 1)))
-    print("group us/task-step: %.0f -> %.0f (%+.1f %%)" % (tot["grp_dep"], tot["grp_new"],
-                                                          100 * (tot["grp_new"] / tot["grp_dep"] - 1)))
-    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    for side, k0, k1 in (("solo  us/step", "solo_dep", "solo_new"), ("group us/task-step", "grp_dep", "grp_new")):
+        if tot[k0] > 0:
+            print("%s: %.0f -> %.0f (%+.1f %%)" % (side, tot[k0], tot[k1], 100 * (tot[k1] / tot[k0] - 1)))
     fams = list(dict.fromkeys(fams))
     open(a.out + "_plans.txt", "w").write("\n".join(plans) + "\n")
     open(a.out + "_family.txt", "w").write("\n".join(fams) + "\n")
