@@ -100,6 +100,7 @@ def main():
         if tot[k0] > 0:
             print("%s: %.0f -> %.0f (%+.1f %%)" % (side, tot[k0], tot[k1], 100 * (tot[k1] / tot[k0] - 1)))
     fams = list(dict.fromkeys(fams))
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     open(a.out + "_plans.txt", "w").write("\n".join(plans) + "\n")
     open(a.out + "_family.txt", "w").write("\n".join(fams) + "\n")
     print(f"{len(plans)} re-planned shapes -> {a.out}_plans.txt / {a.out}_family.txt")
