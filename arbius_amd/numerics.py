@@ -16,7 +16,7 @@ import os
 from typing import Callable, Dict, List, Tuple
 
 # bump on ANY change of output bytes (kernels, conv plans, sampler arithmetic, PNG/MP4 encoders)
-NUMERICS_VERSION = "r5.1-k2-latency-splits-segmented-png"
+NUMERICS_VERSION = "r5.2-gn-slice-one-launch"
 
 # Environment knobs that select a different kernel library, plan table, tiling or reference ops.
 # They exist for A/B measurement only; ``start`` refuses to mine with any of them set.
@@ -30,7 +30,7 @@ NUMERICS_ENV_KNOBS = (
     # neutrality then rests on a run-time file or an untested combination: refused all the same)
     "ARB_CONV_FAMILY", "ARB_NO_FAMILY", "ARB_DMA_BUF", "ARB_STAG2_PD", "ARB_GN_APPLY2", "ARB_GN_FUSED",
     "ARB_LN_PACKED", "ARB_ATTN512", "ARB_CAPTURE_SIDE", "ARB_QUEUE_CHECK", "ARB_RVM_GPU_YUV",
-    "ARB_RVM_BLOCKING_SYNC", "ARB_K2_SPLIT_CFG", "ARB_GN_TAIL",
+    "ARB_RVM_BLOCKING_SYNC", "ARB_K2_SPLIT_CFG", "ARB_GN_TAIL", "ARB_GN_SLICE",
 )
 
 

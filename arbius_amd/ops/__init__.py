@@ -353,6 +353,21 @@ class NormSpec:
         self.x, self.gamma, self.beta, self.groups, self.eps = x, gamma, beta, groups, eps
         self.mod, self.one_plus, self.silu, self._table = mod, one_plus, silu, None
 
+    def slice_ok(self):
+        """Whether this GroupNorm runs as ONE launch producing the transformed tensor
+        (``_lib.group_norm_slice``: small (group, image) slices; chosen by shape only)."""
+        x = self.x
+        a, b = (x.a, x.b) if isinstance(x, CatPair) else (x, None)
+        return (_hip(a) and a.dtype == torch.bfloat16 and "gnstats" not in _EXP_SKIP and "gnapply" not in _EXP_SKIP
+                and _lib.group_norm_slice_ok(a, self.groups, b))
+
+    def applied(self):
+        """The transformed tensor (GN [+ modulation] [+ SiLU]) in one launch - see ``slice_ok``."""
+        x = self.x
+        a, b = (x.a, x.b) if isinstance(x, CatPair) else (x, None)
+        return _lib.group_norm_slice(a, self.gamma, self.beta, self.groups, self.eps, self.mod, self.one_plus,
+                                     self.silu, x2=b)
+
     def table(self):
         if self._table is None:
             self._table = group_norm_table(self.x, self.gamma, self.beta, self.groups, self.eps, self.mod,
@@ -373,6 +388,10 @@ def conv2d(x, w, b=None, stride=1, padding=1, upsample=False, residual=None, tem
     (+bias, +temb[b, n] per-batch bias, +residual); ``norm = (table, silu)`` applies a
     GroupNorm(+SiLU) prologue from ``group_norm_table`` inside the conv's operand load."""
     kern_ok = (w.shape[1] in (1, 3) and w.shape[1] == w.shape[2]) or tuple(w.shape[1:3]) == (3, 1)
+    if (isinstance(norm, NormSpec) and kern_ok and not _norm_prologue(w) and w.shape[0] % 8 == 0
+            and x.shape[-1] % 64 == 0 and norm.slice_ok()):
+        # small slices: statistics, table and transform in one launch instead of three
+        x, norm = norm.applied().view(tuple(x.shape)), None
     if isinstance(x, CatPair):
         if (norm is not None and _hip(x.a) and not _norm_prologue(w) and kern_ok and x.shape[-1] % 64 == 0
                 and w.shape[0] % 8 == 0 and "gnapply" not in _EXP_SKIP):

@@ -55,6 +55,9 @@ _SIGS = {
     "arb_sampler_step": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "arb_dwconv_f16": (c_int, [c_void_p] * 4 + [c_int] * 8 + [c_void_p]),
     "arb_softmax_rows": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p]),
+    "arb_group_norm_slice_ok": (c_int, [c_int] * 3),
+    "arb_group_norm_slice": (c_int, [c_void_p] * 2 + [c_int] + [c_void_p] * 4 + [c_float] + [c_int] * 4
+                             + [c_float, c_int, c_void_p]),
     "arb_group_norm_table_cat": (c_int, [c_void_p] * 2 + [c_int] + [c_void_p] * 3 + [c_float] + [c_void_p] * 2
                                  + [c_int] * 4 + [c_float, c_void_p]),
     "arb_norm_table_apply_cat": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_long, c_int, c_int,
@@ -117,6 +120,7 @@ def loaded() -> bool:
 # selection of this module (no GPU, no data).  Host-only queries still call the library.
 _AUDIT = None
 _HOST_SYMBOLS = ("arb_conv2d_plan", "arb_conv_family", "arb_conv2d_workspace", "arb_group_norm_workspace",
+                 "arb_group_norm_slice_ok",
                  "arb_rvm_args_sizes", "arb_attention512_workspace")
 
 
@@ -549,6 +553,38 @@ def cfg_name(cfg: int) -> str:
     if cfg < 20:
         return "igemm<%s>" % _CFG4[cfg - 10]
     return _CFG_NAMES.get(cfg, f"cfg{cfg}")
+
+
+def group_norm_slice_ok(x, groups, x2=None) -> bool:
+    """Whether ``group_norm_slice`` serves this GroupNorm: a function of (rows per image, C, G) only."""
+    C = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
+    HW = x.numel() // (x.shape[0] * x.shape[-1])
+    return bool(_fn("arb_group_norm_slice_ok")(HW, C, groups))
+
+
+def group_norm_slice(x, gamma, beta, groups, eps, mod=None, one_plus=0.0, silu=False, x2=None):
+    """GroupNorm (+ scale-shift ``mod`` [B, 2C])(+SiLU) of x [B, *, C] - or of the channel concat
+    [x | x2] read in place - applied, in one launch per (group, image) slice (csrc/groupnorm.hip
+    ``gn_slice_kernel``; small slices only, see ``group_norm_slice_ok``).  Returns the bf16 output."""
+    _bf16(x, gamma, beta, mod)
+    C1 = 0
+    if x2 is not None:
+        x, x2 = _cat_parts(x, x2)
+        C1 = x.shape[-1]
+    x = x.contiguous()
+    B, C = x.shape[0], x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
+    HW = x.numel() // (B * x.shape[-1])
+    if mod is not None:
+        mod = mod.contiguous()
+        if tuple(mod.shape) != (B, 2 * C):
+            raise ValueError("group_norm_slice: mod must be [B, 2C]")
+    y = torch.empty(*x.shape[:-1], C, dtype=x.dtype, device=x.device)
+    audit_note("group_norm_slice", M=B * HW, N=C, K=groups)
+    if _skip("gnstats"):
+        return y
+    _check(_fn("arb_group_norm_slice")(_p(x), _p(x2), C1, _p(y), _p(gamma), _p(beta), _p(mod), float(one_plus), B,
+                                       HW, C, groups, float(eps), int(bool(silu)), _stream()), "group_norm_slice")
+    return y
 
 
 def group_norm_table(x, gamma, beta, groups, eps, mod=None, one_plus=0.0, x2=None):

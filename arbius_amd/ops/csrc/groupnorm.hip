@@ -867,3 +867,122 @@ static int gn_table_run(const void* x, const void* x2, int C1, const void* gamma
                                                         G, eps);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// GroupNorm (+scale-shift modulation)(+SiLU) of SMALL (group, image) slices in ONE launch: statistics,
+// affine table and the transformed output (what stats + table + norm_table_apply produce in three
+// ~5 us launches).  Grid (G, B), one block per slice of HW rows x Cg channels (HW * Cg <= GN_SLICE_MAX,
+// Cg even and <= 64).  Thread (p, rl) owns channel pair p (one dword of every row) of rows
+// rl, rl + R, ... (R = 256 / (Cg / 2) row lanes), kept in registers; the mean and then the sum of
+// squared deviations are exact two-pass fp32 sums, each thread's in row order, combined by a fixed
+// xor butterfly per wave and the 4 wave partials in wave order (LDS).  Table: sc = rstd * gamma
+// (* (mod + one_plus)), sf = beta - mean * sc (then fma(sf, m, mod_shift)) - the formula of the table
+// kernels; apply: silu?(fma(x, sc, sf)) - the formula of norm_table_apply.  The choice depends on
+// (HW, C, G) only, so lock-step groups stay bitwise equal to solo tasks.  x2 != null: channels
+// [C1, C) come from x2 (the skip concat read in place); the output is the full C-channel tensor.
+#define GN_SLICE_MAX 24576
+#define GN_SLICE_MAXD 56          // rows per thread: ceil(GN_SLICE_MAX / 2 / 225) (R * P >= 225)
+
+__device__ __forceinline__ float gn_block_sum(float v, float* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+__global__ void __launch_bounds__(256) gn_slice_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ x2,
+                                                       int C1, bf16_t* __restrict__ y,
+                                                       const bf16_t* __restrict__ gamma,
+                                                       const bf16_t* __restrict__ beta,
+                                                       const bf16_t* __restrict__ mod, float one_plus, int HW,
+                                                       int C, int G, float eps, int silu) {
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int Cg = C / G, P = Cg >> 1, R = 256 / P;
+  const int p = t % P, rl = t / P;
+  const bool act = rl < R;
+  const int c = g * Cg + 2 * p;
+  const bool second = x2 != nullptr && c >= C1;
+  const int cs = x2 == nullptr ? C : (second ? C - C1 : C1);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>((second ? x2 : x) + (size_t)b * HW * cs +
+                                                          (second ? c - C1 : c));
+  const int rs = cs >> 1;                         // row stride in dwords
+  __shared__ float sh[4];
+  __shared__ float2 tab[64];
+  uint32_t w[GN_SLICE_MAXD];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < GN_SLICE_MAXD; ++i) {
+    const int r = rl + i * R;
+    w[i] = (act && r < HW) ? src[(size_t)r * rs] : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < GN_SLICE_MAXD; ++i)
+    s += __uint_as_float(w[i] << 16) + __uint_as_float(w[i] & 0xffff0000u);
+  const float n = (float)HW * (float)Cg;
+  const float mean = gn_block_sum(s, sh) / n;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < GN_SLICE_MAXD; ++i) {
+    const int r = rl + i * R;
+    if (act && r < HW) {
+      const float d0 = __uint_as_float(w[i] << 16) - mean, d1 = __uint_as_float(w[i] & 0xffff0000u) - mean;
+      q += d0 * d0 + d1 * d1;
+    }
+  }
+  const float rstd = rsqrtf(gn_block_sum(q, sh) / n + eps);
+  if (t < Cg) {
+    const int cc = g * Cg + t;
+    float sc = rstd * bf2f(gamma[cc]);
+    float sf = bf2f(beta[cc]) - mean * sc;
+    if (mod) {
+      const float m = bf2f(mod[(size_t)b * 2 * C + cc]) + one_plus, a = bf2f(mod[(size_t)b * 2 * C + C + cc]);
+      sc *= m;
+      sf = fmaf(sf, m, a);
+    }
+    tab[t] = make_float2(sc, sf);
+  }
+  __syncthreads();
+  if (!act) return;
+  const float2 t0 = tab[2 * p], t1 = tab[2 * p + 1];
+  uint32_t* dst = reinterpret_cast<uint32_t*>(y + (size_t)b * HW * C + c);
+#pragma unroll
+  for (int i = 0; i < GN_SLICE_MAXD; ++i) {
+    const int r = rl + i * R;
+    if (r < HW) {
+      float o0 = fmaf(__uint_as_float(w[i] << 16), t0.x, t0.y);
+      float o1 = fmaf(__uint_as_float(w[i] & 0xffff0000u), t1.x, t1.y);
+      if (silu) { o0 = silu_f(o0); o1 = silu_f(o1); }
+      dst[(size_t)r * (C >> 1)] = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
+    }
+  }
+}
+
+static bool gn_slice_shape_ok(int HW, int C, int G) {
+  if (C % 8 != 0 || G <= 0 || C % G != 0) return false;
+  const int Cg = C / G;
+  return Cg % 2 == 0 && Cg <= 64 && (long)HW * Cg <= GN_SLICE_MAX;
+}
+
+// Off switch (A/B): ARB_GN_SLICE=0 -> the caller takes stats + table + table-apply.
+ARB_API int arb_group_norm_slice_ok(int HW, int C, int G) {
+  static const bool on = [] {
+    const char* e = std::getenv("ARB_GN_SLICE");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on && gn_slice_shape_ok(HW, C, G) ? 1 : 0;
+}
+
+ARB_API int arb_group_norm_slice(const void* x, const void* x2, int C1, void* y, const void* gamma, const void* beta,
+                                 const void* mod, float one_plus, int B, int HW, int C, int G, float eps, int silu,
+                                 hipStream_t stream) {
+  if (!gn_slice_shape_ok(HW, C, G)) return -1;
+  if (x2 == nullptr) C1 = C;
+  else if (C1 <= 0 || C1 >= C || C1 % 8 != 0) return -1;
+  gn_slice_kernel<<<dim3(G, B), 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)x2, C1, (bf16_t*)y,
+                                                  (const bf16_t*)gamma, (const bf16_t*)beta, (const bf16_t*)mod,
+                                                  one_plus, HW, C, G, eps, silu);
+  return (int)hipGetLastError();
+}

@@ -713,6 +713,38 @@ def test_group_norm_fused_tail_bitwise_equals_two_launches(cuda, B, HW, C, G, mo
     assert _rel(t_one, r) < 1e-4
 
 
+@pytest.mark.parametrize("B,HW,C,G,mod,silu,cat", [(2, 576, 1152, 32, True, True, False),
+                                                   (2, 144, 1536, 32, False, True, False),
+                                                   (8, 144, 2048, 32, False, True, True),
+                                                   (8, 256, 1280, 32, False, False, False),
+                                                   (2, 1024, 640, 32, True, True, False),
+                                                   (8, 64, 1920, 32, False, True, True),
+                                                   (3, 100, 64, 4, False, True, False)])
+def test_group_norm_slice_one_launch(cuda, B, HW, C, G, mod, silu, cat):
+    """Small-slice GroupNorm (+scale-shift)(+SiLU) in one launch == the fp32 reference, also with the skip
+    concat read in place; each (group, image) slice is one block, so an image's bytes do not depend on
+    the batch it shares a launch with (lock-step groups == solo), and reruns are bitwise equal."""
+    from arbius_amd import ops
+    torch.manual_seed(17)
+    x = (torch.randn(B, HW, C, device=cuda) * 2 + 0.7).bfloat16()
+    g = (torch.rand(C, device=cuda) + 0.5).bfloat16()
+    bt = torch.randn(C, device=cuda).bfloat16()
+    m = (torch.randn(B, 2 * C, device=cuda) * 0.3).bfloat16() if mod else None
+    op = 1.0 if mod else 0.0
+    xa, xb = (x[..., :C // 2].contiguous(), x[..., C // 2:].contiguous()) if cat else (x, None)
+    assert _lib.group_norm_slice_ok(xa, G, xb)
+    y = _lib.group_norm_slice(xa, g, bt, G, 1e-5, m, op, silu, x2=xb)
+    assert torch.equal(y, _lib.group_norm_slice(xa, g, bt, G, 1e-5, m, op, silu, x2=xb))
+    rt = ref.group_norm_table(x.float(), g.float(), bt.float(), G, 1e-5, None if m is None else m.float(), op)
+    r = ops.apply_norm_table(x.float(), rt, silu)
+    assert _rel(y, r) < 1e-2
+    if B > 1:   # image 1 alone == image 1 inside the batch
+        m1 = None if m is None else m[1:2].contiguous()
+        y1 = _lib.group_norm_slice(xa[1:2].contiguous(), g, bt, G, 1e-5, m1, op, silu,
+                                   x2=None if xb is None else xb[1:2].contiguous())
+        assert torch.equal(y1[0], y[1])
+
+
 @pytest.mark.parametrize("F", [97, 200])
 def test_temporal_attention_long_clips_via_flash(cuda, F):
     """damo accepts up to 500 frames: beyond the register-resident kernel's 96 the op gathers the
