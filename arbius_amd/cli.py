@@ -75,10 +75,10 @@ def build_pool(cfg, models):
                                   model_streams=cfg.mi355x.model_streams,
                                   lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir,
                                   hang_timeout=cfg.mi355x.hang_timeout_s, force_group=n == 1,
-                                  dispatch=cfg.mi355x.dispatch_policy)
+                                  dispatch=cfg.mi355x.dispatch_policy, model_lockstep=cfg.mi355x.model_lockstep)
     from .node.pool import LocalSolverPool
     return LocalSolverPool("cuda:0" if n == 1 else "cpu", capacity=cfg.mi355x.workers_per_gpu,
-                           model_streams=cfg.mi355x.model_streams,
+                           model_streams=cfg.mi355x.model_streams, model_lockstep=cfg.mi355x.model_lockstep,
                            lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir)
 
 

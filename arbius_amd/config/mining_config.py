@@ -15,7 +15,11 @@ from pydantic import BaseModel, ConfigDict, Field, model_validator
 
 # Task streams per GPU where a model's best differs from ``mi355x.workers_per_gpu`` (bench.py sweeps:
 # profiles/bench_r4_stream_group_sweep.md).
-DEFAULT_MODEL_STREAMS = {"kandinsky2": 4, "zeroscopev2xl": 2, "damo": 2, "robust_video_matting": 2}
+DEFAULT_MODEL_STREAMS = {"anythingv3": 3, "kandinsky2": 4, "zeroscopev2xl": 2, "damo": 2, "robust_video_matting": 2}
+# Lock-step group size where a model's best differs from ``mi355x.lockstep_group``.  anythingv3: 3 streams x
+# groups of 8 (batch 16 on the batch-8 canonical plans, with tile families tuned for the batch-16 shapes at
+# the pinned splits - bitwise neutral) measured +2.2 % over 4 x 4 on one box (profiles/sd_groups_r5.md).
+DEFAULT_MODEL_LOCKSTEP = {"anythingv3": 8}
 
 
 class _Base(BaseModel):
@@ -119,6 +123,7 @@ class MI355XConfig(_Base):
     lockstep_group: int = 4               # queued compatible SD tasks solved per stream in ONE batch
                                           # (batch-invariant plans: same CIDs as solo; a lone task
                                           # never waits for company)
+    model_lockstep: Dict[str, int] = Field(default_factory=lambda: dict(DEFAULT_MODEL_LOCKSTEP))
 
 
 class MiningConfig(_Base):

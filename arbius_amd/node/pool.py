@@ -67,7 +67,8 @@ class LocalSolverPool:
     and hipGraphs each) - concurrency never changes a solution's bytes."""
 
     def __init__(self, device="cpu", pipeline_factory: Callable = None, capacity: int = 1, lockstep: int = 1,
-                 model_streams: Optional[Dict[str, int]] = None, **factory_kw):
+                 model_streams: Optional[Dict[str, int]] = None, model_lockstep: Optional[Dict[str, int]] = None,
+                 **factory_kw):
         from ..models.registry import build_pipeline
         self.device = device
         self.streams = max(1, int(capacity))
@@ -76,12 +77,16 @@ class LocalSolverPool:
         # lock-step groups only where launches are batch-invariant (the HIP kernels); the CPU
         # reference path's library GEMMs are not, so grouping there would change CIDs
         self.lockstep = max(1, int(lockstep)) if str(device).startswith("cuda") else 1
+        # per-model group size (mi355x.model_lockstep), same GPU-only rule
+        self.model_lockstep = ({k: max(1, int(v)) for k, v in (model_lockstep or {}).items()}
+                               if str(device).startswith("cuda") else {})
+        group_max = max([self.lockstep] + list(self.model_lockstep.values()))
         # concurrent solves the orchestrator may hand us: every stream takes lock-step groups, and
         # with lock-step grouping one more group per stream waits in the pool - a stream that frees
         # up must find its next FULL group already pending (a group forms from whatever is queued at
         # that instant; at depth 1 the replacements were still being leased: 3.0 tasks per group of 4)
-        self.depth = 2 if self.lockstep > 1 else 1
-        self.capacity = self.streams * self.lockstep * self.depth
+        self.depth = 2 if group_max > 1 else 1
+        self.capacity = self.streams * group_max * self.depth
         self._exec = None
         self.factory = pipeline_factory or build_pipeline
         self.factory_kw = factory_kw
@@ -133,8 +138,8 @@ class LocalSolverPool:
                 first = pending.get_nowait()
             except queue.Empty:
                 return                      # an earlier turn already took this request in its group
-            batch = take_group(pending, first, self.lockstep, lambda r: r[0].kind, lambda r: r[1],
-                               lambda r: r[0].name)
+            batch = take_group(pending, first, self.model_lockstep.get(first[0].name, self.lockstep),
+                               lambda r: r[0].kind, lambda r: r[1], lambda r: r[0].name)
             if len(batch) > 1 and hasattr(pipe, "run_group"):
                 imgs, tm = infer_images(pipe, [r[1] for r in batch])
             else:
@@ -178,7 +183,7 @@ class LocalSolverPool:
 
     async def _solve(self, model, taskid, inp) -> Solution:
         loop = asyncio.get_running_loop()
-        if self.lockstep <= 1:
+        if self.model_lockstep.get(model.name, self.lockstep) <= 1:
             return await loop.run_in_executor(None, self.solve_sync, model, taskid, inp)
         import concurrent.futures as cf
         with self._lock:

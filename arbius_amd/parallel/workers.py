@@ -53,7 +53,7 @@ def _free_port() -> int:
 def _worker_main(rank: int, world: int, port: int, device_type: str, models: List[str], tiny: bool,
                  in_q, out_q, group: bool, weight_seed: int, streams: int = 1, lockstep: int = 1,
                  weights_dir: Optional[str] = None, beats=None, force_group: bool = False,
-                 model_streams: Optional[Dict[str, int]] = None):
+                 model_streams: Optional[Dict[str, int]] = None, model_lockstep: Optional[Dict[str, int]] = None):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import queue as _queue
     import threading
@@ -165,7 +165,8 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 if msg is None:
                     return
                 # lock-step group: queued compatible image tasks share one batch (same bytes as solo)
-                batch = take_group(jobs, msg, lockstep, lambda m: m[2], lambda m: m[5], lambda m: m[1])
+                batch = take_group(jobs, msg, (model_lockstep or {}).get(msg[1], lockstep), lambda m: m[2],
+                                   lambda m: m[5], lambda m: m[1])
                 jid, mname, kind, mid, taskid, inp = msg
                 pipe = forks[mname].get()           # idle (beat 0) while every fork of the model solves
                 with fork_mu:
@@ -239,7 +240,7 @@ class MultiGPUSolverPool:
                  weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1,
                  lockstep: int = 1, weights_dir: Optional[str] = None, hang_timeout: float = 300.0,
                  force_group: bool = False, model_streams: Optional[Dict[str, int]] = None,
-                 dispatch: str = "spread"):
+                 dispatch: str = "spread", model_lockstep: Optional[Dict[str, int]] = None):
         if dispatch not in POLICIES:
             raise ValueError(f"dispatch policy {dispatch!r} not in {POLICIES}")
         self.dispatch = dispatch
@@ -267,9 +268,13 @@ class MultiGPUSolverPool:
         self.beats = self.ctx.Array("d", 2 * n * self.streams, lock=False)
         # tasks per lock-step group on one stream (HIP kernels only: batch-invariant launches)
         self.lockstep = max(1, int(lockstep)) if device_type == "cuda" else 1
+        # per-model group size (mi355x.model_lockstep), same GPU-only rule
+        self.model_lockstep = ({k: max(1, int(v)) for k, v in (model_lockstep or {}).items()}
+                               if device_type == "cuda" else {})
+        group_max = max([self.lockstep] + list(self.model_lockstep.values()))
         # one more lock-step group per stream queued in the worker (node/pool.py LocalSolverPool.depth)
-        self.depth = 2 if self.lockstep > 1 else 1
-        self.slots_per_rank = self.streams * self.lockstep * self.depth
+        self.depth = 2 if group_max > 1 else 1
+        self.slots_per_rank = self.streams * group_max * self.depth
         self.busy: Dict[int, int] = {}           # job id -> rank
         self._started: Dict[int, float] = {}     # job id -> dispatch time
         self._gpu: Dict[int, dict] = {}          # rank -> {"task_s", "tasks"} (/metrics)
@@ -343,7 +348,7 @@ class MultiGPUSolverPool:
                              args=(rank, self.n, port, self.device_type, self.models, self.tiny,
                                    self.in_qs[rank], self.out_qs[rank], group, self.weight_seed, self.streams,
                                    self.lockstep, self.weights_dir, self.beats, group and self.force_group,
-                                   self.model_streams))
+                                   self.model_streams, self.model_lockstep))
         p.start()
         self.procs[rank] = p
 

@@ -44,11 +44,12 @@ def parse_args(argv=None):
                     help="video models: frames (config #4: 24); matting: clip length (default 48 = 2 s at 24 fps)")
     ap.add_argument("--concurrent", type=int, default=None,
                     help="task streams per GPU (pipeline forks on private HIP streams); default: the node's "
-                         "(mi355x.workers_per_gpu = 4, capped per model by mi355x.model_streams: 2 for "
-                         "kandinsky2 / video / matting)")
-    ap.add_argument("--group", type=int, default=4,
-                    help="SD family: tasks solved lock-step per stream (one batch-2k UNet launch sequence; "
-                         "batch-invariant plans keep every CID equal to its solo solve)")
+                         "(mi355x.workers_per_gpu = 4, capped per model by mi355x.model_streams: anythingv3 3, "
+                         "kandinsky2 4, video / matting 2)")
+    ap.add_argument("--group", type=int, default=None,
+                    help="image models: tasks solved lock-step per stream (one batch-2k UNet launch sequence; "
+                         "batch-invariant plans keep every CID equal to its solo solve); default: the node's "
+                         "(mi355x.model_lockstep: 8 for anythingv3, else mi355x.lockstep_group = 4)")
     ap.add_argument("--res", type=int, default=None, help="default 512 (anythingv3) / 768 (kandinsky2)")
     ap.add_argument("--height", type=int, default=None,
                     help="image height when it differs from --res (default: --res; zeroscope 320, matting 1080)")
@@ -72,9 +73,11 @@ def parse_args(argv=None):
     ap.add_argument("--node-outstanding", type=int, default=0,
                     help="--node: tasks kept in flight (default 2 x pool capacity: a saturated node)")
     args = ap.parse_args(argv)
+    from arbius_amd.config.mining_config import DEFAULT_MODEL_LOCKSTEP, DEFAULT_MODEL_STREAMS, MI355XConfig
     if args.concurrent is None:
-        from arbius_amd.config.mining_config import DEFAULT_MODEL_STREAMS, MI355XConfig
         args.concurrent = DEFAULT_MODEL_STREAMS.get(args.model, MI355XConfig().workers_per_gpu)
+    if args.group is None:
+        args.group = DEFAULT_MODEL_LOCKSTEP.get(args.model, MI355XConfig().lockstep_group)
     k2 = args.model == "kandinsky2"
     vid = args.model in ("zeroscopev2xl", "damo")
     rvm = args.model == "robust_video_matting"

@@ -91,10 +91,13 @@ def main():
                 fams.append(f"{{{M}, {N}, {K}, {best}, {GM // M}, {scfg}}},")
         if best is not None:
             gcfg = times(rs[0], best)[3]
-            plans.append(f"{{{GM}, {N}, {K}, {gcfg}, {best}}},")
-            fams.append(f"{{{GM}, {N}, {K}, {best}, 1, {gcfg}}},")
+            gratio = rs[0].get("group_ratio", 1)
+            if gratio == 1:     # the canonical group itself: its plan entry carries the cfg
+                plans.append(f"{{{GM}, {N}, {K}, {gcfg}, {best}}},")
+            fams.append(f"{{{GM}, {N}, {K}, {best}, {gratio}, {gcfg}}},")
             if best == S0 and gcfg == rs[0]["group_cfg"]:
-                plans.pop()
+                if gratio == 1:
+                    plans.pop()
                 fams.pop()
     for side, k0, k1 in (("solo  us/step", "solo_dep", "solo_new"), ("group us/task-step", "grp_dep", "grp_new")):
         if tot[k0] > 0:

@@ -51,11 +51,11 @@ def _tile(cfg):
     return at.KCFG[cfg % 10]
 
 
-def launches(model):
+def launches(model, group=4):
     if model == "kandinsky2":
-        solo, grp = audit.kandinsky2(768, 768, 1), audit.kandinsky2(768, 768, 4)
+        solo, grp = audit.kandinsky2(768, 768, 1), audit.kandinsky2(768, 768, group)
     else:
-        solo, grp = audit.sd15(512, 512, 1), audit.sd15(512, 512, 4)
+        solo, grp = audit.sd15(512, 512, 1), audit.sd15(512, 512, group)
     out = Counter()
     for x, y in zip(audit.launches(solo), audit.launches(grp)):
         if not x.get("plan_b") or x["M"] == y["M"]:
@@ -130,10 +130,13 @@ def main():
     ap.add_argument("--cold", action="store_true", help="weights from a > Infinity-Cache pool (cold reads)")
     ap.add_argument("--only", default="both", choices=("both", "solo", "group"))
     ap.add_argument("--keep-split", action="store_true", help="families at the pinned split only (bitwise)")
+    ap.add_argument("--group-size", type=int, default=4, help="lock-step group (4 = the canonical batch 8)")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     dev = torch.device("cuda")
-    todo = [(k, n) for k, n in launches(a.model).items() if k[2] <= a.max_m]
+    todo = [(k, n) for k, n in launches(a.model, a.group_size).items() if k[2] <= a.max_m]
+    # family-table ratio of the group launches: canonical batch / group batch, 0 when not a divisor
+    gratio = 8 // (2 * a.group_size) if 8 % (2 * a.group_size) == 0 else 0
     todo.sort(key=lambda kn: -kn[0][2] * kn[0][3] * kn[0][4] * kn[1])
     print(f"{len(todo)} launches", flush=True)
     with open(a.out, "w") as f:
@@ -141,7 +144,8 @@ def main():
             t0 = time.time()
             splits = (ssplit,) if a.keep_split else SPLITS
             rec = {"kind": kind, "solo_shape": sshape, "group_shape": gshape, "MNK": [M, N, K], "GM": GM,
-                   "calls": n, "split": ssplit, "solo_cfg": scfg, "group_cfg": gcfg, "cold": a.cold}
+                   "calls": n, "split": ssplit, "solo_cfg": scfg, "group_cfg": gcfg, "cold": a.cold,
+                   "group_ratio": gratio}
             for side, shape, rows, cfgs, conc, dcfg in (("solo", sshape, M, SMALL + BIG, 1, scfg),
                                                         ("group", gshape, GM, BIG + [0, 3, 5, 7, 8, 13], a.conc,
                                                          gcfg)):

@@ -3,7 +3,7 @@ concurrently solving worker slots than the GPU's stream count."""
 import threading
 import time
 
-from arbius_amd.config.mining_config import DEFAULT_MODEL_STREAMS, MI355XConfig
+from arbius_amd.config.mining_config import DEFAULT_MODEL_LOCKSTEP, DEFAULT_MODEL_STREAMS, MI355XConfig
 from arbius_amd.node.pool import LocalSolverPool
 
 
@@ -25,6 +25,24 @@ def test_defaults():
     assert cfg.workers_per_gpu == 4
     assert cfg.model_streams == DEFAULT_MODEL_STREAMS and cfg.model_streams["kandinsky2"] == 4
     assert MI355XConfig(model_streams={"kandinsky2": 3}).model_streams == {"kandinsky2": 3}
+    # SD1.5 (anythingv3): 3 streams x lock-step groups of 8 (profiles/sd_groups_r5.md); others groups of 4
+    assert cfg.model_streams["anythingv3"] == 3 and cfg.model_lockstep == DEFAULT_MODEL_LOCKSTEP
+    assert cfg.model_lockstep["anythingv3"] == 8 and cfg.lockstep_group == 4
+
+
+def test_pool_group_size_per_model(monkeypatch):
+    """mi355x.model_lockstep: the pool forms each model's lock-step groups at that model's size and sizes
+    its capacity for the largest group (GPU only - the CPU reference path never groups)."""
+    import arbius_amd.node.solver as solver
+    seen = []
+    monkeypatch.setattr(solver, "take_group", lambda jobs, first, n, *a: seen.append(n) or [first])
+    gpu = LocalSolverPool.__new__(LocalSolverPool)
+    LocalSolverPool.__init__(gpu, "cuda:0", pipeline_factory=lambda name, **kw: _Pipe(), capacity=3, lockstep=4,
+                             model_lockstep={"anythingv3": 8})
+    assert gpu.capacity == 3 * 8 * 2 and gpu.model_lockstep == {"anythingv3": 8}
+    cpu = LocalSolverPool("cpu", pipeline_factory=lambda name, **kw: _Pipe(), capacity=3, lockstep=4,
+                          model_lockstep={"anythingv3": 8})
+    assert cpu.lockstep == 1 and cpu.model_lockstep == {} and cpu.capacity == 3
 
 
 def test_local_pool_caps_forks_per_model():

@@ -160,6 +160,19 @@ def test_lockstep_group_bitwise_equals_solo(cuda):
     assert [s.cid for s in solve_images(pipe, inps[:2])] == solo[:2]
 
 
+def test_lockstep_group_of_8_at_512_bitwise_equals_solo(cuda):
+    """The deployed SD1.5 groups of 8 (batch 16, mi355x.model_lockstep) run the batch-8 canonical plans'
+    splits on tile families tuned for the batch-16 shapes (ratio-0 entries of conv_family.inc): every
+    task's CID is its solo CID at the benchmark resolution, where those families apply."""
+    from arbius_amd.node.solver import solve_image, solve_images
+    pipe = build_pipeline("anythingv3", device=cuda)
+    inps = [{"prompt": f"harbour at dawn {i}", "negative_prompt": "", "width": 512, "height": 512,
+             "num_inference_steps": 3, "guidance_scale": 7.5, "scheduler": "DPMSolverMultistep",
+             "seed": 70 + i} for i in range(8)]
+    solo = [solve_image(pipe, i).cid for i in inps]
+    assert [s.cid for s in solve_images(pipe, inps)] == solo
+
+
 def test_local_pool_lockstep_groups_match_solo(cuda):
     """The node's single-GPU pool batches queued compatible tasks into lock-step groups; the
     solutions are the solo ones."""
