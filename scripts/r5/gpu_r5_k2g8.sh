@@ -1,0 +1,14 @@
+#!/bin/bash
+# Kandinsky2 lock-step groups of 8 (batch 16 on the batch-8 canonical plans, batch-8 families) vs 4 x 4, one box.
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-k2g8}; mkdir -p $O
+export TMPDIR=/tmp
+one() {   # name, bench args...
+  local n=$1; shift
+  timeout -k 10 400 python3 bench.py --model kandinsky2 "$@" > $O/$n.log 2> $O/$n.err || { tail -20 $O/$n.err; exit 1; }
+  echo "$n $(tail -1 $O/$n.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["p50_task_latency_ms"], d.get("peak_hbm_gb"))')"
+}
+one c4g4 --steps 3 --warmup 1 || exit 1
+one c3g8 --concurrent 3 --group 8 --steps 2 --warmup 1 || exit 1
+one c2g8 --concurrent 2 --group 8 --steps 2 --warmup 1 || exit 1
+one c4g8 --concurrent 4 --group 8 --steps 2 --warmup 1 || exit 1
