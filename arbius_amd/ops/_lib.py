@@ -821,10 +821,16 @@ class _SampTask(ctypes.Structure):
 
 
 def sampler_step(tasks):
-    """One launch of the fused CFG + sampler update for up to 8 tasks (dicts from
-    ``models.schedulers.TaskSampler.task_args``).  Shapes / dtypes / contiguity are checked here."""
-    if not 1 <= len(tasks) <= 8:
-        raise ValueError("sampler_step: 1..8 tasks per launch")
+    """The fused CFG + sampler update of a lock-step group (dicts from
+    ``models.schedulers.TaskSampler.task_args``): one launch per 8 tasks (the kernel's per-launch task
+    table; every task's arithmetic is its own, so the chunking moves no byte).  Shapes / dtypes /
+    contiguity are checked here."""
+    if not tasks:
+        raise ValueError("sampler_step: no tasks")
+    if len(tasks) > 8:
+        for i in range(0, len(tasks), 8):
+            sampler_step(tasks[i:i + 8])
+        return
     x0 = tasks[0]["x"]
     n_pix = x0.numel() // 4
     cout = tasks[0]["u"].shape[-1]
