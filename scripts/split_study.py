@@ -52,6 +52,17 @@ def _tile(cfg):
 
 
 def launches(model, group=4):
+    if model in ("zeroscopev2xl", "damo"):   # no lock-step groups: every launch runs its own shape's plan
+        out = Counter()
+        for x in audit.launches(audit.video(model, 576 if model == "zeroscopev2xl" else 256,
+                                            320 if model == "zeroscopev2xl" else 256, 24)):
+            if x["kind"] == "conv":     # the library's own (pinned) plan for the actual shape
+                cfg, split = _lib.conv_plan(*x["shape"])
+            else:
+                cfg, split = _lib.conv_plan(1, 1, x["M"], x["K"], x["N"], 1, 0, 0, 1)
+            key = (x["kind"], x.get("shape"), x["M"], x["N"], x["K"], cfg, split, x.get("shape"), x["M"], cfg)
+            out[key] += 1
+        return out
     if model == "kandinsky2":
         solo, grp = audit.kandinsky2(768, 768, 1), audit.kandinsky2(768, 768, group)
     else:
@@ -137,6 +148,8 @@ def main():
     todo = [(k, n) for k, n in launches(a.model, a.group_size).items() if k[2] <= a.max_m]
     # family-table ratio of the group launches: canonical batch / group batch, 0 when not a divisor
     gratio = 8 // (2 * a.group_size) if 8 % (2 * a.group_size) == 0 else 0
+    if a.model in ("zeroscopev2xl", "damo"):
+        gratio = 1          # the launch's own plan entry carries the tile config (split-pinned: bitwise)
     todo.sort(key=lambda kn: -kn[0][2] * kn[0][3] * kn[0][4] * kn[1])
     print(f"{len(todo)} launches", flush=True)
     with open(a.out, "w") as f:
