@@ -83,18 +83,13 @@ async def deploy(client, artifact, args: Sequence[Any] = (), gas: int = 8_000_00
     checked against the CREATE address of the signer's nonce)."""
     abi_json, code = load_artifact(artifact)
     data = creation_data(abi_json, code, args)
-    if client.chain_id is None:
-        client.chain_id = int(await client.rpc("eth_chainId", []), 16)
-    nonce = client._nonce
-    if nonce is None:
-        nonce = int(await client.rpc("eth_getTransactionCount", [client.address, "pending"]), 16)
-    expect = create_address(client.address, nonce)
-    txh = await client._send_raw("", data, gas, 0, False)
-    rc = await client.wait_receipt(txh)
+    p = await client.submit_tx("", data, gas, 0)
+    expect = create_address(client.address, p.nonce)
+    rc = await client.wait_receipt(p.hash)
     addr = (rc or {}).get("contractAddress") or expect
     if addr.lower() != expect.lower():
-        raise RuntimeError(f"contract created at {addr}, expected {expect} (nonce {nonce})")
-    return {"tx": txh, "address": addr}
+        raise RuntimeError(f"contract created at {addr}, expected {expect} (nonce {p.nonce})")
+    return {"tx": p.hash, "address": addr}
 
 
 async def deploy_core(client, engine_artifact, proxy_artifact, base_token: str, treasury: str = None,

@@ -8,11 +8,22 @@ getTransactionReceipt, getTransactionByHash, getLogs, plus hardhat's
 ``evm_increaseTime`` / ``evm_mine``.
 
     python -m arbius_amd.chain.mock_node --port 8545
+
+Production-shaped mode (``block_time_s`` > 0): transactions enter a per-sender mempool (future
+nonces are held, a same-nonce replacement must outbid by 10 %, ``pending`` nonces count the
+consecutive run) and a block producer mines everything executable every ``block_time_s`` in ONE
+block.  ``latency_s`` delays every HTTP request (one delay per JSON-RPC batch), ``clock`` drives
+block timestamps (accelerated simulations), ``drop_next`` silently loses accepted transactions
+(a sequencer / mempool drop) and ``load_rate`` submits tasks from a user account every block
+(the offered load of a node benchmark).  JSON-RPC batches (arrays) are answered element-wise.
 """
 from __future__ import annotations
 
 import argparse
-from typing import Dict
+import asyncio
+import bisect
+import json
+from typing import Callable, Dict, List, Optional
 
 from aiohttp import web
 
@@ -36,7 +47,8 @@ def _h(b: bytes) -> str:
 
 
 class MockNode:
-    def __init__(self, engine: MockEngine = None, token_address: str = TOKEN_ADDRESS):
+    def __init__(self, engine: MockEngine = None, token_address: str = TOKEN_ADDRESS, latency_s: float = 0.0,
+                 block_time_s: float = 0.0, clock: Optional[Callable[[], float]] = None):
         from .mock_governance import MockBaseToken
         self.engine = engine or MockEngine(MockBaseToken(address=token_address))
         if getattr(self.engine.token, "clock", False) is None:
@@ -48,6 +60,16 @@ class MockNode:
         self.txs: Dict[str, dict] = {}
         self.by_selector = {abi.selector(sig): (name, sig, rets) for name, (sig, rets) in FUNCS.items()}
         self.contracts: Dict[str, object] = {}     # extra twins by address (governance: deploy_basic)
+        self.latency_s = latency_s
+        self.block_time_s = block_time_s
+        self.clock = clock
+        self.mempool: Dict[str, Dict[int, tuple]] = {}   # sender -> nonce -> (fields, hash)
+        self.drop_next = 0
+        self.dropped: List[str] = []
+        self.min_gas_price = 0                          # mempool txs priced below it are held, not mined
+        self.load: Optional[dict] = None                # {"rate", "model", "user", "input", "acc", "n"}
+        self.stats = {"requests": 0, "calls": 0, "blocks": 0, "mined_txs": 0, "replaced": 0}
+        self._ev_blocks: List[int] = []                 # block of engine.events[i] (getLogs bisect)
 
     # ------------------------------------------------------------------ views
     def _view(self, to: str, data: bytes) -> bytes:
@@ -169,6 +191,8 @@ class MockNode:
     def send_raw(self, raw_hex: str) -> str:
         raw = bytes.fromhex(raw_hex[2:])
         f, sender = decode_raw_tx(raw)
+        if self.block_time_s > 0:
+            return self._to_mempool(f, sender)
         if not f["data"]:                      # plain value transfer (send-eth)
             return self._value_transfer(f, sender)
         if f["chain_id"] != self.engine.chain_id:
@@ -176,7 +200,10 @@ class MockNode:
         expected = self.nonces.get(sender, 0)
         if f["nonce"] != expected:
             raise ValueError(f"nonce too {'low' if f['nonce'] < expected else 'high'}")
-        self.nonces[sender] = expected + 1
+        return self._apply(f, sender)
+
+    def _apply(self, f, sender) -> str:
+        self.nonces[sender] = f["nonce"] + 1
         txh = f["hash"]
         n_ev = len(self.engine.events)
         status, reason = 1, None
@@ -184,7 +211,8 @@ class MockNode:
             self._exec(sender, f["to"].lower(), f["data"])
         except Revert as ex:
             status, reason = 0, str(ex)
-            self.engine.mine(1)
+            if not getattr(self.engine, "_open_block", False):
+                self.engine.mine(1)
         new = self.engine.events[n_ev:]
         for ev in new:
             ev.tx = txh
@@ -201,7 +229,95 @@ class MockNode:
                          "nonce": hex(f["nonce"]), "blockNumber": hex(blk)}
         return txh
 
-    def _value_transfer(self, f, sender):
+    # ------------------------------------------------------------------ mempool + blocks
+    def _price(self, f) -> int:
+        return int(f.get("gas_price") or f.get("max_fee") or 0)
+
+    def _to_mempool(self, f, sender) -> str:
+        if f["chain_id"] is not None and f["chain_id"] != self.engine.chain_id:
+            raise ValueError("invalid chain id")
+        mined = self.nonces.get(sender, 0)
+        if f["nonce"] < mined:
+            raise ValueError("nonce too low")
+        pool = self.mempool.setdefault(sender, {})
+        old = pool.get(f["nonce"])
+        if old is not None:
+            if old[1] == f["hash"]:
+                raise ValueError("already known")
+            if self._price(f) * 10 < self._price(old[0]) * 11:
+                raise ValueError("replacement transaction underpriced")
+            self.stats["replaced"] += 1
+        if self.drop_next > 0:                 # accepted, then lost by the sequencer
+            self.drop_next -= 1
+            self.dropped.append(f["hash"])
+            return f["hash"]
+        pool[f["nonce"]] = (f, f["hash"])
+        return f["hash"]
+
+    def pending_nonce(self, sender: str) -> int:
+        n = self.nonces.get(sender, 0)
+        pool = self.mempool.get(sender, {})
+        while n in pool:
+            n += 1
+        return n
+
+    def produce_block(self):
+        """Mine every executable mempool transaction (consecutive nonces per sender) in ONE block,
+        plus this block's share of the offered task load."""
+        e = self.engine
+        if self.clock is not None:
+            e.timestamp = max(e.timestamp + 1, int(self.clock()))
+        else:
+            e.timestamp += max(1, int(round(self.block_time_s)))
+        with e.one_block():
+            self._load_block()
+            for sender in list(self.mempool):
+                pool = self.mempool[sender]
+                n = self.nonces.get(sender, 0)
+                for k in [k for k in pool if k < n]:
+                    del pool[k]
+                while n in pool and self._price(pool[n][0]) >= self.min_gas_price:
+                    f, _ = pool.pop(n)
+                    if not f["data"]:
+                        self._value_transfer(f, sender, mine=False)
+                    else:
+                        self._apply(f, sender)
+                    self.stats["mined_txs"] += 1
+                    n += 1
+                if not pool:
+                    del self.mempool[sender]
+        self.stats["blocks"] += 1
+
+    def _load_block(self):
+        ld = self.load
+        if not ld:
+            return
+        ld["acc"] += ld["rate"] * self.block_time_s
+        sig = FUNCS["submitTask"][0]
+        while ld["acc"] >= 1.0:
+            ld["acc"] -= 1.0
+            i = ld["n"]
+            ld["n"] += 1
+            inp = json.dumps(dict(ld["input"], prompt=f"{ld['input'].get('prompt', 'task')} #{i}")).encode()
+            data = abi.encode_call(sig, 0, ld["user"], ld["model"], 0, inp)
+            from ..utils.keccak import keccak256
+            txh = "0x" + keccak256(b"load" + i.to_bytes(8, "big") + data).hex()
+            n_ev = len(self.engine.events)
+            self._exec(ld["user"], self.engine.address, data)
+            for ev in self.engine.events[n_ev:]:
+                ev.tx = txh
+            blk = self.engine.block_number
+            self.receipts[txh] = {"transactionHash": txh, "status": "0x1", "blockNumber": hex(blk), "logs": [],
+                                  "revertReason": None}
+            self.txs[txh] = {"hash": txh, "from": ld["user"], "to": self.engine.address, "input": _h(data),
+                             "nonce": hex(i), "blockNumber": hex(blk)}
+
+    async def block_loop(self):
+        while True:
+            await asyncio.sleep(self.block_time_s)
+            self.produce_block()
+
+    def _value_transfer(self, f, sender, mine: bool = True):
         expected = self.nonces.get(sender, 0)
         if f["nonce"] != expected:
             raise ValueError("nonce mismatch")
@@ -212,7 +328,8 @@ class MockNode:
         to = f["to"].lower()
         self.eth[sender] = bal - f["value"]
         self.eth[to] = self.eth.get(to, DEFAULT_ETH) + f["value"]
-        self.engine.mine(1)
+        if mine:
+            self.engine.mine(1)
         txh = f["hash"]
         self.receipts[txh] = {"transactionHash": txh, "status": "0x1", "blockNumber": hex(self.engine.block_number),
                               "logs": [], "revertReason": None}
@@ -224,9 +341,17 @@ class MockNode:
         lo = int(flt.get("fromBlock", "0x0"), 16)
         hi_raw = flt.get("toBlock", "latest")
         hi = self.engine.block_number if hi_raw == "latest" else int(hi_raw, 16)
+        evs = self.engine.events
+        blocks = self._ev_blocks
+        if len(blocks) > len(evs):
+            blocks.clear()
+        blocks.extend(ev.block for ev in evs[len(blocks):])    # events append in block order
+        start = bisect.bisect_left(blocks, lo)
         out = []
-        for ev in self.engine.events:
-            if lo <= ev.block <= hi and ev.name in _LOGGABLE:
+        for ev in evs[start:]:
+            if ev.block > hi:
+                break
+            if lo <= ev.block and ev.name in _LOGGABLE:
                 topics, data = encode_log(ev.name, ev.args)
                 out.append({"address": self.engine.address, "topics": topics, "data": _h(data),
                             "blockNumber": hex(ev.block), "transactionHash": ev.tx, "logIndex": hex(ev.index)})
@@ -244,9 +369,12 @@ class MockNode:
         if method == "eth_getBalance":
             return hex(self.eth.get(params[0].lower(), DEFAULT_ETH))
         if method == "eth_getTransactionCount":
-            return hex(self.nonces.get(params[0].lower(), 0))
+            a = params[0].lower()
+            if len(params) > 1 and params[1] == "pending" and self.block_time_s > 0:
+                return hex(self.pending_nonce(a))
+            return hex(self.nonces.get(a, 0))
         if method == "eth_gasPrice":
-            return hex(10 ** 8)
+            return hex(max(10 ** 8, self.min_gas_price))
         if method == "eth_estimateGas":
             return hex(500_000)
         if method == "eth_call":
@@ -264,29 +392,68 @@ class MockNode:
             e.timestamp += int(params[0])
             return hex(int(params[0]))
         if method == "evm_mine":
-            e.mine(1)
+            if self.block_time_s > 0:
+                self.produce_block()
+            else:
+                e.mine(1)
             return "0x0"
+        if method == "arbius_dropNext":          # test hook: lose the next N accepted transactions
+            self.drop_next += int(params[0])
+            return hex(self.drop_next)
+        if method == "arbius_minGasPrice":       # test hook: the base fee rises (held txs need a bump)
+            self.min_gas_price = int(params[0])
+            return hex(self.min_gas_price)
+        if method == "arbius_load":              # test hook: offered task load (tasks/s, model id, user)
+            rate, model, user = float(params[0]), params[1], params[2].lower()
+            self.load = {"rate": rate, "model": model, "user": user, "acc": 0.0,
+                         "n": (self.load or {}).get("n", 0), "input": params[3] if len(params) > 3 else {}}
+            return "0x1"
+        if method == "arbius_stats":
+            return dict(self.stats, dropped=list(self.dropped), tasks=len(e.tasks), solutions=len(e.solutions),
+                        claimed=sum(1 for x in e.solutions.values() if x.claimed),
+                        mempool=sum(len(v) for v in self.mempool.values()), block=e.block_number,
+                        timestamp=e.timestamp)
         raise KeyError(method)
+
+    def _answer(self, body):
+        self.stats["calls"] += 1
+        rid = body.get("id") if isinstance(body, dict) else None
+        try:
+            res = self.handle(body["method"], body.get("params", []))
+            return {"jsonrpc": "2.0", "id": rid, "result": res}
+        except Revert as ex:
+            return {"jsonrpc": "2.0", "id": rid, "error": {"code": 3, "message": f"execution reverted: {ex}"}}
+        except Exception as ex:  # noqa: BLE001
+            return {"jsonrpc": "2.0", "id": rid, "error": {"code": -32000, "message": str(ex)}}
 
     def app(self) -> web.Application:
         app = web.Application()
 
         async def rpc(req):
             body = await req.json()
-            try:
-                res = self.handle(body["method"], body.get("params", []))
-                return web.json_response({"jsonrpc": "2.0", "id": body.get("id"), "result": res})
-            except Revert as ex:
-                return web.json_response({"jsonrpc": "2.0", "id": body.get("id"),
-                                          "error": {"code": 3, "message": f"execution reverted: {ex}"}})
-            except Exception as ex:  # noqa: BLE001
-                return web.json_response({"jsonrpc": "2.0", "id": body.get("id"),
-                                          "error": {"code": -32000, "message": str(ex)}})
+            self.stats["requests"] += 1
+            if self.latency_s > 0:
+                await asyncio.sleep(self.latency_s)
+            if isinstance(body, list):
+                return web.json_response([self._answer(b) for b in body])
+            return web.json_response(self._answer(body))
 
+        async def start_blocks(app_):
+            if self.block_time_s > 0:
+                app_[_BLOCKS] = asyncio.ensure_future(self.block_loop())
+
+        async def stop_blocks(app_):
+            t = app_.get(_BLOCKS)
+            if t is not None:
+                t.cancel()
+
+        app.on_startup.append(start_blocks)
+        app.on_cleanup.append(stop_blocks)
         app.router.add_post("/", rpc)
         return app
 
 
+_BLOCKS = web.AppKey("blocks", asyncio.Task)
 _LOGGABLE = {"TaskSubmitted", "TaskRetracted", "SignalCommitment", "SolutionSubmitted", "SolutionClaimed",
              "ContestationSubmitted", "ContestationVote", "ContestationVoteFinish", "VersionChanged",
              "ModelRegistered", "ValidatorDeposit"}

@@ -1,21 +1,26 @@
 """ChainClient over Ethereum JSON-RPC (Arbitrum Nova in production): eth_call
-reads, locally signed transactions with a single nonce manager, receipts, and
+reads, locally signed transactions through a pipelined sender, receipts, and
 ``eth_getLogs`` event back-fill (replaces ethers v5 ``.on`` polling, fixes Q8).
 
-One RpcChainClient owns the wallet; GPU workers never sign:
-concurrent solves serialise only on the nonce lock, not on inference.
+One RpcChainClient owns the wallet; GPU workers never sign.
+Transport for a node that runs tens of tasks per second over a latent endpoint:
+
+* reads issued in the same event-loop turn go out as ONE JSON-RPC batch (``batch=True``;
+  ``max_batch`` calls per POST) - concurrent task / solution / claim lookups share round trips;
+* transactions go through ``txpipe.TxPipeline``: local nonces, nonce-ordered batched broadcasts,
+  batched receipt polling, cached gas price, re-broadcast / fee-bump of a stuck nonce.
 """
 from __future__ import annotations
 
 import asyncio
 import itertools
 import logging
-from typing import List, Optional
+from typing import List, Optional, Sequence, Tuple
 
 from . import abi, secp256k1
-from .client import ChainClient, ChainEvent, TxError
+from .client import ChainClient, ChainEvent
 from .engine_abi import FUNCS, TOPIC_TO_EVENT, decode_log
-from .tx import Tx
+from .txpipe import PendingTx, TxPipeline
 
 log = logging.getLogger("arbius.chain")
 
@@ -27,13 +32,26 @@ GAS = {  # explicit gas limits of the reference (index.ts:620-739, 476-485)
 
 
 class RpcError(Exception):
-    pass
+    def __init__(self, message: str, code: Optional[int] = None):
+        super().__init__(message)
+        self.code = code
+
+    @property
+    def is_revert(self) -> bool:
+        """An EVM revert / invalid opcode / panic (the call itself failed), as opposed to a transport,
+        rate-limit or node error that says nothing about the call."""
+        m = str(self).lower()
+        return self.code == 3 or "revert" in m or "invalid opcode" in m or "panic" in m
+
+
+def _err(e: dict) -> RpcError:
+    return RpcError(e.get("message", str(e)), e.get("code"))
 
 
 class RpcChainClient(ChainClient):
     def __init__(self, url: str, private_key: str, engine_address: str, token_address: str,
                  chain_id: Optional[int] = None, timeout: float = 30.0, receipt_poll: float = 0.25,
-                 eip1559: bool = False):
+                 eip1559: bool = False, batch: bool = True, max_batch: int = 50, stuck_s: float = 12.0):
         import httpx
         self.url = url
         self.priv = private_key
@@ -41,12 +59,17 @@ class RpcChainClient(ChainClient):
         self._engine = engine_address.lower()
         self.token = token_address.lower()
         self.chain_id = chain_id
-        self.http = httpx.AsyncClient(timeout=timeout)
+        self.http = httpx.AsyncClient(timeout=timeout,
+                                      limits=httpx.Limits(max_connections=64, max_keepalive_connections=64))
         self._ids = itertools.count(1)
-        self._nonce: Optional[int] = None
-        self._nonce_lock = asyncio.Lock()
         self.receipt_poll = receipt_poll
         self.eip1559 = eip1559
+        self.batch = batch
+        self.max_batch = max(1, int(max_batch))
+        self._reads: List[Tuple[str, list, asyncio.Future]] = []
+        self._read_flush = False
+        self.txs = TxPipeline(self, poll_s=receipt_poll, stuck_s=stuck_s)
+        self.rpc_stats = {"posts": 0, "calls": 0}
 
     @property
     def engine_address(self) -> str:
@@ -56,14 +79,92 @@ class RpcChainClient(ChainClient):
     def token_address(self) -> str:
         return self.token
 
-    async def rpc(self, method: str, params: list):
-        r = await self.http.post(self.url, json={"jsonrpc": "2.0", "id": next(self._ids), "method": method,
-                                                 "params": params})
+    # ------------------------------------------------------------------ transport
+    async def _post(self, body):
+        r = await self.http.post(self.url, json=body)
         r.raise_for_status()
-        j = r.json()
+        self.rpc_stats["posts"] += 1
+        self.rpc_stats["calls"] += len(body) if isinstance(body, list) else 1
+        return r.json()
+
+    async def _rpc_one(self, method: str, params: list):
+        j = await self._post({"jsonrpc": "2.0", "id": next(self._ids), "method": method, "params": params})
         if "error" in j:
-            raise RpcError(j["error"].get("message", str(j["error"])))
+            raise _err(j["error"])
         return j["result"]
+
+    async def _post_batch(self, calls: Sequence[Tuple[str, list]]) -> list:
+        """One POST carrying ``calls`` as a JSON-RPC batch: results (or RpcError) in call order."""
+        if len(calls) == 1:
+            try:
+                return [await self._rpc_one(*calls[0])]
+            except RpcError as e:
+                return [e]
+        ids = [next(self._ids) for _ in calls]
+        out = await self._post([{"jsonrpc": "2.0", "id": i, "method": m, "params": p}
+                                for i, (m, p) in zip(ids, calls)])
+        if isinstance(out, dict):          # a node that refuses batches answers with one error object
+            raise _err(out.get("error", {"message": "batch refused"}))
+        by_id = {r.get("id"): r for r in out}
+        res = []
+        for i in ids:
+            r = by_id.get(i)
+            if r is None:
+                res.append(RpcError("missing response in batch"))
+            elif "error" in r:
+                res.append(_err(r["error"]))
+            else:
+                res.append(r["result"])
+        return res
+
+    async def rpc_batch(self, calls: Sequence[Tuple[str, list]]) -> list:
+        """Results (or RpcError instances) of ``calls``, sent in order.  Batched in one POST per
+        ``max_batch`` calls unless batching is off (or ``rpc`` was replaced by a test stub)."""
+        if not self.batch or "rpc" in self.__dict__:
+            res = []
+            for m, p in calls:
+                try:
+                    res.append(await self.rpc(m, p))
+                except RpcError as e:
+                    res.append(e)
+            return res
+        res = []
+        for i in range(0, len(calls), self.max_batch):
+            res.extend(await self._post_batch(calls[i:i + self.max_batch]))
+        return res
+
+    async def rpc(self, method: str, params: list):
+        """One JSON-RPC call; with batching on, it rides in the batch of this event-loop turn."""
+        if not self.batch:
+            return await self._rpc_one(method, params)
+        fut = asyncio.get_running_loop().create_future()
+        self._reads.append((method, params, fut))
+        if not self._read_flush:
+            self._read_flush = True
+            asyncio.get_running_loop().call_soon(self._flush_reads)
+        return await fut
+
+    def _flush_reads(self):
+        self._read_flush = False
+        q, self._reads = self._reads, []
+        for i in range(0, len(q), self.max_batch):
+            asyncio.ensure_future(self._serve(q[i:i + self.max_batch]))
+
+    async def _serve(self, part):
+        try:
+            out = await self._post_batch([(m, p) for m, p, _ in part])
+        except Exception as e:  # noqa: BLE001 - transport failure: every caller in the batch sees it
+            for _, _, f in part:
+                if not f.done():
+                    f.set_exception(e)
+            return
+        for (_, _, f), r in zip(part, out):
+            if f.done():
+                continue
+            if isinstance(r, Exception):
+                f.set_exception(r)
+            else:
+                f.set_result(r)
 
     async def _call(self, to: str, name: str, *args):
         sig, rets = FUNCS[name]
@@ -120,8 +221,10 @@ class RpcChainClient(ChainClient):
             try:
                 await self._call(self._engine, name, taskid, i)
                 return True
-            except RpcError:
-                return False
+            except RpcError as e:
+                if e.is_revert:          # array getter past the end: Panic(0x32) / revert
+                    return False
+                raise                    # rate limit / node error: not an answer (caller retries)
 
         async def length(name):
             if not await has(name, 0):
@@ -166,37 +269,18 @@ class RpcChainClient(ChainClient):
         data = abi.encode_call(sig, *args)
         return await self._send_raw(to, data, GAS.get(name, 1_000_000), 0, wait)
 
-    async def _send_raw(self, to: str, data: bytes, gas: int, value: int, wait: bool) -> str:
-        async with self._nonce_lock:
-            if self.chain_id is None:
-                self.chain_id = int(await self.rpc("eth_chainId", []), 16)
-            if self._nonce is None:
-                self._nonce = int(await self.rpc("eth_getTransactionCount", [self.address, "pending"]), 16)
-            gas_price = int(await self.rpc("eth_gasPrice", []), 16)
-            if self.eip1559:
-                tx = Tx(self._nonce, to, data, gas, self.chain_id, value, None, gas_price * 2, 0)
-            else:
-                tx = Tx(self._nonce, to, data, gas, self.chain_id, value, gas_price)
-            raw = tx.sign(self.priv)
-            try:
-                txh = await self.rpc("eth_sendRawTransaction", ["0x" + raw.hex()])
-            except RpcError as e:
-                self._nonce = None  # resync on next send
-                raise TxError(str(e)) from None
-            self._nonce += 1
-        if wait:
-            await self.wait_receipt(txh)
-        return txh
+    async def submit_tx(self, to: str, data: bytes, gas: int, value: int = 0) -> PendingTx:
+        """Broadcast through the pipelined sender; the returned handle carries ``hash`` and ``nonce``."""
+        return await self.txs.send(to, data, gas, value)
 
-    async def wait_receipt(self, txh: str, timeout: float = 120.0):
-        for _ in range(int(timeout / self.receipt_poll)):
-            rc = await self.rpc("eth_getTransactionReceipt", [txh])
-            if rc:
-                if int(rc["status"], 16) != 1:
-                    raise TxError(rc.get("revertReason", "transaction reverted"))
-                return rc
-            await asyncio.sleep(self.receipt_poll)
-        raise TxError("receipt timeout")
+    async def _send_raw(self, to: str, data: bytes, gas: int, value: int, wait: bool) -> str:
+        p = await self.txs.send(to, data, gas, value)
+        if wait:
+            await self.txs.wait(p)
+        return p.hash
+
+    async def wait_receipt(self, txh: str, timeout: float = 300.0):
+        return await self.txs.wait_hash(txh, timeout)
 
     async def signal_commitment(self, commitment, wait=False):
         return await self._send(self._engine, "signalCommitment", commitment, wait=wait)
@@ -246,4 +330,5 @@ class RpcChainClient(ChainClient):
         return out
 
     async def close(self):
+        await self.txs.close()
         await self.http.aclose()

@@ -123,4 +123,5 @@ def decode_raw_tx(raw: bytes) -> Tuple[dict, str]:
                 int.from_bytes(value, "big"), int.from_bytes(gp, "big"))
     sender = secp256k1.recover_address(tx.signing_hash(), int.from_bytes(r, "big"), int.from_bytes(s, "big"), rec_id)
     return {"nonce": tx.nonce, "to": tx.to, "data": tx.data, "gas": tx.gas, "chain_id": tx.chain_id,
-            "value": tx.value, "hash": "0x" + keccak256(raw).hex()}, sender
+            "value": tx.value, "gas_price": tx.gas_price, "max_fee": tx.max_fee,
+            "hash": "0x" + keccak256(raw).hex()}, sender

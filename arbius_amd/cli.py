@@ -47,8 +47,10 @@ def _fmt(wei: int) -> str:
 def _chain(cfg):
     from .chain.rpc import RpcChainClient
     from .node.models import CHAIN_CONFIG
+    x = cfg.mi355x
     return RpcChainClient(cfg.blockchain.rpc_url, cfg.blockchain.private_key, CHAIN_CONFIG["engineAddress"],
-                          CHAIN_CONFIG["baseTokenAddress"], chain_id=cfg.mi355x.chain_id)
+                          CHAIN_CONFIG["baseTokenAddress"], chain_id=x.chain_id, batch=x.rpc_batch,
+                          max_batch=x.rpc_max_batch, stuck_s=x.tx_stuck_s)
 
 
 def _cfg(path):

@@ -105,8 +105,8 @@ class MI355XConfig(_Base):
     mock_chain: bool = False              # in-process MockEngine (testing / plumbing config)
     selftest: bool = True                 # boot CID self-test (index.ts:981-1001)
     selftest_table: Optional[str] = None  # override of config/selftest.json
-    workers_per_gpu: int = 4              # concurrent task streams per GPU (pipeline forks): the benched
-                                          # SD1.5 default (bench.py --concurrent 4); 1 = latency mode
+    workers_per_gpu: int = 4              # task slots per GPU (pipeline forks), capped per model by
+                                          # model_streams (anythingv3 3, kandinsky2 4); 1 = latency mode
     # per-model cap on those streams.  Kandinsky2, measured on one box with every task stream on its own
     # hardware queue (profiles/sweep_r5.md): 7,236 tasks/h at 2 streams x groups of 4, 7,468 at 3 x 4,
     # 7,591 at 4 x 4, 6,264 at 4 x 2.  Round 4's 3- and 4-stream losses came from task streams sharing a
@@ -124,6 +124,13 @@ class MI355XConfig(_Base):
                                           # (batch-invariant plans: same CIDs as solo; a lone task
                                           # never waits for company)
     model_lockstep: Dict[str, int] = Field(default_factory=lambda: dict(DEFAULT_MODEL_LOCKSTEP))
+    # node-rate control plane (node/miner.py, chain/rpc.py, chain/txpipe.py)
+    job_concurrency: Dict[str, int] = Field(default_factory=dict)   # per job method, over miner.JOB_LIMITS
+    event_poll_ms: int = 1000             # eth_getLogs poll period (its own loop, never behind jobs)
+    event_concurrency: int = 64           # tasks whose events are handled at once within a poll window
+    rpc_batch: bool = True                # JSON-RPC batches for reads issued together (off: one POST each)
+    rpc_max_batch: int = 50               # calls per batch POST (provider limits)
+    tx_stuck_s: float = 12.0              # re-broadcast / fee-bump the lowest unmined nonce after this
 
 
 class MiningConfig(_Base):

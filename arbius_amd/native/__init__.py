@@ -5,7 +5,7 @@ secp256k1 ECDSA.  Built in-tree by ``python -m arbius_amd.native.build``
 reference that tests compare against.  When the extension is not built the
 names are absent and callers use their Python reference (``loaded`` is False)."""
 try:
-    from ._native import (h264_decode, h264_decode_rgb, h264_encode_rgb, h264_encode_rgb_stream,  # noqa: F401
+    from ._native import (deflate_id, h264_decode, h264_decode_rgb, h264_encode_rgb, h264_encode_rgb_stream,  # noqa: F401
                           h264_encode_yuv, h264_encode_yuv420_frames, h264_encode_yuv_stream, h264_parameter_sets,
                           h264_tables_ok, keccak256, pcm_slice_body, png_encode, rgb_to_yuv420_planes,
                           secp256k1_pubkey,

@@ -30,6 +30,7 @@
 #include <functional>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -154,11 +155,22 @@ static std::string zlib_segmented(const uint8_t* data, size_t n, int level) {
     parts[i] = deflate_segment(data + off, len, data + off - dn, dn, level, i + 1 == nseg);
   };
   const size_t nt = std::min(nseg, (size_t)std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+  // an exception must not escape a std::thread (std::terminate would abort the whole GPU worker):
+  // each thread keeps its first failure and the caller rethrows it after the join
+  std::vector<std::exception_ptr> errs(nt);
+  auto lane = [&](size_t t) {
+    try {
+      for (size_t i = t; i < nseg; i += nt) work(i);
+    } catch (...) {
+      errs[t] = std::current_exception();
+    }
+  };
   std::vector<std::thread> th;
-  for (size_t t = 1; t < nt; ++t)
-    th.emplace_back([&, t] { for (size_t i = t; i < nseg; i += nt) work(i); });
-  for (size_t i = 0; i < nseg; i += nt) work(i);
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(lane, t);
+  lane(0);
   for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
   // zlib header: CM 8 / CINFO 7, FLEVEL as zlib's own compress2 writes it, FCHECK
   const int flevel = level == 1 ? 0 : level < 6 && level >= 0 ? 1 : level == 6 || level == -1 ? 2 : 3;
   const unsigned hdr = (0x78u << 8) | (unsigned)(flevel << 6);
@@ -652,6 +664,13 @@ PYBIND11_MODULE(_native, m) {
   m.doc() = "arbius_amd native CPU runtime (keccak256, PNG, H.264 CAVLC codec, secp256k1)";
   m.def("keccak256", &keccak256, "Ethereum keccak-256");
   m.def("png_encode", &png_encode, py::arg("img"), py::arg("level") = 6, "deterministic filter-0 PNG");
+  m.def("deflate_id", [] {
+    // the deflate linked into THIS module (static libz.a, private symbols): its header and runtime
+    // versions must agree, or a foreign libz has been interposed
+    if (std::strcmp(zlibVersion(), ZLIB_VERSION) != 0)
+      return std::string("zlib-mismatch-") + zlibVersion() + "-vs-" + ZLIB_VERSION;
+    return std::string("zlib-") + ZLIB_VERSION;
+  }, "identity of the deflate implementation behind png_encode");
   m.def("pcm_slice_body", &pcm_slice_body, py::arg("frame"), py::arg("threads") = 8,
         "H.264 I_PCM macroblock payload of one RGB frame");
   m.def("h264_encode_yuv420_frames", &h264_encode_yuv420_frames, py::arg("y"), py::arg("cb"), py::arg("cr"),

@@ -15,11 +15,19 @@ MI355X-first differences (all behaviour-compatible on chain):
     its CID is checked against the local one;
   * jobs are leased, not deleted up front (fixes Q4), and the event cursor is
     persisted so missed events are back-filled after a restart (fixes Q8);
-  * ``contestationVoteFinish`` is implemented (the reference processor is a stub, Q11).
+  * ``contestationVoteFinish`` is implemented (the reference processor is a stub, Q11);
+  * the scheduler never awaits a job inline (index.ts:918-958 awaits every non-concurrent job one
+    by one): every job runs as a leased background task under a per-method concurrency limit
+    (``JOB_LIMITS``, ``mi355x.job_concurrency``), solves under the pool's GPU capacity - a solve
+    holds its GPU slot only until the solution's bytes exist, not through its commit / submit
+    receipts - and the event poll runs on its own timer, so due claims (one per solved task,
+    2,120 s later) never delay solve dispatch or ``TaskSubmitted`` handling;
+  * events of one poll window are handled concurrently per task id (in order within a task).
 """
 from __future__ import annotations
 
 import asyncio
+import contextvars
 import json
 import logging
 import time
@@ -37,6 +45,12 @@ log = logging.getLogger("arbius.miner")
 ZERO_ADDR = "0x" + "00" * 20
 MAX_UINT256 = 2 ** 256 - 1
 MINER_VERSION = 0
+_JOB = contextvars.ContextVar("arbius_job", default=None)
+
+# Background concurrency per job method.  1 keeps the reference's one-at-a-time semantics where they
+# matter (stake top-up, automine); claims / vote finishes are independent transactions and run wide.
+JOB_LIMITS = {"task": 256, "pinTaskInput": 64, "claim": 128, "contestationVoteFinish": 8,
+              "validatorStake": 1, "automine": 1}
 
 
 class Metrics:
@@ -100,8 +114,16 @@ class Miner:
         self.poll_s = float(getattr(cfg.mi355x, "poll_interval_ms", 100)) / 1000.0
         self.log_window = max(1, int(getattr(cfg.mi355x, "log_window_blocks", 2000)))
         self._bg: set = set()
-        self._running_solves: Dict[int, asyncio.Task] = {}
+        self._solving: set = set()           # solve job ids holding a GPU slot
+        self._running: Dict[str, int] = {}   # method -> jobs running in this process
         self._inflight: set = set()          # job ids leased and running in this process
+        self.limits = dict(JOB_LIMITS)
+        self.limits.update({k: max(1, int(v)) for k, v in
+                            (getattr(cfg.mi355x, "job_concurrency", None) or {}).items()})
+        self.event_poll_s = float(getattr(cfg.mi355x, "event_poll_ms", 1000)) / 1000.0
+        self.event_concurrency = int(getattr(cfg.mi355x, "event_concurrency", 64))
+        self._last_poll: Optional[float] = None
+        self.max_poll_gap_s = 0.0
         self.stopped = False
 
     # ------------------------------------------------------------------ helpers
@@ -233,7 +255,7 @@ class Miner:
     async def on_event(self, ev):
         a = ev.args
         if ev.name == "TaskSubmitted":
-            await self.lookup_and_insert_task(a["id"])
+            await self.lookup_and_insert_task(a["id"])      # cached in the DB after the first read
             self.queue("task", 10, 0, True, {"taskid": a["id"], "txid": ev.tx})
             self.metrics.inc("tasks_seen")
         elif ev.name == "TaskRetracted":
@@ -267,10 +289,39 @@ class Miner:
         elif ev.name == "VersionChanged":
             await self.version_check()
 
+    async def _handle_events(self, evs):
+        """Handlers of one window: events of one task in log order, different tasks concurrently
+        (each handler is a few chain reads; at node rate a window holds hundreds of events)."""
+        groups: Dict[str, list] = {}
+        for ev in evs:
+            key = ev.args.get("id") or ev.args.get("task") or ev.name
+            groups.setdefault(str(key).lower(), []).append(ev)
+        sem = asyncio.Semaphore(max(1, self.event_concurrency))
+
+        async def run(group):
+            async with sem:
+                for ev in group:
+                    try:
+                        await self.on_event(ev)
+                    except SystemExit:
+                        raise
+                    except Exception as e:  # noqa: BLE001
+                        log.error("event handler %s failed: %r", ev.name, e)
+        if len(groups) == 1:
+            await run(next(iter(groups.values())))
+        elif groups:
+            await asyncio.gather(*(run(g) for g in groups.values()))
+
     async def poll_events(self):
         """Back-fill ``eth_getLogs`` from the persisted cursor in bounded windows (providers cap the
         block range / result size of one call; after downtime on Nova the gap is large).  The
         cursor is persisted after every window; a failing window is halved until it passes."""
+        t = time.monotonic()
+        if self._last_poll is not None:
+            gap = t - self._last_poll
+            self.max_poll_gap_s = max(self.max_poll_gap_s, gap)
+            self.metrics.observe("event_poll_gap_s", gap)
+        self._last_poll = t
         latest = await self.chain.block_number()
         cur = self.db.get_cursor()
         if cur is None:      # first boot: only new events (reference .on semantics)
@@ -288,11 +339,7 @@ class Miner:
                 self.log_window = max(1, self.log_window // 2)
                 log.warning("eth_getLogs %d..%d failed (%r): window -> %d blocks", start, end, e, self.log_window)
                 continue
-            for ev in evs:
-                try:
-                    await self.on_event(ev)
-                except Exception as e:  # noqa: BLE001
-                    log.error("event handler %s failed: %r", ev.name, e)
+            await self._handle_events(evs)
             self.db.set_cursor(end)
             n += len(evs)
             start = end + 1
@@ -392,24 +439,34 @@ class Miner:
             log.warning("Task (%s) input not found in db", taskid)
             return
         inp = json.loads(row["data"])
-        cid = await self.get_cid(m, taskid, inp)
+        try:
+            cid = await self.get_cid(m, taskid, inp)
+        finally:
+            self._release_gpu()              # the bytes exist: the chain phase holds no GPU slot
         if not cid:
             return
         commitment = generate_commitment(self.wallet, taskid, cid)
         t_c = time.perf_counter()
-        try:
-            # wait for the commitment's receipt: submitSolution requires the commitment in an EARLIER
-            # block (EngineV1.sol:797-802); the reference sends both back to back (index.ts:619-639)
-            # and relies on its retry delay, paying for a reverted submit whenever both land in one
-            # block.  The GPU slot was released when the solve returned, so waiting costs no throughput.
-            # (a commitment already on chain - a restarted solve - is not signalled twice: the second
-            # signalCommitment would revert "commitment exists", EngineV1.sol:764-768)
-            if await self.chain.commitment_block(commitment) == 0:
+        # wait for the commitment's receipt: submitSolution requires the commitment in an EARLIER
+        # block (EngineV1.sol:797-802); the reference sends both back to back (index.ts:619-639)
+        # and relies on its retry delay, paying for a reverted submit whenever both land in one
+        # block.  The GPU slot was released when the solve returned, so waiting costs no throughput.
+        # (a commitment already on chain - a restarted solve - is not signalled twice: the second
+        # signalCommitment would revert "commitment exists", EngineV1.sol:764-768)
+        blk = await self._retry(lambda: self.chain.commitment_block(commitment))
+        if not blk:
+            try:
                 await self.chain.signal_commitment(commitment, wait=True)
-        except Exception as e:  # noqa: BLE001
-            log.error("Commitment submission failed %r", e)
-            self.metrics.inc("tx_failures")
-            return
+            except Exception as e:  # noqa: BLE001
+                # a receipt timeout or a revert does not mean the commitment is missing (a slow
+                # sequencer, or an earlier attempt of this solve that landed meanwhile): ask the
+                # chain; only a commitment that is really absent drops the task
+                self.metrics.inc("tx_failures")
+                blk = await self._retry(lambda: self.chain.commitment_block(commitment))
+                if not blk:
+                    log.error("Commitment submission failed %r", e)
+                    return
+                log.warning("Commitment wait failed (%r) but it is on chain: submitting", e)
         self.metrics.observe("commit_tx_s", time.perf_counter() - t_c)
 
         async def submit():
@@ -615,52 +672,63 @@ class Miner:
             await asyncio.sleep(max(0.05, self.lease_s / 3.0))
             self.db.renew_lease(jobid, self.lease_s)
 
+    def _release_gpu(self):
+        jid = _JOB.get()
+        if jid is not None:
+            self._solving.discard(jid)
+
     async def _run_job(self, job):
+        _JOB.set(job["id"])
         hb = asyncio.ensure_future(self._renew(job["id"]))
+        method = job["method"]
         try:
-            await self._dispatch(job["method"], json.loads(job["data"]))
-            self.metrics.inc(f"jobs_ok_{job['method']}")
+            await self._dispatch(method, json.loads(job["data"]))
+            self.metrics.inc(f"jobs_ok_{method}")
         except SystemExit:
             raise
         except Exception as e:  # noqa: BLE001
-            log.error("Job (%s) [%s] failed: %r", job["id"], job["method"], e)
+            log.error("Job (%s) [%s] failed: %r", job["id"], method, e)
             self.db.store_failed_job(job)
-            self.metrics.inc(f"jobs_failed_{job['method']}")
+            self.metrics.inc(f"jobs_failed_{method}")
         finally:
             hb.cancel()
             self.db.delete_job(job["id"])
             self._inflight.discard(job["id"])
+            self._solving.discard(job["id"])
+            self._running[method] = self._running.get(method, 1) - 1
+
+    def _start(self, job, worker: str) -> bool:
+        if job["id"] in self._inflight or not self.db.lease_job(job["id"], worker, self.lease_s):
+            return False
+        self._inflight.add(job["id"])
+        self._running[job["method"]] = self._running.get(job["method"], 0) + 1
+        self._spawn(self._run_job(job))
+        return True
 
     async def process_jobs(self) -> int:
-        """One scheduler pass: concurrent jobs fire-and-forget, solves fill the GPU
-        pool, other blocking jobs run in priority order."""
+        """One scheduler pass; it starts jobs and never awaits one.  Solves fill the GPU pool's
+        capacity; every other method runs up to its concurrency limit as a leased background task."""
         # jobs already running in this process are skipped even if their lease lapsed (they renew
         # it, but a stalled event loop could still let one expire)
-        jobs = [j for j in self.db.runnable_jobs(self.now()) if j["id"] not in self._inflight]
+        now = self.now()
         n = 0
-        for job in jobs:
-            if job["concurrent"]:
-                if self.db.lease_job(job["id"], "node", self.lease_s):
-                    self._inflight.add(job["id"])
-                    self._spawn(self._run_job(job))
+        cap = max(1, int(getattr(self.pool, "capacity", 1)))
+        free = cap - len(self._solving)
+        if free > 0:
+            for job in self.db.runnable_jobs_of(now, ["solve"], free + len(self._inflight)):
+                if len(self._solving) >= cap:
+                    break
+                if self._start(job, "gpu"):
+                    self._solving.add(job["id"])
                     n += 1
-        for job in jobs:
-            if job["concurrent"]:
+        for method, lim in self.limits.items():
+            free = lim - self._running.get(method, 0)
+            if free <= 0:
                 continue
-            if job["method"] == "solve":
-                if len(self._running_solves) >= max(1, getattr(self.pool, "capacity", 1)):
-                    continue
-                if self.db.lease_job(job["id"], "gpu", self.lease_s):
-                    self._inflight.add(job["id"])
-                    t = self._spawn(self._run_job(job))
-                    self._running_solves[job["id"]] = t
-                    t.add_done_callback(lambda _t, jid=job["id"]: self._running_solves.pop(jid, None))
-                    n += 1
-                continue
-            if self.db.lease_job(job["id"], "node", self.lease_s):
-                self._inflight.add(job["id"])
-                await self._run_job(job)
-                n += 1
+            for job in self.db.runnable_jobs_of(now, [method], free + len(self._inflight)):
+                if self._running.get(method, 0) >= lim:
+                    break
+                n += self._start(job, "node")
         return n
 
     async def drain(self, max_rounds=10000):
@@ -674,17 +742,35 @@ class Miner:
             if n == 0 and not self.db.runnable_jobs(self.now()):
                 return
 
-    async def run(self, stop: asyncio.Event = None):
-        await self.boot()
-        stop = stop or asyncio.Event()
-        last_poll = 0.0
+    async def _poll_loop(self, stop: asyncio.Event):
         while not stop.is_set():
-            if time.monotonic() - last_poll >= 1.0:
-                try:
-                    await self.poll_events()
-                except Exception as e:  # noqa: BLE001
-                    log.error("event poll failed: %r", e)
-                last_poll = time.monotonic()
-            n = await self.process_jobs()
-            if n == 0:
-                await self.sleep(self.poll_s)
+            t0 = time.monotonic()
+            try:
+                await self.poll_events()
+            except SystemExit:
+                raise
+            except Exception as e:  # noqa: BLE001
+                log.error("event poll failed: %r", e)
+            await asyncio.sleep(max(0.0, self.event_poll_s - (time.monotonic() - t0)))
+
+    async def run(self, stop: asyncio.Event = None):
+        """Boot, then two independent loops: the event poll on its own timer and the job scheduler
+        (index.ts:1078-1101 runs both in one loop and awaits blocking jobs in it)."""
+        await self.boot()
+        for m in self.db.job_methods():      # reference: an unknown method stops the miner (index.ts:914)
+            if m not in self.limits and m != "solve":
+                raise SystemExit(f"method ({m}) has no implementation")
+        stop = stop or asyncio.Event()
+        poller = asyncio.ensure_future(self._poll_loop(stop))
+        try:
+            while not stop.is_set():
+                if poller.done():
+                    poller.result()          # SystemExit from a handler (VersionChanged) ends the node
+                    poller = asyncio.ensure_future(self._poll_loop(stop))
+                n = await self.process_jobs()
+                if n == 0:
+                    await self.sleep(self.poll_s)
+                else:
+                    await asyncio.sleep(0.005)   # finishing jobs free slots continuously: bound the pass rate
+        finally:
+            poller.cancel()

@@ -86,6 +86,12 @@ async def _run(args, device: str) -> dict:
     tok.approve(USER, e.address, 2 ** 256 - 1)
     mid = e.register_model(USER, USER, 0, template_bytes(model))
     C, G = max(1, args.concurrent), max(1, args.group)
+    ms, ml = None, None
+    if getattr(args, "shipped_pool", False):
+        # the pool exactly as `start` builds it from MiningConfig defaults (cli.py): workers_per_gpu slots,
+        # each model capped by model_streams forks and grouped by model_lockstep
+        x = MiningConfig.from_dict({}).mi355x
+        C, G, ms, ml = x.workers_per_gpu, x.lockstep_group, dict(x.model_streams), dict(x.model_lockstep)
     cfg = MiningConfig.from_dict({"db_path": ":memory:", "mi355x": {
         "selftest": False, "workers_per_gpu": C, "lockstep_group": G, "poll_interval_ms": 2}})
     t_init = time.perf_counter()
@@ -93,10 +99,12 @@ async def _run(args, device: str) -> dict:
         from ..parallel.workers import MultiGPUSolverPool
         pool = MultiGPUSolverPool(args.gpus, [model], "cuda" if device.startswith("cuda") else "cpu",
                                   tiny=args.tiny, streams_per_gpu=C, lockstep=G, weights_dir=args.weights_dir,
-                                  force_group=getattr(args, "rccl_group", False))
+                                  force_group=getattr(args, "rccl_group", False), model_streams=ms,
+                                  model_lockstep=ml)
     else:
         from .pool import LocalSolverPool
-        pool = LocalSolverPool(device, capacity=C, lockstep=G, tiny=args.tiny, weights_dir=args.weights_dir)
+        pool = LocalSolverPool(device, capacity=C, lockstep=G, tiny=args.tiny, weights_dir=args.weights_dir,
+                               model_streams=ms, model_lockstep=ml)
     done: Dict[str, float] = {}
     chain = _Timed(MockChainClient(e, MINER), done)
     miner = Miner(cfg, DB(":memory:"), chain, LocalPinner(), pool, default_models({model: mid}),

@@ -28,18 +28,31 @@ class FakeSolverPool:
     hardware = "fake"
     weights_id = "synthetic"
 
-    def __init__(self, capacity: int = 1, delay: float = 0.0):
+    def __init__(self, capacity: int = 1, delay: float = 0.0, servers: int = 0):
+        """``servers`` > 0 models a GPU node: at most that many solves run at once (each ``delay``
+        seconds, so the node's rate is servers / delay), the rest queue - as the real pools queue one
+        more lock-step group per stream behind the running one (``capacity`` = what the orchestrator
+        may hand over)."""
         self.capacity = capacity
         self.delay = delay
         self.calls = []
         self.fail_next = 0
+        self.servers = servers
+        self._sem = None
+        self.busy_s = 0.0
 
     async def solve(self, model, taskid, inp) -> Solution:
         self.calls.append((model.id, taskid, dict(inp)))
         if self.fail_next:
             self.fail_next -= 1
             raise RuntimeError("injected GPU worker failure")
-        if self.delay:
+        if self.servers:
+            if self._sem is None:
+                self._sem = asyncio.Semaphore(self.servers)
+            async with self._sem:
+                await asyncio.sleep(self.delay)
+                self.busy_s += self.delay
+        elif self.delay:
             await asyncio.sleep(self.delay)
         h = hashlib.sha256((model.id + repr(sorted(inp.items()))).encode()).digest()
         img = np.frombuffer(h * 48, dtype=np.uint8)[: 16 * 16 * 3].reshape(16, 16, 3)

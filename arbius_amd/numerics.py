@@ -17,6 +17,11 @@ from typing import Callable, Dict, List, Tuple
 
 # bump on ANY change of output bytes (kernels, conv plans, sampler arithmetic, PNG/MP4 encoders)
 NUMERICS_VERSION = "r5.2-gn-slice-one-launch"
+# The deflate implementation behind every PNG's IDAT stream (consensus bytes: zlib-ng or another zlib
+# version emits different streams for the same pixels).  The native runtime links this one statically
+# (native/build.py); ``check_mining_env`` refuses any other, and tests/test_encoder_golden.py pins the
+# exact PNG / MP4 bytes of fixed inputs on the CPU.
+DEFLATE_ID = "zlib-1.2.11"
 
 # Environment knobs that select a different kernel library, plan table, tiling or reference ops.
 # They exist for A/B measurement only; ``start`` refuses to mine with any of them set.
@@ -39,13 +44,30 @@ def numerics_env_overrides(env=None) -> Dict[str, str]:
     return {k: env[k] for k in NUMERICS_ENV_KNOBS if env.get(k, "") != ""}
 
 
-def check_mining_env(env=None) -> None:
-    """Refuse to mine with a numerics-changing knob set: it would produce non-consensus CIDs."""
+def deflate_identity() -> str:
+    """The deflate that would encode this node's PNGs: the native module's static zlib, else the
+    Python ``zlib`` module's runtime library (the pure-Python encoder path)."""
+    from . import native
+    if native.loaded:
+        return native.deflate_id()
+    import zlib
+    return f"zlib-{zlib.ZLIB_RUNTIME_VERSION}"
+
+
+def check_mining_env(env=None, deflate_id=None) -> None:
+    """Refuse to mine with a numerics-changing knob set, or with a PNG deflate other than the pinned
+    one: either would produce non-consensus CIDs."""
     bad = numerics_env_overrides(env)
     if bad:
         raise SystemExit("refusing to mine: numerics-changing environment knobs are set "
                          f"({', '.join(f'{k}={v}' for k, v in sorted(bad.items()))}); their outputs differ from "
                          f"every other node on NUMERICS_VERSION {NUMERICS_VERSION}. Unset them.")
+    got = deflate_identity() if deflate_id is None else deflate_id
+    if got != DEFLATE_ID:
+        raise SystemExit(f"refusing to mine: the PNG encoder's deflate is {got}, consensus pins {DEFLATE_ID} "
+                         "(NUMERICS_VERSION " + NUMERICS_VERSION + "): its IDAT bytes - and every image CID - would "
+                         "differ. Rebuild the native runtime (python -m arbius_amd.native.build) against the "
+                         "pinned static zlib.")
 
 
 # ---------------------------------------------------------------------------------------------

@@ -164,11 +164,14 @@ def _worker_main(rank: int, world: int, port: int, device_type: str, models: Lis
                 msg = jobs.get()
                 if msg is None:
                     return
+                jid, mname, kind, mid, taskid, inp = msg
+                # the fork FIRST, then the group: with more slots than forks of a model (4
+                # slots, 3 anythingv3 forks) a slot that formed its group before waiting for a fork held
+                # a partial group; now the group forms from whatever queued while it waited
+                pipe = forks[mname].get()           # idle (beat 0) while every fork of the model solves
                 # lock-step group: queued compatible image tasks share one batch (same bytes as solo)
                 batch = take_group(jobs, msg, (model_lockstep or {}).get(msg[1], lockstep), lambda m: m[2],
                                    lambda m: m[5], lambda m: m[1])
-                jid, mname, kind, mid, taskid, inp = msg
-                pipe = forks[mname].get()           # idle (beat 0) while every fork of the model solves
                 with fork_mu:
                     st = fork_stats[mname]
                     st["in_use"] += 1
@@ -274,8 +277,9 @@ class MultiGPUSolverPool:
         group_max = max([self.lockstep] + list(self.model_lockstep.values()))
         # one more lock-step group per stream queued in the worker (node/pool.py LocalSolverPool.depth)
         self.depth = 2 if group_max > 1 else 1
-        self.slots_per_rank = self.streams * group_max * self.depth
+        self.slots_per_rank = max(self.model_slots(m) for m in models) if models else self.streams
         self.busy: Dict[int, int] = {}           # job id -> rank
+        self._job_model: Dict[int, str] = {}     # job id -> model name (per-model admission)
         self._started: Dict[int, float] = {}     # job id -> dispatch time
         self._gpu: Dict[int, dict] = {}          # rank -> {"task_s", "tasks"} (/metrics)
         self.idle: List[int] = []                # one entry per free task slot (rank repeated)
@@ -336,6 +340,14 @@ class MultiGPUSolverPool:
                 else f"random-init-seed{self.weight_seed}")
         return base + ("-tiny" if self.tiny else "")
 
+    def model_slots(self, name: str) -> int:
+        """Tasks of model ``name`` one worker admits: its forks (streams capped by ``model_streams``) x
+        its lock-step group x queue depth (one more group per fork) - a capped model (Kandinsky2,
+        video) no longer queues at the largest model's group size."""
+        forks = max(1, min(self.streams, int(self.model_streams.get(name, self.streams))))
+        g = self.model_lockstep.get(name, self.lockstep)
+        return forks * g * (2 if g > 1 else 1)
+
     @property
     def capacity(self) -> int:
         return self.slots_per_rank * sum(1 for p in self.procs if p is not None and p.is_alive())
@@ -364,6 +376,7 @@ class MultiGPUSolverPool:
             self.arch = self.arch or msg[2].get("arch")
             return
         _, jid, rank, payload = msg
+        self._job_model.pop(jid, None)
         if self.busy.pop(jid, None) is not None:
             self.idle.append(rank)
         t0 = self._started.pop(jid, None)
@@ -421,6 +434,7 @@ class MultiGPUSolverPool:
                 log.error("GPU worker %d died (exit %s): failing its tasks over, respawning", r, p.exitcode)
                 for jid in [j for j, rr in self.busy.items() if rr == r]:
                     del self.busy[jid]
+                    self._job_model.pop(jid, None)
                     if jid in self.futures:
                         self.futures.pop(jid).set_exception(RuntimeError(f"worker {r} died"))
                 self.idle = [x for x in self.idle if x != r]
@@ -430,23 +444,34 @@ class MultiGPUSolverPool:
                 self.out_qs[r] = self.ctx.Queue()
                 self._spawn(r, _free_port(), group=False)   # standalone: deterministic init / load
 
+    def _eligible(self, name: str) -> List[int]:
+        """Ranks with a free slot that still admit a task of model ``name``."""
+        cap = self.model_slots(name)
+        held: Dict[int, int] = {}
+        for jid, r in self.busy.items():
+            if self._job_model.get(jid) == name:
+                held[r] = held.get(r, 0) + 1
+        return [r for r in set(self.idle) if held.get(r, 0) < cap]
+
     async def solve(self, model, taskid, inp):
         self._watchdog()
         self._drain_nowait()
-        while not self.idle:
+        while not self._eligible(model.name):
             await asyncio.sleep(0.01)
             self._watchdog()
             self._drain_nowait()
         # dispatch policy (parallel/dispatch.py): "spread" (default) = least-loaded GPU first - below
-        # saturation a task starts at once on an idle GPU (p50 354 ms vs ~3.7 s when GPUs are packed,
-        # profiles/dispatch_r5.md); groups still form where a GPU's own queue builds up
-        load = {r: sum(1 for rr in self.busy.values() if rr == r) for r in set(self.idle)}
-        rank = pick_rank(self.dispatch, self.idle, load)
+        # saturation a task starts at once on an idle GPU (p50 at the solo latency vs ~3.7 s when GPUs
+        # are packed, profiles/dispatch_r5.md); groups still form where a GPU's own queue builds up
+        cand = self._eligible(model.name)
+        load = {r: sum(1 for rr in self.busy.values() if rr == r) for r in cand}
+        rank = pick_rank(self.dispatch, cand, load)
         self.idle.remove(rank)
         jid = next(self._ids)
         fut = asyncio.get_running_loop().create_future()
         self.futures[jid] = fut
         self.busy[jid] = rank
+        self._job_model[jid] = model.name
         self._started[jid] = time.time()
         self.in_qs[rank].put((jid, model.name, model.kind, model.id, taskid, dict(inp)))
         self._ensure_pump()

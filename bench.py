@@ -74,6 +74,9 @@ def parse_args(argv=None):
                     help="--node: tasks kept in flight (default 2 x pool capacity: a saturated node)")
     args = ap.parse_args(argv)
     from arbius_amd.config.mining_config import DEFAULT_MODEL_LOCKSTEP, DEFAULT_MODEL_STREAMS, MI355XConfig
+    # no --concurrent / --group: the node's shipped pool config (node bench: workers_per_gpu slots, capped
+    # per model by model_streams, model_lockstep groups - e.g. anythingv3 4 slots on 3 forks x groups of 8)
+    args.shipped_pool = args.concurrent is None and args.group is None
     if args.concurrent is None:
         args.concurrent = DEFAULT_MODEL_STREAMS.get(args.model, MI355XConfig().workers_per_gpu)
     if args.group is None:
