@@ -72,12 +72,15 @@ def build_pool(cfg, models):
     # device_count() does not initialise HIP: the dispatcher process stays GPU-free
     n = cfg.mi355x.gpus if cfg.mi355x.gpus is not None else torch.cuda.device_count()
     if n > 1 or (n == 1 and cfg.mi355x.worker_processes):
+        from .parallel.cpu_budget import model_gpu_caps
         from .parallel.workers import MultiGPUSolverPool
+        caps = model_gpu_caps(names, n, cfg.mi355x.host_cores) if cfg.mi355x.cpu_admission else {}
         return MultiGPUSolverPool(n, names, "cuda", streams_per_gpu=cfg.mi355x.workers_per_gpu,
                                   model_streams=cfg.mi355x.model_streams,
                                   lockstep=cfg.mi355x.lockstep_group, weights_dir=cfg.mi355x.weights_dir,
                                   hang_timeout=cfg.mi355x.hang_timeout_s, force_group=n == 1,
-                                  dispatch=cfg.mi355x.dispatch_policy, model_lockstep=cfg.mi355x.model_lockstep)
+                                  dispatch=cfg.mi355x.dispatch_policy, model_lockstep=cfg.mi355x.model_lockstep,
+                                  model_gpu_cap=caps)
     from .node.pool import LocalSolverPool
     return LocalSolverPool("cuda:0" if n == 1 else "cpu", capacity=cfg.mi355x.workers_per_gpu,
                            model_streams=cfg.mi355x.model_streams, model_lockstep=cfg.mi355x.model_lockstep,

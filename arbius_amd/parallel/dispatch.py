@@ -11,9 +11,11 @@ Policies (``MultiGPUSolverPool(dispatch=...)``, ``mi355x.dispatch_policy``):
 
 The model (``simulate``) runs the pool's admission rule (slots per GPU = streams x group x depth) and
 the worker's slot loop (a free stream takes up to ``group`` queued tasks as one lock-step batch) with
-GPU service times fitted to measured single-GPU points (``SD15_MODEL``: profiles/bench_r4_stream_group_sweep.md
-and the latency-mode line): a group of k tasks is W(k) = w0 + w1 k ms of whole-GPU work, and n
-concurrent streams share the GPU at total rate eff[n] (n streams fill the chip better than one).  The
+GPU service times fitted to measured single-GPU points of the SHIPPED configurations: a group of k tasks
+is W(k) = w0 + w1 k ms of whole-GPU work, and n concurrent streams share the GPU at total rate eff[n]
+(n streams fill the chip better than one).  ``SERVICE_MODELS`` holds one fit per model family
+(``SD15_MODEL``: anythingv3 at its 3 x 8 default, round-5 kernels; ``K2_MODEL``: Kandinsky2 at 4 x 4);
+``fit_points`` lists the measured (streams, group, ms per round) points each reproduces.  The
 dispatch decision itself is ``pick_rank`` - the same function the pool calls.
 """
 from __future__ import annotations
@@ -49,9 +51,26 @@ class ServiceModel:
         return self.w0 + self.w1 * k
 
 
-# anythingv3 512^2, 50 steps (4 streams x groups of 4: 1995 ms per round of 16 tasks; 4 x 2 / 4 x 3: 1254 /
-# 1646 ms; 3 x 4 / 3 x 3: 1541 / 1281 ms; 2 x 6 / 2 x 8: 1692 / 2188 ms; 1 stream solo: 354 ms)
-SD15_MODEL = ServiceModel(w0=204.5, w1=149.7, eff=[1.0, 1.30, 1.56, 1.61])
+# anythingv3 512^2, 50 steps, round-5 kernels with the batch-16 families (profiles/sd_groups_r5.md, one box):
+# 4 x 4 30,560 tasks/h = 1,885 ms per round of 16; 4 x 8 31,102 = 3,704 ms per 32; 3 x 8 (shipped) 31,245 =
+# 2,765 ms per 24; 2 x 8 (batch-8 families) 30,215 = 1,906 ms per 16; solo 324 ms (profiles/bench_r5_last).
+# The 4 x 4 / 4 x 8 pair pins w0 / w1 (a group of 8 costs 1.97x a group of 4 at 4 streams: batching
+# saves little beyond batch 8 rows), the rest the stream efficiencies.  (The round-4 fit on 4 x 4
+# groups - w0 204.5, w1 149.7 - described the batch-8 families of that round.)
+SD15_MODEL = ServiceModel(w0=41.1, w1=282.9, eff=[1.0, 2.418, 2.500, 2.488])
+# kandinsky2 768^2, 100 steps + prior (profiles/sweep_r5.md, one box): 2 x 4 3,980 ms, 3 x 4 5,785, 4 x 4
+# (shipped) 7,588, 4 x 2 4,598 ms per round; solo 926 ms (k2_plan_r5.md)
+K2_MODEL = ServiceModel(w0=480.0, w1=446.0, eff=[1.0, 1.138, 1.174, 1.193])
+SERVICE_MODELS = {"anythingv3": SD15_MODEL, "kandinsky2": K2_MODEL}
+FIT_POINTS = {"anythingv3": [(4, 4, 1885), (4, 8, 3704), (3, 8, 2765), (2, 8, 1906), (1, 1, 324)],
+              "kandinsky2": [(2, 4, 3980), (3, 4, 5785), (4, 4, 7588), (4, 2, 4598), (1, 1, 926)]}
+SHIPPED = {"anythingv3": (3, 8), "kandinsky2": (4, 4)}   # streams x lock-step group (config/mining_config.py)
+
+
+def fit_points(model: str):
+    """(streams, group, measured ms per round, modelled ms per round) of ``model``'s fit."""
+    m = SERVICE_MODELS[model]
+    return [(n, k, ms, m.work(k) * n / m.eff[n - 1]) for n, k, ms in FIT_POINTS[model]]
 
 
 @dataclass
@@ -63,7 +82,7 @@ class _GPU:
     groups: int = 0
 
 
-def simulate(policy: str, rate_per_s: float, n_gpus: int = 8, streams: int = 4, group: int = 4, depth: int = 2,
+def simulate(policy: str, rate_per_s: float, n_gpus: int = 8, streams: int = 3, group: int = 8, depth: int = 2,
              model: ServiceModel = SD15_MODEL, n_tasks: int = 4000, seed: int = 1) -> dict:
     """Poisson arrivals at ``rate_per_s``; returns throughput, latency percentiles, mean lock-step group
     size and per-GPU task counts over the tasks after a warm-up tenth."""
@@ -102,15 +121,21 @@ def simulate(policy: str, rate_per_s: float, n_gpus: int = 8, streams: int = 4, 
             gp.groups += 1
             group_sizes.append(len(batch))
 
+    def stream_rate(n, k):
+        # n streams share the GPU at total rate eff[n]; a lone task (group of 1) never runs faster than
+        # the measured solo latency (the linear fit's eff > n would otherwise let concurrent solo tasks
+        # beat it - the batching gain of larger groups is folded into eff by the fit)
+        r = model.eff[min(n, len(model.eff)) - 1] / n
+        return min(r, 1.0) if k == 1 else r
+
     def next_completion():
         best = None
         for r, gp in enumerate(gpus):
             n = len(gp.active)
             if not n:
                 continue
-            rate = model.eff[min(n, len(model.eff)) - 1] / n
-            for s, (rem, _) in gp.active.items():
-                dt = rem / rate
+            for s, (rem, batch) in gp.active.items():
+                dt = rem / stream_rate(n, len(batch))
                 if best is None or dt < best[0]:
                     best = (dt, r, s)
         return best
@@ -120,9 +145,8 @@ def simulate(policy: str, rate_per_s: float, n_gpus: int = 8, streams: int = 4, 
             n = len(gp.active)
             if not n:
                 continue
-            rate = model.eff[min(n, len(model.eff)) - 1] / n
             for s in gp.active:
-                gp.active[s][0] -= rate * dt
+                gp.active[s][0] -= stream_rate(n, len(gp.active[s][1])) * dt
 
     while len(done) < n_tasks:
         nc = next_completion()
@@ -156,7 +180,7 @@ def simulate(policy: str, rate_per_s: float, n_gpus: int = 8, streams: int = 4, 
             "gpu_tasks": [gp.tasks for gp in gpus], "span_s": round(span, 1)}
 
 
-def node_capacity_per_s(n_gpus: int = 8, streams: int = 4, group: int = 4, model: ServiceModel = SD15_MODEL) -> float:
+def node_capacity_per_s(n_gpus: int = 8, streams: int = 3, group: int = 8, model: ServiceModel = SD15_MODEL) -> float:
     """Saturated node throughput of the model (every stream running full groups)."""
     per_round_ms = model.work(group) * streams / model.eff[min(streams, len(model.eff)) - 1]
     return n_gpus * streams * group / per_round_ms * 1000.0

@@ -243,11 +243,14 @@ class MultiGPUSolverPool:
                  weight_seed: int = 0, start_timeout: float = 1800.0, streams_per_gpu: int = 1,
                  lockstep: int = 1, weights_dir: Optional[str] = None, hang_timeout: float = 300.0,
                  force_group: bool = False, model_streams: Optional[Dict[str, int]] = None,
-                 dispatch: str = "spread", model_lockstep: Optional[Dict[str, int]] = None):
+                 dispatch: str = "spread", model_lockstep: Optional[Dict[str, int]] = None,
+                 model_gpu_cap: Optional[Dict[str, int]] = None):
         if dispatch not in POLICIES:
             raise ValueError(f"dispatch policy {dispatch!r} not in {POLICIES}")
         self.dispatch = dispatch
         self.n = n
+        # host-CPU admission (parallel/cpu_budget.py): model -> how many workers (ranks 0..cap-1) take it
+        self.model_gpu_cap = {k: max(1, int(v)) for k, v in (model_gpu_cap or {}).items()}
         self.model_streams = dict(model_streams or {})
         self.force_group = bool(force_group)
         self.arch = None                         # gcnArchName reported by the workers (no GPU call here)
@@ -447,11 +450,12 @@ class MultiGPUSolverPool:
     def _eligible(self, name: str) -> List[int]:
         """Ranks with a free slot that still admit a task of model ``name``."""
         cap = self.model_slots(name)
+        ranks = self.model_gpu_cap.get(name, self.n)
         held: Dict[int, int] = {}
         for jid, r in self.busy.items():
             if self._job_model.get(jid) == name:
                 held[r] = held.get(r, 0) + 1
-        return [r for r in set(self.idle) if held.get(r, 0) < cap]
+        return [r for r in set(self.idle) if r < ranks and held.get(r, 0) < cap]
 
     async def solve(self, model, taskid, inp):
         self._watchdog()

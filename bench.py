@@ -456,14 +456,18 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
     if args.dispatch_sim:
-        from arbius_amd.parallel.dispatch import node_capacity_per_s, simulate
+        from arbius_amd.parallel.dispatch import SERVICE_MODELS, node_capacity_per_s, simulate
         n = max(1, args.gpus)
-        cap = node_capacity_per_s(n_gpus=n, streams=args.concurrent, group=args.group)
+        sm = SERVICE_MODELS.get(args.model)
+        if sm is None:
+            raise SystemExit(f"--dispatch-sim: no service model for {args.model} ({sorted(SERVICE_MODELS)})")
+        cap = node_capacity_per_s(n_gpus=n, streams=args.concurrent, group=args.group, model=sm)
         for frac in (0.25, 0.5, 0.75, 1.0):
             for pol in ("spread", "pack"):
-                r = simulate(pol, cap * frac, n_gpus=n, streams=args.concurrent, group=args.group, n_tasks=4000)
-                print(json.dumps(dict(r, load=frac, n_gpus=n, model="anythingv3 service model (measured r4 points)")),
-                      flush=True)
+                r = simulate(pol, cap * frac, n_gpus=n, streams=args.concurrent, group=args.group, model=sm,
+                             n_tasks=4000)
+                print(json.dumps(dict(r, load=frac, n_gpus=n, streams=args.concurrent, group=args.group,
+                                      model=f"{args.model} service model (measured r5 points)")), flush=True)
         return
     launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
     if args.node:

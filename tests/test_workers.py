@@ -163,18 +163,85 @@ def test_dispatch_policies_and_model():
     """pick_rank: spread = least-loaded GPU, pack = most-loaded GPU with a free slot; the dispatch model
     (parallel/dispatch.py) reproduces the measured single-GPU points it was fitted to, and below
     saturation spread answers faster than pack at the same completed throughput."""
-    from arbius_amd.parallel.dispatch import SD15_MODEL, pick_rank, simulate, node_capacity_per_s
+    from arbius_amd.parallel.dispatch import (SERVICE_MODELS, SHIPPED, fit_points, node_capacity_per_s, pick_rank,
+                                              simulate)
     load = {0: 3, 1: 0, 2: 5, 3: 1}
     assert pick_rank("spread", [0, 1, 2, 3], load) == 1
     assert pick_rank("pack", [0, 1, 2, 3], load) == 2
     with pytest.raises(ValueError):
         pick_rank("random", [0], load)
-    for (s, g, ms) in ((4, 4, 1995), (4, 2, 1254), (3, 4, 1541), (1, 1, 354)):
-        assert abs(SD15_MODEL.work(g) * s / SD15_MODEL.eff[s - 1] - ms) / ms < 0.02
-    cap = node_capacity_per_s()
-    sp = simulate("spread", 0.5 * cap, n_tasks=1500)
-    pk = simulate("pack", 0.5 * cap, n_tasks=1500)
-    assert sp["p50_ms"] * 3 < pk["p50_ms"]
-    assert sp["completed_per_h"] >= 0.97 * pk["completed_per_h"]
+    from arbius_amd.config.mining_config import DEFAULT_MODEL_LOCKSTEP, DEFAULT_MODEL_STREAMS, MI355XConfig
+    for model, (st, grp) in SHIPPED.items():      # the fits describe the configurations that ship
+        assert st == DEFAULT_MODEL_STREAMS[model]
+        assert grp == DEFAULT_MODEL_LOCKSTEP.get(model, MI355XConfig().lockstep_group)
+        for n, k, ms, mod in fit_points(model):
+            assert abs(mod - ms) / ms < 0.03, (model, n, k, ms, mod)
+    for model, (st, grp) in SHIPPED.items():
+        sm = SERVICE_MODELS[model]
+        cap = node_capacity_per_s(streams=st, group=grp, model=sm)
+        sp = simulate("spread", 0.5 * cap, streams=st, group=grp, model=sm, n_tasks=1500)
+        pk = simulate("pack", 0.5 * cap, streams=st, group=grp, model=sm, n_tasks=1500)
+        assert sp["p50_ms"] * 2 < pk["p50_ms"], (model, sp, pk)
+        assert sp["completed_per_h"] >= 0.97 * pk["completed_per_h"]
     with pytest.raises(ValueError):
         MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, dispatch="random")
+
+
+def test_cpu_budget_caps():
+    """Host-CPU admission (parallel/cpu_budget.py): RVM's 13.4 cores per GPU fit 4 GPUs of a 64-core
+    host, the diffusion models fit all 8; no cap when everything fits."""
+    from arbius_amd.parallel.cpu_budget import model_gpu_caps
+    caps = model_gpu_caps(["anythingv3", "kandinsky2", "robust_video_matting"], 8, cores=64)
+    assert caps == {"robust_video_matting": 4}
+    assert model_gpu_caps(["robust_video_matting"], 8, cores=128) == {}
+    assert model_gpu_caps(["robust_video_matting", "anythingv3"], 8, cores=16) == {"robust_video_matting": 1,
+                                                                                  "anythingv3": 2}
+
+
+@pytest.mark.timeout(900)
+def test_eight_workers_two_killed_under_load_keep_cids():
+    """8 gloo ranks (weights broadcast from rank 0), solves in flight on 6, two workers
+    hard-killed at once mid-load; their tasks fail over (the miner's retry re-dispatches them), both
+    respawn, and every CID - before, during and after - equals the solo CID (16 solves in flight).  A host-CPU cap keeps the
+    model's tasks on ranks 0..5."""
+    seeds = list(range(16))
+    ref = {s: LocalSolverPool("cpu", tiny=True).solve_sync(MODEL, "t", dict(INP, seed=s)).cid for s in seeds[:6]}
+
+    async def solve_retry(pool, s):
+        for _ in range(5):
+            try:
+                return s, await pool.solve(MODEL, f"t{s}", dict(INP, seed=s % 6))
+            except RuntimeError:
+                await asyncio.sleep(0.1)
+        raise AssertionError("task never completed")
+
+    async def go():
+        pool = MultiGPUSolverPool(8, ["anythingv3"], device_type="cpu", tiny=True,
+                                  model_gpu_cap={"anythingv3": 6})
+        try:
+            assert pool.world["world_size"] == 8 and all(pool.broadcast_stats[r]["bytes"] > 0 for r in range(8))
+            ranks_seen = set()
+            orig = pool.in_qs
+
+            tasks = [asyncio.ensure_future(solve_retry(pool, s)) for s in seeds]
+            while len(pool.busy) < 6:
+                await asyncio.sleep(0.01)
+            ranks_seen |= set(pool.busy.values())
+            victims = sorted(ranks_seen)[:2]
+            for r in victims:                        # two at once, both holding tasks
+                p = pool.procs[r]
+                p.kill()
+            for r in victims:
+                pool.procs[r].join(30)
+            done = await asyncio.wait_for(asyncio.gather(*tasks), 600)
+            for s, sol in done:
+                assert sol.cid == ref[s % 6], s
+            assert pool.restarts >= 2
+            assert orig is pool.in_qs
+            assert max(ranks_seen) < 6
+            again = await asyncio.wait_for(asyncio.gather(*[solve_retry(pool, s) for s in seeds[:6]]), 300)
+            assert all(sol.cid == ref[s % 6] for s, sol in again)
+        finally:
+            await pool.close()
+
+    asyncio.run(go())
