@@ -35,7 +35,7 @@ NUMERICS_ENV_KNOBS = (
     # neutrality then rests on a run-time file or an untested combination: refused all the same)
     "ARB_CONV_FAMILY", "ARB_NO_FAMILY", "ARB_DMA_BUF", "ARB_STAG2_PD", "ARB_GN_APPLY2", "ARB_GN_FUSED",
     "ARB_LN_PACKED", "ARB_ATTN512", "ARB_CAPTURE_SIDE", "ARB_QUEUE_CHECK", "ARB_RVM_GPU_YUV",
-    "ARB_RVM_BLOCKING_SYNC", "ARB_K2_SPLIT_CFG", "ARB_GN_TAIL", "ARB_GN_SLICE",
+    "ARB_RVM_BLOCKING_SYNC", "ARB_K2_SPLIT_CFG", "ARB_GN_TAIL", "ARB_GN_SLICE", "ARB_ATTN_ILP",
 )
 
 

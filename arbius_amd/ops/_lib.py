@@ -42,6 +42,7 @@ _SIGS = {
     "arb_set_stag2_pd": (None, [c_int]),
     "arb_set_stag2_buf": (None, [c_int]),
     "arb_set_attn_pp": (None, [c_int]),
+    "arb_set_attn_ilp": (None, [c_int]),
     "arb_conv2d_nhwc_tld": (c_int, [c_void_p] * 4 + [c_int] + [c_void_p] * 4 + [c_int] * 12 + [c_void_p]),
     "arb_conv2d_nhwc_f16": (c_int, [c_void_p] * 7 + [c_int] * 11 + [c_void_p]),
     "arb_group_norm_table": (c_int, [c_void_p] * 4 + [c_float] + [c_void_p] * 2 + [c_int] * 4 + [c_float, c_void_p]),

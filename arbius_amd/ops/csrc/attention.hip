@@ -61,7 +61,7 @@ __device__ __attribute__((aligned(16))) uint4 g_attn_ones[1] = {{0x3F80u, 0u, 0u
 // by (row & 7) on the SOURCE address (lane-linear LDS image, rule 21) and on the QK read; V rows
 // are VROW/8 chunks, already lane-linear; padding chunks read a zero page, V's row-sum column a
 // ones page.  One LDS array for everything (hipcc's vmcnt trap with two __shared__ objects).
-template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false, bool PP = false, bool PS = true>
+template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false, bool PP = false, bool PS = true, bool ILP = true>
 __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   static_assert(!GLDS || KSTEPS == 2, "LDS-DMA staging: 8-chunk K rows only");
   constexpr int KROW = GLDS ? KSTEPS * 32 : KSTEPS * 32 + 8;   // K tile row (elements)
@@ -88,6 +88,16 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   const int wave = tid >> 6, lane = tid & 63;
   const int lq = lane & 15, g = lane >> 4, g4 = 4 * g;
   const int D = a.D;
+  // lane-pair reductions: the gfx950 lane swaps (VALU) where the registers allow; at 4 query tiles of a
+  // 48/64-wide head (and the 129..160-wide heads) they push the kernel past 256 VGPRs (up to 45 spills),
+  // so those keep the LDS permute
+  constexpr bool SWAPS = !(QT >= 4 && (DT >= 4 || !ONES)) && KSTEPS < 5;
+  auto mx16 = [](float x) __attribute__((always_inline)) {
+    return SWAPS ? max_xor16(x) : vmax2(x, __shfl_xor(x, 16, 64));
+  };
+  auto mx32 = [](float x) __attribute__((always_inline)) {
+    return SWAPS ? max_xor32(x) : vmax2(x, __shfl_xor(x, 32, 64));
+  };
   // ONES: D % 16 != 0 -> the spare zero-padded V column D carries the row sum
 
   const bf16_t* qbase = a.q + b * a.q_sb + h * a.q_sh;
@@ -235,17 +245,31 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       gv[i] = vbase + (long)row * a.v_sn + col;
     }
   }
+  // per-lane DMA sources resolved once (data row / zero page / ones page): a tile then costs one uniform
+  // offset per chunk, and the range check runs only on a partial tile (the same bytes as resolving
+  // them per tile, without the divergent page selection on every tile)
+  const char* kb0[KBW];
+  const char* vb0[VBW];
+  if constexpr (GLDS) {
+#pragma unroll
+    for (int i = 0; i < KBW; ++i) kb0[i] = gkm[i] ? (const char*)gk[i] : (const char*)g_attn_zero;
+#pragma unroll
+    for (int i = 0; i < VBW; ++i)
+      vb0[i] = gvm[i] == 1 ? (const char*)gv[i] : gvm[i] == 2 ? (const char*)g_attn_ones : (const char*)g_attn_zero;
+  }
   auto issue_kv = [&](int kv, bf16_t* dst) __attribute__((always_inline)) {
-    const long ko = (long)kv * a.k_sn, vo = (long)kv * a.v_sn;
+    const long ko = (long)kv * a.k_sn * 2, vo = (long)kv * a.v_sn * 2;   // bytes, uniform
+    const bool full = kv + KV_BLK <= a.Nk;
 #pragma unroll
     for (int i = 0; i < KBW; ++i) {
-      const void* src = (gkm[i] && kv + gkr[i] < a.Nk) ? (const void*)(gk[i] + ko) : (const void*)g_attn_zero;
+      const char* src = kb0[i] + (gkm[i] ? ko : 0);
+      if (!full && kv + gkr[i] >= a.Nk) src = (const char*)g_attn_zero;
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (wave + 4 * i) * 512), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < VBW; ++i) {
-      const void* src = gvm[i] == 2 ? (const void*)g_attn_ones
-                        : (gvm[i] == 1 && kv + gvr[i] < a.Nk) ? (const void*)(gv[i] + vo) : (const void*)g_attn_zero;
+      const char* src = vb0[i] + (gvm[i] == 1 ? vo : 0);
+      if (!full && gvm[i] == 1 && kv + gvr[i] >= a.Nk) src = (const char*)g_attn_zero;
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + KV_BLK * KROW + gvb[i] * 512), 16, 0, 0);
     }
   };
@@ -299,8 +323,8 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     mloc = vmax3(mloc, st[qt][2][3], st[qt][3][0]);
     mloc = vmax3(mloc, st[qt][3][1], st[qt][3][2]);
     mloc = vmax2(mloc, st[qt][3][3]);
-    mloc = vmax2(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = vmax2(mloc, __shfl_xor(mloc, 32, 64));
+    mloc = mx16(mloc);
+    mloc = mx32(mloc);
     // lazy rescale (T13): keep the running max unless it grew by > 8 (log2 units), so
     // p <= 2^8; the O/l rescale then runs only on the (rare) tiles where some lane needs it.
     if constexpr (PS) {
@@ -402,14 +426,93 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
     for (int dt = 0; dt < DT; ++dt) o[qt][dt] *= alpha;
   };
 
+  // ---- ILP form of the prescaled (PS) online softmax, all query tiles of one key tile at once: bitwise
+  // `softmax` + `rescale` per query tile, written so the query tiles' dependency chains interleave.  The
+  // row max is a max3 tree (max is exact and order-free); every step runs over all query tiles before
+  // the next; the lazy rescale is a wave-uniform branch per query tile with per-lane selects inside (a
+  // lane that needs none subtracts 0: x - 0 == x bit for bit) - `softmax`'s divergent per-tile branches
+  // cut the schedule into one serial chain per query tile (max -> lane swaps -> decision -> exp -> cvt).
+  auto softmax_all = [&](int kv0, f32x4 (&st)[QT][4], bf16x8 (&pf)[QT][2]) __attribute__((always_inline)) {
+    const bool full = !a.causal && kv0 + KV_BLK <= a.Nk;
+    if (!full) {
+      const int lim = a.Nk - kv0;
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        const int qrel = a.causal ? qidx[qt] - kv0 : 0x7fffffff;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bool masked = g4 >= lim - (16 * t + r) || g4 > qrel - (16 * t + r);
+            st[qt][t][r] = masked ? -INFINITY : st[qt][t][r];
+          }
+      }
+    }
+    float mloc[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      const f32x4* x = st[qt];
+      const float a0 = vmax3(x[0][0], x[0][1], x[0][2]), a1 = vmax3(x[0][3], x[1][0], x[1][1]);
+      const float a2 = vmax3(x[1][2], x[1][3], x[2][0]), a3 = vmax3(x[2][1], x[2][2], x[2][3]);
+      const float a4 = vmax3(x[3][0], x[3][1], x[3][2]);
+      mloc[qt] = vmax2(vmax3(a0, a1, a2), vmax3(a3, a4, x[3][3]));
+    }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) mloc[qt] = mx16(mloc[qt]);
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) mloc[qt] = mx32(mloc[qt]);
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      const float m_old = m_run[qt];
+      const float m_cand = (m_old == -INFINITY ? 0.f : m_old) + mloc[qt];
+      const bool need = m_cand > m_old + 8.f;
+      float alpha = 1.f;
+      const bool any = __any(need);
+      if (any) {                                   // wave-uniform, rare (lazy rescale)
+        const float al = (m_old == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_old - m_cand);
+        alpha = need ? al : 1.f;
+        m_run[qt] = need ? m_cand : m_old;
+        const float sub = need ? mloc[qt] : 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) st[qt][t][r] -= sub;
+      }
+      float lsum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          st[qt][t][r] = __builtin_amdgcn_exp2f(st[qt][t][r]);
+          if (!ONES) lsum += st[qt][t][r];
+        }
+      if (!ONES) l_run[qt] = l_run[qt] * alpha + lsum;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 p;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          p[j] = (__bf16)st[qt][2 * ks][j];
+          p[j + 4] = (__bf16)st[qt][2 * ks + 1][j];
+        }
+        pf[qt][ks] = p;
+      }
+      if (any) rescale(qt, alpha);
+    }
+  };
+
   auto compute = [&](int kv0, const bf16_t* cK, const bf16_t* cV) __attribute__((always_inline)) {
     f32x4 st[QT][4];
     bf16x8 pf[QT][2];
     qk(cK, st);
+    if constexpr (PS && ILP) {
+      softmax_all(kv0, st, pf);
+    } else {
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-      float alpha;
-      if (softmax(kv0, qt, st, pf, alpha)) rescale(qt, alpha);
+      for (int qt = 0; qt < QT; ++qt) {
+        float alpha;
+        if (softmax(kv0, qt, st, pf, alpha)) rescale(qt, alpha);
+      }
     }
     pv(cV, pf);
   };
@@ -530,8 +633,8 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       l = __shfl(cand, ((D & 15) >> 2) * 16 + lq, 64);
     } else {
       l = l_run[qt];
-      l += __shfl_xor(l, 16, 64);
-      l += __shfl_xor(l, 32, 64);
+      l = SWAPS ? sum_xor16(l) : l + __shfl_xor(l, 16, 64);
+      l = SWAPS ? sum_xor32(l) : l + __shfl_xor(l, 32, 64);
     }
     const float inv = l > 0.f ? 1.f / l : 0.f;
     if (qidx[qt] < a.Nq) {
@@ -582,6 +685,18 @@ static bool attn_prescale_enabled() {
 }
 ARB_API void arb_set_attn_prescale(int on) { g_attn_prescale = on ? 1 : 0; }
 
+// ARB_ATTN_ILP=0 / arb_set_attn_ilp(0): the per-query-tile softmax instead of softmax_all (bitwise equal:
+// the A/B of the ILP form, and its bitwise test)
+static int g_attn_ilp = -1;
+static bool attn_ilp_enabled() {
+  if (g_attn_ilp < 0) {
+    const char* e = std::getenv("ARB_ATTN_ILP");
+    g_attn_ilp = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_ilp == 1;
+}
+ARB_API void arb_set_attn_ilp(int on) { g_attn_ilp = on ? 1 : 0; }
+
 template <int KSTEPS, int DT, int QT, bool PS>
 static void launch_fa_ps(const AttnArgs& a, hipStream_t s) {
   constexpr int QBLK = 4 * QT * 16;
@@ -598,6 +713,11 @@ static void launch_fa_ps(const AttnArgs& a, hipStream_t s) {
             flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, true, PS><<<grid, 256, 0, s>>>(a);
           return;
         }
+      }
+      if (PS && !attn_ilp_enabled()) {
+        if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true, false, PS, false><<<grid, 256, 0, s>>>(a);
+        else flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, false, PS, false><<<grid, 256, 0, s>>>(a);
+        return;
       }
       if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true, false, PS><<<grid, 256, 0, s>>>(a);
       else flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, false, PS><<<grid, 256, 0, s>>>(a);

@@ -179,8 +179,8 @@ __global__ void __launch_bounds__(256, 1) attn512_kernel(A5Args a) {
     mloc = vmax3(mloc, st[0][3], st[1][0]);
     mloc = vmax3(mloc, st[1][1], st[1][2]);
     mloc = vmax2(mloc, st[1][3]);
-    mloc = vmax2(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = vmax2(mloc, __shfl_xor(mloc, 32, 64));
+    mloc = max_xor16(mloc);
+    mloc = max_xor32(mloc);
     // lazy rescale (attention.hip T13): the running max moves only when it grew by > 8 (log2 units)
     const float m_old = m_run;
     const float m_cand = (m_old == -INFINITY ? 0.f : m_old) + mloc;
@@ -246,8 +246,8 @@ __global__ void __launch_bounds__(256, 1) attn512_kernel(A5Args a) {
   }
 
   float l = l_run;
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  l = sum_xor16(l);
+  l = sum_xor32(l);
   if (qi >= a.Nq) return;
   if constexpr (S_ONE) {
     const float inv = l > 0.f ? 1.f / l : 0.f;

@@ -30,6 +30,29 @@ __device__ __forceinline__ float vmax2(float a, float b) {
   return r;
 }
 
+// Lane pairs (l, l ^ 16) and (l, l ^ 32) combined with the gfx950 lane-swap VALU ops instead of
+// __shfl_xor, which hipcc lowers to ds_bpermute_b32 (an LDS round trip in the softmax's critical
+// chain).  permlane{16,32}_swap(x, x) returns {x with its odd 16-lane rows (upper 32 lanes) replaced by
+// the even rows (lower half), x with its even rows (lower half) replaced by the odd rows (upper half)}:
+// in every lane one element is x[l] and the other x[l ^ 16] (x[l ^ 32]).  max / + of the pair are
+// exact and commutative, so the results are bitwise those of the shuffle forms.
+__device__ __forceinline__ float max_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // n zero-initialised int tickets for one launch on stream s (conv.hip's per-device pool): a region
 // of its own per graph-captured launch, one shared region per stream for eager launches (same-
 // stream kernels are serialised).  The launch's last arriving block re-arms its ticket to 0.

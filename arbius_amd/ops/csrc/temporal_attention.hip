@@ -10,7 +10,11 @@
 //   softmax over keys: in-lane over the 4 C rows x key tiles, then xor 16/32
 //   O^T = V^T P^T: P^T is consumed from the S^T accumulators in place through
 //                a permuted key order (slot 8g+j <-> key tile/row held by lane
-//                group g), V^T gathered with the same permutation.
+//                group g); V^T comes from the wave's V rows staged in LDS by
+//                16-byte loads and read back with the CDNA4 transposing read
+//                ds_read_b64_tr_b16 (the flash kernel's PV fragment path, row
+//                stride 16*(odd) elements: conflict free) - round 5 gathered it
+//                with 2-byte loads, 32 per lane (MFMA:VALU 1:45, pmc_r4_zeroscope).
 //
 // Activations stay in the UNet's frame-major channels-last layout
 // [B*F, H, W, C] (fused QKV adds a 3x): element (b, f, p, h, d) is at
@@ -63,18 +67,30 @@ __global__ void __launch_bounds__(256) temporal_attn_kernel(TAArgs a) {
   }
   // V^T as the A operand of O^T, permuted key slots: slot 8g+j <-> key
   //   j < 4: tile 2s, row 4g+j      j >= 4: tile 2s+1, row 4g+j-4
+  // V rows [0, 32*KT32) of this wave's problem -> LDS (keys >= F zero), 16-byte chunks
+  constexpr int VROWT = 16 * (DT | 1);
+  constexpr int CPR = DD / 8;
+  __shared__ __attribute__((aligned(16))) bf16_t sV[4][32 * KT32 * VROWT];
+  bf16_t* myV = sV[wave];
+#pragma unroll
+  for (int c = lane; c < 32 * KT32 * CPR; c += 64) {
+    const int row = c / CPR, col = (c % CPR) * 8;
+    st16(&myV[row * VROWT + col], row < F ? ld16(vb + row * a.v_sf + col) : make_uint4(0, 0, 0, 0));
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's rows are in LDS (reads are wave-local)
+  __builtin_amdgcn_wave_barrier();
   bf16x8 vf[KT32][DT];
+  const int qq = (lane & 15) >> 2, pp = lane & 3;
 #pragma unroll
   for (int s = 0; s < KT32; ++s) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      u16x8 u;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int key = (j < 4) ? (2 * s) * 16 + 4 * g + j : (2 * s + 1) * 16 + 4 * g + (j - 4);
-        u[j] = key < F ? vb[key * a.v_sf + dt * 16 + r16] : (unsigned short)0;
-      }
-      vf[s][dt] = __builtin_bit_cast(bf16x8, u);
+      const bf16_t* a0 = &myV[(32 * s + 4 * g + qq) * VROWT + 16 * dt + 4 * pp];
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0 + 16 * VROWT));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      vf[s][dt] = __builtin_bit_cast(bf16x8, vv);
     }
   }
 
@@ -105,8 +121,8 @@ __global__ void __launch_bounds__(256) temporal_attn_kernel(TAArgs a) {
       }
       mx = vmax3(mx, vmax2(sc[kt][0], sc[kt][1]), vmax2(sc[kt][2], sc[kt][3]));   // common.h
     }
-    mx = vmax2(mx, __shfl_xor(mx, 16, 64));
-    mx = vmax2(mx, __shfl_xor(mx, 32, 64));
+    mx = max_xor16(mx);
+    mx = max_xor32(mx);
     float sum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
@@ -117,8 +133,8 @@ __global__ void __launch_bounds__(256) temporal_attn_kernel(TAArgs a) {
         sum += e;
       }
     }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
+    sum = sum_xor16(sum);
+    sum = sum_xor32(sum);
     f32x4 oc[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) oc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -58,6 +58,24 @@ def main():
         s[0] += dev_us
         s[1] += 1
         s[2].update(k.name[:60] for k in ev.kernels)
+    # device copies (hipMemcpy*: the __amd_rocclr_copyBuffer blit kernels of the PMC passes) by the
+    # source line of the runtime call, or of the nearest enclosing op with a stack
+    copies = collections.defaultdict(lambda: [0, 0.0])
+    for ev in prof.events():
+        if ev.device_type.name != "CPU" or "emcpy" not in ev.name and "emset" not in ev.name:
+            continue
+        where, e = "?", ev
+        while e is not None and where == "?":
+            for fr in e.stack or []:
+                if "/arbius_amd/" in fr or "/scripts/" in fr:
+                    where = fr.split("/arbius_amd/")[-1]
+                    break
+            e = e.cpu_parent
+        c = copies[(ev.name, where)]
+        c[0] += 1
+        c[1] += sum(k.duration for k in ev.kernels) if ev.kernels else 0.0
+    for (name, where), (n, us) in sorted(copies.items(), key=lambda kv: -kv[1][0])[:20]:
+        print(json.dumps({"copy_api": name, "site": where, "calls": n, "gpu_ms": round(us / 1e3, 3)}), flush=True)
     total = sum(v[0] for v in sites.values())
     print(json.dumps({"model": a.model, "steps": a.steps, "aten_gpu_ms": round(total / 1e3, 3)}), flush=True)
     for (name, where), (us, n, ks) in sorted(sites.items(), key=lambda kv: -kv[1][0])[:40]:

@@ -783,6 +783,35 @@ def test_flash_attention_pipelined_ring_bitwise(cuda, B, N, Nk, H, D, causal):
     assert _rel(piped, r) < 2e-2
 
 
+@pytest.mark.parametrize("B,N,Nk,H,D,causal", [(16, 4096, 4096, 8, 40, False), (2, 4096, 4096, 8, 40, False),
+                                               (8, 1024, 1024, 10, 64, False), (3, 2880, 2880, 5, 64, False),
+                                               (4, 2000, 2000, 8, 40, True), (8, 1500, 700, 4, 64, False),
+                                               (32, 1100, 1100, 8, 32, False), (16, 4096, 77, 8, 40, False),
+                                               (48, 700, 77, 8, 24, False), (2, 130, 130, 3, 40, True),
+                                               (4, 300, 333, 5, 64, False), (1, 64, 64, 1, 8, False)])
+def test_flash_attention_ilp_softmax_bitwise(cuda, B, N, Nk, H, D, causal):
+    """The ILP softmax (all query tiles of a key tile at once: max3 tree, gfx950 lane swaps, wave-uniform
+    lazy-rescale branch with per-lane selects) == the per-query-tile softmax, bit for bit - including
+    late rescales (a spiked second half of the keys), partial and causal tiles."""
+    torch.manual_seed(23)
+    q = torch.randn(B, N, H, D, device=cuda).bfloat16()
+    k = torch.randn(B, Nk, H, D, device=cuda).bfloat16() * 1.5
+    v = torch.randn(B, Nk, H, D, device=cuda).bfloat16()
+    k[B // 2, Nk // 2:] *= 8.0           # a late rescale in one batch entry
+    fn = _lib._fn("arb_set_attn_ilp")
+    try:
+        fn(0)
+        plain = _lib.flash_attention(q, k, v, 1 / math.sqrt(D), causal)
+        fn(1)
+        ilp = _lib.flash_attention(q, k, v, 1 / math.sqrt(D), causal)
+        ilp2 = _lib.flash_attention(q, k, v, 1 / math.sqrt(D), causal)
+    finally:
+        fn(1)
+    assert torch.equal(plain, ilp) and torch.equal(ilp, ilp2)
+    r = ref.attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), causal)
+    assert _rel(ilp, r) < 2e-2
+
+
 @pytest.mark.parametrize("B,N,Nk,H,D,causal", [(8, 4096, 4096, 8, 40, False), (8, 1024, 1024, 8, 80, False),
                                                (2, 77, 77, 12, 64, True), (2, 256, 256, 8, 160, False),
                                                (4, 300, 333, 5, 64, False), (2, 130, 130, 3, 40, True)])
