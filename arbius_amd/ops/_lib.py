@@ -43,6 +43,7 @@ _SIGS = {
     "arb_set_stag2_buf": (None, [c_int]),
     "arb_set_attn_pp": (None, [c_int]),
     "arb_set_attn_ilp": (None, [c_int]),
+    "arb_set_attn_glds": (None, [c_int]),
     "arb_conv2d_nhwc_tld": (c_int, [c_void_p] * 4 + [c_int] + [c_void_p] * 4 + [c_int] * 12 + [c_void_p]),
     "arb_conv2d_nhwc_f16": (c_int, [c_void_p] * 7 + [c_int] * 11 + [c_void_p]),
     "arb_group_norm_table": (c_int, [c_void_p] * 4 + [c_float] + [c_void_p] * 2 + [c_int] * 4 + [c_float, c_void_p]),
@@ -84,6 +85,10 @@ _SIGS = {
     "arb_rgb_to_yuv420": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "arb_attention512": (c_int, [c_void_p] * 5 + [c_int] * 4 + [c_float, c_void_p, c_void_p]),
     "arb_attention512_workspace": (c_long, [c_int] * 4),
+    "arb_h264_intra_workspace": (c_size_t, [c_int] * 3),
+    "arb_h264_intra_encode": (c_int, [c_void_p] * 3 + [c_int] * 4 + [c_void_p, c_void_p, ctypes.c_longlong, c_void_p,
+                                                                    c_void_p]),
+    "arb_h264_intra_host": (c_int, [c_void_p] * 3 + [c_int] * 4 + [c_void_p, ctypes.c_longlong, c_void_p]),
 }
 
 
@@ -122,7 +127,8 @@ def loaded() -> bool:
 _AUDIT = None
 _HOST_SYMBOLS = ("arb_conv2d_plan", "arb_conv_family", "arb_conv2d_workspace", "arb_group_norm_workspace",
                  "arb_group_norm_slice_ok",
-                 "arb_rvm_args_sizes", "arb_attention512_workspace")
+                 "arb_rvm_args_sizes", "arb_attention512_workspace", "arb_h264_intra_workspace",
+                 "arb_h264_intra_host")
 
 
 def auditing() -> bool:
@@ -1036,4 +1042,57 @@ def rgb_to_yuv420(x, out=None):
         raise ValueError("rgb_to_yuv420: bad destination planes")
     _check(_fn("arb_rgb_to_yuv420")(_p(x), _p(y), _p(cb), _p(cr), T, H, W, _stream()), "rgb_to_yuv420")
     return y, cb, cr
+
+
+def _h264_planes(y, cb, cr):
+    if y.dim() != 3 or y.dtype != torch.uint8:
+        raise ValueError("h264_intra: y uint8 [F, H16, W16]")
+    F, H16, W16 = y.shape
+    if F < 1 or H16 % 16 or W16 % 16 or H16 < 16 or W16 < 16:
+        raise ValueError("h264_intra: planes must be macroblock-padded (multiples of 16)")
+    for c in (cb, cr):
+        if c.dtype != torch.uint8 or tuple(c.shape) != (F, H16 // 2, W16 // 2):
+            raise ValueError("h264_intra: cb / cr uint8 [F, H16 / 2, W16 / 2]")
+    if not all(t.is_contiguous() for t in (y, cb, cr)):
+        raise ValueError("h264_intra: planes must be contiguous")
+    return int(F), int(H16), int(W16)
+
+
+def h264_intra_capacity(F: int, H16: int, W16: int) -> int:
+    """Output bytes reserved for F pictures: 2 bytes per 4:2:0 sample (a picture past it is re-encoded
+    on the host)."""
+    return F * (H16 * W16 * 3 + 64)
+
+
+def h264_intra_encode(y, cb, cr, qp: int):
+    """avc-intra slices of F pictures on the GPU (csrc/h264_intra.hip): macroblock-padded 4:2:0 planes
+    (device uint8) -> (out, meta) device tensors; picture f's RBSP is out[meta[f]:] with
+    meta[2 + F + f] bits before the stop bit, meta[F + 1] != 0 on an error (the caller falls back
+    to the native encoder).  Queued on the current stream; nothing is synchronised here."""
+    F, H16, W16 = _h264_planes(y, cb, cr)
+    if not 0 <= int(qp) <= 51:
+        raise ValueError("h264_intra: qp in [0, 51]")
+    ws = torch.empty(int(_fn("arb_h264_intra_workspace")(F, W16, H16)), dtype=torch.uint8, device=y.device)
+    cap = h264_intra_capacity(F, H16, W16)
+    out = torch.empty(cap, dtype=torch.uint8, device=y.device)
+    meta = torch.empty(2 * F + 2, dtype=torch.int64, device=y.device)
+    _check(_fn("arb_h264_intra_encode")(_p(y), _p(cb), _p(cr), F, W16, H16, int(qp), _p(ws), _p(out), cap, _p(meta),
+                                        _stream()), "h264_intra_encode")
+    return out, meta
+
+
+def h264_intra_host(y, cb, cr, qp: int):
+    """The GPU encoder's per-macroblock functions run on the CPU (numpy planes) -> (out, meta) numpy
+    arrays in the layout of ``h264_intra_encode`` (tests on machines without a GPU)."""
+    import numpy as np
+    yt, cbt, crt = (torch.from_numpy(np.ascontiguousarray(a)) for a in (y, cb, cr))
+    F, H16, W16 = _h264_planes(yt, cbt, crt)
+    cap = h264_intra_capacity(F, H16, W16)
+    out = np.zeros(cap, np.uint8)
+    meta = np.zeros(2 * F + 2, np.int64)
+    rc = _fn("arb_h264_intra_host")(yt.data_ptr(), cbt.data_ptr(), crt.data_ptr(), F, W16, H16, int(qp),
+                                    out.ctypes.data, cap, meta.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"h264_intra_host failed ({rc})")
+    return out, meta
 

@@ -61,7 +61,8 @@ __device__ __attribute__((aligned(16))) uint4 g_attn_ones[1] = {{0x3F80u, 0u, 0u
 // by (row & 7) on the SOURCE address (lane-linear LDS image, rule 21) and on the QK read; V rows
 // are VROW/8 chunks, already lane-linear; padding chunks read a zero page, V's row-sum column a
 // ones page.  One LDS array for everything (hipcc's vmcnt trap with two __shared__ objects).
-template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false, bool PP = false, bool PS = true, bool ILP = true>
+template <int KSTEPS, int DT, int QT, bool ONES, bool GLDS = false, bool PP = false, bool PS = true, bool ILP = true,
+          bool PFX = false>
 __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   static_assert(!GLDS || KSTEPS == 2, "LDS-DMA staging: 8-chunk K rows only");
   constexpr int KROW = GLDS ? KSTEPS * 32 : KSTEPS * 32 + 8;   // K tile row (elements)
@@ -258,7 +259,32 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
       vb0[i] = gvm[i] == 1 ? (const char*)gv[i] : gvm[i] == 2 ? (const char*)g_attn_ones : (const char*)g_attn_zero;
   }
   auto issue_kv = [&](int kv, bf16_t* dst) __attribute__((always_inline)) {
-    const long ko = (long)kv * a.k_sn * 2, vo = (long)kv * a.v_sn * 2;   // bytes, uniform
+    if (PFX && kv < a.Np) {
+      // a tile holding PREFIX keys (Kandinsky joint attention: the first one or two tiles): every row
+      // picks its segment - prefix row j from kp/vp, main row j - Np from k/v
+#pragma unroll
+      for (int i = 0; i < KBW; ++i) {
+        const int j = kv + gkr[i], col = ((lane & 7) ^ (gkr[i] & 7)) * 8;
+        const void* src = !gkm[i] || j >= a.Nk ? (const void*)g_attn_zero
+                          : j < a.Np ? (const void*)(kpbase + (long)j * a.kp_sn + col)
+                                     : (const void*)(kbase + (long)(j - a.Np) * a.k_sn + col);
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (wave + 4 * i) * 512), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < VBW; ++i) {
+        const int j = kv + gvr[i], col = ((gvb[i] * 64 + lane) % VCPR) * 8;
+        const void* src = gvm[i] == 2 ? (const void*)g_attn_ones
+                          : gvm[i] != 1 || j >= a.Nk ? (const void*)g_attn_zero
+                          : j < a.Np ? (const void*)(vpbase + (long)j * a.vp_sn + col)
+                                     : (const void*)(vbase + (long)(j - a.Np) * a.v_sn + col);
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + KV_BLK * KROW + gvb[i] * 512), 16, 0, 0);
+      }
+      return;
+    }
+    // main-segment tile: the row offset is uniform (PFX: the kernel serves a prefix launch; the others
+    // never see one and keep the prefix-free addressing and register budget)
+    const int np = PFX ? a.Np : 0;
+    const long ko = (long)(kv - np) * a.k_sn * 2, vo = (long)(kv - np) * a.v_sn * 2;   // bytes
     const bool full = kv + KV_BLK <= a.Nk;
 #pragma unroll
     for (int i = 0; i < KBW; ++i) {
@@ -652,13 +678,16 @@ __global__ void __launch_bounds__(256, 2) flash_attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+static int g_attn_glds = -1;
 static bool attn_glds_enabled() {
-  static const bool on = [] {
+  if (g_attn_glds < 0) {
     const char* e = std::getenv("ARB_ATTN_GLDS");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
+    g_attn_glds = (e == nullptr || e[0] != '0') ? 1 : 0;
+  }
+  return g_attn_glds == 1;
 }
+// register-staged K/V (0) vs LDS-DMA (1, default): bitwise-equal paths (test hook / A/B)
+ARB_API void arb_set_attn_glds(int on) { g_attn_glds = on ? 1 : 0; }
 
 // A/B switch (bitwise-equal paths): ARB_ATTN_PP=1 runs the software-pipelined K / V ring (PV of
 // tile j-1 overlapped with QK and softmax of tile j) on the LDS-DMA kernels
@@ -703,14 +732,23 @@ static void launch_fa_ps(const AttnArgs& a, hipStream_t s) {
   const int nqb = (a.Nq + QBLK - 1) / QBLK;
   dim3 grid(nqb * a.H * a.B);
   if constexpr (KSTEPS == 2) {
-    if (a.Np == 0 && attn_glds_enabled()) {     // LDS-DMA staging (no prefix segment)
+    if (attn_glds_enabled()) {     // LDS-DMA staging (a K/V prefix segment included)
       // pipelined variants that fit the 256-VGPR budget of two waves per SIMD without spilling
-      // (the 4-q-tile d = 48 / 64 ones carry two S tile sets + P(j-1) past it)
+      // (the 4-q-tile d = 48 / 64 ones carry two S tile sets + P(j-1) past it); no prefix
       if constexpr (PS && (QT <= 2 || DT == 3)) {
-        if (attn_pp_enabled() && (QT <= 2 || (a.D & 15))) {
+        if (a.Np == 0 && attn_pp_enabled() && (QT <= 2 || (a.D & 15))) {
           if (a.D & 15) flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true, true, PS><<<grid, 256, 0, s>>>(a);
           else if constexpr (QT <= 2)
             flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, true, PS><<<grid, 256, 0, s>>>(a);
+          return;
+        }
+      }
+      if constexpr (QT <= 2) {   // K/V prefix segment (joint attention; never a 4-q-tile launch)
+        if (a.Np > 0) {
+          if (a.D & 15)
+            flash_attn_fwd_kernel<KSTEPS, DT, QT, true, true, false, PS, true, true><<<grid, 256, 0, s>>>(a);
+          else
+            flash_attn_fwd_kernel<KSTEPS, DT, QT, false, true, false, PS, true, true><<<grid, 256, 0, s>>>(a);
           return;
         }
       }

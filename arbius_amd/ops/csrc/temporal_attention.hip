@@ -94,70 +94,92 @@ __global__ void __launch_bounds__(256) temporal_attn_kernel(TAArgs a) {
     }
   }
 
+  // two query tiles per pass (F = 24: both of them): their QK -> max -> exp -> PV chains are independent,
+  // so the scheduler interleaves them; per query tile the arithmetic (and the order of the row sum) is
+  // unchanged.  A second tile past F (odd tile counts) computes masked garbage and stores nothing.
   const int QT = (F + 15) >> 4;
-  for (int qt = 0; qt < QT; ++qt) {
-    const int qrow = qt * 16 + r16;
-    bf16x8 qf[KS];
+  for (int qt0 = 0; qt0 < QT; qt0 += 2) {
+    int qrow[2];
+    f32x4 sc[2][NKT];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      qf[ks] = qrow < F ? __builtin_bit_cast(bf16x8, ld16(qb + qrow * a.q_sf + ks * 32 + 8 * g)) : zero8;
-    f32x4 sc[NKT];
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      sc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 2; ++u) {
+      qrow[u] = (qt0 + u) * 16 + r16;
+      bf16x8 qf[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][ks], qf[ks], sc[kt], 0, 0, 0);
-    }
-    // sc[kt][r] = S^T[key = kt*16 + 4g + r][query = qt*16 + r16]
-    float mx = -INFINITY;
+        qf[ks] = qrow[u] < F ? __builtin_bit_cast(bf16x8, ld16(qb + qrow[u] * a.q_sf + ks * 32 + 8 * g)) : zero8;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
+      for (int kt = 0; kt < NKT; ++kt) {
+        sc[u][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt * 16 + 4 * g + r;
-        const float v = key < F ? sc[kt][r] * a.scale_log2 : -INFINITY;
-        sc[kt][r] = v;
-      }
-      mx = vmax3(mx, vmax2(sc[kt][0], sc[kt][1]), vmax2(sc[kt][2], sc[kt][3]));   // common.h
-    }
-    mx = max_xor16(mx);
-    mx = max_xor32(mx);
-    float sum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = __builtin_amdgcn_exp2f(sc[kt][r] - mx);
-        sc[kt][r] = e;
-        sum += e;
+        for (int ks = 0; ks < KS; ++ks)
+          sc[u][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][ks], qf[ks], sc[u][kt], 0, 0, 0);
       }
     }
-    sum = sum_xor16(sum);
-    sum = sum_xor32(sum);
-    f32x4 oc[DT];
+    // sc[u][kt][r] = S^T[key = kt*16 + 4g + r][query = (qt0 + u)*16 + r16]
+    float mx[2], sum[2];
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) oc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 2; ++u) {
+      mx[u] = -INFINITY;
 #pragma unroll
-    for (int s = 0; s < KT32; ++s) {
-      u16x8 pu;
+      for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pu[j] = f2bf(sc[2 * s][j]);
-        pu[4 + j] = f2bf(sc[2 * s + 1][j]);
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * 16 + 4 * g + r;
+          const float v = key < F ? sc[u][kt][r] * a.scale_log2 : -INFINITY;
+          sc[u][kt][r] = v;
+        }
+        mx[u] = vmax3(mx[u], vmax2(sc[u][kt][0], sc[u][kt][1]), vmax2(sc[u][kt][2], sc[u][kt][3]));
       }
-      const bf16x8 pb = __builtin_bit_cast(bf16x8, pu);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) oc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][dt], pb, oc[dt], 0, 0, 0);
     }
-    // oc[dt][r] = O^T[d = dt*16 + 4g + r][query = qrow]
-    if (qrow < F) {
-      const float inv = 1.f / sum;
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const uint32_t w0 = (uint32_t)f2bf(oc[dt][0] * inv) | ((uint32_t)f2bf(oc[dt][1] * inv) << 16);
-        const uint32_t w1 = (uint32_t)f2bf(oc[dt][2] * inv) | ((uint32_t)f2bf(oc[dt][3] * inv) << 16);
-        *reinterpret_cast<uint2*>(ob + qrow * a.o_sf + dt * 16 + 4 * g) = make_uint2(w0, w1);
+    for (int u = 0; u < 2; ++u) mx[u] = max_xor16(mx[u]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) mx[u] = max_xor32(mx[u]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      sum[u] = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(sc[u][kt][r] - mx[u]);
+          sc[u][kt][r] = e;
+          sum[u] += e;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) sum[u] = sum_xor16(sum[u]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) sum[u] = sum_xor32(sum[u]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x4 oc[DT];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) oc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KT32; ++s) {
+        u16x8 pu;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pu[j] = f2bf(sc[u][2 * s][j]);
+          pu[4 + j] = f2bf(sc[u][2 * s + 1][j]);
+        }
+        const bf16x8 pb = __builtin_bit_cast(bf16x8, pu);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+          oc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[s][dt], pb, oc[dt], 0, 0, 0);
+      }
+      // oc[dt][r] = O^T[d = dt*16 + 4g + r][query = qrow]
+      if (qrow[u] < F) {
+        const float inv = 1.f / sum[u];
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const uint32_t w0 = (uint32_t)f2bf(oc[dt][0] * inv) | ((uint32_t)f2bf(oc[dt][1] * inv) << 16);
+          const uint32_t w1 = (uint32_t)f2bf(oc[dt][2] * inv) | ((uint32_t)f2bf(oc[dt][3] * inv) << 16);
+          *reinterpret_cast<uint2*>(ob + qrow[u] * a.o_sf + dt * 16 + 4 * g) = make_uint2(w0, w1);
+        }
       }
     }
   }

@@ -37,10 +37,44 @@ def main():
         pipe.cfg.num_steps = a.steps
     if a.model in ("zeroscopev2xl", "damo"):   # BASELINE config #4: 576 x 320 x 24 frames
         inp.update(width=a.res or 576, height=320 if a.model == "zeroscopev2xl" else inp["height"], num_frames=24)
-    pipe.solve(inp)
+    if hasattr(pipe, "solve"):
+        run = lambda: pipe.solve(inp)  # noqa: E731
+    else:                              # image pipelines: the node's solve path
+        from arbius_amd.node.solver import solve_image
+        inp.update(guidance_scale=7, scheduler="DPMSolverMultistep")
+        run = lambda: solve_image(pipe, inp)  # noqa: E731
+    run()
     torch.cuda.synchronize()
+    # every tensor copy that touches the GPU (device <-> host, device <-> device), by the model source line:
+    # hipMemcpy* calls have no Python stack in the profiler, the dispatch mode sees the ATen op and the stack
+    import traceback
+    from torch.utils._python_dispatch import TorchDispatchMode
+    copies = collections.Counter()
+
+    class CopySites(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            name = str(func)
+            if name.startswith(("aten.copy_", "aten._to_copy", "aten.clone", "aten._copy_from")):
+                devs = {str(t.device) for t in list(args) + list((kwargs or {}).values()) if torch.is_tensor(t)}
+                dst = (kwargs or {}).get("device")
+                if dst is not None:
+                    devs.add(str(dst))
+                if any(d.startswith("cuda") for d in devs):
+                    site = "?"
+                    for fr in reversed(traceback.extract_stack()[:-1]):
+                        if "/arbius_amd/" in fr.filename:
+                            site = f"{fr.filename.split('/arbius_amd/')[1]}:{fr.lineno}"
+                            break
+                    copies[(name.split(".")[1] if "." in name else name, "->".join(sorted(devs)), site)] += 1
+            return func(*args, **(kwargs or {}))
+
+    with CopySites():
+        run()
+        torch.cuda.synchronize()
+    for (op, devs, site), n in copies.most_common(25):
+        print(json.dumps({"copy_op": op, "devices": devs, "site": site, "calls": n}), flush=True)
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
-        pipe.solve(inp)
+        run()
         torch.cuda.synchronize()
     sites = collections.defaultdict(lambda: [0.0, 0, set()])
     for ev in prof.events():
@@ -58,24 +92,6 @@ def main():
         s[0] += dev_us
         s[1] += 1
         s[2].update(k.name[:60] for k in ev.kernels)
-    # device copies (hipMemcpy*: the __amd_rocclr_copyBuffer blit kernels of the PMC passes) by the
-    # source line of the runtime call, or of the nearest enclosing op with a stack
-    copies = collections.defaultdict(lambda: [0, 0.0])
-    for ev in prof.events():
-        if ev.device_type.name != "CPU" or "emcpy" not in ev.name and "emset" not in ev.name:
-            continue
-        where, e = "?", ev
-        while e is not None and where == "?":
-            for fr in e.stack or []:
-                if "/arbius_amd/" in fr or "/scripts/" in fr:
-                    where = fr.split("/arbius_amd/")[-1]
-                    break
-            e = e.cpu_parent
-        c = copies[(ev.name, where)]
-        c[0] += 1
-        c[1] += sum(k.duration for k in ev.kernels) if ev.kernels else 0.0
-    for (name, where), (n, us) in sorted(copies.items(), key=lambda kv: -kv[1][0])[:20]:
-        print(json.dumps({"copy_api": name, "site": where, "calls": n, "gpu_ms": round(us / 1e3, 3)}), flush=True)
     total = sum(v[0] for v in sites.values())
     print(json.dumps({"model": a.model, "steps": a.steps, "aten_gpu_ms": round(total / 1e3, 3)}), flush=True)
     for (name, where), (us, n, ks) in sorted(sites.items(), key=lambda kv: -kv[1][0])[:40]:

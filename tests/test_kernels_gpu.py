@@ -464,6 +464,13 @@ def test_flash_attention_kv_prefix(cuda, B, Nq, Np, H, D):
     assert _rel(o, r) < 2e-2
     oc = _lib.flash_attention(q, torch.cat([kp, k], 1), torch.cat([vp, v], 1), 1 / math.sqrt(D), False)
     assert torch.equal(o, oc), "prefix segment must be bitwise identical to the concatenated keys"
+    fn = _lib._fn("arb_set_attn_glds")      # register-staged K/V (the round-5 prefix path) == LDS-DMA
+    try:
+        fn(0)
+        o_reg = _lib.flash_attention(q, k, v, 1 / math.sqrt(D), False, (kp, vp))
+    finally:
+        fn(1)
+    assert torch.equal(o, o_reg)
 
 
 @pytest.mark.parametrize("cfg", [0, 3, 5])

@@ -202,8 +202,8 @@ def test_cpu_budget_caps():
 def test_eight_workers_two_killed_under_load_keep_cids():
     """8 gloo ranks (weights broadcast from rank 0), solves in flight on 6, two workers
     hard-killed at once mid-load; their tasks fail over (the miner's retry re-dispatches them), both
-    respawn, and every CID - before, during and after - equals the solo CID (16 solves in flight).  A host-CPU cap keeps the
-    model's tasks on ranks 0..5."""
+    respawn, and every CID - before, during and after - equals the solo CID (16 solves in flight).  A
+    host-CPU cap keeps the model's tasks on ranks 0..5."""
     seeds = list(range(16))
     ref = {s: LocalSolverPool("cpu", tiny=True).solve_sync(MODEL, "t", dict(INP, seed=s)).cid for s in seeds[:6]}
 
