@@ -46,6 +46,10 @@ _PINNED_OUT_MAX = int(os.environ.get("ARB_RVM_PINNED_OUT_MAX", str(640 << 20)))
 # the solve path downloads GPU-converted 4:2:0 planes instead of RGB (ARB_RVM_GPU_YUV=0: RGB + host
 # conversion, A/B; same bytes)
 _GPU_YUV = os.environ.get("ARB_RVM_GPU_YUV", "1") != "0"
+# ... and encodes them on the GPU too (ops/csrc/h264_intra.hip, the native encoder's bytes): only the
+# compressed slices come back, the host keeps emulation prevention + the MP4 mux
+# (ARB_RVM_GPU_H264=0: download the planes and encode on the host, A/B)
+_GPU_H264 = os.environ.get("ARB_RVM_GPU_H264", "1") != "0"
 # the slot thread's waits on its uploads / downloads yield the CPU (hipEventBlockingSync) instead of
 # spinning: RVM is host-bound (profiles/cpu_budget_r5.md) and a spinning wait takes a core from the
 # H.264 encoders of the other slots' tails (ARB_RVM_BLOCKING_SYNC=0: spin, A/B)
@@ -402,6 +406,8 @@ class RVMPipeline(PipelineBase):
         T, H, W, _ = frames.shape
         n = self.cfg.chunk
         yuv = yuv and _GPU_YUV
+        if yuv and _GPU_H264:
+            return self._matte_fast_h264(frames, output_type, ratio)
         nout = T * ((H + 15) // 16 * 16) * ((W + 15) // 16 * 16) * 3 // 2 if yuv else T * H * W * 3
         if _PINNED_OUT and nout <= _PINNED_OUT_MAX:
             # the page-locked result array comes from PyTorch's caching host allocator,
@@ -495,6 +501,65 @@ class RVMPipeline(PipelineBase):
             from ..utils.mp4 import Yuv420Clip
             return Yuv420Clip(*(pl.numpy() for pl in planes), W, H, keep=res)
         return res.view(T, H, W, 3).numpy()
+
+    def _matte_fast_h264(self, frames: np.ndarray, output_type: str, ratio: float):
+        """As ``_matte_fast_pinned`` with ``yuv``, but the 4:2:0 planes stay on the GPU and are encoded
+        there (``ops.h264_intra_encode``): returns a ``utils.mp4.H264IntraClip`` (the slices' RBSPs,
+        page-locked) whose MP4 is byte-identical to the host encode of the same planes.  A clip the
+        GPU encoder flags (output capacity) is downloaded as planes and encoded on the host."""
+        from .rvm_fast import FastMatting
+        from ..utils.mp4 import INTRA_QP, H264IntraClip, Yuv420Clip
+        if getattr(self, "_fast", None) is None:
+            self._fast = FastMatting(self.net)
+        T, H, W, _ = frames.shape
+        n = self.cfg.chunk
+        fb = H * W * 3
+        H16, W16 = (H + 15) // 16 * 16, (W + 15) // 16 * 16
+        dev = self.device
+        planes = (torch.empty(T, H16, W16, dtype=torch.uint8, device=dev),
+                  torch.empty(T, H16 // 2, W16 // 2, dtype=torch.uint8, device=dev),
+                  torch.empty(T, H16 // 2, W16 // 2, dtype=torch.uint8, device=dev))
+        stream = torch.cuda.current_stream(dev)
+        rec = [None] * 4
+        ups = []
+        for j, i in enumerate(range(0, T, n)):
+            beat()
+            t = min(n, T - i)
+            st = self._pinned(("in", j % 2), n * fb)[:t * fb]
+            if len(ups) >= 2:
+                ups[-2].synchronize()     # the staging buffer's previous upload has been consumed
+            if _NUMPY_IN:
+                st.numpy()[:] = frames[i:i + t].reshape(-1)
+            else:
+                st.copy_(torch.from_numpy(np.ascontiguousarray(frames[i:i + t]).reshape(-1)))
+            x = st.to(dev, non_blocking=True).view(t, H, W, 3)
+            ev = _event()
+            ev.record(stream)
+            ups.append(ev)
+            out, rec = self._fast(x, rec, ratio, output_type, GREEN)
+            ops.rgb_to_yuv420(out, out=tuple(p[i:i + t] for p in planes))
+        enc, meta = ops.h264_intra_encode(*planes, INTRA_QP)
+        meta_h = torch.empty(meta.numel(), dtype=torch.int64, pin_memory=True)
+        meta_h.copy_(meta, non_blocking=True)
+        done = _event()
+        done.record(stream)
+        done.synchronize()
+        m = meta_h.numpy()
+        if m[T + 1] != 0:                 # flagged: the host encoder takes the planes (same bytes)
+            host = [torch.empty(p.shape, dtype=torch.uint8, pin_memory=True) for p in planes]
+            for h, p in zip(host, planes):
+                h.copy_(p, non_blocking=True)
+            done = _event()
+            done.record(stream)
+            done.synchronize()
+            return Yuv420Clip(*(h.numpy() for h in host), W, H, keep=host)
+        total = int(m[T])
+        buf = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+        buf[:total].copy_(enc[:total], non_blocking=True)
+        done = _event()
+        done.record(stream)
+        done.synchronize()
+        return H264IntraClip(buf.numpy()[:total], m.copy(), W, H, INTRA_QP, keep=buf)
 
     @torch.no_grad()
     def matte_for_encode(self, frames: np.ndarray, output_type: str = "green-screen"):

@@ -130,12 +130,9 @@ struct BitReader {
   }
 };
 
-std::string add_emulation_prevention(const std::string& rbsp) {
+void append_emulation_prevented(std::string& out, const char* p, size_t n) {
   // copy runs up to each 00 00 pair (rare in coded data), then apply the 00 00 0x -> 00 00 03 0x rule
-  std::string out;
-  out.reserve(rbsp.size() + rbsp.size() / 64 + 4);
-  const char* p = rbsp.data();
-  const size_t n = rbsp.size();
+  out.reserve(out.size() + n + n / 64 + 4);
   size_t i = 0;
   int zeros = 0;
   while (i < n) {
@@ -155,6 +152,11 @@ std::string add_emulation_prevention(const std::string& rbsp) {
     zeros = b == 0 ? zeros + 1 : 0;
     ++i;
   }
+}
+
+std::string add_emulation_prevention(const std::string& rbsp) {
+  std::string out;
+  append_emulation_prevented(out, rbsp.data(), rbsp.size());
   return out;
 }
 
@@ -1935,6 +1937,12 @@ void parameter_sets(int width, int height, int qp, std::string& sps, std::string
   p.put(0, 1);    // redundant_pic_cnt_present_flag
   p.trailing();
   pps = std::string(1, char(0x68)) + add_emulation_prevention(p.out);
+}
+
+std::string rbsp_to_nal(uint8_t nal_header, const uint8_t* rbsp, size_t n) {
+  std::string out(1, char(nal_header));
+  append_emulation_prevented(out, reinterpret_cast<const char*>(rbsp), n);
+  return out;
 }
 
 std::string encode_idr(const uint8_t* y, const uint8_t* cb, const uint8_t* cr, int W, int H, int qp, int idr_pic_id,

@@ -21,6 +21,10 @@ struct Picture {          // decoded 4:2:0 planes at macroblock-padded size
 std::string encode_idr(const uint8_t* y, const uint8_t* cb, const uint8_t* cr, int W, int H, int qp,
                        int idr_pic_id, uint8_t* recon_y, uint8_t* recon_cb, uint8_t* recon_cr);
 
+// A NAL unit (header byte + emulation-prevented payload) from a finished RBSP, e.g. the GPU
+// encoder's slices (ops/csrc/h264_intra.hip): encode_idr's bytes for the same RBSP.
+std::string rbsp_to_nal(uint8_t nal_header, const uint8_t* rbsp, size_t n);
+
 // SPS + PPS NALs (header byte included, no start code) matching encode_idr's / encode_stream's slices.
 void parameter_sets(int width, int height, int qp, std::string& sps, std::string& pps, int max_refs = 1);
 

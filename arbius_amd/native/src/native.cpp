@@ -398,6 +398,34 @@ static py::tuple h264_encode_yuv420_frames(u8arr y, u8arr cb, u8arr cr, int W, i
   return py::make_tuple(py::bytes(sps), py::bytes(pps), out);
 }
 
+// The GPU intra encoder's output (ops/csrc/h264_intra.hip) -> IDR NAL units: buf holds every
+// picture's RBSP at meta[f] (bytes), meta[F + 2 + f] RBSP bits before the stop bit (the layout of
+// arb_h264_intra_encode / arb_h264_intra_host).  Same NALs as h264_encode_yuv420_frames.
+static py::list h264_nals_from_rbsp(py::array_t<uint8_t, py::array::c_style> buf,
+                                    py::array_t<int64_t, py::array::c_style> meta, int F, int threads) {
+  auto bb = buf.request(), bm = meta.request();
+  if (F < 1 || bm.ndim != 1 || bm.shape[0] < 2 * F + 2 || bb.ndim != 1)
+    throw std::invalid_argument("h264_nals_from_rbsp: meta [2F + 2] int64, buf 1-D uint8");
+  const int64_t* m = static_cast<const int64_t*>(bm.ptr);
+  const uint8_t* b = static_cast<const uint8_t*>(bb.ptr);
+  if (m[F + 1] != 0) throw std::runtime_error("h264_nals_from_rbsp: the encoder flagged an error");
+  for (int f = 0; f < F; ++f) {
+    const int64_t bytes = (m[F + 2 + f] + 8) / 8;
+    if (m[f] < 0 || m[F + 2 + f] < 0 || m[f] + bytes > (int64_t)bb.shape[0])
+      throw std::invalid_argument("h264_nals_from_rbsp: picture outside buf");
+  }
+  std::vector<std::string> nals(F);
+  {
+    py::gil_scoped_release nogil;
+    run_parallel(F, threads, [&](int f) {
+      nals[f] = h264::rbsp_to_nal(0x65, b + m[f], (size_t)((m[F + 2 + f] + 8) / 8));
+    });
+  }
+  py::list out;
+  for (auto& n : nals) out.append(py::bytes(n));
+  return out;
+}
+
 // the host conversion on its own (tests: the GPU planes equal these)
 static py::tuple rgb_to_yuv420_planes(u8arr frames) {
   auto b = frames.request();
@@ -675,6 +703,8 @@ PYBIND11_MODULE(_native, m) {
         "H.264 I_PCM macroblock payload of one RGB frame");
   m.def("h264_encode_yuv420_frames", &h264_encode_yuv420_frames, py::arg("y"), py::arg("cb"), py::arg("cr"),
         py::arg("width"), py::arg("height"), py::arg("qp"), py::arg("threads") = 8, py::arg("nice") = 0);
+  m.def("h264_nals_from_rbsp", &h264_nals_from_rbsp, py::arg("buf"), py::arg("meta"), py::arg("frames"),
+        py::arg("threads") = 4, "GPU intra encoder RBSPs -> IDR NALs (emulation prevention)");
   m.def("rgb_to_yuv420_planes", &rgb_to_yuv420_planes, py::arg("frames"));
   m.def("h264_encode_rgb", &h264_encode_rgb, py::arg("frames"), py::arg("qp"), py::arg("threads") = 8,
         py::arg("nice") = 0, "H.264 CAVLC intra: RGB frames [F, H, W, 3] -> (sps, pps, [IDR NAL]); nice > 0 runs "

@@ -679,14 +679,27 @@ def native_loaded() -> bool:
     return _lib.loaded()
 
 
-def rgb_to_yuv420(x):
+def rgb_to_yuv420(x, out=None):
     """uint8 RGB frames [T, H, W, 3] -> the H.264 encoder's macroblock-padded BT.601 4:2:0 planes
-    (y [T, H16, W16], cb, cr [T, H16 / 2, W16 / 2]).  GPU: one HIP pass; CPU: the native host
-    conversion (the same integer arithmetic, so the same samples)."""
+    (y [T, H16, W16], cb, cr [T, H16 / 2, W16 / 2]).  GPU: one HIP pass (``out``: optional device
+    destination planes); CPU: the native host conversion (the same integer arithmetic, so the same
+    samples)."""
     if _hip(x):
-        return _lib.rgb_to_yuv420(x)
+        return _lib.rgb_to_yuv420(x, out)
+    if out is not None:
+        raise ValueError("rgb_to_yuv420: out= is for GPU planes")
     from .. import native
     return tuple(torch.from_numpy(p) for p in native.rgb_to_yuv420_planes(x.contiguous().numpy()))
+
+
+def h264_intra_encode(y, cb, cr, qp: int):
+    """avc-intra slices of macroblock-padded 4:2:0 planes (csrc/h264_intra.hip): GPU uint8 planes ->
+    (out, meta) device tensors, queued on the current stream (layout: native ``h264_nals_from_rbsp``);
+    CPU numpy / tensors -> the same functions run on the host (numpy out, meta)."""
+    if isinstance(y, torch.Tensor) and _hip(y):
+        return _lib.h264_intra_encode(y, cb, cr, qp)
+    as_np = [t.numpy() if isinstance(t, torch.Tensor) else t for t in (y, cb, cr)]
+    return _lib.h264_intra_host(*as_np, qp)
 
 
 def image_u8(x, mode: int):

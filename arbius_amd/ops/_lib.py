@@ -88,7 +88,9 @@ _SIGS = {
     "arb_h264_intra_workspace": (c_size_t, [c_int] * 3),
     "arb_h264_intra_encode": (c_int, [c_void_p] * 3 + [c_int] * 4 + [c_void_p, c_void_p, ctypes.c_longlong, c_void_p,
                                                                     c_void_p]),
-    "arb_h264_intra_host": (c_int, [c_void_p] * 3 + [c_int] * 4 + [c_void_p, ctypes.c_longlong, c_void_p]),
+    "arb_h264_intra_host": (c_int, [c_void_p] * 3 + [c_int] * 4 + [c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
+    "arb_set_h264_sync": (None, [c_int]),
+    "arb_h264_debug": (None, [c_void_p, c_int]),
 }
 
 
@@ -1064,7 +1066,7 @@ def h264_intra_capacity(F: int, H16: int, W16: int) -> int:
     return F * (H16 * W16 * 3 + 64)
 
 
-def h264_intra_encode(y, cb, cr, qp: int):
+def h264_intra_encode(y, cb, cr, qp: int, return_ws: bool = False):
     """avc-intra slices of F pictures on the GPU (csrc/h264_intra.hip): macroblock-padded 4:2:0 planes
     (device uint8) -> (out, meta) device tensors; picture f's RBSP is out[meta[f]:] with
     meta[2 + F + f] bits before the stop bit, meta[F + 1] != 0 on an error (the caller falls back
@@ -1078,10 +1080,10 @@ def h264_intra_encode(y, cb, cr, qp: int):
     meta = torch.empty(2 * F + 2, dtype=torch.int64, device=y.device)
     _check(_fn("arb_h264_intra_encode")(_p(y), _p(cb), _p(cr), F, W16, H16, int(qp), _p(ws), _p(out), cap, _p(meta),
                                         _stream()), "h264_intra_encode")
-    return out, meta
+    return (out, meta, ws) if return_ws else (out, meta)
 
 
-def h264_intra_host(y, cb, cr, qp: int):
+def h264_intra_host(y, cb, cr, qp: int, return_ws: bool = False):
     """The GPU encoder's per-macroblock functions run on the CPU (numpy planes) -> (out, meta) numpy
     arrays in the layout of ``h264_intra_encode`` (tests on machines without a GPU)."""
     import numpy as np
@@ -1090,9 +1092,10 @@ def h264_intra_host(y, cb, cr, qp: int):
     cap = h264_intra_capacity(F, H16, W16)
     out = np.zeros(cap, np.uint8)
     meta = np.zeros(2 * F + 2, np.int64)
+    ws = np.zeros(int(_fn("arb_h264_intra_workspace")(F, W16, H16)), np.uint8) if return_ws else None
     rc = _fn("arb_h264_intra_host")(yt.data_ptr(), cbt.data_ptr(), crt.data_ptr(), F, W16, H16, int(qp),
-                                    out.ctypes.data, cap, meta.ctypes.data)
+                                    out.ctypes.data, cap, meta.ctypes.data, None if ws is None else ws.ctypes.data)
     if rc != 0:
         raise RuntimeError(f"h264_intra_host failed ({rc})")
-    return out, meta
+    return (out, meta, ws) if return_ws else (out, meta)
 

@@ -238,6 +238,22 @@ class Yuv420Clip:
         return int(self.y.shape[0])
 
 
+class H264IntraClip:
+    """A clip already encoded by the GPU intra encoder (``ops.h264_intra_encode``): every picture's
+    slice RBSP in ``buf`` at ``meta[f]`` with ``meta[F + 2 + f]`` bits (the native
+    ``h264_nals_from_rbsp`` layout).  ``encode_mp4`` of it adds emulation prevention and muxes: the
+    bytes of ``encode_mp4`` of the same 4:2:0 planes (avc-intra at ``qp``)."""
+    __slots__ = ("buf", "meta", "width", "height", "qp", "keep")
+
+    def __init__(self, buf: np.ndarray, meta: np.ndarray, width: int, height: int, qp: int, keep=None):
+        self.buf, self.meta = buf, np.ascontiguousarray(meta, dtype=np.int64)
+        self.width, self.height, self.qp = int(width), int(height), int(qp)
+        self.keep = keep          # the pinned host block ``buf`` views
+
+    def __len__(self):
+        return (len(self.meta) - 2) // 2
+
+
 def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra", threads: int = 16,
                nice: int = 0) -> bytes:
     """uint8 RGB frames [H, W, 3] (all the same size), or one uint8 array [F, H, W, 3] (passed to
@@ -246,6 +262,8 @@ def encode_mp4(frames: Sequence[np.ndarray], fps: int, codec: str = "avc-intra",
     background tail next to GPU-feeding threads); bytes never depend on it."""
     if isinstance(frames, Yuv420Clip):
         return _encode_mp4_yuv(frames, fps, codec, threads, nice)
+    if isinstance(frames, H264IntraClip):
+        return _encode_mp4_slices(frames, fps, codec, threads)
     if isinstance(frames, np.ndarray) and frames.ndim == 4:
         if frames.dtype != np.uint8 or frames.shape[3] != 3:
             raise ValueError("encode_mp4: frames must be uint8 [F, H, W, 3]")
@@ -297,6 +315,21 @@ def _encode_mp4_yuv(clip: "Yuv420Clip", fps: int, codec: str, threads: int, nice
     sps, pps = sps_pps(W, H, INTRA_QP)
     _, _, nals = native.h264_encode_yuv420_frames(clip.y, clip.cb, clip.cr, W, H, INTRA_QP, threads, nice)
     return _mux(W, H, max(1, int(fps)), sps, pps, [[n] for n in nals], False, None)
+
+
+def _encode_mp4_slices(clip: "H264IntraClip", fps: int, codec: str, threads: int) -> bytes:
+    if codec != "avc-intra" or clip.qp != INTRA_QP:
+        raise ValueError("encode_mp4: an H264IntraClip is avc-intra at INTRA_QP")
+    from .. import native
+    if not native.loaded:
+        raise RuntimeError("encode_mp4: the native runtime is not built; run python -m arbius_amd.native.build")
+    F = len(clip)
+    if F < 1:
+        raise ValueError("encode_mp4: no frames")
+    nals = native.h264_nals_from_rbsp(np.ascontiguousarray(clip.buf, dtype=np.uint8).reshape(-1), clip.meta, F,
+                                      max(1, min(int(threads), 4)))
+    sps, pps = sps_pps(clip.width, clip.height, INTRA_QP)
+    return _mux(clip.width, clip.height, max(1, int(fps)), sps, pps, [[n] for n in nals], False, None)
 
 
 def _mux(W, H, fps, sps, pps, pics, pcm, sync) -> bytes:

@@ -147,18 +147,28 @@ def test_gpu_yuv420_equals_host_conversion(cuda, T, H, W):
 
 
 def test_rvm_solve_path_yuv_planes_encode_to_the_rgb_bytes(cuda, monkeypatch):
-    """The solve path downloads GPU-converted 4:2:0 planes (RVMPipeline.matte_for_encode): the MP4 is
-    byte-identical to encoding the RGB composite, on the pinned and on the staged download."""
+    """The solve path (RVMPipeline.matte_for_encode) encodes the GPU-converted 4:2:0 planes on the GPU
+    (csrc/h264_intra.hip): the MP4 is byte-identical to encoding the RGB composite on the host, and so
+    are the A/B paths - planes downloaded for the host encoder, the staged RGB download, and a clip
+    the GPU encoder flags (capacity) falling back to the host encode."""
     from arbius_amd.models import rvm
     from arbius_amd.models.rvm import RVMConfig, RVMPipeline
-    from arbius_amd.utils.mp4 import Yuv420Clip, encode_mp4
+    from arbius_amd.utils.mp4 import H264IntraClip, Yuv420Clip, encode_mp4
     pipe = RVMPipeline(RVMConfig(chunk=4), device=cuda)
     rng = np.random.default_rng(9)
     clip = rng.integers(0, 256, (9, 181, 322, 3), dtype=np.uint8)
     rgb = pipe(clip, "green-screen")
+    want = encode_mp4(rgb, 24)
+    enc = pipe.matte_for_encode(clip, "green-screen")
+    assert isinstance(enc, H264IntraClip) and len(enc) == 9
+    assert encode_mp4(enc, 24) == want
+    monkeypatch.setattr(_lib, "h264_intra_capacity", lambda F, H16, W16: 64)   # flagged -> host encode
+    flagged = pipe.matte_for_encode(clip, "green-screen")
+    assert isinstance(flagged, Yuv420Clip) and encode_mp4(flagged, 24) == want
+    monkeypatch.setattr(rvm, "_GPU_H264", False)
     planes = pipe.matte_for_encode(clip, "green-screen")
     assert isinstance(planes, Yuv420Clip) and len(planes) == 9
-    assert encode_mp4(planes, 24) == encode_mp4(rgb, 24)
+    assert encode_mp4(planes, 24) == want
     monkeypatch.setattr(rvm, "_PINNED_OUT_MAX", 0)        # staged download: RGB frames, same bytes
     staged = pipe.matte_for_encode(clip, "green-screen")
-    assert not isinstance(staged, Yuv420Clip) and encode_mp4(staged, 24) == encode_mp4(rgb, 24)
+    assert not isinstance(staged, (Yuv420Clip, H264IntraClip)) and encode_mp4(staged, 24) == want
