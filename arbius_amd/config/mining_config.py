@@ -132,7 +132,8 @@ class MI355XConfig(_Base):
     rpc_max_batch: int = 50               # calls per batch POST (provider limits)
     tx_stuck_s: float = 12.0              # re-broadcast / fee-bump the lowest unmined nonce after this
     # host-CPU admission (parallel/cpu_budget.py): a model whose per-GPU core budget does not fit every GPU
-    # (robust_video_matting: 13.4 cores per GPU) runs on fewer workers; host_cores overrides sched_getaffinity
+    # (robust_video_matting with host H.264 encode: 13.4 cores per GPU) runs on fewer workers;
+    # host_cores overrides sched_getaffinity
     cpu_admission: bool = True
     host_cores: Optional[int] = None
 

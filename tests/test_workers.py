@@ -187,10 +187,15 @@ def test_dispatch_policies_and_model():
         MultiGPUSolverPool(1, ["anythingv3"], device_type="cpu", tiny=True, dispatch="random")
 
 
-def test_cpu_budget_caps():
-    """Host-CPU admission (parallel/cpu_budget.py): RVM's 13.4 cores per GPU fit 4 GPUs of a 64-core
-    host, the diffusion models fit all 8; no cap when everything fits."""
+def test_cpu_budget_caps(monkeypatch):
+    """Host-CPU admission (parallel/cpu_budget.py): with the GPU H.264 encoder RVM needs ~2.2 cores per
+    GPU and fits every GPU of a 64-core host; host-encoded (ARB_RVM_GPU_H264=0) its 13.4 cores fit 4;
+    the diffusion models fit all 8; no cap when everything fits."""
     from arbius_amd.parallel.cpu_budget import model_gpu_caps
+    assert model_gpu_caps(["anythingv3", "kandinsky2", "robust_video_matting"], 8, cores=64) == {}
+    assert model_gpu_caps(["robust_video_matting", "anythingv3"], 8, cores=16) == {"robust_video_matting": 6,
+                                                                                  "anythingv3": 2}
+    monkeypatch.setenv("ARB_RVM_GPU_H264", "0")
     caps = model_gpu_caps(["anythingv3", "kandinsky2", "robust_video_matting"], 8, cores=64)
     assert caps == {"robust_video_matting": 4}
     assert model_gpu_caps(["robust_video_matting"], 8, cores=128) == {}
