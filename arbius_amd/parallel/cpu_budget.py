@@ -7,9 +7,10 @@ cores; robust video matting needs ~2 with the GPU H.264 encoder (``profiles/r6/r
 and 13.4 when its 48-frame 1080p clips are encoded on the host (``ARB_RVM_GPU_H264=0``) - an 8-GPU
 node on a 64-core host that runs host-encoded RVM on every GPU gets ~60 % of the GPU rate and
 starves its own control plane.  So at boot the pool compares the cores this process may use
-(``os.sched_getaffinity``) with each model's budget and lets a model's tasks onto at most ``floor((cores - reserve) / budget)`` workers (the
-lowest ranks; the others keep every other model).  The cap is logged; ``mi355x.host_cores``
-overrides the core count, ``mi355x.cpu_admission = false`` turns the cap off.
+(``os.sched_getaffinity``) with each model's budget and lets a model's tasks onto at most
+``floor((cores - reserve) / budget)`` workers (the lowest ranks; the others keep every other model).
+The cap is logged; ``mi355x.host_cores`` overrides the core count, ``mi355x.cpu_admission = false``
+turns the cap off.
 """
 from __future__ import annotations
 
