@@ -15,11 +15,13 @@ from pydantic import BaseModel, ConfigDict, Field, model_validator
 
 # Task streams per GPU where a model's best differs from ``mi355x.workers_per_gpu`` (bench.py sweeps:
 # profiles/bench_r4_stream_group_sweep.md).
-DEFAULT_MODEL_STREAMS = {"anythingv3": 3, "kandinsky2": 4, "zeroscopev2xl": 2, "damo": 2, "robust_video_matting": 2}
+DEFAULT_MODEL_STREAMS = {"anythingv3": 3, "kandinsky2": 2, "zeroscopev2xl": 2, "damo": 2, "robust_video_matting": 2}
 # Lock-step group size where a model's best differs from ``mi355x.lockstep_group``.  anythingv3: 3 streams x
 # groups of 8 (batch 16 on the batch-8 canonical plans, with tile families tuned for the batch-16 shapes at
 # the pinned splits - bitwise neutral) measured +2.2 % over 4 x 4 on one box (profiles/sd_groups_r5.md).
-DEFAULT_MODEL_LOCKSTEP = {"anythingv3": 8}
+# kandinsky2: 2 streams x groups of 8 with its batch-16 families, +1.8 % over 4 x 4 at the same p50 latency
+# and 3.3 instead of 5.3 host cores (profiles/r6/k2/).
+DEFAULT_MODEL_LOCKSTEP = {"anythingv3": 8, "kandinsky2": 8}
 
 
 class _Base(BaseModel):
@@ -106,11 +108,11 @@ class MI355XConfig(_Base):
     selftest: bool = True                 # boot CID self-test (index.ts:981-1001)
     selftest_table: Optional[str] = None  # override of config/selftest.json
     workers_per_gpu: int = 4              # task slots per GPU (pipeline forks), capped per model by
-                                          # model_streams (anythingv3 3, kandinsky2 4); 1 = latency mode
+                                          # model_streams (anythingv3 3, kandinsky2 2); 1 = latency mode
     # per-model cap on those streams.  Kandinsky2, measured on one box with every task stream on its own
-    # hardware queue (profiles/sweep_r5.md): 7,236 tasks/h at 2 streams x groups of 4, 7,468 at 3 x 4,
-    # 7,591 at 4 x 4, 6,264 at 4 x 2.  Round 4's 3- and 4-stream losses came from task streams sharing a
-    # queue.  The video UNet's activations fill the GPU at 2 streams (zeroscope 3 streams: 1,129).
+    # hardware queue (round 6, batch-16 families, profiles/r6/k2/): 7,860-7,902 tasks/h at 2 streams x
+    # groups of 8, 7,697-7,799 at 4 x 4, 7,836-7,959 at 3 x 8 (p50 +48 %), 7,790 at 4 x 8, 7,398 at 5 x 4.
+    # The video UNet's activations fill the GPU at 2 streams (zeroscope 3 streams: 1,129).
     model_streams: Dict[str, int] = Field(default_factory=lambda: dict(DEFAULT_MODEL_STREAMS))
     # IPFS gateway (http(s) base URL) for the input of a task whose transaction is not a plain
     # submitTask call (submitted through a contract): the bytes are fetched by the

@@ -6,7 +6,8 @@
     N x { CFG batch-2 UNet3D over [2F, h, w, 4] (hipGraph replay) -> guidance
           -> sampler step }
     KL-VAE decode per frame (chunks) -> uint8 RGB frames -> deterministic MP4
-    (H.264 I_PCM, utils/mp4.py) -> out-1.mp4
+    (H.264 avc-intra, utils/mp4.py; the solve path encodes on the GPU, ops.h264_intra_encode,
+    same bytes) -> out-1.mp4
 
 damo has no negative prompt input (empty uncond).  Random-init weights
 (BASELINE.json); byte-parity with the Replicate containers is "parity unpinned".
@@ -14,6 +15,7 @@ damo has no negative prompt input (empty uncond).  Random-init weights
 from __future__ import annotations
 
 import functools
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, Optional
@@ -22,6 +24,7 @@ import torch
 
 from ..utils.mp4 import encode_mp4
 from ..utils.progress import beat
+
 from .clip_text import CLIPTextConfig, CLIPTextEncoder
 from .. import ops
 from .graphs import GraphCache, PipelineBase
@@ -30,6 +33,9 @@ from .schedulers import GroupSampler, TaskSampler, make_scheduler
 from .tokenizer import CLIPTokenizer
 from .unet3d import UNet3DCondition, UNet3DConfig
 from .vae import VAEConfig, VAEDecoder
+
+# the solve path encodes the decoded frames on the GPU (ARB_VIDEO_GPU_H264=0: host encode, A/B; same bytes)
+_GPU_H264 = os.environ.get("ARB_VIDEO_GPU_H264", "1") != "0"
 
 
 @dataclass
@@ -102,12 +108,15 @@ class VideoPipeline(PipelineBase):
     def __call__(self, prompt: str, negative_prompt: Optional[str] = None, num_frames: Optional[int] = None,
                  width: Optional[int] = None, height: Optional[int] = None,
                  num_inference_steps: Optional[int] = None, guidance_scale: Optional[float] = None,
-                 seed: int = 0):
+                 seed: int = 0, for_encode: bool = False):
+        """uint8 RGB frames [F, H, W, 3]; ``for_encode`` on a GPU: the clip already encoded there
+        (``utils.mp4.H264IntraClip``, the avc-intra bytes of those frames)."""
         with self._stream_ctx():
             return self._run(prompt, negative_prompt, num_frames, width, height, num_inference_steps,
-                             guidance_scale, seed)
+                             guidance_scale, seed, for_encode)
 
-    def _run(self, prompt, negative_prompt, num_frames, width, height, num_inference_steps, guidance_scale, seed):
+    def _run(self, prompt, negative_prompt, num_frames, width, height, num_inference_steps, guidance_scale, seed,
+             for_encode=False):
         cfg = self.cfg
         F = int(num_frames or cfg.num_frames)
         W, H = int(width or cfg.width), int(height or cfg.height)
@@ -144,20 +153,36 @@ class VideoPipeline(PipelineBase):
             samp.step(i, unet(xin, tbuf, ctx))
         sync()
         t2 = time.perf_counter()
-        frames = self.decode(ts.x)
+        frames = self.decode(ts.x, for_encode)
         sync()
         t3 = time.perf_counter()
         self.timings = {"text_s": t1 - t0, "denoise_s": t2 - t1, "vae_s": t3 - t2}
         return frames
 
     @torch.no_grad()
-    def decode(self, latent):
+    def decode(self, latent, for_encode: bool = False):
         z = (latent / self.cfg.vae.scaling_factor).to(self.dtype)
+        if for_encode and _GPU_H264 and z.is_cuda:
+            return self._decode_encoded(z)
         out = []
         for i in range(0, z.shape[0], self.cfg.vae_chunk):
             beat()
             out.append(ops.image_u8(self.vae(z[i:i + self.cfg.vae_chunk]), 0).cpu())
         return torch.cat(out).numpy()                             # [F, H, W, 3]
+
+    def _decode_encoded(self, z):
+        """Decoded frames -> 4:2:0 planes -> avc-intra slices, all on the GPU; only the compressed
+        slices come back (``utils.mp4.H264IntraClip``).  A clip the encoder flags (output capacity)
+        returns the RGB frames for the host encoder (same bytes)."""
+        from ..utils.mp4 import INTRA_QP, H264IntraClip
+        u8 = torch.cat([ops.image_u8(self.vae(z[i:i + self.cfg.vae_chunk]), 0)
+                        for i in range(0, z.shape[0], self.cfg.vae_chunk)])
+        F, H, W, _ = u8.shape
+        enc, meta = ops.h264_intra_encode(*ops.rgb_to_yuv420(u8), INTRA_QP)
+        m = meta.cpu().numpy()
+        if m[F + 1] != 0:
+            return u8.cpu().numpy()
+        return H264IntraClip(enc[:int(m[F])].cpu().numpy(), m, W, H, INTRA_QP)
 
     def solve(self, inp: dict):
         from ..node.solver import solve_files
@@ -165,9 +190,9 @@ class VideoPipeline(PipelineBase):
         frames = self(prompt=inp["prompt"], negative_prompt=inp.get("negative_prompt"),
                       num_frames=inp.get("num_frames"), width=inp.get("width"), height=inp.get("height"),
                       num_inference_steps=inp.get("num_inference_steps"), guidance_scale=inp.get("guidance_scale"),
-                      seed=int(inp["seed"]))
+                      seed=int(inp["seed"]), for_encode=True)
         t1 = time.perf_counter()
-        mp4 = encode_mp4(list(frames), int(inp.get("fps", self.cfg.fps)))
+        mp4 = encode_mp4(frames if not hasattr(frames, "ndim") else list(frames), int(inp.get("fps", self.cfg.fps)))
         tm = dict(self.timings)
         tm.update({"infer_s": t1 - t0, "encode_cid_s": time.perf_counter() - t1})
         return solve_files([("out-1.mp4", mp4)], tm)

@@ -14,7 +14,8 @@ the worker's slot loop (a free stream takes up to ``group`` queued tasks as one 
 GPU service times fitted to measured single-GPU points of the SHIPPED configurations: a group of k tasks
 is W(k) = w0 + w1 k ms of whole-GPU work, and n concurrent streams share the GPU at total rate eff[n]
 (n streams fill the chip better than one).  ``SERVICE_MODELS`` holds one fit per model family
-(``SD15_MODEL``: anythingv3 at its 3 x 8 default, round-5 kernels; ``K2_MODEL``: Kandinsky2 at 4 x 4);
+(``SD15_MODEL``: anythingv3 at its 3 x 8 default, round-5 kernels; ``K2_MODEL``: Kandinsky2 at its
+2 x 8 default, round-6 kernels);
 ``fit_points`` lists the measured (streams, group, ms per round) points each reproduces.  The
 dispatch decision itself is ``pick_rank`` - the same function the pool calls.
 """
@@ -58,13 +59,16 @@ class ServiceModel:
 # saves little beyond batch 8 rows), the rest the stream efficiencies.  (The round-4 fit on 4 x 4
 # groups - w0 204.5, w1 149.7 - described the batch-8 families of that round.)
 SD15_MODEL = ServiceModel(w0=41.1, w1=282.9, eff=[1.0, 2.418, 2.500, 2.488])
-# kandinsky2 768^2, 100 steps + prior (profiles/sweep_r5.md, one box): 2 x 4 3,980 ms, 3 x 4 5,785, 4 x 4
-# (shipped) 7,588, 4 x 2 4,598 ms per round; solo 926 ms (k2_plan_r5.md)
-K2_MODEL = ServiceModel(w0=480.0, w1=446.0, eff=[1.0, 1.138, 1.174, 1.193])
+# kandinsky2 768^2, 100 steps + prior, round-6 kernels with the batch-16 families (profiles/r6/k2/, one box
+# per line): 2 x 8 (shipped) 7,300 ms per round of 16, 4 x 4 7,420, 3 x 8 11,000, 4 x 8 14,780, 5 x 4 9,733;
+# solo 924 ms.  The 4 x 4 / 4 x 8 pair pins w0 / w1 (a group of 8 costs 1.99x a group of 4: the batch-16
+# families make batching nearly free of fixed cost), the rest the stream efficiencies.  (Round 5 fitted
+# 4 x 4 with the batch-8 families only: w0 480, w1 446.)
+K2_MODEL = ServiceModel(w0=28.9, w1=895.1, eff=[1.0, 1.970, 1.961, 1.946, 1.854])
 SERVICE_MODELS = {"anythingv3": SD15_MODEL, "kandinsky2": K2_MODEL}
 FIT_POINTS = {"anythingv3": [(4, 4, 1885), (4, 8, 3704), (3, 8, 2765), (2, 8, 1906), (1, 1, 324)],
-              "kandinsky2": [(2, 4, 3980), (3, 4, 5785), (4, 4, 7588), (4, 2, 4598), (1, 1, 926)]}
-SHIPPED = {"anythingv3": (3, 8), "kandinsky2": (4, 4)}   # streams x lock-step group (config/mining_config.py)
+              "kandinsky2": [(2, 8, 7300), (4, 4, 7420), (3, 8, 11000), (4, 8, 14780), (5, 4, 9733), (1, 1, 924)]}
+SHIPPED = {"anythingv3": (3, 8), "kandinsky2": (2, 8)}   # streams x lock-step group (config/mining_config.py)
 
 
 def fit_points(model: str):

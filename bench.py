@@ -45,11 +45,11 @@ def parse_args(argv=None):
     ap.add_argument("--concurrent", type=int, default=None,
                     help="task streams per GPU (pipeline forks on private HIP streams); default: the node's "
                          "(mi355x.workers_per_gpu = 4, capped per model by mi355x.model_streams: anythingv3 3, "
-                         "kandinsky2 4, video / matting 2)")
+                         "kandinsky2 2, video / matting 2)")
     ap.add_argument("--group", type=int, default=None,
                     help="image models: tasks solved lock-step per stream (one batch-2k UNet launch sequence; "
                          "batch-invariant plans keep every CID equal to its solo solve); default: the node's "
-                         "(mi355x.model_lockstep: 8 for anythingv3, else mi355x.lockstep_group = 4)")
+                         "(mi355x.model_lockstep: 8 for anythingv3 / kandinsky2, else mi355x.lockstep_group = 4)")
     ap.add_argument("--res", type=int, default=None, help="default 512 (anythingv3) / 768 (kandinsky2)")
     ap.add_argument("--height", type=int, default=None,
                     help="image height when it differs from --res (default: --res; zeroscope 320, matting 1080)")

@@ -23,11 +23,13 @@ class _Model:
 def test_defaults():
     cfg = MI355XConfig()
     assert cfg.workers_per_gpu == 4
-    assert cfg.model_streams == DEFAULT_MODEL_STREAMS and cfg.model_streams["kandinsky2"] == 4
+    assert cfg.model_streams == DEFAULT_MODEL_STREAMS and cfg.model_streams["kandinsky2"] == 2
     assert MI355XConfig(model_streams={"kandinsky2": 3}).model_streams == {"kandinsky2": 3}
-    # SD1.5 (anythingv3): 3 streams x lock-step groups of 8 (profiles/sd_groups_r5.md); others groups of 4
+    # SD1.5 (anythingv3): 3 streams x lock-step groups of 8 (profiles/sd_groups_r5.md), Kandinsky2 2 x 8
+    # (profiles/r6/k2/); others groups of 4
     assert cfg.model_streams["anythingv3"] == 3 and cfg.model_lockstep == DEFAULT_MODEL_LOCKSTEP
-    assert cfg.model_lockstep["anythingv3"] == 8 and cfg.lockstep_group == 4
+    assert cfg.model_lockstep["anythingv3"] == 8 and cfg.model_lockstep["kandinsky2"] == 8
+    assert cfg.lockstep_group == 4
 
 
 def test_pool_group_size_per_model(monkeypatch):

@@ -203,6 +203,19 @@ def test_kandinsky2_lockstep_group_bitwise_equals_solo(cuda):
     assert [s.cid for s in solve_images(pipe, inps)] == solo
 
 
+def test_kandinsky2_group_of_8_at_768_bitwise_equals_solo(cuda):
+    """The shipped Kandinsky2 lock-step group (8 tasks = UNet batch 16 on the batch-16 tile families at
+    the pinned splits, config/mining_config.py DEFAULT_MODEL_LOCKSTEP) at the template's 768^2: every
+    CID equals its solo solve."""
+    from arbius_amd.node.solver import solve_images
+    pipe = build_pipeline("kandinsky2", device=cuda)
+    pipe.cfg.num_steps = 3
+    inps = [{"prompt": f"arbius group {i}" + " long" * (3 * i), "width": 768, "height": 768, "seed": 4242 + i}
+            for i in range(8)]
+    solo = [pipe.solve(i).cid for i in inps]
+    assert [s.cid for s in solve_images(pipe, inps)] == solo
+
+
 def _clear_derived_caches(pipe):
     ops._LN_FOLD.clear()
     ops._GEGLU_W.clear()

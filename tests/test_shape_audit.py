@@ -2,7 +2,8 @@
 models' forward passes run on the META device through the real host-side op code (eligibility,
 zero-padding onto the kernels, validation, batch-invariant plan selection from the built library's
 pinned tables); a shape with no HIP kernel would raise ``ops.LibraryFallback``.  For the image
-templates a lock-step group of 4 is checked launch by launch against the solo task (same split-K
+templates lock-step groups of 4 and 8 (the shipped SD / K2 group) are checked launch by launch against
+the solo task (same split-K
 for every conv / GEMM whose rows grow with the group: the reduction order of each output)."""
 import pytest
 import torch
@@ -11,18 +12,21 @@ from arbius_amd import ops
 from arbius_amd.ops import audit
 
 
-def test_anythingv3_every_resolution_solo_and_group():
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("g", [4, 8])
+def test_anythingv3_every_resolution_solo_and_group(g):
     for w in audit.SD_SIZES:
         for h in audit.SD_SIZES:
-            solo, group = audit.sd15(w, h, 1), audit.sd15(w, h, 4)
+            solo, group = audit.sd15(w, h, 1), audit.sd15(w, h, g)
             assert audit.launches(solo), (w, h)
             assert audit.check_invariance(solo, group) == [], (w, h)
 
 
-def test_kandinsky2_every_resolution_solo_and_group():
+@pytest.mark.parametrize("g", [4, 8])
+def test_kandinsky2_every_resolution_solo_and_group(g):
     for w in audit.K2_SIZES:
         for h in audit.K2_SIZES:
-            solo, group = audit.kandinsky2(w, h, 1), audit.kandinsky2(w, h, 4)
+            solo, group = audit.kandinsky2(w, h, 1), audit.kandinsky2(w, h, g)
             assert audit.check_invariance(solo, group) == [], (w, h)
 
 
