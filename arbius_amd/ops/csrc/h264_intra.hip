@@ -223,8 +223,20 @@ struct WBuf {
   HD uint32_t& operator[](int j) const { return p[j * stride]; }
   HD WBuf at(int off) const { return WBuf{p + off * stride, stride}; }
 };
-constexpr int kWork = 192;   // dwords per lane: luma src 64 | luma pred 64 | Cb, Cr src 16 + 16 | Cb, Cr pred 16 + 16
 HD inline int byte_of(const WBuf& s, int i) { return int((s[i >> 2] >> (8 * (i & 3))) & 255u); }
+// acc + sum |a.byte[k] - b.byte[k]| (v_sad_u8 on the device: 4 samples per instruction; the mode
+// decisions' SADs are integer sums, so the two forms are the same number)
+HD inline uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sad_u8(a, b, acc);
+#else
+  for (int k = 0; k < 4; ++k) {
+    const int d = int((a >> (8 * k)) & 255u) - int((b >> (8 * k)) & 255u);
+    acc += uint32_t(d < 0 ? -d : d);
+  }
+  return acc;
+#endif
+}
 
 // Intra_16x16 prediction sample (8.3.3): mode 0 V, 1 H, 2 DC, 3 plane
 struct Pred16 {
@@ -247,348 +259,450 @@ struct PredC {
   }
 };
 
-// the chosen prediction packed 4 samples per dword (one divergent section per macroblock instead of
-// a mode branch per sample), and the SAD of a source block against one mode
-template <int M>
-HD inline void fill16(const Pred16& P, const WBuf& pr) {
+// One 4x4 block's residual (source - prediction, a row of `n` samples per picture row: 16 luma, 8
+// chroma), forward transform and AC quantisation: the DC coefficient is returned, the 15 AC levels
+// (zig-zag positions 1..15) go to ac.  The reconstruction recomputes them (ALU) instead of reading
+// back the levels it stored (a global-memory round trip per block on the serial diagonal path).
+template <int n>
+HD inline int block_ac(const WBuf& s, const WBuf& pr, int bx, int by, int q6, int f, int qbits, int* ac) {
+  int res[16], w4[16];
 #pragma unroll
-  for (int i = 0; i < 64; ++i) {
-    uint32_t v = 0;
+  for (int y = 0; y < 4; ++y)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v |= uint32_t(P.at(M, (4 * i + k) & 15, (4 * i + k) >> 4)) << (8 * k);
-    pr[i] = v;
+    for (int x = 0; x < 4; ++x) {
+      const int i = n * (4 * by + y) + 4 * bx + x;
+      res[4 * y + x] = byte_of(s, i) - byte_of(pr, i);
+    }
+  fwd4x4(res, w4);
+#pragma unroll
+  for (int k = 0; k < 15; ++k) {
+    const int r = kZigzag[k + 1];
+    ac[k] = quant(w4[r], kMF[q6][pos_class(r)], f, qbits);
   }
-}
-template <int M>
-HD inline int sad16(const WBuf& s, const Pred16& P) {
-  int sad = 0;
-#pragma unroll
-  for (int i = 0; i < 256; ++i) {
-    const int d = byte_of(s, i) - P.at(M, i & 15, i >> 4);
-    sad += d < 0 ? -d : d;
-  }
-  return sad;
-}
-template <int M>
-HD inline void fillc(const PredC& Q, const WBuf& pr) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v |= uint32_t(Q.at(M, (4 * i + k) & 7, (4 * i + k) >> 3)) << (8 * k);
-    pr[i] = v;
-  }
-}
-template <int M>
-HD inline int sadc(const WBuf& s, const PredC& Q) {
-  int sad = 0;
-#pragma unroll
-  for (int i = 0; i < 64; ++i) {
-    const int d = byte_of(s, i) - Q.at(M, i & 7, i >> 3);
-    sad += d < 0 ? -d : d;
-  }
-  return sad;
+  return w4[0];
 }
 
-// ---- the per-macroblock decisions, levels and reconstruction (native encode_mb)
-HD inline void analyse_mb(const Pic& p, int mx, int my, const WBuf& wk, uint32_t* dbg = nullptr) {
-  const int W = p.W, Wc = W / 2, mb = my * p.mbw + mx;
-  const bool L = mx > 0, T = my > 0, TL = L && T;
-  const int x0 = 16 * mx, y0 = 16 * my;
-  int16_t* lv = p.lv + (size_t)mb * kLevels;
+// ---- the per-macroblock decisions, levels and reconstruction (native encode_mb), by 4 lanes
+//
+// Lane q of a macroblock owns luma quadrant q (8x8 samples = 4x4 blocks 4q..4q+3 in blkIdx order) and
+// half h = q & 1 of chroma component c = q >> 1 (rows 4h..4h+3 = 4x4 blocks 2h, 2h+1).  Three phases,
+// a mailbox exchange between them (16 dwords per lane):
+//   A  neighbours, predictor parameters, partial SADs of the 4 luma / 4 chroma modes over its samples
+//   B  modes from the summed SADs; its blocks' prediction, residual, transform, AC levels; block DCs
+//   C  luma / chroma DC transform + levels from all blocks' DCs (every lane, redundantly); the
+//      reconstruction of its blocks; lane 0 writes the macroblock's DC levels and mode / cbp word.
+// On the GPU the 4 lanes are neighbours in one wave and the phases are separated by an LDS fence; on
+// the host (arb_h264_intra_host) the phases run lane after lane - the same functions, the same bytes.
+constexpr int kMail = 16;      // mailbox dwords per lane: SADs 0..7, luma DCs 8..11, chroma DCs 12..13, flags 14
+// work dwords per lane: luma src 16 | luma pred 16 | chroma src 8 | chroma pred 8 | dequantised luma DCs 16 |
+// dequantised chroma DCs 4 (per-lane indexing goes through this buffer: indexing a private array by the
+// lane's quadrant would put the lane's state in scratch memory)
+constexpr int kLaneWork = 68;
 
-  // ---- luma: neighbours and the 4 candidate predictions
+HD inline uint32_t pack4(int a, int b, int c, int d) {
+  return uint32_t(a) | uint32_t(b) << 8 | uint32_t(c) << 16 | uint32_t(d) << 24;
+}
+
+struct MbLane {
+  Pic p;
+  int mx, my, q, c, h;
+  bool L, T, TL;
+  WBuf s, pr, sc, pc;   // luma quadrant src / pred (8 rows x 2 dwords), chroma half src / pred (4 x 2)
+  uint32_t* mail;       // the macroblock's mailbox: dword j of lane l at mail[j * mail_stride + l]
+  int mail_stride;      // >= 4 (the 4 lanes' copies of one dword are adjacent)
   Pred16 P;
-  int tl = 0;
-  for (int i = 0; i < 16; ++i) {
-    P.top[i] = T ? p.ry[(size_t)(y0 - 1) * W + x0 + i] : 0;
-    P.left[i] = L ? p.ry[(size_t)(y0 + i) * W + x0 - 1] : 0;
+  PredC C;
+  uint32_t t4[4], ct2[2], t4q[2];
+  int tq[8], lq[8], clq[4], cdq[2];   // this lane's part of the neighbours (no per-lane array indexing)
+  const uint8_t* rcc;                 // component c's reconstruction, source, TotalCoeff planes
+  const uint8_t* scc;
+  uint8_t* tccc;
+  int mode, cmode;
+
+  HD uint32_t& box(int lane, int j) const { return mail[j * mail_stride + lane]; }
+
+  HD void init(const Pic& pic, int mx_, int my_, int q_, const WBuf& wk, uint32_t* mail_, int mstride) {
+    p = pic; mx = mx_; my = my_; q = q_; c = q >> 1; h = q & 1;
+    L = mx > 0; T = my > 0; TL = L && T;
+    s = wk; pr = wk.at(16); sc = wk.at(32); pc = wk.at(40);
+    mail = mail_; mail_stride = mstride;
+    rcc = c ? p.rc[1] : p.rc[0];
+    scc = c ? p.sc[1] : p.sc[0];
+    tccc = c ? p.tcc[1] : p.tcc[0];
   }
-  if (TL) tl = p.ry[(size_t)(y0 - 1) * W + x0 - 1];
-  {
-    int st = 0, sl = 0;
+
+  // ---- A: predictors and partial SADs
+  HD void phase_a() {
+    const int W = p.W, Wc = W / 2, x0 = 16 * mx, y0 = 16 * my, cx0 = 8 * mx, cy0 = 8 * my;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t4[k] = T ? ld32(p.ry + (size_t)(y0 - 1) * W + x0 + 4 * k) : 0u;
+    int tl = TL ? p.ry[(size_t)(y0 - 1) * W + x0 - 1] : 0;
+#pragma unroll
     for (int i = 0; i < 16; ++i) {
-      st += P.top[i];
-      sl += P.left[i];
+      P.top[i] = int((t4[i >> 2] >> (8 * (i & 3))) & 255u);
+      P.left[i] = L ? p.ry[(size_t)(y0 + i) * W + x0 - 1] : 0;
     }
-    P.dc = (L && T) ? (st + sl + 16) >> 5 : L ? (sl + 8) >> 4 : T ? (st + 8) >> 4 : 128;
-    int H = 0, V = 0;
-    for (int i = 0; i < 8; ++i) {
-      const int t0 = P.top[8 + i], t1 = 6 - i < 0 ? tl : P.top[6 - i];
-      const int l0 = P.left[8 + i], l1 = 6 - i < 0 ? tl : P.left[6 - i];
-      H += (i + 1) * (t0 - t1);
-      V += (i + 1) * (l0 - l1);
-    }
-    P.a = 16 * (P.left[15] + P.top[15]);
-    P.b = (5 * H + 32) >> 6;
-    P.c = (5 * V + 32) >> 6;
-  }
-  const WBuf s = wk;   // source macroblock, 16 rows x 16 bytes
-  for (int y = 0; y < 16; ++y)
-    for (int k = 0; k < 4; ++k) s[4 * y + k] = ld32(p.sy + (size_t)(y0 + y) * W + x0 + 4 * k);
-  // candidates in mode order, ties to the lowest mode
-  int mode = 2, best = 1 << 30;
-  if (T) {
-    best = sad16<0>(s, P);
-    mode = 0;
-  }
-  if (L) {
-    const int v = sad16<1>(s, P);
-    if (v < best) { best = v; mode = 1; }
-  }
-  {
-    const int v = sad16<2>(s, P);
-    if (v < best) { best = v; mode = 2; }
-  }
-  if (TL) {
-    const int v = sad16<3>(s, P);
-    if (v < best) { best = v; mode = 3; }
-  }
-  const WBuf pr = wk.at(64);
-  if (mode == 0) fill16<0>(P, pr);
-  else if (mode == 1) fill16<1>(P, pr);
-  else if (mode == 2) fill16<2>(P, pr);
-  else fill16<3>(P, pr);
-
-  // ---- luma levels: AC per block now, the DC after the Hadamard of all 16 block DCs
-  const int qp = p.qp, qp6 = qp % 6, qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
-  int dcm[16];
-  int any_ac = 0;
-#pragma unroll
-  for (int blk = 0; blk < 16; ++blk) {
-    const int bx = kBlkX[blk], by = kBlkY[blk];
-    int res[16], w4[16];
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int i = 16 * (4 * by + y) + 4 * bx + x;
-        res[4 * y + x] = byte_of(s, i) - byte_of(pr, i);
-      }
-    fwd4x4(res, w4);
-    dcm[4 * by + bx] = w4[0];
-    int tc = 0;
-#pragma unroll
-    for (int k = 0; k < 15; ++k) {
-      const int r = kZigzag[k + 1];
-      const int q = quant(w4[r], kMF[qp6][pos_class(r)], fq, qbits);
-      lv[kLvAc + 15 * blk + k] = (int16_t)q;
-      tc += q != 0;
-    }
-    p.tcy[(size_t)(4 * my + by) * 4 * p.mbw + 4 * mx + bx] = (uint8_t)tc;
-    any_ac |= tc;
-  }
-  int hd[16], dc[16];
-  hadamard4(dcm, hd);
-  for (int k = 0; k < 16; ++k) {
-    dc[k] = quant(hd[kZigzag[k]] / 2, kMF[qp6][0], 2 * fq, qbits + 1);
-    lv[k] = (int16_t)dc[k];
-  }
-
-  // ---- luma reconstruction (native recon_luma16)
-  {
-    int c[16], fdc[16];
-    for (int k = 0; k < 16; ++k) c[kZigzag[k]] = dc[k];
-    hadamard4(c, fdc);
-    const int ls = 16 * kV[qp6][0];
-    const Dq dq(qp);
-#pragma unroll
-    for (int blk = 0; blk < 16; ++blk) {
-      const int bx = kBlkX[blk], by = kBlkY[blk];
-      const int fv = fdc[4 * by + bx];
-      int d[16];
-      for (int k = 0; k < 16; ++k) d[k] = 0;
-      d[0] = qp >= 36 ? fv * ls * (1 << (qp / 6 - 6)) : (fv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
-      int any = 0;
-      for (int k = 0; k < 15; ++k) {
-        const int r = kZigzag[k + 1];
-        const int q = lv[kLvAc + 15 * blk + k];
-        d[r] = dq(q, r);
-        any |= q;
-      }
-      int r16[16];
-      if (any) {
-        inv4x4(d, r16);
-      } else {
-        const int v = (d[0] + 32) >> 6;
-        for (int k = 0; k < 16; ++k) r16[k] = v;
-      }
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const int yy = 4 * by + y;
-        uint32_t v = 0;
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-          v |= uint32_t(clip255(byte_of(pr, 16 * yy + 4 * bx + x) + sat16(r16[4 * y + x]))) << (8 * x);
-        *reinterpret_cast<uint32_t*>(p.ry + (size_t)(y0 + yy) * W + x0 + 4 * bx) = v;
-      }
-    }
-  }
-
-  // ---- chroma: one mode for both components by the summed SAD
-  const int qpc = kChromaQp[qp], qc6 = qpc % 6, qcbits = 15 + qpc / 6, fqc = (1 << qcbits) / 3;
-  const int cx0 = 8 * mx, cy0 = 8 * my;
-  PredC C[2];
-  const WBuf sc[2] = {wk.at(128), wk.at(144)};
-  #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    PredC& Q = C[c];
-    const uint8_t* r = p.rc[c];
-    int ctl = 0;
-    for (int i = 0; i < 8; ++i) {
-      Q.top[i] = T ? r[(size_t)(cy0 - 1) * Wc + cx0 + i] : 0;
-      Q.left[i] = L ? r[(size_t)(cy0 + i) * Wc + cx0 - 1] : 0;
-    }
-    if (TL) ctl = r[(size_t)(cy0 - 1) * Wc + cx0 - 1];
-    for (int q = 0; q < 4; ++q) {
-      const int bx = q & 1, by = q >> 1;
+    {
       int st = 0, sl = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { st += P.top[i]; sl += P.left[i]; }
+      P.dc = (L && T) ? (st + sl + 16) >> 5 : L ? (sl + 8) >> 4 : T ? (st + 8) >> 4 : 128;
+      int H = 0, V = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int t1 = 6 - i < 0 ? tl : P.top[6 - i], l1 = 6 - i < 0 ? tl : P.left[6 - i];
+        H += (i + 1) * (P.top[8 + i] - t1);
+        V += (i + 1) * (P.left[8 + i] - l1);
+      }
+      P.a = 16 * (P.left[15] + P.top[15]);
+      P.b = (5 * H + 32) >> 6;
+      P.c = (5 * V + 32) >> 6;
+    }
+    const int qx = q & 1, qy = q >> 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) t4q[k] = T ? ld32(p.ry + (size_t)(y0 - 1) * W + x0 + 8 * qx + 4 * k) : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      tq[k] = int((t4q[k >> 2] >> (8 * (k & 3))) & 255u);
+      lq[k] = L ? p.ry[(size_t)(y0 + 8 * qy + k) * W + x0 - 1] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) s[2 * r + k] = ld32(p.sy + (size_t)(y0 + 8 * qy + r) * W + x0 + 8 * qx + 4 * k);
+    uint32_t sv = 0, sh = 0, sd = 0, sp = 0;
+    const uint32_t dv = uint32_t(P.dc) * 0x01010101u;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int y = 8 * qy + r;
+      const uint32_t lv4 = uint32_t(lq[r]) * 0x01010101u;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint32_t si = s[2 * r + k];
+        const int x = 8 * qx + 4 * k;
+        sv = sad4(si, t4q[k], sv);
+        sh = sad4(si, lv4, sh);
+        sd = sad4(si, dv, sd);
+        sp = sad4(si, pack4(P.at(3, x, y), P.at(3, x + 1, y), P.at(3, x + 2, y), P.at(3, x + 3, y)), sp);
+      }
+    }
+    // chroma component c
+    {
+      const uint8_t* r = rcc;
+      int ctl = TL ? r[(size_t)(cy0 - 1) * Wc + cx0 - 1] : 0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) ct2[k] = T ? ld32(r + (size_t)(cy0 - 1) * Wc + cx0 + 4 * k) : 0u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        C.top[i] = int((ct2[i >> 2] >> (8 * (i & 3))) & 255u);
+        C.left[i] = L ? r[(size_t)(cy0 + i) * Wc + cx0 - 1] : 0;
+      }
+      int H = 0, V = 0;
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
-        st += Q.top[4 * bx + i];
-        sl += Q.left[4 * by + i];
+        const int t1 = 2 - i < 0 ? ctl : C.top[2 - i], l1 = 2 - i < 0 ? ctl : C.left[2 - i];
+        H += (i + 1) * (C.top[4 + i] - t1);
+        V += (i + 1) * (C.left[4 + i] - l1);
       }
-      int v = 128;
-      if (bx == by) {
-        if (T && L) v = (st + sl + 4) >> 3;
-        else if (L) v = (sl + 2) >> 2;
-        else if (T) v = (st + 2) >> 2;
-      } else if (bx == 1) {
-        if (T) v = (st + 2) >> 2;
-        else if (L) v = (sl + 2) >> 2;
-      } else {
-        if (L) v = (sl + 2) >> 2;
-        else if (T) v = (st + 2) >> 2;
-      }
-      Q.dcq[q] = v;
-    }
-    int H = 0, V = 0;
-    for (int i = 0; i < 4; ++i) {
-      const int t1 = 2 - i < 0 ? ctl : Q.top[2 - i], l1 = 2 - i < 0 ? ctl : Q.left[2 - i];
-      H += (i + 1) * (Q.top[4 + i] - t1);
-      V += (i + 1) * (Q.left[4 + i] - l1);
-    }
-    Q.a = 16 * (Q.left[7] + Q.top[7]);
-    Q.b = (34 * H + 32) >> 6;
-    Q.c = (34 * V + 32) >> 6;
-    for (int y = 0; y < 8; ++y)
-      for (int k = 0; k < 2; ++k) sc[c][2 * y + k] = ld32(p.sc[c] + (size_t)(cy0 + y) * Wc + cx0 + 4 * k);
-  }
-  int cmode = 0, cbest = sadc<0>(sc[0], C[0]) + sadc<0>(sc[1], C[1]);
-  if (L) {
-    const int v = sadc<1>(sc[0], C[0]) + sadc<1>(sc[1], C[1]);
-    if (v < cbest) { cbest = v; cmode = 1; }
-  }
-  if (T) {
-    const int v = sadc<2>(sc[0], C[0]) + sadc<2>(sc[1], C[1]);
-    if (v < cbest) { cbest = v; cmode = 2; }
-  }
-  if (TL) {
-    const int v = sadc<3>(sc[0], C[0]) + sadc<3>(sc[1], C[1]);
-    if (v < cbest) { cbest = v; cmode = 3; }
-  }
-  const WBuf pc[2] = {wk.at(160), wk.at(176)};
-  #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    if (cmode == 0) fillc<0>(C[c], pc[c]);
-    else if (cmode == 1) fillc<1>(C[c], pc[c]);
-    else if (cmode == 2) fillc<2>(C[c], pc[c]);
-    else fillc<3>(C[c], pc[c]);
-  }
-  if (dbg) {   // diagnostics (arb_h264_debug): chroma predictor state of one macroblock
-    int o = 0;
-    dbg[o++] = uint32_t(cmode);
-    dbg[o++] = uint32_t(sadc<0>(sc[0], C[0]) + sadc<0>(sc[1], C[1]));
-    dbg[o++] = uint32_t(sadc<3>(sc[0], C[0]) + sadc<3>(sc[1], C[1]));
-    for (int c = 0; c < 2; ++c) {
-      dbg[o++] = uint32_t(C[c].a);
-      dbg[o++] = uint32_t(C[c].b);
-      dbg[o++] = uint32_t(C[c].c);
-      for (int i = 0; i < 4; ++i) dbg[o++] = uint32_t(C[c].dcq[i]);
-      for (int i = 0; i < 8; ++i) dbg[o++] = uint32_t(C[c].top[i]);
-      for (int i = 0; i < 8; ++i) dbg[o++] = uint32_t(C[c].left[i]);
-      for (int i = 0; i < 16; ++i) dbg[o++] = sc[c][i];
-      for (int i = 0; i < 16; ++i) dbg[o++] = pc[c][i];
-    }
-  }
-  int c_any_ac = 0, c_any_dc = 0;
-  int cdc[2][4];
-  #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    int d4[4];
-    for (int blk = 0; blk < 4; ++blk) {
-      const int bx = blk & 1, by = blk >> 1;
-      int res[16], w4[16];
+      C.a = 16 * (C.left[7] + C.top[7]);
+      C.b = (34 * H + 32) >> 6;
+      C.c = (34 * V + 32) >> 6;
 #pragma unroll
-      for (int y = 0; y < 4; ++y)
+      for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const int i = 8 * (4 * by + y) + 4 * bx + x;
-          res[4 * y + x] = byte_of(sc[c], i) - byte_of(pc[c], i);
+        for (int k = 0; k < 2; ++k) sc[2 * rr + k] = ld32(scc + (size_t)(cy0 + 4 * h + rr) * Wc + cx0 + 4 * k);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) clq[k] = L ? r[(size_t)(cy0 + 4 * h + k) * Wc + cx0 - 1] : 0;
+      // the DC predictions of this half's two 4x4 quadrants (bx = k, by = h), from the sums
+      int sl0 = 0, sl1 = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { sl0 += C.left[i]; sl1 += C.left[4 + i]; }
+      const int sl = h ? sl1 : sl0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        int st = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st += C.top[4 * k + i];
+        int v = 128;
+        if (k == h) {
+          if (T && L) v = (st + sl + 4) >> 3;
+          else if (L) v = (sl + 2) >> 2;
+          else if (T) v = (st + 2) >> 2;
+        } else if (k == 1) {
+          if (T) v = (st + 2) >> 2;
+          else if (L) v = (sl + 2) >> 2;
+        } else {
+          if (L) v = (sl + 2) >> 2;
+          else if (T) v = (st + 2) >> 2;
         }
-      fwd4x4(res, w4);
-      d4[blk] = w4[0];
-      int tc = 0;
-      for (int k = 0; k < 15; ++k) {
-        const int r = kZigzag[k + 1];
-        const int q = quant(w4[r], kMF[qc6][pos_class(r)], fqc, qcbits);
-        lv[kLvCac + 60 * c + 15 * blk + k] = (int16_t)q;
-        tc += q != 0;
+        cdq[k] = v;
       }
-      p.tcc[c][(size_t)(2 * my + by) * 2 * p.mbw + 2 * mx + bx] = (uint8_t)tc;
-      c_any_ac |= tc;
     }
-    const int h[4] = {d4[0] + d4[1] + d4[2] + d4[3], d4[0] - d4[1] + d4[2] - d4[3], d4[0] + d4[1] - d4[2] - d4[3],
-                      d4[0] - d4[1] - d4[2] + d4[3]};
-    for (int k = 0; k < 4; ++k) {
-      cdc[c][k] = quant(h[k], kMF[qc6][0], 2 * fqc, qcbits + 1);
-      lv[kLvCdc + 4 * c + k] = (int16_t)cdc[c][k];
-      c_any_dc |= cdc[c][k];
+    uint32_t cd = 0, ch = 0, cv = 0, cpl = 0;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int y = 4 * h + rr;
+      const uint32_t lv4 = uint32_t(clq[rr]) * 0x01010101u;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint32_t si = sc[2 * rr + k];
+        const int x = 4 * k;
+        cd = sad4(si, uint32_t(cdq[k]) * 0x01010101u, cd);
+        ch = sad4(si, lv4, ch);
+        cv = sad4(si, ct2[k], cv);
+        cpl = sad4(si, pack4(C.at(3, x, y), C.at(3, x + 1, y), C.at(3, x + 2, y), C.at(3, x + 3, y)), cpl);
+      }
     }
+    box(q, 0) = sv; box(q, 1) = sh; box(q, 2) = sd; box(q, 3) = sp;
+    box(q, 4) = cd; box(q, 5) = ch; box(q, 6) = cv; box(q, 7) = cpl;
   }
-  const int cbp_chroma = c_any_ac ? 2 : c_any_dc ? 1 : 0;
-  p.info[mb] = uint32_t(mode) | uint32_t(cmode) << 2 | uint32_t(cbp_chroma) << 4 | uint32_t(any_ac != 0) << 6;
 
-  // ---- chroma reconstruction (native recon_chroma)
-  {
-    const int ls = 16 * kV[qc6][0];
-    const Dq dq(qpc);
-    #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int* q4 = cdc[c];
-      const int fv4[4] = {q4[0] + q4[1] + q4[2] + q4[3], q4[0] - q4[1] + q4[2] - q4[3], q4[0] + q4[1] - q4[2] - q4[3],
-                          q4[0] - q4[1] - q4[2] + q4[3]};
-      for (int blk = 0; blk < 4; ++blk) {
-        const int bx = blk & 1, by = blk >> 1;
+  // ---- B: modes, prediction, AC levels of this lane's blocks, block DCs to the mailbox
+  HD void phase_b() {
+    uint32_t sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum[j] += box(l, j);
+    int best = 1 << 30;   // candidates in mode order, ties to the lowest mode
+    mode = 2;
+    if (T) { best = int(sum[0]); mode = 0; }
+    if (L && int(sum[1]) < best) { best = int(sum[1]); mode = 1; }
+    if (int(sum[2]) < best) { best = int(sum[2]); mode = 2; }
+    if (TL && int(sum[3]) < best) { best = int(sum[3]); mode = 3; }
+    int cbest = int(sum[4]);
+    cmode = 0;
+    if (L && int(sum[5]) < cbest) { cbest = int(sum[5]); cmode = 1; }
+    if (T && int(sum[6]) < cbest) { cbest = int(sum[6]); cmode = 2; }
+    if (TL && int(sum[7]) < cbest) { cbest = int(sum[7]); cmode = 3; }
+    // this lane's prediction (quadrant / chroma half), one loop per mode: static indices only
+    const int qx = q & 1, qy = q >> 1;
+    if (mode == 0) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) pr[2 * r + k] = t4q[k];
+    } else if (mode == 1) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) pr[2 * r + k] = uint32_t(lq[r]) * 0x01010101u;
+    } else if (mode == 2) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) pr[i] = uint32_t(P.dc) * 0x01010101u;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int x = 8 * qx + 4 * k, y = 8 * qy + r;
+          pr[2 * r + k] = pack4(P.at(3, x, y), P.at(3, x + 1, y), P.at(3, x + 2, y), P.at(3, x + 3, y));
+        }
+    }
+    if (cmode == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) pc[2 * rr + k] = uint32_t(cdq[k]) * 0x01010101u;
+    } else if (cmode == 1) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) pc[2 * rr + k] = uint32_t(clq[rr]) * 0x01010101u;
+    } else if (cmode == 2) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) pc[2 * rr + k] = ct2[k];
+    } else {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int x = 4 * k, y = 4 * h + rr;
+          pc[2 * rr + k] = pack4(C.at(3, x, y), C.at(3, x + 1, y), C.at(3, x + 2, y), C.at(3, x + 3, y));
+        }
+    }
+    const int qp = p.qp, qp6 = qp % 6, qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
+    const int qpc = kChromaQp[qp], qc6 = qpc % 6, qcbits = 15 + qpc / 6, fqc = (1 << qcbits) / 3;
+    int16_t* lv = p.lv + (size_t)(my * p.mbw + mx) * kLevels;
+    uint32_t flags = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // luma blocks 4q + j: (j & 1, j >> 1) inside the quadrant
+      const int blk = 4 * q + j;
+      int ac[15];
+      box(q, 8 + j) = uint32_t(block_ac<8>(s, pr, j & 1, j >> 1, qp6, fq, qbits, ac));
+      int tc = 0;
+#pragma unroll
+      for (int k = 0; k < 15; ++k) {
+        lv[kLvAc + 15 * blk + k] = (int16_t)ac[k];
+        tc += ac[k] != 0;
+      }
+      p.tcy[(size_t)(4 * my + kBlkY[blk]) * 4 * p.mbw + 4 * mx + kBlkX[blk]] = (uint8_t)tc;
+      flags |= uint32_t(tc != 0) << j;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {   // chroma blocks 2h + j of component c: (j, 0) inside the half
+      const int cblk = 2 * h + j;
+      int ac[15];
+      box(q, 12 + j) = uint32_t(block_ac<8>(sc, pc, j, 0, qc6, fqc, qcbits, ac));
+      int tc = 0;
+#pragma unroll
+      for (int k = 0; k < 15; ++k) {
+        lv[kLvCac + 60 * c + 15 * cblk + k] = (int16_t)ac[k];
+        tc += ac[k] != 0;
+      }
+      tccc[(size_t)(2 * my + h) * 2 * p.mbw + 2 * mx + j] = (uint8_t)tc;
+      flags |= uint32_t(tc != 0) << (4 + j);
+    }
+    box(q, 14) = flags;
+  }
+
+  // ---- C: DC levels from every block's DC, reconstruction of this lane's blocks
+  HD void phase_c() {
+    const int qp = p.qp, qp6 = qp % 6, qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
+    const int qpc = kChromaQp[qp], qc6 = qpc % 6, qcbits = 15 + qpc / 6, fqc = (1 << qcbits) / 3;
+    int dcm[16];
+    uint32_t any_ac = 0, c_any_ac = 0;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int blk = 4 * l + j;
+        dcm[4 * kBlkY[blk] + kBlkX[blk]] = int(box(l, 8 + j));
+      }
+      any_ac |= box(l, 14) & 15u;
+      c_any_ac |= (box(l, 14) >> 4) & 3u;
+    }
+    int hd[16], dc[16];
+    hadamard4(dcm, hd);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dc[k] = quant(hd[kZigzag[k]] / 2, kMF[qp6][0], 2 * fq, qbits + 1);
+    int cdc[2][4], c_any_dc = 0;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int d0 = int(box(2 * cc, 12)), d1 = int(box(2 * cc, 13)), d2 = int(box(2 * cc + 1, 12)),
+                d3 = int(box(2 * cc + 1, 13));
+      const int hh[4] = {d0 + d1 + d2 + d3, d0 - d1 + d2 - d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        cdc[cc][k] = quant(hh[k], kMF[qc6][0], 2 * fqc, qcbits + 1);
+        c_any_dc |= cdc[cc][k];
+      }
+    }
+    const int cbp_chroma = c_any_ac ? 2 : c_any_dc ? 1 : 0;
+    const int mb = my * p.mbw + mx;
+    int16_t* lv = p.lv + (size_t)mb * kLevels;
+    if (q == 0) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) lv[k] = (int16_t)dc[k];
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lv[kLvCdc + 4 * cc + k] = (int16_t)cdc[cc][k];
+      p.info[mb] = uint32_t(mode) | uint32_t(cmode) << 2 | uint32_t(cbp_chroma) << 4 | uint32_t(any_ac != 0) << 6;
+    }
+    // luma reconstruction of blocks 4q .. 4q + 3 (native recon_luma16)
+    const int W = p.W, x0 = 16 * mx, y0 = 16 * my, qx = q & 1, qy = q >> 1;
+    {
+      int cz[16], fdc[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) cz[kZigzag[k]] = dc[k];
+      hadamard4(cz, fdc);
+      const WBuf wf = s.at(48);   // this lane's copy of the 16 dequantisation inputs, indexed by quadrant
+#pragma unroll
+      for (int k = 0; k < 16; ++k) wf[k] = uint32_t(fdc[k]);
+      const int ls = 16 * kV[qp6][0];
+      const Dq dq(qp);
+      const uint32_t nz = box(q, 14);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int fv = int(wf[8 * qy + 2 * qx + 4 * (j >> 1) + (j & 1)]);   // fdc[4 by + bx] of block 4q + j
         int d[16];
+#pragma unroll
         for (int k = 0; k < 16; ++k) d[k] = 0;
-        d[0] = (fv4[blk] * ls * (1 << (qpc / 6))) >> 5;
-        int any = 0;
+        d[0] = qp >= 36 ? fv * ls * (1 << (qp / 6 - 6)) : (fv * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+        int ac[15] = {0}, any = 0;
+        if ((nz >> j) & 1) block_ac<8>(s, pr, j & 1, j >> 1, qp6, fq, qbits, ac);
+#pragma unroll
         for (int k = 0; k < 15; ++k) {
           const int r = kZigzag[k + 1];
-          const int q = lv[kLvCac + 60 * c + 15 * blk + k];
-          d[r] = dq(q, r);
-          any |= q;
+          d[r] = dq(ac[k], r);
+          any |= ac[k];
         }
         int r16[16];
         if (any) {
           inv4x4(d, r16);
         } else {
           const int v = (d[0] + 32) >> 6;
+#pragma unroll
           for (int k = 0; k < 16; ++k) r16[k] = v;
         }
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
-          const int yy = 4 * by + y;
+          const int ly = 4 * (j >> 1) + y;   // row inside the quadrant
+          const uint32_t pw = pr[2 * ly + (j & 1)];
           uint32_t v = 0;
 #pragma unroll
           for (int x = 0; x < 4; ++x)
-            v |= uint32_t(clip255(byte_of(pc[c], 8 * yy + 4 * bx + x) + sat16(r16[4 * y + x]))) << (8 * x);
-          *reinterpret_cast<uint32_t*>(p.rc[c] + (size_t)(cy0 + yy) * Wc + cx0 + 4 * bx) = v;
+            v |= uint32_t(clip255(int((pw >> (8 * x)) & 255u) + sat16(r16[4 * y + x]))) << (8 * x);
+          *reinterpret_cast<uint32_t*>(p.ry + (size_t)(y0 + 8 * qy + ly) * W + x0 + 8 * qx + 4 * (j & 1)) = v;
+        }
+      }
+    }
+    // chroma reconstruction of blocks 2h, 2h + 1 of component c (native recon_chroma)
+    {
+      const int Wc = W / 2, cx0 = 8 * mx, cy0 = 8 * my;
+      const WBuf wc = s.at(64);   // component c's 4 dequantisation inputs (both computed, c's kept)
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const int* q4 = cdc[cc];
+        if (cc == c) {
+          wc[0] = uint32_t(q4[0] + q4[1] + q4[2] + q4[3]);
+          wc[1] = uint32_t(q4[0] - q4[1] + q4[2] - q4[3]);
+          wc[2] = uint32_t(q4[0] + q4[1] - q4[2] - q4[3]);
+          wc[3] = uint32_t(q4[0] - q4[1] - q4[2] + q4[3]);
+        }
+      }
+      const int ls = 16 * kV[qc6][0];
+      const Dq dq(qpc);
+      const uint32_t nz = box(q, 14) >> 4;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cblk = 2 * h + j;
+        int d[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = 0;
+        d[0] = (int(wc[2 * h + j]) * ls * (1 << (qpc / 6))) >> 5;
+        int ac[15] = {0}, any = 0;
+        if ((nz >> j) & 1) block_ac<8>(sc, pc, j, 0, qc6, fqc, qcbits, ac);
+#pragma unroll
+        for (int k = 0; k < 15; ++k) {
+          const int r = kZigzag[k + 1];
+          d[r] = dq(ac[k], r);
+          any |= ac[k];
+        }
+        int r16[16];
+        if (any) {
+          inv4x4(d, r16);
+        } else {
+          const int v = (d[0] + 32) >> 6;
+#pragma unroll
+          for (int k = 0; k < 16; ++k) r16[k] = v;
+        }
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const uint32_t pw = pc[2 * y + j];
+          uint32_t v = 0;
+#pragma unroll
+          for (int x = 0; x < 4; ++x)
+            v |= uint32_t(clip255(int((pw >> (8 * x)) & 255u) + sat16(r16[4 * y + x]))) << (8 * x);
+          *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(rcc) + (size_t)(cy0 + 4 * h + y) * Wc + cx0 + 4 * j) = v;
         }
       }
     }
   }
-}
+};
 
 // ---- CAVLC (native write_block) into a bit sink: Count (lengths only) or Put (the bits)
 struct Count {
@@ -818,36 +932,45 @@ struct EncArgs {
   long long cap;
   int F, W16, H16, qp;
   int agent_sync;
-  uint32_t* dbg;
-  int dbg_mb;
 };
 
-// diagonal hand-off between the analyse kernel's waves: 1 = agent-scope release / acquire around the
-// barrier (the acquire invalidates the CU's vector L1, so a neighbour's reconstruction written by
-// another lane is never read from a stale line), 0 = the plain workgroup barrier (A/B)
-static int g_h264_agent_sync = 1;
+// diagonal hand-off between the analyse kernel's waves: 0 = the workgroup barrier (all waves of the
+// workgroup share one CU and its vector L1, so workgroup scope makes a neighbour's reconstruction
+// visible), 1 = agent-scope release / acquire around it (L2 write-back + L1 invalidate per diagonal,
+// A/B: the same bytes, profiles/r6/h264/)
+static int g_h264_agent_sync = 0;
 ARB_API void arb_set_h264_sync(int v) { g_h264_agent_sync = v; }
-// diagnostics: the chroma predictor state of macroblock `mb` of picture 0 goes to `buf` (>= 128 dwords;
-// device memory for the GPU launch, host memory for arb_h264_intra_host); nullptr = off
-static uint32_t* g_h264_dbg = nullptr;
-static int g_h264_dbg_mb = -1;
-ARB_API void arb_h264_debug(void* buf, int mb) {
-  g_h264_dbg = static_cast<uint32_t*>(buf);
-  g_h264_dbg_mb = mb;
-}
 
-__global__ void __launch_bounds__(128) h264_analyse_kernel(EncArgs a) {
-  __shared__ uint32_t work[kWork * 128];
-  const WBuf wk{work + threadIdx.x, 128};
+// 80 macroblocks x 4 lanes per pass: a 1080p anti-diagonal holds <= 68 macroblocks
+constexpr int kAnalyseThreads = 320;
+
+// the mailbox writes of the other 3 lanes (same wave) are visible: one wave's LDS operations complete
+// in order, so this only has to keep the compiler from moving LDS accesses across it
+__device__ __forceinline__ void lane_exchange() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+__global__ void __launch_bounds__(kAnalyseThreads) h264_analyse_kernel(EncArgs a) {
+  __shared__ uint32_t work[kLaneWork * kAnalyseThreads];
+  __shared__ uint32_t mail[kMail * kAnalyseThreads];
+  const int t = threadIdx.x, slot = t >> 2, q = t & 3;
+  const WBuf wk{work + t, kAnalyseThreads};
   const Layout Lo(a.W16, a.H16);
   const Pic p = make_pic(a.ws + (size_t)blockIdx.x * Lo.per_pic, Lo, a.y, a.cb, a.cr, blockIdx.x, a.W16, a.H16, a.qp);
   for (int d = 0; d < p.mbw + p.mbh - 1; ++d) {
     const int lo = d - (p.mbw - 1) > 0 ? d - (p.mbw - 1) : 0;
     const int hi = d < p.mbh - 1 ? d : p.mbh - 1;
-    for (int my = lo + (int)threadIdx.x; my <= hi; my += blockDim.x) {
-      const int mx = d - my;
-      analyse_mb(p, mx, my, wk,
-                 (a.dbg && blockIdx.x == 0 && my * p.mbw + mx == a.dbg_mb) ? a.dbg : nullptr);
+    for (int base = 0; base <= hi - lo; base += kAnalyseThreads / 4) {
+      const int my = lo + base + slot;
+      const bool active = my <= hi;
+      MbLane ln;
+      if (active) {
+        ln.init(p, d - my, my, q, wk, mail + 4 * slot, kAnalyseThreads);
+        ln.phase_a();
+      }
+      lane_exchange();
+      if (active) ln.phase_b();
+      lane_exchange();
+      if (active) ln.phase_c();
+      lane_exchange();
     }
     // this diagonal's reconstruction / TotalCoeff before the next one reads them
     if (a.agent_sync) {
@@ -962,12 +1085,12 @@ ARB_API int arb_h264_intra_encode(const void* y, const void* cb, const void* cr,
                                   void* ws, void* out, long long cap, void* meta, hipStream_t stream) {
   if (!enc_shape_ok(F, W16, H16, qp) || cap < 0) return -1;
   EncArgs a{(const uint8_t*)y, (const uint8_t*)cb, (const uint8_t*)cr, (uint8_t*)ws, (uint32_t*)out,
-            (long long*)meta, cap, F, W16, H16, qp, g_h264_agent_sync, g_h264_dbg, g_h264_dbg_mb};
+            (long long*)meta, cap, F, W16, H16, qp, g_h264_agent_sync};
   hipError_t e = hipMemsetAsync(meta, 0, sizeof(long long) * (2 * (size_t)F + 2), stream);
   if (e != hipSuccess) return (int)e;
   const long long lanes = (long long)F * (W16 / 16) * (H16 / 16);
   const unsigned mb_blocks = (unsigned)((lanes + 255) / 256);
-  h264_analyse_kernel<<<F, 128, 0, stream>>>(a);
+  h264_analyse_kernel<<<F, kAnalyseThreads, 0, stream>>>(a);
   h264_count_kernel<<<mb_blocks, 256, 0, stream>>>(a);
   h264_scan_kernel<<<F, 1024, 0, stream>>>(a);
   h264_frames_kernel<<<1, 64, 0, stream>>>(a);
@@ -983,7 +1106,7 @@ ARB_API int arb_h264_intra_host(const void* y, const void* cb, const void* cr, i
   if (!enc_shape_ok(F, W16, H16, qp) || cap < 0) return -1;
   const Layout Lo(W16, H16);
   std::vector<uint8_t> ws(Lo.per_pic);
-  std::vector<uint32_t> work(kWork);
+  std::vector<uint32_t> work(4 * kLaneWork), mail(4 * kMail);
   const int mbw = W16 / 16, mbh = H16 / 16, nmb = mbw * mbh;
   for (int i = 0; i < 2 * F + 2; ++i) meta[i] = 0;
   long long base = 0;
@@ -994,8 +1117,11 @@ ARB_API int arb_h264_intra_host(const void* y, const void* cb, const void* cr, i
     int err = 0;
     for (int my = 0; my < mbh; ++my)
       for (int mx = 0; mx < mbw; ++mx) {
-        analyse_mb(p, mx, my, WBuf{work.data(), 1},
-                   (g_h264_dbg && f == 0 && my * mbw + mx == g_h264_dbg_mb) ? g_h264_dbg : nullptr);
+        MbLane ln[4];   // the 4 lanes of the GPU kernel, phase after phase
+        for (int q = 0; q < 4; ++q) ln[q].init(p, mx, my, q, WBuf{work.data() + q, 4}, mail.data(), 4);
+        for (int q = 0; q < 4; ++q) ln[q].phase_a();
+        for (int q = 0; q < 4; ++q) ln[q].phase_b();
+        for (int q = 0; q < 4; ++q) ln[q].phase_c();
         Count c;
         mb_syntax(c, p, mx, my);
         p.bits[my * mbw + mx] = c.n;
