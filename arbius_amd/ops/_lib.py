@@ -90,7 +90,6 @@ _SIGS = {
                                                                     c_void_p]),
     "arb_h264_intra_host": (c_int, [c_void_p] * 3 + [c_int] * 4 + [c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
     "arb_set_h264_sync": (None, [c_int]),
-    "arb_h264_debug": (None, [c_void_p, c_int]),
 }
 
 

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Where the GPU intra encoder's workspace first differs from the host run of the same code
 (ops/csrc/h264_intra.hip): per picture, the first macroblock whose info / levels / bit offset /
-reconstruction / TotalCoeff differ, for each diagonal hand-off mode (arb_set_h264_sync 0 / 1)."""
+reconstruction / TotalCoeff differ, for each diagonal hand-off mode (arb_set_h264_sync 0 / 1).
+(The round-6 per-optimisation-level runs in profiles/r6/h264/dbg_O*.log also dumped one macroblock's
+chroma predictor state through a hook of the earlier one-lane kernel, since removed.)"""
 import json
 import os
 import sys
@@ -88,23 +90,6 @@ def main():
                     print(json.dumps(det), flush=True)
             print(json.dumps(rep), flush=True)
     _lib.lib().arb_set_h264_sync(1)
-    # chroma predictor state of macroblock (1, 1) of the first case, host vs GPU
-    y, cb, cr = planes("smooth", 2, 32, 48, 2 * 32 + 48 + 20)
-    hd = np.zeros(256, np.uint32)
-    _lib.lib().arb_h264_debug(hd.ctypes.data, 4)
-    _lib.h264_intra_host(y, cb, cr, 20)
-    gd = torch.zeros(256, dtype=torch.int32, device=dev)
-    _lib.lib().arb_h264_debug(gd.data_ptr(), 4)
-    _lib.h264_intra_encode(*[torch.from_numpy(p).to(dev) for p in (y, cb, cr)], 20)
-    gd = gd.cpu().numpy().view(np.uint32)
-    _lib.lib().arb_h264_debug(None, -1)
-    names = ["cmode", "sad0", "sad3"]
-    for c in ("cb", "cr"):
-        names += [f"{c}_a", f"{c}_b", f"{c}_c"] + [f"{c}_dcq{i}" for i in range(4)] + [f"{c}_top{i}" for i in range(8)]
-        names += [f"{c}_left{i}" for i in range(8)] + [f"{c}_src{i}" for i in range(16)]
-        names += [f"{c}_pred{i}" for i in range(16)]
-    rows = [(n, int(a), int(b)) for n, a, b in zip(names, hd, gd)]
-    print(json.dumps({"dbg_diff": [r for r in rows if r[1] != r[2]], "dbg_host": rows}), flush=True)
 
 
 if __name__ == "__main__":
