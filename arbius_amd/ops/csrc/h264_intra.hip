@@ -7,9 +7,9 @@
 // Work split (one launch each, all on the caller's stream):
 //   analyse  one workgroup per picture walks the macroblock anti-diagonals (mx + my = d): an
 //            Intra_16x16 macroblock reads only its left / top / top-left neighbours' reconstruction,
-//            so every macroblock of a diagonal is independent.  One lane per macroblock runs the
-//            encoder's decisions (mode SADs, forward transform, quantisation, reconstruction);
-//            levels, modes and TotalCoeff go to a workspace.
+//            so every macroblock of a diagonal is independent.  Four lanes per macroblock (MbLane)
+//            run the encoder's decisions (mode SADs, forward transform, quantisation,
+//            reconstruction); levels, modes and TotalCoeff go to a workspace.
 //   count    one lane per macroblock (all pictures at once): its CAVLC bits.
 //   scan     one workgroup per picture: exclusive prefix of the macroblock bit counts after the
 //            slice header -> each macroblock's bit offset and the picture's RBSP length.
@@ -20,7 +20,7 @@
 //            the result is an OR of disjoint bit ranges, so it does not depend on lane order).
 //
 // The per-macroblock code is __host__ __device__: arb_h264_intra_host runs the identical functions
-// on the CPU in raster order (tests/test_h264_gpu_algo.py compares its NALs with the native
+// on the CPU in raster order (the 4 lanes' phases one after another) (tests/test_h264_gpu_algo.py compares its NALs with the native
 // encoder on a machine without a GPU); the GPU path is checked against the native encoder by
 // tests/test_h264_gpu.py.  Integer arithmetic only: nothing here depends on evaluation order.
 #include "common.h"
@@ -238,25 +238,17 @@ HD inline uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
 #endif
 }
 
-// Intra_16x16 prediction sample (8.3.3): mode 0 V, 1 H, 2 DC, 3 plane
+// Intra_16x16 predictor (8.3.3): the neighbours, the DC value and the plane parameters; V / H / DC
+// samples are the neighbours / dc themselves, plane(x, y) the plane sample
 struct Pred16 {
   int top[16], left[16], dc, a, b, c;
-  HD int at(int mode, int x, int y) const {
-    if (mode == 0) return top[x];
-    if (mode == 1) return left[y];
-    if (mode == 2) return dc;
-    return plane_px(a + b * (x - 7) + c * (y - 7) + 16);
-  }
+  HD int plane(int x, int y) const { return plane_px(a + b * (x - 7) + c * (y - 7) + 16); }
 };
-// Intra chroma 8x8 prediction sample (8.3.4): mode 0 DC (per 4x4 quadrant), 1 H, 2 V, 3 plane
+// Intra chroma 8x8 predictor (8.3.4): neighbours and plane parameters (the per-quadrant DC values of
+// a lane's half are MbLane::cdq)
 struct PredC {
-  int top[8], left[8], dcq[4], a, b, c;
-  HD int at(int mode, int x, int y) const {
-    if (mode == 0) return dcq[(y >> 2) * 2 + (x >> 2)];
-    if (mode == 1) return left[y];
-    if (mode == 2) return top[x];
-    return plane_px(a + b * (x - 3) + c * (y - 3) + 16);
-  }
+  int top[8], left[8], a, b, c;
+  HD int plane(int x, int y) const { return plane_px(a + b * (x - 3) + c * (y - 3) + 16); }
 };
 
 // One 4x4 block's residual (source - prediction, a row of `n` samples per picture row: 16 luma, 8
@@ -383,7 +375,7 @@ struct MbLane {
         sv = sad4(si, t4q[k], sv);
         sh = sad4(si, lv4, sh);
         sd = sad4(si, dv, sd);
-        sp = sad4(si, pack4(P.at(3, x, y), P.at(3, x + 1, y), P.at(3, x + 2, y), P.at(3, x + 3, y)), sp);
+        sp = sad4(si, pack4(P.plane(x, y), P.plane(x + 1, y), P.plane(x + 2, y), P.plane(x + 3, y)), sp);
       }
     }
     // chroma component c
@@ -450,7 +442,7 @@ struct MbLane {
         cd = sad4(si, uint32_t(cdq[k]) * 0x01010101u, cd);
         ch = sad4(si, lv4, ch);
         cv = sad4(si, ct2[k], cv);
-        cpl = sad4(si, pack4(C.at(3, x, y), C.at(3, x + 1, y), C.at(3, x + 2, y), C.at(3, x + 3, y)), cpl);
+        cpl = sad4(si, pack4(C.plane(x, y), C.plane(x + 1, y), C.plane(x + 2, y), C.plane(x + 3, y)), cpl);
       }
     }
     box(q, 0) = sv; box(q, 1) = sh; box(q, 2) = sd; box(q, 3) = sp;
@@ -496,7 +488,7 @@ struct MbLane {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           const int x = 8 * qx + 4 * k, y = 8 * qy + r;
-          pr[2 * r + k] = pack4(P.at(3, x, y), P.at(3, x + 1, y), P.at(3, x + 2, y), P.at(3, x + 3, y));
+          pr[2 * r + k] = pack4(P.plane(x, y), P.plane(x + 1, y), P.plane(x + 2, y), P.plane(x + 3, y));
         }
     }
     if (cmode == 0) {
@@ -520,7 +512,7 @@ struct MbLane {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           const int x = 4 * k, y = 4 * h + rr;
-          pc[2 * rr + k] = pack4(C.at(3, x, y), C.at(3, x + 1, y), C.at(3, x + 2, y), C.at(3, x + 3, y));
+          pc[2 * rr + k] = pack4(C.plane(x, y), C.plane(x + 1, y), C.plane(x + 2, y), C.plane(x + 3, y));
         }
     }
     const int qp = p.qp, qp6 = qp % 6, qbits = 15 + qp / 6, fq = (1 << qbits) / 3;
