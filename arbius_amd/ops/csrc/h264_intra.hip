@@ -22,7 +22,8 @@
 // The per-macroblock code is __host__ __device__: arb_h264_intra_host runs the identical functions
 // on the CPU in raster order, the 4 lanes' phases one after another (tests/test_h264_gpu_algo.py
 // compares its NALs with the native encoder on a machine without a GPU); the GPU path is checked
-// against the native encoder by tests/test_h264_gpu.py.  Integer arithmetic only: nothing here depends on evaluation order.
+// against the native encoder by tests/test_h264_gpu.py.  Integer arithmetic only: nothing here
+// depends on evaluation order.
 #include "common.h"
 
 #include <algorithm>
